@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Device-resident push scatter-add benchmark (BASELINE.json metric).
+
+One step = one push of a batch of (key, value) records that is already resident in HBM into the
+rank's HBM shard: `glint_vec_push_dev` (include/glint_gpu.h), i.e. PartialVector.update
+(src/main/scala/glint/models/server/PartialVector.scala:35-43) on the GPU.
+
+Workload (default): BASELINE.json configs[1] -- 1 GPU, 2^28-key Double vector, dense contiguous
+push (keys[i] = start + i, values U[-1,1) from seed 42). With N GPUs (torchrun), the key space is
+RangePartitioner(N, N * 2^28) and every rank pushes its own dense range (cfg4a: clients own
+contiguous key ranges, no exchange step) -- weak scaling, no collective in the timed region.
+
+Algorithmic bytes per record: 8 (key) + 8 (value) + 8 + 8 (shard read + write)
+= 32 B; value = all ranks' algorithmic bytes / max-over-ranks wall time of the K timed steps.
+The roofline figure uses the push kernel's own device time from HIP events recorded around each
+launch on its stream (glint_prof_*); PMC HBM traffic comes from profiles/ when present.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log2-keys 28] [--pattern dense|zipf]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import glob
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2-keys", type=int, default=28, help="keys per GPU shard (cfg2: 28, north star: 30)")
+    ap.add_argument("--pattern", choices=["dense", "zipf"], default="dense")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the post-run shard check")
+    return ap.parse_args()
+
+
+def pmc_traffic(workload_tag: str):
+    """Per-launch HBM bytes of push_seq from the newest committed PMC summary for this workload
+    (tools/pmc_traffic.py writes profiles/<round>/pmc_<tag>.json), or None."""
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*" / f"pmc_{workload_tag}.json")))
+    if not files:
+        return None
+    try:
+        d = json.loads(Path(files[-1]).read_text())
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(log2_keys: int, seconds: float):
+    """The oracle's scalar PartialVector.update loop (one thread = one actor) on a bounded sample of
+    the same dense workload, timed on this host."""
+    import numpy as np
+    from oracle import oracle as O
+    n = 1 << min(log2_keys, 26)
+    keys = np.arange(n, dtype=np.int64)
+    vals = np.random.default_rng(42).uniform(-1, 1, n)
+    data = np.zeros(n, np.float64)
+    O.vec_update_f64_parallel([0], [n], [data], [keys], [vals], 1)  # warm (page-in)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        O.vec_update_f64_parallel([0], [n], [data], [keys], [vals], 1)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gbs = 32.0 * n * passes / el / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} x PartialVector[Double].update of 2^{min(log2_keys, 26)} dense records "
+                      f"(oracle/glint_oracle.c scalar loop, 1 thread = 1 actor), {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import glint_amd
+    from glint_amd import PartialVector, RangePartitioner
+    from glint_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lib = N.load()
+    per = 1 << args.log2_keys
+    partitioner = RangePartitioner.apply(world, world * per)
+    part = partitioner.all()[rank]
+    shard = PartialVector(part, "double", device=local)
+    n = part.size
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42 + rank)
+    vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+    if args.pattern == "dense":
+        keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
+        nrec, uniq = n, n
+        tag = f"dense_2p{args.log2_keys}"
+        workload = (f"cfg2: dense contiguous-range push, 2^{args.log2_keys}-key Double vector per GPU"
+                    if world == 1 else
+                    f"cfg4a: {world} GPUs, RangePartitioner({world}, {world}x2^{args.log2_keys}), "
+                    f"each rank pushes its own dense range")
+    else:
+        # cfg3: Zipf(1.1) ranks mapped through a seeded permutation of the shard, n = N/4 records
+        rng = np.random.default_rng(42 + rank)
+        nrec = n // 4
+        ranks = rng.zipf(1.1, size=int(nrec * 1.3))
+        ranks = ranks[ranks <= n][:nrec] - 1
+        nrec = ranks.size
+        perm = rng.permutation(n)
+        k = perm[ranks].astype(np.int64) + part.start
+        uniq = int(np.unique(k).size)
+        keys = torch.from_numpy(k).to(dev)
+        vals = vals[:nrec].contiguous()
+        tag = f"zipf_2p{args.log2_keys}"
+        workload = f"cfg3: Zipf(1.1) push of {nrec} records into a 2^{args.log2_keys}-key Double shard"
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    h = shard.handle
+
+    def step():
+        rc = lib.glint_vec_push_dev(h, keys.data_ptr(), vals.data_ptr(), nrec, 0, stream)
+        if rc:
+            raise RuntimeError(N.strerror(rc))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    shard.sync(stream)
+    lib.glint_prof_reset(h)
+    lib.glint_prof_enable(h, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    lib.glint_prof_enable(h, 0)
+    shard.sync(stream)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    ms = C.c_double()
+    cnt = C.c_int64()
+    lib.glint_prof_read(h, N.GLINT_K_PUSH_SEQ, C.byref(ms), C.byref(cnt))
+    seq_ms, seq_n = ms.value, cnt.value
+    lib.glint_prof_read(h, N.GLINT_K_PUSH_SCATTER, C.byref(ms), C.byref(cnt))
+    sc_ms, sc_n = ms.value, cnt.value
+
+    # post-run check: the shard must hold (W+K) sequential additions of each value (bit-exact for
+    # the ordered path); for zipf, a sample checked against the oracle would need the CPU: skip
+    ok = None
+    if not args.no_check and args.pattern == "dense":
+        acc = torch.zeros_like(vals)
+        for _ in range(args.warmup + args.steps):
+            acc += vals
+        got = shard.get(keys)
+        ok = bool(torch.equal(got, acc))
+        del acc, got
+        if not ok:
+            raise SystemExit("post-run shard check FAILED")
+
+    bytes_per_step = 16.0 * nrec + 16.0 * uniq  # n(8+8) + U(8+8)
+    value = world * bytes_per_step * args.steps / dt / 1e9
+    if args.pattern == "dense":
+        kern = "push_seq_kernel"
+        kern_ms = seq_ms / max(seq_n, 1)
+    else:
+        kern = "push_scatter_kernel"
+        kern_ms = (sc_ms / max(sc_n, 1)) + (seq_ms / max(seq_n, 1))
+    achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(tag)
+    out = {
+        "metric": "device-resident push scatter-add GB/s (and % HBM peak) at 1/2/4/8 GPUs",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (keys per BASELINE.md config, values U[-1,1) seed 42+rank), resident in HBM",
+        "config": {"workload": workload, "keys_per_gpu": n, "records_per_step_per_gpu": nrec,
+                   "distinct_keys_per_step_per_gpu": uniq, "key_dtype": "i64", "value_dtype": "f64",
+                   "parallelism": f"range-sharded x{world}, no exchange"},
+        "pct_hbm_peak_per_gpu": round(100.0 * value / world / HBM_PEAK_GBS, 2),
+        "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_launch": bytes_per_step,
+                     "launches_timed": seq_n},
+        "check": ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.log2_keys, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    shard.destroy()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

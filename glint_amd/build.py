@@ -1,0 +1,86 @@
+"""Builds the in-tree native libraries.
+
+* ``glint_amd/lib/libglint_gpu.so`` -- the product: HIP kernels + C ABI (include/glint_gpu.h),
+  compiled for gfx950 only. hipcc cross-compiles it without a GPU.
+* ``oracle/build/libglint_oracle.so`` -- the CPU restatement used by tests as the parity checker
+  (never linked into the product).
+
+Outputs stay in-tree so they travel to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "glint_amd"
+LIB_DIR = PKG / "lib"
+LIB = LIB_DIR / "libglint_gpu.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "build" / "libglint_oracle.so"
+
+HIP_SOURCES = [PKG / "csrc" / "glint_gpu.hip"]
+HIP_DEPS = HIP_SOURCES + [PKG / "csrc" / "glint_kernels.h", ROOT / "include" / "glint_gpu.h"]
+ORACLE_SOURCES = [ORACLE_DIR / "glint_oracle.c"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the glint_amd native library cannot be built")
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_gpu_lib(force: bool = False, verbose: bool = False) -> Path:
+    """Compile libglint_gpu.so for gfx950 (no other target)."""
+    if not force and not _stale(LIB, HIP_DEPS):
+        return LIB
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [
+        _hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+        "-Wall", "-Wno-unused-result",
+        "-o", str(tmp), *map(str, HIP_SOURCES),
+    ]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=str(ROOT))
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the CPU restatement (test infrastructure) with gcc."""
+    if not force and not _stale(ORACLE_LIB, ORACLE_SOURCES):
+        return ORACLE_LIB
+    ORACLE_LIB.parent.mkdir(parents=True, exist_ok=True)
+    tmp = ORACLE_LIB.with_suffix(".so.tmp")
+    cc = shutil.which("gcc") or "cc"
+    cmd = [cc, "-O2", "-std=c11", "-fPIC", "-shared", "-fwrapv", "-pthread", "-o", str(tmp),
+           *map(str, ORACLE_SOURCES)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=str(ROOT))
+    os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_gpu_lib(force=force, verbose=verbose)
+    build_oracle(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)
+    print(LIB)
+    print(ORACLE_LIB)

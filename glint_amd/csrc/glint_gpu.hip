@@ -1,0 +1,1230 @@
+// glint_gpu.hip -- MI355X (gfx950) implementation of include/glint_gpu.h.
+//
+// Device side: the shard loops of Glint's partial models
+//   PartialVector.update / get          src/main/scala/glint/models/server/PartialVector.scala:35-60
+//   PartialMatrix.update / get / getRows src/main/scala/glint/models/server/PartialMatrix.scala:37-83
+// as hand-written HIP kernels (see glint_kernels.h for the push design).
+// Host side: the C ABI (shard lifetime, host-pointer and device-pointer entry points, wire
+// ingest of RequestSerializer payloads, src/main/scala/glint/serialization/RequestSerializer.scala).
+//
+// There is no CPU fallback anywhere in this library: without a GPU every entry point that touches
+// a shard returns GLINT_EDEVICE.
+#include "glint_kernels.h"
+#include "../../include/glint_gpu.h"
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <mutex>
+#include <vector>
+#include <utility>
+#include <new>
+#include <cstring>
+#include <cstdio>
+#include <algorithm>
+#include <cstdlib>
+
+namespace glint {
+
+// ------------------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------------------
+template <typename V> struct Vec2;
+template <> struct Vec2<double> { typedef __attribute__((ext_vector_type(2))) double T; };
+template <> struct Vec2<float> { typedef __attribute__((ext_vector_type(2))) float T; };
+template <> struct Vec2<long long> { typedef __attribute__((ext_vector_type(2))) unsigned long long T; };
+template <> struct Vec2<int> { typedef __attribute__((ext_vector_type(2))) unsigned int T; };
+
+typedef __attribute__((ext_vector_type(2))) long long K2;
+typedef __attribute__((ext_vector_type(2))) int C2;
+
+// Semiring `+` of spire on JVM primitives: IEEE round-to-nearest for Float/Double, two's-complement
+// wrap for Int/Long (PartialVector.scala:39 `data(key) += values(i)`).
+__device__ __forceinline__ double vadd(double a, double b) { return a + b; }
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ long long vadd(long long a, long long b) { return (long long)((u64)a + (u64)b); }
+__device__ __forceinline__ int vadd(int a, int b) { return (int)((u32)a + (u32)b); }
+
+template <typename V> __device__ __forceinline__ typename Vec2<V>::T as2(V x, V y);
+template <> __device__ __forceinline__ Vec2<double>::T as2(double x, double y) { return {x, y}; }
+template <> __device__ __forceinline__ Vec2<float>::T as2(float x, float y) { return {x, y}; }
+template <> __device__ __forceinline__ Vec2<long long>::T as2(long long x, long long y) { return {(u64)x, (u64)y}; }
+template <> __device__ __forceinline__ Vec2<int>::T as2(int x, int y) { return {(u32)x, (u32)y}; }
+
+// device-scope atomic add, no return (global_atomic_add_f64 / _f32 / _x2 / plain)
+__device__ __forceinline__ void gadd(double* p, double v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void gadd(float* p, float v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void gadd(long long* p, long long v) { atomicAdd((u64*)p, (u64)v); }
+__device__ __forceinline__ void gadd(int* p, int v) { atomicAdd((u32*)p, (u32)v); }
+
+__device__ __forceinline__ u32 ld_relaxed(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(u32* p, u32 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void record_error(ErrState* e, i64 idx) {
+  atomicMax(&e->min_bad_enc, ~(u64)idx);
+  atomicAdd(&e->count, 1ull);
+}
+
+// address of a record; false when the JVM would throw ArrayIndexOutOfBoundsException
+template <bool MAT>
+__device__ __forceinline__ bool rec_addr(const PartDesc& p, i64 key, int32_t col, i64& addr) {
+  const int32_t l = g2l(p, key);
+  bool ok = l >= 0 && l < p.size;
+  if (MAT) {
+    ok = ok && col >= 0 && col < p.cols;
+    addr = (i64)l * p.pitch + (i64)col;
+  } else {
+    addr = (i64)l;
+  }
+  return ok;
+}
+
+// ------------------------------------------------------------------------------------------------
+// push_seq: ticketed persistent kernel with decoupled look-back (see glint_kernels.h)
+// ------------------------------------------------------------------------------------------------
+
+// Inclusive-prefix "every address so far strictly increasing" for tile t, computed by the whole
+// block: each of the 256 threads reads 4 status words (sc1, L1-bypassing), so one round trip covers
+// the 1024 tiles before t -- about every tile that can be in flight at once. A_OK tiles are passed
+// over; the nearest P_OK / bad word decides; an EMPTY word (tile not yet checked) is re-polled.
+// A poll that exceeds the spin limit answers "bad", which is always safe: the tile then leaves its
+// records to push_scatter. Called by all threads of the block (contains barriers).
+template <typename V>
+__device__ bool lookback(const PushArgs<V>& a, u32 t, int tid, int* s_red) {
+  const u32 bad = ld_relaxed(&a.ctl->bad_enc);
+  if (bad != 0u && a.ntiles - bad < t) return false;  // a locally unsorted tile precedes t
+  i64 top = (i64)t - 1;                                // nearest tile whose status is unknown
+  u32 spins = 0;
+  const int lane = tid & 63, wid = tid >> 6;
+  while (top >= 0) {
+    // nearest non-A_OK word in this window, encoded (distance << 3) | status for one min-reduce
+    int best = 0x7FFFFFFF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = 4 * tid + q;
+      const i64 idx = top - d;
+      const u32 s = idx >= 0 ? ld_relaxed(a.status + idx) : ST_P_OK;  // before tile 0: prefix OK
+      if (s != ST_A_OK) best = min(best, (d << 3) | (int)s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
+    if (lane == 0) s_red[wid] = best;
+    __syncthreads();
+    best = min(min(s_red[0], s_red[1]), min(s_red[2], s_red[3]));
+    __syncthreads();
+    if (best == 0x7FFFFFFF) { top -= 4 * kTPB; continue; }  // 1024 A_OK tiles: keep walking
+    const int d = best >> 3;
+    const u32 s = (u32)(best & 7);
+    if (s == ST_EMPTY) {
+      top -= d;  // tiles above it are settled A_OK
+      if (++spins > kLookbackSpinLimit) {
+        if (tid == 0) atomicAdd(&a.ctl->timeouts, 1u);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    return s == ST_P_OK;
+  }
+  return true;
+}
+
+// addresses are element indices: int32 for vectors (Partition.globalToLocal is an Int), int64 for
+// matrices (row * pitch + col)
+template <bool MAT> struct AddrT { typedef int32_t T; };
+template <> struct AddrT<true> { typedef i64 T; };
+
+template <bool MAT>
+__device__ __forceinline__ bool rec_addr_t(const PartDesc& p, i64 key, int32_t col, typename AddrT<MAT>::T& addr) {
+  i64 ad;
+  const bool ok = rec_addr<MAT>(p, key, col, ad);
+  addr = (typename AddrT<MAT>::T)ad;
+  return ok;
+}
+
+// One tile in flight per block, software-pipelined over two of the block's tickets:
+//   iteration i:  CHECK(t_i)  -- load keys (+cols) of t_i, compute its addresses, test that they are
+//                                strictly increasing (and above the last address of tile t_i - 1),
+//                                publish A_OK / A_BAD;
+//                 APPLY(t_{i-1}) -- look back for t_{i-1}'s prefix (its predecessors were checked an
+//                                iteration ago, so the walk rarely waits), and if the prefix is
+//                                increasing read-modify-write its shard elements with plain stores.
+// The loads of iteration i -- keys of t_i, values and shard elements of t_{i-1} -- are issued
+// together before the look-back, so each HBM byte is read once and the look-back latency hides
+// under them. The shard read of t_{i-1} is speculative: harmless when the tile is not applied, and
+// when it is, no other tile of the launch touches those elements (all applied tiles' addresses are
+// strictly increasing across tiles).
+template <typename V, bool MAT>
+__global__ __launch_bounds__(kTPB) void push_seq_kernel(PushArgs<V> a) {
+  typedef typename Vec2<V>::T V2;
+  typedef typename AddrT<MAT>::T A;
+  __shared__ int s_b[8];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const i64 n = a.n;
+
+  // a ticket is "dead" when a break before it is already resolved: it and every later ticket stay
+  // unapplied (push_scatter takes them). Decided by thread 0 and broadcast (block-uniform).
+  auto dead_ticket = [&](u32 tt) {
+    const u32 brk = ld_relaxed(&a.ctl->brk_enc);
+    return brk != 0u && a.ntiles - brk < tt;
+  };
+
+  // pending tile (checked, not yet applied)
+  u32 tp = 0xFFFFFFFFu;
+  bool p_ok = false;  // its local check
+  A pa0[kSeqPPT], pa1[kSeqPPT];
+  unsigned pmask = 0;  // bit 2j: record 2p valid, bit 2j+1: record 2p+1 valid
+
+  if (tid == 0) {
+    const u32 tt = atomicAdd(&a.ctl->ticket, 1u);
+    s_b[0] = (int)tt;
+    s_b[1] = dead_ticket(tt);
+  }
+  __syncthreads();
+  u32 t = (u32)s_b[0];
+  bool dead = s_b[1] != 0;
+  __syncthreads();
+
+  for (;;) {
+    const bool have_cur = t < a.ntiles && !dead;
+    if (t < a.ntiles && dead && tid == 0) st_relaxed(a.status + t, ST_P_BAD);  // nobody waits on it
+    const bool have_pend = tp != 0xFFFFFFFFu;
+    if (!have_cur && !have_pend) break;
+
+    u32 t_next = 0xFFFFFFFFu;
+    if (have_cur && tid == 0) t_next = atomicAdd(&a.ctl->ticket, 1u);
+
+    // ---- issue every load of this iteration -----------------------------------------------------
+    K2 k[kSeqPPT];
+    C2 c[kSeqPPT];
+    const i64 pbase = (i64)t * (kSeqTile / 2);
+    if (have_cur) {
+#pragma unroll
+      for (int j = 0; j < kSeqPPT; ++j) {
+        const i64 p = pbase + tid + (i64)j * kTPB;
+        const i64 r = 2 * p;
+        if (r + 1 < n) {
+          k[j] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(a.keys) + p);
+          if (MAT) c[j] = __builtin_nontemporal_load(reinterpret_cast<const C2*>(a.cols) + p);
+        } else if (r < n) {
+          k[j] = K2{a.keys[r], 0};
+          if (MAT) c[j] = C2{a.cols[r], 0};
+        } else {
+          k[j] = K2{0, 0};
+          if (MAT) c[j] = C2{0, 0};
+        }
+      }
+    }
+    V2 v[kSeqPPT], d[kSeqPPT];
+    if (have_pend && p_ok) {
+      const i64 qbase = (i64)tp * (kSeqTile / 2);
+#pragma unroll
+      for (int j = 0; j < kSeqPPT; ++j) {
+        const i64 p = qbase + tid + (i64)j * kTPB;
+        const i64 r = 2 * p;
+        if (r + 1 < n) v[j] = __builtin_nontemporal_load(reinterpret_cast<const V2*>(a.vals) + p);
+        else if (r < n) v[j] = as2<V>(a.vals[r], V(0));
+        else v[j] = as2<V>(V(0), V(0));
+      }
+#pragma unroll
+      for (int j = 0; j < kSeqPPT; ++j) {
+        const bool o0 = (pmask >> (2 * j)) & 1u, o1 = (pmask >> (2 * j + 1)) & 1u;
+        if (o0 && o1 && pa1[j] == pa0[j] + 1 && (pa0[j] & 1) == 0) {
+          d[j] = *reinterpret_cast<const V2*>(a.data + pa0[j]);
+        } else {
+          d[j] = as2<V>(o0 ? a.data[pa0[j]] : V(0), o1 ? a.data[pa1[j]] : V(0));
+        }
+      }
+    }
+
+    // ---- APPLY(pending): look-back overlaps the loads above -----------------------------------
+    if (have_pend) {
+      const bool pre = p_ok ? lookback(a, tp, tid, s_b + 4) : false;
+      if (tid == 0) {
+        st_relaxed(a.status + tp, pre ? ST_P_OK : ST_P_BAD);
+        if (!pre) atomicMax(&a.ctl->brk_enc, a.ntiles - tp);
+      }
+      if (pre) {
+#pragma unroll
+        for (int j = 0; j < kSeqPPT; ++j) {
+          const bool o0 = (pmask >> (2 * j)) & 1u, o1 = (pmask >> (2 * j + 1)) & 1u;
+          const V x = vadd((V)d[j].x, (V)v[j].x);
+          const V y = vadd((V)d[j].y, (V)v[j].y);
+          if (o0 && o1 && pa1[j] == pa0[j] + 1 && (pa0[j] & 1) == 0) {
+            *reinterpret_cast<V2*>(a.data + pa0[j]) = as2<V>(x, y);
+          } else {
+            if (o0) a.data[pa0[j]] = x;
+            if (o1) a.data[pa1[j]] = y;
+          }
+        }
+      }
+      tp = 0xFFFFFFFFu;
+    }
+
+    // ---- CHECK(current): addresses, validity, strictly increasing --------------------------------
+    if (have_cur) {
+      bool mono = true;
+      unsigned mask = 0;
+#pragma unroll
+      for (int j = 0; j < kSeqPPT; ++j) {
+        const i64 p = pbase + tid + (i64)j * kTPB;
+        const i64 r = 2 * p;
+        const bool h0 = r < n, h1 = r + 1 < n;
+        const bool o0 = rec_addr_t<MAT>(a.part, k[j].x, MAT ? c[j].x : 0, pa0[j]) && h0;
+        const bool o1 = rec_addr_t<MAT>(a.part, k[j].y, MAT ? c[j].y : 0, pa1[j]) && h1;
+        mask |= (o0 ? 1u : 0u) << (2 * j);
+        mask |= (o1 ? 1u : 0u) << (2 * j + 1);
+        if (h1) mono = mono && (pa1[j] > pa0[j]);
+        // predecessor of record r is record r-1: the previous lane's second record, or, for lane 0,
+        // a record of another wave / tile read straight from memory (L2-resident)
+        A prev = __shfl_up(pa1[j], 1);
+        if (lane == 0 && r > 0 && h0) {
+          const i64 kp = a.keys[r - 1];
+          const int32_t cp = MAT ? a.cols[r - 1] : 0;
+          rec_addr_t<MAT>(a.part, kp, cp, prev);
+        }
+        if (h0 && r > 0) mono = mono && (pa0[j] > prev);
+        if (h0 && !o0) record_error(a.err, r);
+        if (h1 && !o1) record_error(a.err, r + 1);
+      }
+      pmask = mask;
+      const int ok = __syncthreads_and(mono ? 1 : 0);
+      if (tid == 0) {
+        st_relaxed(a.status + t, ok ? ST_A_OK : ST_A_BAD);
+        if (!ok) atomicMax(&a.ctl->bad_enc, a.ntiles - t);
+      }
+      tp = t;
+      p_ok = ok != 0;
+    }
+
+    // ---- next ticket ----------------------------------------------------------------------------
+    if (tid == 0) {
+      s_b[0] = (int)t_next;
+      s_b[1] = have_cur ? dead_ticket(t_next) : 1;
+    }
+    __syncthreads();
+    t = have_cur ? (u32)s_b[0] : 0xFFFFFFFFu;
+    dead = s_b[1] != 0;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// push_scatter: LDS-binned aggregation + device atomics for records [break*TILE, n)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void lds_add(double* p, double v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void lds_add(float* p, float v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void lds_add(long long* p, long long v) { atomicAdd((u64*)p, (u64)v); }
+__device__ __forceinline__ void lds_add(int* p, int v) { atomicAdd((u32*)p, (u32)v); }
+
+constexpr u64 kEmpty = ~0ull;
+
+template <typename V, bool MAT>
+__global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int force_all) {
+  i64 r0 = 0;
+  if (!force_all) {
+    const u32 brk = a.ctl->brk_enc;  // written by push_seq; ordered by the kernel boundary
+    if (brk == 0u) return;
+    r0 = (i64)(a.ntiles - brk) * kSeqTile;
+  }
+  if (r0 >= a.n) return;
+  const i64 rem = a.n - r0;
+  const i64 nchunks = (rem + kScatterChunk - 1) / kScatterChunk;
+  if ((i64)blockIdx.x >= nchunks) return;
+
+  __shared__ u64 hk[kHashSlots];
+  __shared__ V hv[kHashSlots];
+  const int tid = threadIdx.x;
+  for (int s = tid; s < kHashSlots; s += kTPB) { hk[s] = kEmpty; hv[s] = V(0); }
+  __syncthreads();
+
+  for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const i64 cbase = r0 + ch * kScatterChunk;
+    // a chunk lies inside one push_seq tile (kSeqTile % kScatterChunk == 0); a tile push_seq
+    // applied (P_OK) is skipped, every other tile is applied here -- each record exactly once
+    if (!force_all && a.status[cbase / kSeqTile] == ST_P_OK) continue;
+#pragma unroll 2
+    for (int q = tid; q < kScatterChunk; q += kTPB) {
+      const i64 i = cbase + q;
+      if (i >= a.n) break;
+      const i64 key = a.keys[i];
+      const int32_t col = MAT ? a.cols[i] : 0;
+      const V val = a.vals[i];
+      i64 addr;
+      if (!rec_addr<MAT>(a.part, key, col, addr)) { record_error(a.err, i); continue; }
+      const u64 ua = (u64)addr;
+      u32 h = (u32)((ua * 0x9E3779B97F4A7C15ull) >> (64 - 12));
+      for (;;) {
+        const u64 cur = __hip_atomic_load(&hk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == ua) break;
+        if (cur == kEmpty) {
+          const u64 prev = atomicCAS(&hk[h], kEmpty, ua);
+          if (prev == kEmpty || prev == ua) break;
+        }
+        h = (h + 1) & (kHashSlots - 1);
+      }
+      lds_add(&hv[h], val);
+    }
+    __syncthreads();
+    for (int s = tid; s < kHashSlots; s += kTPB) {
+      const u64 key = hk[s];
+      if (key != kEmpty) {
+        gadd(a.data + key, hv[s]);
+        hk[s] = kEmpty;
+        hv[s] = V(0);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// deterministic tail: stable sort by address, then an in-order fold per address starting from the
+// shard's current value -- the reference's sequential `+=` order, bit for bit
+// ------------------------------------------------------------------------------------------------
+template <bool MAT>
+__global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, const int32_t* cols, i64 r0, i64 m,
+                                                           PartDesc part, u64 sentinel, u64* addr, u32* idx,
+                                                           ErrState* err) {
+  for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
+    i64 ad;
+    const bool ok = rec_addr<MAT>(part, keys[r0 + i], MAT ? cols[r0 + i] : 0, ad);
+    if (!ok) record_error(err, r0 + i);
+    addr[i] = ok ? (u64)ad : sentinel;
+    idx[i] = (u32)i;
+  }
+}
+
+template <typename V>
+__global__ __launch_bounds__(kTPB) void det_fold_kernel(const u64* addr, const u32* idx, i64 m, const V* vals,
+                                                        i64 r0, u64 sentinel, V* data) {
+  for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
+    const u64 ad = addr[i];
+    if (ad == sentinel) continue;
+    if (i > 0 && addr[i - 1] == ad) continue;  // not the head of its run
+    V acc = data[ad];
+    for (i64 j = i; j < m && addr[j] == ad; ++j) acc = vadd(acc, vals[r0 + idx[j]]);
+    data[ad] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// pulls
+// ------------------------------------------------------------------------------------------------
+// PartialVector.get (PartialVector.scala:51-60): out[i] = data(globalToLocal(keys(i)))
+template <typename V, bool PAIRS>
+__global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, const V* data, PartDesc part,
+                                                        V* out, ErrState* err) {
+  typedef typename Vec2<V>::T V2;
+  const i64 stride = (i64)gridDim.x * kTPB;
+  if (PAIRS) {
+    const i64 npairs = (n + 1) >> 1;
+    for (i64 p = (i64)blockIdx.x * kTPB + threadIdx.x; p < npairs; p += stride) {
+      const i64 r = 2 * p;
+      if (r + 1 < n) {
+        const K2 k = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p);
+        i64 l0, l1;
+        const bool o0 = rec_addr<false>(part, k.x, 0, l0);
+        const bool o1 = rec_addr<false>(part, k.y, 0, l1);
+        V2 o;
+        if (o0 && o1 && l1 == l0 + 1 && (l0 & 1) == 0) {
+          o = *reinterpret_cast<const V2*>(data + l0);
+        } else {
+          if (!o0) record_error(err, r);
+          if (!o1) record_error(err, r + 1);
+          o = as2<V>(o0 ? data[l0] : V(0), o1 ? data[l1] : V(0));
+        }
+        *reinterpret_cast<V2*>(out + r) = o;
+      } else {
+        i64 l0;
+        const bool o0 = rec_addr<false>(part, keys[r], 0, l0);
+        if (!o0) record_error(err, r);
+        out[r] = o0 ? data[l0] : V(0);
+      }
+    }
+  } else {
+    for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+      i64 l;
+      const bool o = rec_addr<false>(part, keys[i], 0, l);
+      if (!o) record_error(err, i);
+      out[i] = o ? data[l] : V(0);
+    }
+  }
+}
+
+// PartialMatrix.get (PartialMatrix.scala:55-65)
+template <typename V>
+__global__ __launch_bounds__(kTPB) void mat_pull_kernel(const i64* rows, const int32_t* cols, i64 n, const V* data,
+                                                        PartDesc part, V* out, ErrState* err) {
+  for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += (i64)gridDim.x * kTPB) {
+    i64 ad;
+    const bool o = rec_addr<true>(part, rows[i], cols[i], ad);
+    if (!o) record_error(err, i);
+    out[i] = o ? data[ad] : V(0);
+  }
+}
+
+// PartialMatrix.getRows (PartialMatrix.scala:37-46) + the row flattening of ResponseSerializer
+// (ResponseSerializer.scala:52-61): one wave per requested row, 16 B per lane when rows allow.
+template <typename V, bool VEC16>
+__global__ __launch_bounds__(kTPB) void mat_pull_rows_kernel(const i64* rows, i64 n, const V* data, PartDesc part,
+                                                             V* out, ErrState* err) {
+  const int lane = threadIdx.x & 63;
+  const i64 w0 = (i64)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
+  const i64 nw = (i64)gridDim.x * (kTPB / 64);
+  const i64 cols = part.cols;
+  for (i64 i = w0; i < n; i += nw) {
+    const int32_t l = g2l(part, rows[i]);
+    const bool ok = l >= 0 && l < part.size;
+    if (!ok && lane == 0) record_error(err, i);
+    if (VEC16) {
+      typedef __attribute__((ext_vector_type(4))) unsigned int U4;
+      const i64 chunks = cols * (i64)sizeof(V) / 16;
+      const U4* src = reinterpret_cast<const U4*>(data + (ok ? (i64)l : 0) * part.pitch);
+      U4* dst = reinterpret_cast<U4*>(out + i * cols);
+#pragma unroll 4
+      for (i64 c = lane; c < chunks; c += 64) dst[c] = ok ? src[c] : U4{0, 0, 0, 0};
+    } else {
+      const V* src = data + (ok ? (i64)l : 0) * part.pitch;
+      V* dst = out + i * cols;
+      for (i64 c = lane; c < cols; c += 64) dst[c] = ok ? src[c] : V(0);
+    }
+  }
+}
+
+}  // namespace glint
+
+// ================================================================================================
+// host side
+// ================================================================================================
+using namespace glint;
+
+struct glint_shard {
+  int device = 0;
+  int dtype = 0;
+  size_t vsize = 0;
+  PartDesc part{};
+  i64 elems = 0;  // allocated elements (size * pitch for matrices)
+  void* data = nullptr;
+  hipStream_t stream = nullptr;
+  int cus = 256;
+  // per-launch control region: [LaunchCtl (16 B)][status u32 x cap_tiles]
+  void* d_ctl = nullptr;
+  size_t ctl_bytes = 0;
+  ErrState* d_err = nullptr;
+  // grow-only device scratch for host-pointer calls and the deterministic path
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* d_det = nullptr;
+  size_t det_bytes = 0;
+  i64 last_bad = -1;
+  // kernel timing (glint_prof_*): HIP event pairs recorded on the launch stream, summed lazily
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[GLINT_K_COUNT];
+  double prof_ms[GLINT_K_COUNT] = {0};
+  int64_t prof_n[GLINT_K_COUNT] = {0};
+  std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+#define HIPCHK(x)                                   \
+  do {                                              \
+    hipError_t e_ = (x);                            \
+    if (e_ != hipSuccess) {                         \
+      (void)hipGetLastError();                      \
+      return GLINT_EDEVICE;                         \
+    }                                               \
+  } while (0)
+
+size_t dtype_size(int dt) { return (dt == GLINT_I32 || dt == GLINT_F32) ? 4 : 8; }
+size_t pad16(size_t b) { return (b + 15) & ~(size_t)15; }
+size_t pad256(size_t b) { return (b + 255) & ~(size_t)255; }
+bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+int grow(void** buf, size_t* cap, size_t need) {
+  if (*cap >= need) return GLINT_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  size_t sz = std::max(need, (size_t)1 << 20);
+  if (hipMalloc(buf, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    *buf = nullptr;
+    return GLINT_ENOMEM;
+  }
+  *cap = sz;
+  return GLINT_OK;
+}
+
+// device-resident calls run on the caller's stream exactly as given (NULL = the HIP null stream,
+// as in every HIP API), so they order with the caller's producers and consumers of the buffers
+hipStream_t pick(glint_shard*, void* stream) { return (hipStream_t)stream; }
+
+// Brackets one kernel launch with events on its stream when profiling is on.
+struct ProfScope {
+  glint_shard* s;
+  int id;
+  hipStream_t st;
+  hipEvent_t b = nullptr, e = nullptr;
+  ProfScope(glint_shard* s_, int id_, hipStream_t st_) : s(s_), id(id_), st(st_) {
+    if (!s->prof) return;
+    if (hipEventCreate(&b) != hipSuccess || hipEventCreate(&e) != hipSuccess) {
+      (void)hipGetLastError();
+      b = e = nullptr;
+      return;
+    }
+    (void)hipEventRecord(b, st);
+  }
+  ~ProfScope() {
+    if (!b) return;
+    (void)hipEventRecord(e, st);
+    s->prof_ev[id].emplace_back(b, e);
+  }
+};
+
+void prof_drain(glint_shard* s) {
+  for (int k = 0; k < GLINT_K_COUNT; ++k) {
+    for (auto& pr : s->prof_ev[k]) {
+      float ms = 0.f;
+      if (hipEventSynchronize(pr.second) == hipSuccess && hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+        s->prof_ms[k] += ms;
+        s->prof_n[k] += 1;
+      }
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    s->prof_ev[k].clear();
+  }
+  (void)hipGetLastError();
+}
+
+unsigned grid_for(i64 units, i64 per_block, i64 cap) {
+  i64 g = (units + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---- push -------------------------------------------------------------------------------------
+template <typename V, bool MAT>
+int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
+  // where does the non-increasing tail start? (a host round trip: this is the strict-order path)
+  i64 r0 = 0;
+  if (from_break) {
+    LaunchCtl h{};
+    HIPCHK(hipMemcpyAsync(&h, s->d_ctl, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (h.brk_enc == 0u) return GLINT_OK;
+    r0 = (i64)(a.ntiles - h.brk_enc) * kSeqTile;
+  }
+  if (r0 >= a.n) return GLINT_OK;
+  const i64 m = a.n - r0;
+  const u64 sentinel = (u64)s->elems;
+  int end_bit = 1;
+  while (end_bit < 64 && ((u64)1 << end_bit) <= sentinel) ++end_bit;
+  size_t tmp_bytes = 0;
+  u64* nul64 = nullptr;
+  u32* nul32 = nullptr;
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, nul64, nul64, nul32, nul32, (size_t)m, 0, end_bit, st));
+  const size_t b_addr = pad256((size_t)m * 8), b_idx = pad256((size_t)m * 4);
+  const size_t need = 2 * b_addr + 2 * b_idx + pad256(tmp_bytes);
+  int rc = grow(&s->d_det, &s->det_bytes, need);
+  if (rc) return rc;
+  char* base = (char*)s->d_det;
+  u64* addr_in = (u64*)base;
+  u64* addr_out = (u64*)(base + b_addr);
+  u32* idx_in = (u32*)(base + 2 * b_addr);
+  u32* idx_out = (u32*)(base + 2 * b_addr + b_idx);
+  void* tmp = base + 2 * b_addr + 2 * b_idx;
+  const unsigned g = grid_for(m, kTPB, (i64)s->cus * 8);
+  det_prepare_kernel<MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, r0, m, a.part, sentinel, addr_in, idx_in, a.err);
+  HIPCHK(hipGetLastError());
+  HIPCHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, addr_in, addr_out, idx_in, idx_out, (size_t)m, 0, end_bit, st));
+  det_fold_kernel<V><<<g, kTPB, 0, st>>>(addr_out, idx_out, m, a.vals, r0, sentinel, a.data);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
+template <typename V, bool MAT>
+int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void* vals, i64 n, int flags,
+                hipStream_t st) {
+  if (n <= 0) return GLINT_OK;
+  if (!keys || !vals || (MAT && !cols)) return GLINT_EINVAL;
+  PushArgs<V> a;
+  a.keys = keys;
+  a.cols = cols;
+  a.vals = (const V*)vals;
+  a.n = n;
+  a.data = (V*)s->data;
+  a.part = s->part;
+  a.err = s->d_err;
+  const i64 ntiles = (n + kSeqTile - 1) / kSeqTile;
+  if (ntiles >= (i64)0xFFFFFFF0ll) return GLINT_EINVAL;
+  a.ntiles = (u32)ntiles;
+  const bool vec_ok = aligned(keys, 16) && aligned(vals, 2 * sizeof(V)) && (!MAT || aligned(cols, 8));
+  const bool det = (flags & GLINT_PUSH_DETERMINISTIC) && (s->dtype == GLINT_F32 || s->dtype == GLINT_F64);
+  const size_t ctl_need = sizeof(LaunchCtl) + pad16((size_t)ntiles * 4);
+  int rc = grow(&s->d_ctl, &s->ctl_bytes, ctl_need);
+  if (rc) return rc;
+  a.ctl = (LaunchCtl*)s->d_ctl;
+  a.status = (u32*)((char*)s->d_ctl + sizeof(LaunchCtl));
+  if (vec_ok) {
+    HIPCHK(hipMemsetAsync(s->d_ctl, 0, ctl_need, st));
+    static int per_cu = 0;  // resident blocks per CU of this instantiation (occupancy query, once)
+    if (per_cu == 0) {
+      int b = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, push_seq_kernel<V, MAT>, kTPB, 0) != hipSuccess || b < 1) {
+        (void)hipGetLastError();
+        b = 2;
+      }
+      const char* env = getenv("GLINT_SEQ_BLOCKS_PER_CU");
+      if (env && atoi(env) > 0) b = atoi(env);
+      per_cu = b;
+    }
+    const unsigned g = grid_for(ntiles, 1, (i64)s->cus * per_cu);
+    ProfScope ps(s, GLINT_K_PUSH_SEQ, st);
+    push_seq_kernel<V, MAT><<<g, kTPB, 0, st>>>(a);
+    HIPCHK(hipGetLastError());
+  }
+  if (det) return push_det_tail<V, MAT>(s, a, vec_ok, st);
+  const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
+  ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
+  push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, vec_ok ? 0 : 1);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
+// ---- pulls ------------------------------------------------------------------------------------
+template <typename V>
+int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream_t st) {
+  if (n <= 0) return GLINT_OK;
+  if (!keys || !out) return GLINT_EINVAL;
+  const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
+  ProfScope ps(s, GLINT_K_VEC_PULL, st);
+  if (pairs) {
+    const unsigned g = grid_for((n + 1) / 2, kTPB, (i64)s->cus * 8);
+    vec_pull_kernel<V, true><<<g, kTPB, 0, st>>>(keys, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+  } else {
+    const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);
+    vec_pull_kernel<V, false><<<g, kTPB, 0, st>>>(keys, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+  }
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
+template <typename V>
+int launch_mat_pull(glint_shard* s, const i64* rows, const int32_t* cols, void* out, i64 n, hipStream_t st) {
+  if (n <= 0) return GLINT_OK;
+  if (!rows || !cols || !out) return GLINT_EINVAL;
+  const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);
+  ProfScope ps(s, GLINT_K_MAT_PULL, st);
+  mat_pull_kernel<V><<<g, kTPB, 0, st>>>(rows, cols, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
+template <typename V>
+int launch_mat_pull_rows(glint_shard* s, const i64* rows, void* out, i64 n, hipStream_t st) {
+  if (n <= 0) return GLINT_OK;
+  if (!rows || !out) return GLINT_EINVAL;
+  const bool v16 = ((i64)s->part.cols * (i64)sizeof(V)) % 16 == 0 && aligned(out, 16);
+  const unsigned g = grid_for(n, kTPB / 64, (i64)s->cus * 8);
+  ProfScope ps(s, GLINT_K_MAT_PULL_ROWS, st);
+  if (v16)
+    mat_pull_rows_kernel<V, true><<<g, kTPB, 0, st>>>(rows, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+  else
+    mat_pull_rows_kernel<V, false><<<g, kTPB, 0, st>>>(rows, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
+// dtype dispatch
+#define GLINT_DISPATCH(dt, FN, ...)                            \
+  switch (dt) {                                                \
+    case GLINT_F64: return FN<double>(__VA_ARGS__);            \
+    case GLINT_F32: return FN<float>(__VA_ARGS__);             \
+    case GLINT_I64: return FN<long long>(__VA_ARGS__);         \
+    case GLINT_I32: return FN<int>(__VA_ARGS__);               \
+    default: return GLINT_EINVAL;                              \
+  }
+
+template <typename V>
+int push_vec_t(glint_shard* s, const i64* k, const int32_t*, const void* v, i64 n, int f, hipStream_t st) {
+  return launch_push<V, false>(s, k, nullptr, v, n, f, st);
+}
+template <typename V>
+int push_mat_t(glint_shard* s, const i64* k, const int32_t* c, const void* v, i64 n, int f, hipStream_t st) {
+  return launch_push<V, true>(s, k, c, v, n, f, st);
+}
+
+// read and clear the device error state (caller has synchronised the stream)
+int collect_errors(glint_shard* s, hipStream_t st, int64_t* first_bad) {
+  ErrState h{};
+  HIPCHK(hipMemcpyAsync(&h, s->d_err, sizeof(h), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (h.min_bad_enc != 0) {
+    HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), st));
+    HIPCHK(hipStreamSynchronize(st));
+    s->last_bad = (i64)~h.min_bad_enc;
+    if (first_bad) *first_bad = s->last_bad;
+    return GLINT_EOUTOFRANGE;
+  }
+  return GLINT_OK;
+}
+
+int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
+  if (dtype < GLINT_I32 || dtype > GLINT_F64 || cols < 0) return GLINT_EINVAL;
+  if (s->part.size < 0) return GLINT_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    (void)hipGetLastError();
+    return GLINT_EDEVICE;
+  }
+  DeviceGuard g(device);
+  if (!g.ok) return GLINT_EDEVICE;
+  s->device = device;
+  s->dtype = dtype;
+  s->vsize = dtype_size(dtype);
+  s->part.cols = cols;
+  const i64 per16 = 16 / (i64)s->vsize;
+  s->part.pitch = cols > 0 ? ((i64)cols + per16 - 1) / per16 * per16 : 1;
+  s->elems = cols > 0 ? (i64)s->part.size * s->part.pitch : (i64)s->part.size;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    s->cus = prop.multiProcessorCount;
+  HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  const size_t bytes = std::max<size_t>((size_t)s->elems * s->vsize, 16);
+  if (hipMalloc(&s->data, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return GLINT_ENOMEM;
+  }
+  if (hipMalloc((void**)&s->d_err, sizeof(ErrState)) != hipSuccess) {
+    (void)hipGetLastError();
+    return GLINT_ENOMEM;
+  }
+  HIPCHK(hipMemsetAsync(s->data, 0, bytes, s->stream));  // new Array[V](size) is zeroed
+  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return GLINT_OK;
+}
+
+void free_shard(glint_shard* s) {
+  if (!s) return;
+  {
+    DeviceGuard g(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    prof_drain(s);
+    if (s->data) (void)hipFree(s->data);
+    if (s->d_err) (void)hipFree(s->d_err);
+    if (s->d_ctl) (void)hipFree(s->d_ctl);
+    if (s->d_scratch) (void)hipFree(s->d_scratch);
+    if (s->d_det) (void)hipFree(s->d_det);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    (void)hipGetLastError();
+  }
+  delete s;
+}
+
+// wire constants (src/main/scala/glint/serialization/SerializationConstants.scala:24-38)
+enum : uint8_t {
+  W_PULL_MATRIX = 0x00, W_PULL_MATRIX_ROWS = 0x01, W_PULL_VECTOR = 0x02,
+  W_PUSH_MAT_D = 0x03, W_PUSH_MAT_F = 0x04, W_PUSH_MAT_I = 0x05, W_PUSH_MAT_L = 0x06,
+  W_PUSH_VEC_D = 0x07, W_PUSH_VEC_F = 0x08, W_PUSH_VEC_I = 0x09, W_PUSH_VEC_L = 0x0A,
+  W_RESP_D = 0x10, W_RESP_F = 0x11, W_RESP_I = 0x12, W_RESP_L = 0x13
+};
+
+int wire_dtype_of_push(uint8_t t, bool* mat) {
+  switch (t) {
+    case W_PUSH_MAT_D: *mat = true; return GLINT_F64;
+    case W_PUSH_MAT_F: *mat = true; return GLINT_F32;
+    case W_PUSH_MAT_I: *mat = true; return GLINT_I32;
+    case W_PUSH_MAT_L: *mat = true; return GLINT_I64;
+    case W_PUSH_VEC_D: *mat = false; return GLINT_F64;
+    case W_PUSH_VEC_F: *mat = false; return GLINT_F32;
+    case W_PUSH_VEC_I: *mat = false; return GLINT_I32;
+    case W_PUSH_VEC_L: *mat = false; return GLINT_I64;
+    default: return -1;
+  }
+}
+uint8_t wire_response_type(int dtype) {
+  switch (dtype) {
+    case GLINT_F64: return W_RESP_D;
+    case GLINT_F32: return W_RESP_F;
+    case GLINT_I32: return W_RESP_I;
+    default: return W_RESP_L;
+  }
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+int glint_version(void) { return 100; }
+
+int glint_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+const char* glint_strerror(int status) {
+  switch (status) {
+    case GLINT_OK: return "ok";
+    case GLINT_EOUTOFRANGE: return "key outside the shard (ArrayIndexOutOfBoundsException in the reference)";
+    case GLINT_EDEVICE: return "HIP device error (or no GPU)";
+    case GLINT_EINVAL: return "invalid argument";
+    case GLINT_ENOMEM: return "out of memory";
+    default: return "unknown status";
+  }
+}
+
+int glint_shard_create(int device, int dtype, int64_t start, int64_t end, int32_t cols, glint_shard_t* out) {
+  if (!out) return GLINT_EINVAL;
+  *out = nullptr;
+  glint_shard* s = new (std::nothrow) glint_shard();
+  if (!s) return GLINT_ENOMEM;
+  s->part.kind = 0;
+  s->part.start = start;
+  s->part.size = (int32_t)(end - start);  // RangePartition.size, RangePartition.scala:24
+  int rc = create_common(s, device, dtype, cols);
+  if (rc) { free_shard(s); return rc; }
+  *out = s;
+  return GLINT_OK;
+}
+
+int glint_shard_create_cyclic(int device, int dtype, int32_t index, int32_t num_partitions, int64_t num_keys,
+                              int32_t cols, glint_shard_t* out) {
+  if (!out || num_partitions <= 0 || index < 0 || index >= num_partitions || num_keys <= 0) return GLINT_EINVAL;
+  *out = nullptr;
+  glint_shard* s = new (std::nothrow) glint_shard();
+  if (!s) return GLINT_ENOMEM;
+  s->part.kind = 1;
+  s->part.cidx = index;
+  s->part.cparts = num_partitions;
+  // CyclicPartition.size (CyclicPartition.scala:30-36): local index of the last key it owns + 1
+  int32_t size = 0;
+  for (int64_t i = 1; i <= (int64_t)num_partitions && num_keys - i >= 0; ++i) {
+    const int64_t k = num_keys - i;
+    if ((int32_t)(k % num_partitions) == index) { size = (int32_t)((k - index) / num_partitions) + 1; break; }
+  }
+  s->part.size = size;
+  int rc = create_common(s, device, dtype, cols);
+  if (rc) { free_shard(s); return rc; }
+  *out = s;
+  return GLINT_OK;
+}
+
+int glint_shard_destroy(glint_shard_t s) {
+  if (!s) return GLINT_EINVAL;
+  free_shard(s);
+  return GLINT_OK;
+}
+
+int glint_shard_zero(glint_shard_t s) {
+  if (!s) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  HIPCHK(hipMemsetAsync(s->data, 0, (size_t)s->elems * s->vsize, s->stream));
+  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return GLINT_OK;
+}
+
+int glint_shard_info(glint_shard_t s, int32_t* size, int32_t* cols, int* dtype, int* device) {
+  if (!s) return GLINT_EINVAL;
+  if (size) *size = s->part.size;
+  if (cols) *cols = s->part.cols;
+  if (dtype) *dtype = s->dtype;
+  if (device) *device = s->device;
+  return GLINT_OK;
+}
+
+int glint_shard_data(glint_shard_t s, void** p) {
+  if (!s || !p) return GLINT_EINVAL;
+  *p = s->data;
+  return GLINT_OK;
+}
+
+int glint_shard_pitch(glint_shard_t s, int64_t* e) {
+  if (!s || !e) return GLINT_EINVAL;
+  *e = s->part.cols > 0 ? s->part.pitch : 1;
+  return GLINT_OK;
+}
+
+int glint_shard_last_error(glint_shard_t s, int64_t* first_bad) {
+  if (!s || !first_bad) return GLINT_EINVAL;
+  *first_bad = s->last_bad;
+  return GLINT_OK;
+}
+
+int glint_prof_enable(glint_shard_t s, int on) {
+  if (!s) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->prof = on != 0;
+  return GLINT_OK;
+}
+
+int glint_prof_read(glint_shard_t s, int kernel_id, double* total_ms, int64_t* launches) {
+  if (!s || kernel_id < 0 || kernel_id >= GLINT_K_COUNT) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  prof_drain(s);
+  if (total_ms) *total_ms = s->prof_ms[kernel_id];
+  if (launches) *launches = s->prof_n[kernel_id];
+  return GLINT_OK;
+}
+
+int glint_prof_reset(glint_shard_t s) {
+  if (!s) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  prof_drain(s);
+  for (int k = 0; k < GLINT_K_COUNT; ++k) { s->prof_ms[k] = 0; s->prof_n[k] = 0; }
+  return GLINT_OK;
+}
+
+int glint_shard_sync(glint_shard_t s, void* stream, int64_t* first_bad) {
+  if (!s) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  hipStream_t st = pick(s, stream);
+  HIPCHK(hipStreamSynchronize(st));
+  return collect_errors(s, st, first_bad);
+}
+
+// ---- device-resident ---------------------------------------------------------------------------
+int glint_vec_push_dev(glint_shard_t s, const int64_t* keys, const void* vals, int64_t n, int flags, void* stream) {
+  if (!s || n < 0) return GLINT_EINVAL;
+  if (s->part.cols != 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)keys, nullptr, vals, n, flags, pick(s, stream));
+}
+
+int glint_mat_push_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols, const void* vals, int64_t n,
+                       int flags, void* stream) {
+  if (!s || n < 0) return GLINT_EINVAL;
+  if (s->part.cols == 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
+}
+
+int glint_vec_pull_dev(glint_shard_t s, const int64_t* keys, void* out, int64_t n, void* stream) {
+  if (!s || n < 0) return GLINT_EINVAL;
+  if (s->part.cols != 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)keys, out, n, pick(s, stream));
+}
+
+int glint_mat_pull_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols, void* out, int64_t n,
+                       void* stream) {
+  if (!s || n < 0) return GLINT_EINVAL;
+  if (s->part.cols == 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  GLINT_DISPATCH(s->dtype, launch_mat_pull, s, (const i64*)rows, cols, out, n, pick(s, stream));
+}
+
+int glint_mat_pull_rows_dev(glint_shard_t s, const int64_t* rows, void* out, int64_t n, void* stream) {
+  if (!s || n < 0) return GLINT_EINVAL;
+  if (s->part.cols == 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  GLINT_DISPATCH(s->dtype, launch_mat_pull_rows, s, (const i64*)rows, out, n, pick(s, stream));
+}
+
+}  // extern "C"
+
+// ---- host-pointer entry points --------------------------------------------------------------------
+namespace {
+
+// stage host arrays into the shard's device scratch: returns device pointers to each section
+struct Staged {
+  char* p[3] = {nullptr, nullptr, nullptr};
+};
+
+int stage(glint_shard* s, const void* const* src, const size_t* bytes, int count, Staged& out, size_t extra,
+          char** extra_ptr) {
+  size_t need = 0;
+  for (int i = 0; i < count; ++i) need += pad256(bytes[i]);
+  need += pad256(extra);
+  int rc = grow(&s->d_scratch, &s->scratch_bytes, need);
+  if (rc) return rc;
+  char* b = (char*)s->d_scratch;
+  for (int i = 0; i < count; ++i) {
+    out.p[i] = b;
+    if (bytes[i]) HIPCHK(hipMemcpyAsync(b, src[i], bytes[i], hipMemcpyHostToDevice, s->stream));
+    b += pad256(bytes[i]);
+  }
+  if (extra_ptr) *extra_ptr = b;
+  return GLINT_OK;
+}
+
+int finish(glint_shard* s) {
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return collect_errors(s, s->stream, nullptr);
+}
+
+int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols, const void* vals, int64_t n,
+              int flags) {
+  if (n < 0 || (n > 0 && (!keys || !vals || (mat && !cols)))) return GLINT_EINVAL;
+  if (mat != (s->part.cols != 0)) return GLINT_EINVAL;
+  if (n == 0) return GLINT_OK;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  Staged st;
+  const void* src[3] = {keys, mat ? (const void*)cols : vals, vals};
+  size_t bytes[3] = {(size_t)n * 8, mat ? (size_t)n * 4 : (size_t)n * s->vsize, (size_t)n * s->vsize};
+  int rc = stage(s, src, bytes, mat ? 3 : 2, st, 0, nullptr);
+  if (rc) return rc;
+  if (mat) {
+    rc = [&]() -> int {
+      GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)st.p[0], (const int32_t*)st.p[1], st.p[2], n, flags,
+                     s->stream);
+    }();
+  } else {
+    rc = [&]() -> int {
+      GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)st.p[0], nullptr, st.p[1], n, flags, s->stream);
+    }();
+  }
+  if (rc) return rc;
+  return finish(s);
+}
+
+// kind: 0 vector get, 1 matrix get, 2 matrix rows
+int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols, void* out, int64_t n) {
+  if (n < 0 || (n > 0 && (!keys || !out || (kind == 1 && !cols)))) return GLINT_EINVAL;
+  if ((kind == 0) != (s->part.cols == 0)) return GLINT_EINVAL;
+  if (n == 0) return GLINT_OK;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  const size_t out_bytes = (size_t)n * s->vsize * (kind == 2 ? (size_t)s->part.cols : 1);
+  Staged st;
+  const void* src[2] = {keys, cols};
+  size_t bytes[2] = {(size_t)n * 8, kind == 1 ? (size_t)n * 4 : 0};
+  char* d_out = nullptr;
+  int rc = stage(s, src, bytes, kind == 1 ? 2 : 1, st, out_bytes, &d_out);
+  if (rc) return rc;
+  if (kind == 0) {
+    rc = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)st.p[0], d_out, n, s->stream); }();
+  } else if (kind == 1) {
+    rc = [&]() -> int {
+      GLINT_DISPATCH(s->dtype, launch_mat_pull, s, (const i64*)st.p[0], (const int32_t*)st.p[1], d_out, n,
+                     s->stream);
+    }();
+  } else {
+    rc = [&]() -> int {
+      GLINT_DISPATCH(s->dtype, launch_mat_pull_rows, s, (const i64*)st.p[0], d_out, n, s->stream);
+    }();
+  }
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s->stream));
+  return finish(s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int glint_vec_push(glint_shard_t s, const int64_t* keys, const void* vals, int64_t n, int flags) {
+  if (!s) return GLINT_EINVAL;
+  return host_push(s, false, keys, nullptr, vals, n, flags);
+}
+
+int glint_vec_pull(glint_shard_t s, const int64_t* keys, void* out, int64_t n) {
+  if (!s) return GLINT_EINVAL;
+  return host_pull(s, 0, keys, nullptr, out, n);
+}
+
+int glint_mat_push(glint_shard_t s, const int64_t* rows, const int32_t* cols, const void* vals, int64_t n,
+                   int flags) {
+  if (!s) return GLINT_EINVAL;
+  return host_push(s, true, rows, cols, vals, n, flags);
+}
+
+int glint_mat_pull(glint_shard_t s, const int64_t* rows, const int32_t* cols, void* out, int64_t n) {
+  if (!s) return GLINT_EINVAL;
+  return host_pull(s, 1, rows, cols, out, n);
+}
+
+int glint_mat_pull_rows(glint_shard_t s, const int64_t* rows, void* out, int64_t n) {
+  if (!s) return GLINT_EINVAL;
+  return host_pull(s, 2, rows, nullptr, out, n);
+}
+
+// RequestSerializer.fromBinary (RequestSerializer.scala:59-130) for the push messages, applied
+// straight to the shard: the unaligned key/col/value sections are copied to the device as they lie.
+int glint_push_wire(glint_shard_t s, const uint8_t* payload, size_t len, int32_t* id, int flags) {
+  if (!s || !payload || len < 9) return GLINT_EINVAL;
+  bool mat = false;
+  const int dt = wire_dtype_of_push(payload[0], &mat);
+  if (dt < 0 || dt != s->dtype || mat != (s->part.cols != 0)) return GLINT_EINVAL;
+  int32_t n = 0, mid = 0;
+  std::memcpy(&n, payload + 1, 4);
+  std::memcpy(&mid, payload + 5, 4);
+  if (n < 0) return GLINT_EINVAL;
+  const size_t want = 9 + (size_t)n * (8 + (mat ? 4 : 0) + s->vsize);
+  if (len != want) return GLINT_EINVAL;
+  if (id) *id = mid;
+  const uint8_t* keys = payload + 9;
+  const uint8_t* cols = keys + (size_t)n * 8;
+  const uint8_t* vals = cols + (mat ? (size_t)n * 4 : 0);
+  return host_push(s, mat, (const int64_t*)keys, (const int32_t*)cols, vals, n, flags);
+}
+
+// RequestSerializer.fromBinary for the pull messages + ResponseSerializer.toBinary of the answer
+// (ResponseSerializer.scala:43-117; row answers are flattened rows x cols, :52-61).
+int glint_pull_wire(glint_shard_t s, const uint8_t* payload, size_t len, uint8_t* response, size_t cap,
+                    size_t* out_len) {
+  if (!s || !payload || len < 5 || !out_len) return GLINT_EINVAL;
+  const uint8_t t = payload[0];
+  int32_t n = 0;
+  std::memcpy(&n, payload + 1, 4);
+  if (n < 0) return GLINT_EINVAL;
+  int kind;
+  size_t want;
+  if (t == W_PULL_VECTOR) { kind = 0; want = 5 + (size_t)n * 8; }
+  else if (t == W_PULL_MATRIX) { kind = 1; want = 5 + (size_t)n * 12; }
+  else if (t == W_PULL_MATRIX_ROWS) { kind = 2; want = 5 + (size_t)n * 8; }
+  else return GLINT_EINVAL;
+  if (len != want) return GLINT_EINVAL;
+  if ((kind == 0) != (s->part.cols == 0)) return GLINT_EINVAL;
+  const int64_t count = kind == 2 ? (int64_t)n * s->part.cols : (int64_t)n;
+  if (count > INT32_MAX) return GLINT_EINVAL;  // the response header carries an Int count
+  const size_t resp = 5 + (size_t)count * s->vsize;
+  *out_len = resp;
+  if (!response || cap < resp) return GLINT_EINVAL;
+  response[0] = wire_response_type(s->dtype);
+  const int32_t c32 = (int32_t)count;
+  std::memcpy(response + 1, &c32, 4);
+  const uint8_t* keys = payload + 5;
+  const uint8_t* cols = keys + (size_t)n * 8;
+  return host_pull(s, kind, (const int64_t*)keys, kind == 1 ? (const int32_t*)cols : nullptr, response + 5, n);
+}
+
+}  // extern "C"

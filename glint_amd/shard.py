@@ -1,0 +1,314 @@
+"""Host-side mirror of Glint's server-side partial models, backed by HBM shards.
+
+``PartialVector`` / ``PartialMatrix`` keep the reference's method names and argument meaning
+(src/main/scala/glint/models/server/PartialVector.scala:16-64, PartialMatrix.scala:17-87):
+
+    vec = PartialVector(RangePartition(0, 0, 1000), "double")
+    vec.update(keys, values)      # PartialVector.update  -> True
+    vec.get(keys)                 # PartialVector.get     -> array of values
+
+Every operation runs the HIP kernels through the C ABI (include/glint_gpu.h). Arguments may be
+numpy arrays (host path: staged H2D, synchronous like the actor's ``update``) or torch CUDA tensors
+on the shard's device (device-resident path, stream-ordered on torch's current stream; the call
+synchronises only when ``sync=True``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+from .errors import ArrayIndexOutOfBoundsException, GlintDeviceError
+from .partitioning import CyclicPartition, Partition, RangePartition
+
+_DTYPES = {
+    "int": (N.GLINT_I32, np.int32), "int32": (N.GLINT_I32, np.int32), "i32": (N.GLINT_I32, np.int32),
+    "long": (N.GLINT_I64, np.int64), "int64": (N.GLINT_I64, np.int64), "i64": (N.GLINT_I64, np.int64),
+    "float": (N.GLINT_F32, np.float32), "float32": (N.GLINT_F32, np.float32), "f32": (N.GLINT_F32, np.float32),
+    "double": (N.GLINT_F64, np.float64), "float64": (N.GLINT_F64, np.float64), "f64": (N.GLINT_F64, np.float64),
+}
+
+
+def resolve_dtype(dtype) -> tuple:
+    """Map a value type ('double', np.float64, 'Int', ...) to (GLINT_* code, numpy dtype)."""
+    if isinstance(dtype, str):
+        key = dtype.lower()
+    else:
+        key = np.dtype(dtype).name
+    if key not in _DTYPES:
+        raise ValueError(f"unsupported value type {dtype!r} (Int, Long, Float or Double)")
+    return _DTYPES[key]
+
+
+def check(rc: int, handle=None) -> None:
+    """Translate a C ABI status into the reference's exception types."""
+    if rc == N.GLINT_OK:
+        return
+    if rc == N.GLINT_EOUTOFRANGE:
+        rec = -1
+        if handle is not None:
+            v = C.c_int64(-1)
+            N.load().glint_shard_last_error(handle, C.byref(v))
+            rec = v.value
+        raise ArrayIndexOutOfBoundsException(f"record {rec} is outside the partition", rec)
+    if rc == N.GLINT_EDEVICE:
+        raise GlintDeviceError(N.strerror(rc))
+    if rc == N.GLINT_ENOMEM:
+        raise MemoryError(N.strerror(rc))
+    raise ValueError(N.strerror(rc))
+
+
+def _is_torch_cuda(x) -> bool:
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+def _host(x, dtype) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=dtype))
+
+
+class _Shard:
+    def __init__(self, partition: Partition, dtype, cols: int = 0, device: int = 0):
+        self.lib = N.load()
+        self.partition = partition
+        self.code, self.np_dtype = resolve_dtype(dtype)
+        self.device = int(device)
+        self._h = C.c_void_p()
+        if isinstance(partition, RangePartition):
+            rc = self.lib.glint_shard_create(self.device, self.code, partition.start, partition.end, int(cols),
+                                             C.byref(self._h))
+        elif isinstance(partition, CyclicPartition):
+            rc = self.lib.glint_shard_create_cyclic(self.device, self.code, partition.index,
+                                                    partition.numberOfPartitions, partition.numberOfKeys,
+                                                    int(cols), C.byref(self._h))
+        else:
+            raise TypeError(f"unsupported partition type {type(partition).__name__}")
+        check(rc)
+        sz, cl = C.c_int32(), C.c_int32()
+        check(self.lib.glint_shard_info(self._h, C.byref(sz), C.byref(cl), None, None), self._h)
+        self.size = sz.value
+        self.cols = cl.value
+
+    # lifetime -------------------------------------------------------------------------------
+    @property
+    def handle(self) -> C.c_void_p:
+        if not self._h:
+            raise ValueError("shard already destroyed")
+        return self._h
+
+    def destroy(self) -> None:
+        if self._h:
+            self.lib.glint_shard_destroy(self._h)
+            self._h = C.c_void_p()
+
+    close = destroy
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
+
+    def zero(self) -> None:
+        """What an Akka restart produces: a freshly constructed, zeroed partial model."""
+        check(self.lib.glint_shard_zero(self.handle), self.handle)
+
+    def data_ptr(self) -> int:
+        p = C.c_void_p()
+        check(self.lib.glint_shard_data(self.handle, C.byref(p)), self.handle)
+        return p.value or 0
+
+    def sync(self, stream: Optional[int] = None) -> None:
+        """Wait for device-resident calls and raise if any of them rejected a record."""
+        bad = C.c_int64(-1)
+        rc = self.lib.glint_shard_sync(self.handle, stream, C.byref(bad))
+        if rc == N.GLINT_EOUTOFRANGE:
+            raise ArrayIndexOutOfBoundsException(f"record {bad.value} is outside the partition", bad.value)
+        check(rc, self.handle)
+
+    @staticmethod
+    def _stream_of(t) -> int:
+        import torch
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def _check_dev(self, *tensors) -> None:
+        for t in tensors:
+            if t.device.index != self.device:
+                raise ValueError(f"tensor on cuda:{t.device.index}, shard on cuda:{self.device}")
+            if not t.is_contiguous():
+                raise ValueError("device tensors must be contiguous")
+
+
+class PartialVector(_Shard):
+    """glint.models.server.PartialVector (PartialVector.scala:16-64) on one MI355X."""
+
+    def __init__(self, partition: Partition, dtype="double", device: int = 0):
+        super().__init__(partition, dtype, 0, device)
+
+    def update(self, keys, values, deterministic: bool = False, sync: bool = True) -> bool:
+        """PartialVector.update (PartialVector.scala:35-43): data(globalToLocal(k)) += v."""
+        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+        if _is_torch_cuda(keys):
+            import torch
+            self._check_dev(keys, values)
+            assert keys.dtype == torch.int64 and values.numel() == keys.numel()
+            rc = self.lib.glint_vec_push_dev(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(), flags,
+                                             self._stream_of(keys))
+            check(rc, self.handle)
+            if sync:
+                self.sync(self._stream_of(keys))
+            return True
+        k = _host(keys, np.int64)
+        v = _host(values, self.np_dtype)
+        if k.shape != v.shape:
+            raise ValueError("keys and values differ in length")
+        check(self.lib.glint_vec_push(self.handle, k.ctypes.data, v.ctypes.data, k.size, flags), self.handle)
+        return True
+
+    def get(self, keys, out=None, sync: bool = True):
+        """PartialVector.get (PartialVector.scala:51-60): a new array of data(globalToLocal(k))."""
+        if _is_torch_cuda(keys):
+            import torch
+            self._check_dev(keys)
+            if out is None:
+                out = torch.empty(keys.numel(), dtype=getattr(torch, np.dtype(self.np_dtype).name),
+                                  device=keys.device)
+            rc = self.lib.glint_vec_pull_dev(self.handle, keys.data_ptr(), out.data_ptr(), keys.numel(),
+                                             self._stream_of(keys))
+            check(rc, self.handle)
+            if sync:
+                self.sync(self._stream_of(keys))
+            return out
+        k = _host(keys, np.int64)
+        res = np.empty(k.shape, dtype=self.np_dtype) if out is None else out
+        check(self.lib.glint_vec_pull(self.handle, k.ctypes.data, res.ctypes.data, k.size), self.handle)
+        return res
+
+    def push_wire(self, payload: bytes, deterministic: bool = False) -> int:
+        """Apply a RequestSerializer Push*Vector* byte image; returns its message id."""
+        buf = (C.c_uint8 * len(payload)).from_buffer_copy(payload)
+        mid = C.c_int32()
+        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+        check(self.lib.glint_push_wire(self.handle, buf, len(payload), C.byref(mid), flags), self.handle)
+        return mid.value
+
+    def pull_wire(self, payload: bytes) -> bytes:
+        """Answer a RequestSerializer PullVector byte image with the ResponseSerializer image."""
+        return _pull_wire(self, payload)
+
+    def to_numpy(self) -> np.ndarray:
+        """Whole shard to host (a pull of every local key through the product path)."""
+        p = self.partition
+        if isinstance(p, RangePartition):
+            keys = np.arange(p.start, p.start + self.size, dtype=np.int64)
+        else:
+            keys = np.arange(self.size, dtype=np.int64) * p.numberOfPartitions + p.index
+        return self.get(keys)
+
+
+class PartialMatrix(_Shard):
+    """glint.models.server.PartialMatrix (PartialMatrix.scala:17-87) on one MI355X."""
+
+    def __init__(self, partition: Partition, cols: int, dtype="double", device: int = 0):
+        if int(cols) <= 0:
+            raise ValueError("a matrix shard needs cols > 0")
+        super().__init__(partition, dtype, int(cols), device)
+        self.rows = self.size
+
+    def update(self, rows, cols, values, deterministic: bool = False, sync: bool = True) -> bool:
+        """PartialMatrix.update (PartialMatrix.scala:74-83)."""
+        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+        if _is_torch_cuda(rows):
+            self._check_dev(rows, cols, values)
+            rc = self.lib.glint_mat_push_dev(self.handle, rows.data_ptr(), cols.data_ptr(), values.data_ptr(),
+                                             rows.numel(), flags, self._stream_of(rows))
+            check(rc, self.handle)
+            if sync:
+                self.sync(self._stream_of(rows))
+            return True
+        r = _host(rows, np.int64)
+        c = _host(cols, np.int32)
+        v = _host(values, self.np_dtype)
+        if not (r.shape == c.shape == v.shape):
+            raise ValueError("rows, cols and values differ in length")
+        check(self.lib.glint_mat_push(self.handle, r.ctypes.data, c.ctypes.data, v.ctypes.data, r.size, flags),
+              self.handle)
+        return True
+
+    def get(self, rows, cols, out=None, sync: bool = True):
+        """PartialMatrix.get (PartialMatrix.scala:55-65)."""
+        if _is_torch_cuda(rows):
+            import torch
+            self._check_dev(rows, cols)
+            if out is None:
+                out = torch.empty(rows.numel(), dtype=getattr(torch, np.dtype(self.np_dtype).name),
+                                  device=rows.device)
+            rc = self.lib.glint_mat_pull_dev(self.handle, rows.data_ptr(), cols.data_ptr(), out.data_ptr(),
+                                             rows.numel(), self._stream_of(rows))
+            check(rc, self.handle)
+            if sync:
+                self.sync(self._stream_of(rows))
+            return out
+        r = _host(rows, np.int64)
+        c = _host(cols, np.int32)
+        res = np.empty(r.shape, dtype=self.np_dtype) if out is None else out
+        check(self.lib.glint_mat_pull(self.handle, r.ctypes.data, c.ctypes.data, res.ctypes.data, r.size),
+              self.handle)
+        return res
+
+    def getRows(self, rows, out=None, sync: bool = True):
+        """PartialMatrix.getRows (PartialMatrix.scala:37-46) as one (n, cols) array -- the flattened
+        row-major image ResponseSerializer sends (ResponseSerializer.scala:52-61)."""
+        if _is_torch_cuda(rows):
+            import torch
+            self._check_dev(rows)
+            if out is None:
+                out = torch.empty((rows.numel(), self.cols), dtype=getattr(torch, np.dtype(self.np_dtype).name),
+                                  device=rows.device)
+            rc = self.lib.glint_mat_pull_rows_dev(self.handle, rows.data_ptr(), out.data_ptr(), rows.numel(),
+                                                  self._stream_of(rows))
+            check(rc, self.handle)
+            if sync:
+                self.sync(self._stream_of(rows))
+            return out
+        r = _host(rows, np.int64)
+        res = np.empty((r.size, self.cols), dtype=self.np_dtype) if out is None else out
+        check(self.lib.glint_mat_pull_rows(self.handle, r.ctypes.data, res.ctypes.data, r.size), self.handle)
+        return res
+
+    def push_wire(self, payload: bytes, deterministic: bool = False) -> int:
+        buf = (C.c_uint8 * len(payload)).from_buffer_copy(payload)
+        mid = C.c_int32()
+        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+        check(self.lib.glint_push_wire(self.handle, buf, len(payload), C.byref(mid), flags), self.handle)
+        return mid.value
+
+    def pull_wire(self, payload: bytes) -> bytes:
+        return _pull_wire(self, payload)
+
+    def to_numpy(self) -> np.ndarray:
+        p = self.partition
+        if isinstance(p, RangePartition):
+            rows = np.arange(p.start, p.start + self.size, dtype=np.int64)
+        else:
+            rows = np.arange(self.size, dtype=np.int64) * p.numberOfPartitions + p.index
+        return self.getRows(rows)
+
+
+def _pull_wire(shard: _Shard, payload: bytes) -> bytes:
+    lib = shard.lib
+    buf = (C.c_uint8 * len(payload)).from_buffer_copy(payload)
+    need = C.c_size_t(0)
+    rc = lib.glint_pull_wire(shard.handle, buf, len(payload), None, 0, C.byref(need))
+    if rc != N.GLINT_OK and need.value == 0:
+        check(rc, shard.handle)
+    out = (C.c_uint8 * need.value)()
+    check(lib.glint_pull_wire(shard.handle, buf, len(payload), out, need.value, C.byref(need)), shard.handle)
+    return bytes(out)

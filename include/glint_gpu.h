@@ -1,0 +1,169 @@
+/*
+ * glint_gpu.h -- C ABI of the MI355X push/pull reduction plane for Glint's parameter server.
+ *
+ * A "shard" is the device-resident replacement of one Glint partial model: the JVM array
+ * `data` of PartialVector[V] (src/main/scala/glint/models/server/PartialVector.scala:27) or
+ * PartialMatrix[V] (src/main/scala/glint/models/server/PartialMatrix.scala:28), now held in HBM
+ * of one MI355X. The entry points below are exactly the methods of those classes that the
+ * server actors call (PartialVectorDouble.scala:17-23, PartialMatrixDouble.scala:21-28), plus
+ * shard lifetime, device-resident variants for stream-ordered callers, and a raw wire-format
+ * ingest of the reference's RequestSerializer payloads.
+ *
+ * Plain C: pointers, sizes and status codes only. Thread-safety: calls on DIFFERENT shards may
+ * run concurrently from any threads; calls on ONE shard are serialized internally (the Akka
+ * actor already serializes them, PartialVector.scala:16-17). Every host-pointer call is
+ * synchronous: when it returns, its effect is visible to the next call on the same shard.
+ */
+#ifndef GLINT_GPU_H
+#define GLINT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Value types of the typed partial models (PartialVector{Int,Long,Float,Double}.scala,
+ * PartialMatrix{Int,Long,Float,Double}.scala). */
+enum glint_dtype { GLINT_I32 = 0, GLINT_I64 = 1, GLINT_F32 = 2, GLINT_F64 = 3 };
+
+/* Status codes. GLINT_EOUTOFRANGE is where the reference throws
+ * ArrayIndexOutOfBoundsException inside update/get (a key whose local index falls outside the
+ * partition array); the JNI shim raises that exception type so Akka supervision behaves as in
+ * the reference (restart => the actor re-creates a zeroed shard). */
+enum glint_status {
+  GLINT_OK = 0,
+  GLINT_EOUTOFRANGE = 1, /* a key/row/col outside the shard; see glint_shard_last_error */
+  GLINT_EDEVICE = 2,     /* HIP runtime error */
+  GLINT_EINVAL = 3,      /* bad argument (null handle, wrong dtype, malformed payload ...) */
+  GLINT_ENOMEM = 4       /* device or pinned-host allocation failed */
+};
+
+/* Push flags. */
+enum glint_push_flags {
+  GLINT_PUSH_DEFAULT = 0,
+  /* Bit-exact reproduction of the reference's strictly sequential `data(k) += v` order for
+   * Float/Double even when keys repeat (PartialVector.scala:37-41). Without it, repeated keys in
+   * a push are summed by device atomics in arbitrary order (<= 1e-6 relative for Double; Int and
+   * Long are exact either way). Unique-key pushes are bit-exact in both modes. */
+  GLINT_PUSH_DETERMINISTIC = 1
+};
+
+typedef struct glint_shard* glint_shard_t;
+
+/* ---- lifetime ------------------------------------------------------------------------------ */
+
+/* Range-partitioned shard = `new PartialVector*(RangePartition(index, start, end))`
+ * (RangePartition.scala:8; PartialVectorDouble.scala:15 allocates Array[Double](size), zeroed).
+ * cols == 0 creates a vector shard of size (int)(end - start) elements (RangePartition.scala:24);
+ * cols > 0 creates a matrix shard of (int)(end - start) rows x cols (PartialMatrixDouble.scala:19).
+ * Replaces `Props(classOf[PartialVectorDouble], partition)` (src/main/scala/glint/Client.scala:178)
+ * and `Props(classOf[PartialMatrixDouble], partition, cols)` (Client.scala:130). */
+int glint_shard_create(int device, int dtype, int64_t start, int64_t end, int32_t cols,
+                       glint_shard_t* out);
+
+/* Cyclic-partitioned shard (CyclicPartition(index, numberOfPartitions, numberOfKeys),
+ * src/main/scala/glint/partitioning/cyclic/CyclicPartition.scala:12). */
+int glint_shard_create_cyclic(int device, int dtype, int32_t index, int32_t num_partitions,
+                              int64_t num_keys, int32_t cols, glint_shard_t* out);
+
+/* Frees the device memory (actor postStop / `destroy()`, AsyncBigVector.scala:135-140). */
+int glint_shard_destroy(glint_shard_t shard);
+
+/* Zeroes the shard: what an Akka restart of the partial-model actor produces. */
+int glint_shard_zero(glint_shard_t shard);
+
+/* Shape: size = Partition.size (elements for a vector, rows for a matrix), cols (0 = vector),
+ * dtype, device. Any out-pointer may be NULL. */
+int glint_shard_info(glint_shard_t shard, int32_t* size, int32_t* cols, int* dtype, int* device);
+
+/* ---- host-pointer hot path (what the JNI shim calls) ---------------------------------------- */
+
+/* PartialVector.update(keys, values) -- PartialVector.scala:35-43. vals: n elements of dtype. */
+int glint_vec_push(glint_shard_t shard, const int64_t* keys, const void* vals, int64_t n, int flags);
+
+/* PartialVector.get(keys) -- PartialVector.scala:51-60. out: n elements of dtype. */
+int glint_vec_pull(glint_shard_t shard, const int64_t* keys, void* out, int64_t n);
+
+/* PartialMatrix.update(rows, cols, values) -- PartialMatrix.scala:74-83. */
+int glint_mat_push(glint_shard_t shard, const int64_t* rows, const int32_t* cols, const void* vals,
+                   int64_t n, int flags);
+
+/* PartialMatrix.get(rows, cols) -- PartialMatrix.scala:55-65. */
+int glint_mat_pull(glint_shard_t shard, const int64_t* rows, const int32_t* cols, void* out, int64_t n);
+
+/* PartialMatrix.getRows(rows) -- PartialMatrix.scala:37-46, written flattened row-major
+ * (n x cols) the way ResponseSerializer sends ResponseRows* (ResponseSerializer.scala:52-61). */
+int glint_mat_pull_rows(glint_shard_t shard, const int64_t* rows, void* out, int64_t n);
+
+/* After GLINT_EOUTOFRANGE: index (within the failing call) of the first rejected record. */
+int glint_shard_last_error(glint_shard_t shard, int64_t* first_bad_record);
+
+/* ---- device-resident variants (stream-ordered, no host synchronisation) --------------------- *
+ * All pointers are device pointers on the shard's device; `stream` is a hipStream_t used exactly
+ * as given (NULL = the HIP null stream, as in the HIP API). All device-resident calls on one shard
+ * must be ordered (one stream, or event-ordered streams), as the actor model orders its messages.
+ * Errors are accumulated on the device and reported by glint_shard_sync. */
+int glint_vec_push_dev(glint_shard_t shard, const int64_t* keys, const void* vals, int64_t n,
+                       int flags, void* stream);
+int glint_vec_pull_dev(glint_shard_t shard, const int64_t* keys, void* out, int64_t n, void* stream);
+int glint_mat_push_dev(glint_shard_t shard, const int64_t* rows, const int32_t* cols,
+                       const void* vals, int64_t n, int flags, void* stream);
+int glint_mat_pull_dev(glint_shard_t shard, const int64_t* rows, const int32_t* cols, void* out,
+                       int64_t n, void* stream);
+int glint_mat_pull_rows_dev(glint_shard_t shard, const int64_t* rows, void* out, int64_t n,
+                            void* stream);
+
+/* Waits for the shard's pending device work on `stream` and returns GLINT_EOUTOFRANGE if any
+ * device-resident call since the last sync saw an out-of-range record (first_bad_record = its
+ * index within the call that saw it, may be NULL). Clears the device error state. */
+int glint_shard_sync(glint_shard_t shard, void* stream, int64_t* first_bad_record);
+
+/* Device pointer to the shard's data (row-major, row pitch from glint_shard_pitch) for
+ * stream-ordered consumers (RCCL exchange buffers, checkpoint dumps, tests). */
+int glint_shard_data(glint_shard_t shard, void** device_ptr);
+int glint_shard_pitch(glint_shard_t shard, int64_t* elements_per_row);
+
+/* ---- wire ingest (RequestSerializer / ResponseSerializer byte images) ----------------------- *
+ * payload is the exact byte image RequestSerializer.toBinary produces
+ * (src/main/scala/glint/serialization/RequestSerializer.scala:92-205): native-endian
+ * [u8 type][i32 n]([i32 id])[i64 keys x n]([i32 cols x n])([V values x n]); keys start at the
+ * unaligned offset 5 or 9. */
+
+/* Applies a Push{Vector,Matrix}{Int,Long,Float,Double} message; *id receives its id. */
+int glint_push_wire(glint_shard_t shard, const uint8_t* payload, size_t len, int32_t* id, int flags);
+
+/* Answers a PullVector / PullMatrix / PullMatrixRows message with the ResponseSerializer image
+ * [u8 type][i32 n][V x n] (ResponseSerializer.scala:43-117). *out_len receives the image size;
+ * if cap is too small nothing is written, *out_len is set and GLINT_EINVAL returned. */
+int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uint8_t* response,
+                    size_t cap, size_t* out_len);
+
+/* ---- kernel timing ------------------------------------------------------------------------- *
+ * With profiling on, every kernel launch of the shard is bracketed by HIP events recorded on the
+ * stream it is launched on; glint_prof_read waits for them and returns the summed device time and
+ * launch count of one kernel kind since the last reset. Used by bench.py for the roofline figure. */
+enum glint_kernel_id {
+  GLINT_K_PUSH_SEQ = 0,     /* ordered plain-RMW push (the dense hot path) */
+  GLINT_K_PUSH_SCATTER = 1, /* LDS-aggregated atomic push of the unordered tail */
+  GLINT_K_VEC_PULL = 2,
+  GLINT_K_MAT_PULL = 3,
+  GLINT_K_MAT_PULL_ROWS = 4,
+  GLINT_K_COUNT = 5
+};
+int glint_prof_enable(glint_shard_t shard, int on);
+int glint_prof_read(glint_shard_t shard, int kernel_id, double* total_ms, int64_t* launches);
+int glint_prof_reset(glint_shard_t shard);
+
+/* ---- misc ---------------------------------------------------------------------------------- */
+const char* glint_strerror(int status);
+/* Number of visible devices (0 without a GPU; never fails). */
+int glint_device_count(void);
+/* Library version (major*10000 + minor*100 + patch). */
+int glint_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GLINT_GPU_H */

@@ -1,0 +1,37 @@
+"""Shared pytest setup.
+
+Markers: ``gpu`` -- needs an MI355X (run with ``-m gpu`` on the GPU box); everything else runs on CPU.
+The native libraries are built in-tree (glint_amd/build.py) before the session if they are stale.
+"""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")
+    config.addinivalue_line("markers", "slow: long-running")
+    from glint_amd.build import build_all
+    build_all()
+
+
+@pytest.fixture(scope="session")
+def kat():
+    import json
+    return json.loads((ROOT / "tests" / "golden" / "reference_kat.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """Device index used by GPU tests. Fails (never skips) when no GPU is visible: `-m gpu` runs are
+    meant for the MI355X box, and a silent skip would hide a broken HIP path."""
+    import glint_amd._native as N
+    if N.load().glint_device_count() < 1:
+        pytest.fail("no GPU visible to libglint_gpu.so")
+    return int(os.environ.get("GLINT_TEST_DEVICE", "0"))

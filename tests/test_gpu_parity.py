@@ -1,0 +1,326 @@
+"""GPU parity: the HIP push/pull path against the oracle, through the C ABI.
+
+Bar: bit-exact for Int/Long everywhere and for Float/Double whenever a push touches each element
+at most once or runs with GLINT_PUSH_DETERMINISTIC; <= 1e-6 relative (north star) for Double sums of
+repeated keys in the default (atomic) mode. Run on the MI355X box: pytest -m gpu.
+"""
+import zlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import glint_amd
+from glint_amd import _native as N
+from glint_amd import ArrayIndexOutOfBoundsException, Client, CyclicPartition, PartialMatrix, PartialVector, \
+    RangePartition
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+DT = ["double", "float", "long", "int"]
+
+
+def rand_vals(rng, dtype, n):
+    npd = glint_amd.shard.resolve_dtype(dtype)[1]
+    if np.issubdtype(npd, np.floating):
+        return rng.uniform(-1, 1, n).astype(npd)
+    info = np.iinfo(npd)
+    return rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
+
+
+def oracle_vec(part, dtype):
+    code = O.CODE[dtype]
+    if isinstance(part, RangePartition):
+        return O.OracleVector(O.part_range(part.start, part.end), code)
+    return O.OracleVector(O.part_cyclic(part.index, part.numberOfPartitions, part.numberOfKeys), code)
+
+
+# ---- the reference's known-answer scenarios, through the GPU client -----------------------------------
+def test_reference_scenarios_on_gpu(kat, gpu):
+    from test_oracle_kat import expected_array
+    for sc in kat["scenarios"]:
+        client = Client([gpu] * sc["servers"])  # `servers` parameter servers, all on this GPU
+        if sc["model"] == "vector":
+            m = client.vector(sc["keys"], sc["dtype"], sc["modelsPerServer"])
+        else:
+            m = client.matrix(sc["rows"], sc["cols"], sc["dtype"], sc["modelsPerServer"])
+        assert m.nrOfPartitions == min(sc.get("keys", sc.get("rows")), sc["modelsPerServer"] * sc["servers"])
+        code = O.CODE[sc["dtype"]]
+        for op in sc["ops"]:
+            if op["op"] == "push":
+                if sc["model"] == "vector":
+                    m.push(op["keys"], op["values"])
+                else:
+                    m.push(op["rows"], op["cols"], op["values"])
+            else:
+                if op["op"] == "pull_rows":
+                    got = m.pull(op["rows"])
+                elif sc["model"] == "vector":
+                    got = m.pull(op["keys"])
+                else:
+                    got = m.pull(op["rows"], op["cols"])
+                np.testing.assert_array_equal(got, expected_array(op, code, sc.get("cols")), err_msg=sc["spec"])
+        m.destroy()
+
+
+def test_granular_big_vector_on_gpu(kat, gpu):
+    """GranularBigVectorSpec.scala:14-35 through the GPU shards (2 servers, messages of 1000)."""
+    spec = kat["large"][0]
+    n = spec["keys"]
+    values = O.JavaRandom(42).nextDoubles(n)
+    keys = np.arange(n, dtype=np.int64)
+    m = Client([gpu, gpu]).vector(n, "double")
+    for i in range(0, n, 100_000):  # message chunking does not change the result; fewer calls
+        m.push(keys[i:i + 100_000], values[i:i + 100_000])
+    np.testing.assert_array_equal(m.pull(keys), values)
+    m.destroy()
+
+
+@pytest.mark.parametrize("which", [1, 2])
+def test_granular_big_matrix_on_gpu(kat, gpu, which):
+    spec = kat["large"][which]
+    i = np.arange(1_000_000, dtype=np.int64)
+    rows, cols, vals = i % 1000, (i // 1000).astype(np.int32), i.astype(np.float64) * 3.14
+    m = Client([gpu] * spec["servers"]).matrix(1000, 1000, "double")
+    for s0 in range(0, rows.size, spec["maximumMessageSize"] * 10):
+        s1 = s0 + spec["maximumMessageSize"] * 10
+        m.push(rows[s0:s1], cols[s0:s1], vals[s0:s1])
+    if spec["pull"] == "elements":
+        np.testing.assert_array_equal(m.pull(rows, cols), vals)
+    else:
+        full = m.pull(np.arange(1000, dtype=np.int64))
+        np.testing.assert_array_equal(full[rows, cols], vals)
+    m.destroy()
+
+
+# ---- vector push/pull vs oracle --------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("pattern", ["dense", "dense_odd", "sorted_sparse", "permutation", "duplicates",
+                                     "dense_then_repeat", "single", "empty"])
+def test_vector_push_pull(gpu, dtype, pattern):
+    rng = np.random.default_rng(zlib.crc32(f"{dtype}/{pattern}".encode()))
+    start, size = 1_000_003, 300_001
+    part = RangePartition(2, start, start + size)
+    if pattern == "dense":
+        keys = np.arange(start, start + size, dtype=np.int64)
+    elif pattern == "dense_odd":
+        keys = np.arange(start + 1, start + size, dtype=np.int64)[:123_457]
+    elif pattern == "sorted_sparse":
+        keys = np.sort(rng.choice(size, 50_000, replace=False)).astype(np.int64) + start
+    elif pattern == "permutation":
+        keys = rng.permutation(size).astype(np.int64) + start
+    elif pattern == "duplicates":
+        keys = rng.integers(0, 1000, 200_000).astype(np.int64) + start
+    elif pattern == "dense_then_repeat":  # increasing for many tiles, then the whole range again
+        k = np.arange(start, start + size, dtype=np.int64)
+        keys = np.concatenate([k, k[:100_000]])
+    elif pattern == "single":
+        keys = np.array([start + 17], np.int64)
+    else:
+        keys = np.zeros(0, np.int64)
+    vals = rand_vals(rng, dtype, keys.size)
+    ref = oracle_vec(part, dtype)
+    with PartialVector(part, dtype, gpu) as sh:
+        for _ in range(2):  # push twice: accumulation onto non-zero state
+            assert sh.update(keys, vals)
+            assert ref.update(keys, vals) == -1
+        got = sh.to_numpy()
+        exact = dtype in ("long", "int") or pattern not in ("duplicates", "dense_then_repeat")
+        if exact:
+            np.testing.assert_array_equal(got, ref.data)
+        else:
+            # atomic (unordered) sums of ~400 values per key: <= 1e-6 relative for Double (north star);
+            # the absolute floor covers sums that cancel to ~0
+            np.testing.assert_allclose(got, ref.data, rtol=1e-6 if dtype == "double" else 1e-4,
+                                       atol=1e-9 if dtype == "double" else 2e-3)
+        # pull == the shard's own state at those keys (bit-exact), and == the oracle where exact
+        q = keys if keys.size else np.zeros(0, np.int64)
+        np.testing.assert_array_equal(sh.get(q), got[q - start])
+        if exact and q.size:
+            np.testing.assert_array_equal(sh.get(q), ref.get(q)[0])
+
+
+@pytest.mark.parametrize("dtype", ["double", "float"])
+def test_deterministic_push_is_bit_exact(gpu, dtype):
+    """GLINT_PUSH_DETERMINISTIC reproduces the sequential order bit for bit, duplicates included."""
+    z = np.load(GOLD / "zipf_push.npz")
+    start, size = int(z["start"]), int(z["size"])
+    part = RangePartition(0, start, start + size)
+    keys = z["keys"]
+    vals = z["values_f64"].astype(glint_amd.shard.resolve_dtype(dtype)[1])
+    ref = oracle_vec(part, dtype)
+    assert ref.update(keys, vals) == -1
+    if dtype == "double":
+        np.testing.assert_array_equal(ref.data, z["expect_f64"])
+    with PartialVector(part, dtype, gpu) as sh:
+        sh.update(keys, vals, deterministic=True)
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+        # a sorted head followed by an unsorted tail: the tail continues from the head's sums
+        k2 = np.concatenate([np.arange(start, start + size, dtype=np.int64), keys])
+        v2 = np.concatenate([np.full(size, 0.1, vals.dtype), vals])
+        sh.update(k2, v2, deterministic=True)
+        assert ref.update(k2, v2) == -1
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+def test_zipf_fixture_default_mode(gpu):
+    z = np.load(GOLD / "zipf_push.npz")
+    start, size = int(z["start"]), int(z["size"])
+    part = RangePartition(0, start, start + size)
+    with PartialVector(part, "long", gpu) as sh:
+        sh.update(z["keys"], z["values_i64"])
+        np.testing.assert_array_equal(sh.to_numpy(), z["expect_i64"])
+    with PartialVector(part, "double", gpu) as sh:
+        sh.update(z["keys"], z["values_f64"])
+        np.testing.assert_allclose(sh.to_numpy(), z["expect_f64"], rtol=1e-6, atol=1e-9)
+
+
+def test_int_wraparound(gpu):
+    """Int/Long adds wrap (two's complement), as on the JVM."""
+    part = RangePartition(0, 0, 4)
+    with PartialVector(part, "int", gpu) as sh:
+        sh.update([0, 0, 1, 1], np.array([2**31 - 1, 5, -2**31, -1], np.int32))
+        np.testing.assert_array_equal(sh.get([0, 1]), np.array([-2**31 + 4, 2**31 - 1], np.int32))
+    with PartialVector(part, "long", gpu) as sh:
+        sh.update([2, 2], np.array([2**63 - 1, 1], np.int64))
+        assert sh.get([2])[0] == -2**63
+
+
+def test_cyclic_partition_shard(gpu):
+    P, Nk = 7, 100_003
+    rng = np.random.default_rng(5)
+    for idx in (0, 3, 6):
+        part = CyclicPartition(idx, P, Nk)
+        owned = np.arange(idx, Nk, P, dtype=np.int64)
+        keys = rng.choice(owned, 40_000)
+        vals = rng.uniform(-1, 1, keys.size)
+        ref = oracle_vec(part, "double")
+        with PartialVector(part, "double", gpu) as sh:
+            assert sh.size == ref.size
+            sh.update(np.sort(owned), np.ones(owned.size))
+            ref.update(np.sort(owned), np.ones(owned.size))
+            sh.update(keys, vals, deterministic=True)
+            ref.update(keys, vals)
+            np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+def test_out_of_range_raises(gpu):
+    part = RangePartition(1, 100, 200)
+    with PartialVector(part, "long", gpu) as sh:
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.update([100, 150, 200, 120], [1, 1, 1, 1])
+        assert ei.value.record == 2
+        with pytest.raises(ArrayIndexOutOfBoundsException):
+            sh.get([99])
+        sh.zero()  # Akka restart semantics
+        assert sh.get([100, 150]).tolist() == [0, 0]
+        # the reference's (key - start).toInt aliasing is reproduced, not rejected
+        sh.update([100 + (1 << 32) + 7], [5])
+        assert sh.get([107])[0] == 5
+
+
+# ---- matrix ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("cols", [512, 300, 7, 1])
+def test_matrix_push_pull(gpu, dtype, cols):
+    rng = np.random.default_rng(cols * 31 + len(dtype))
+    start, nrows = 4096, 2000
+    part = RangePartition(1, start, start + nrows)
+    ref = O.OracleMatrix(O.part_range(start, start + nrows), cols, O.CODE[dtype])
+    n = 150_000
+    rows = rng.integers(0, nrows, n).astype(np.int64) + start
+    cl = rng.integers(0, cols, n).astype(np.int32)
+    vals = rand_vals(rng, dtype, n)
+    # dense row-major sweep (unique, increasing addresses) then random triplets with duplicates
+    dr = np.repeat(np.arange(start, start + nrows, dtype=np.int64), cols)
+    dc = np.tile(np.arange(cols, dtype=np.int32), nrows)
+    dv = rand_vals(rng, dtype, dr.size)
+    with PartialMatrix(part, cols, dtype, gpu) as sh:
+        sh.update(dr, dc, dv)
+        ref.update(dr, dc, dv)
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+        sh.update(rows, cl, vals, deterministic=True)
+        ref.update(rows, cl, vals)
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+        np.testing.assert_array_equal(sh.get(rows[:5000], cl[:5000]), ref.get(rows[:5000], cl[:5000])[0])
+        q = rng.integers(0, nrows, 777).astype(np.int64) + start
+        np.testing.assert_array_equal(sh.getRows(q), ref.get_rows(q)[0])
+        with pytest.raises(ArrayIndexOutOfBoundsException):
+            sh.update([start], [cols], np.ones(1, dtype=sh.np_dtype))
+        with pytest.raises(ArrayIndexOutOfBoundsException):
+            sh.getRows([start + nrows])
+
+
+# ---- wire ingest --------------------------------------------------------------------------------
+def test_wire_push_pull_vector(gpu):
+    rng = np.random.default_rng(9)
+    part = RangePartition(0, 0, 10_000)
+    keys = rng.integers(0, 10_000, 5001).astype(np.int64)
+    vals = rng.uniform(-1, 1, keys.size)
+    ref = oracle_vec(part, "double")
+    ref.update(keys, vals)
+    with PartialVector(part, "double", gpu) as sh:
+        mid = sh.push_wire(O.encode_push_vector(O.O_F64, 77, keys, vals), deterministic=True)
+        assert mid == 77
+        resp = sh.pull_wire(O.encode_pull_vector(keys))
+        d = O.decode_response(resp)
+        assert resp[0] == 0x10
+        np.testing.assert_array_equal(d["values"], ref.get(keys)[0])
+        with pytest.raises(ValueError):
+            sh.push_wire(O.encode_push_vector(O.O_F32, 1, keys, vals))  # wrong value type
+
+
+def test_wire_push_pull_matrix(gpu):
+    rng = np.random.default_rng(10)
+    part = RangePartition(0, 50, 150)
+    ref = O.OracleMatrix(O.part_range(50, 150), 64, O.O_I32)
+    rows = rng.integers(50, 150, 3000).astype(np.int64)
+    cols = rng.integers(0, 64, 3000).astype(np.int32)
+    vals = rng.integers(-1000, 1000, 3000).astype(np.int32)
+    ref.update(rows, cols, vals)
+    with PartialMatrix(part, 64, "int", gpu) as sh:
+        assert sh.push_wire(O.encode_push_matrix(O.O_I32, 5, rows, cols, vals)) == 5
+        d = O.decode_response(sh.pull_wire(O.encode_pull_matrix(rows[:100], cols[:100])))
+        np.testing.assert_array_equal(d["values"], ref.get(rows[:100], cols[:100])[0])
+        q = np.array([50, 149, 77], np.int64)
+        resp = sh.pull_wire(O.encode_pull_matrix_rows(q))
+        assert resp == O.encode_response_rows(O.O_I32, ref.get_rows(q)[0])
+
+
+# ---- device-resident path (torch tensors in HBM) -----------------------------------------------------
+def test_device_resident_push_pull(gpu):
+    import torch
+    dev = torch.device("cuda", gpu)
+    n = 1 << 20
+    part = RangePartition(0, 0, n)
+    with PartialVector(part, "double", gpu) as sh:
+        keys = torch.arange(n, dtype=torch.int64, device=dev)
+        vals = torch.rand(n, dtype=torch.float64, device=dev)
+        sh.update(keys, vals)
+        sh.update(keys, vals)
+        out = sh.get(keys)
+        torch.testing.assert_close(out, vals + vals, rtol=0, atol=0)
+        # misaligned (odd offset) device pointers take the scalar path
+        sh.update(keys[1:], vals[1:])
+        out = sh.get(keys[1:])
+        torch.testing.assert_close(out, 3 * vals[1:], rtol=0, atol=0)
+        with pytest.raises(ArrayIndexOutOfBoundsException):
+            sh.update(torch.tensor([n], dtype=torch.int64, device=dev),
+                      torch.ones(1, dtype=torch.float64, device=dev))
+
+
+@pytest.mark.slow
+def test_large_dense_push_property(gpu):
+    """BASELINE cfg2 size (2^28 keys): push the same dense stream twice, every element == 2 v."""
+    import torch
+    dev = torch.device("cuda", gpu)
+    n = 1 << 28
+    part = RangePartition(0, 0, n)
+    with PartialVector(part, "double", gpu) as sh:
+        keys = torch.arange(n, dtype=torch.int64, device=dev)
+        vals = torch.rand(n, dtype=torch.float64, device=dev)
+        sh.update(keys, vals)
+        sh.update(keys, vals)
+        out = sh.get(keys)
+        assert torch.equal(out, vals * 2)
