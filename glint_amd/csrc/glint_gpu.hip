@@ -83,55 +83,8 @@ __device__ __forceinline__ bool rec_addr(const PartDesc& p, i64 key, int32_t col
 }
 
 // ------------------------------------------------------------------------------------------------
-// push_seq: ticketed persistent kernel with decoupled look-back (see glint_kernels.h)
+// push, ordered part: push_check + push_apply
 // ------------------------------------------------------------------------------------------------
-
-// Inclusive-prefix "every address so far strictly increasing" for tile t, computed by the whole
-// block: each of the 256 threads reads 4 status words (sc1, L1-bypassing), so one round trip covers
-// the 1024 tiles before t -- about every tile that can be in flight at once. A_OK tiles are passed
-// over; the nearest P_OK / bad word decides; an EMPTY word (tile not yet checked) is re-polled.
-// A poll that exceeds the spin limit answers "bad", which is always safe: the tile then leaves its
-// records to push_scatter. Called by all threads of the block (contains barriers).
-template <typename V>
-__device__ bool lookback(const PushArgs<V>& a, u32 t, int tid, int* s_red) {
-  const u32 bad = ld_relaxed(&a.ctl->bad_enc);
-  if (bad != 0u && a.ntiles - bad < t) return false;  // a locally unsorted tile precedes t
-  i64 top = (i64)t - 1;                                // nearest tile whose status is unknown
-  u32 spins = 0;
-  const int lane = tid & 63, wid = tid >> 6;
-  while (top >= 0) {
-    // nearest non-A_OK word in this window, encoded (distance << 3) | status for one min-reduce
-    int best = 0x7FFFFFFF;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int d = 4 * tid + q;
-      const i64 idx = top - d;
-      const u32 s = idx >= 0 ? ld_relaxed(a.status + idx) : ST_P_OK;  // before tile 0: prefix OK
-      if (s != ST_A_OK) best = min(best, (d << 3) | (int)s);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o));
-    if (lane == 0) s_red[wid] = best;
-    __syncthreads();
-    best = min(min(s_red[0], s_red[1]), min(s_red[2], s_red[3]));
-    __syncthreads();
-    if (best == 0x7FFFFFFF) { top -= 4 * kTPB; continue; }  // 1024 A_OK tiles: keep walking
-    const int d = best >> 3;
-    const u32 s = (u32)(best & 7);
-    if (s == ST_EMPTY) {
-      top -= d;  // tiles above it are settled A_OK
-      if (++spins > kLookbackSpinLimit) {
-        if (tid == 0) atomicAdd(&a.ctl->timeouts, 1u);
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    return s == ST_P_OK;
-  }
-  return true;
-}
-
 // addresses are element indices: int32 for vectors (Partition.globalToLocal is an Int), int64 for
 // matrices (row * pitch + col)
 template <bool MAT> struct AddrT { typedef int32_t T; };
@@ -145,171 +98,113 @@ __device__ __forceinline__ bool rec_addr_t(const PartDesc& p, i64 key, int32_t c
   return ok;
 }
 
-// One tile in flight per block, software-pipelined over two of the block's tickets:
-//   iteration i:  CHECK(t_i)  -- load keys (+cols) of t_i, compute its addresses, test that they are
-//                                strictly increasing (and above the last address of tile t_i - 1),
-//                                publish A_OK / A_BAD;
-//                 APPLY(t_{i-1}) -- look back for t_{i-1}'s prefix (its predecessors were checked an
-//                                iteration ago, so the walk rarely waits), and if the prefix is
-//                                increasing read-modify-write its shard elements with plain stores.
-// The loads of iteration i -- keys of t_i, values and shard elements of t_{i-1} -- are issued
-// together before the look-back, so each HBM byte is read once and the look-back latency hides
-// under them. The shard read of t_{i-1} is speculative: harmless when the tile is not applied, and
-// when it is, no other tile of the launch touches those elements (all applied tiles' addresses are
-// strictly increasing across tiles).
-template <typename V, bool MAT>
-__global__ __launch_bounds__(kTPB) void push_seq_kernel(PushArgs<V> a) {
-  typedef typename Vec2<V>::T V2;
+// push_check: the first tile whose record addresses are not strictly increasing -- within the tile
+// or against the last record of the tile before it. Reads keys (and cols) only: 8 (12) B/record.
+// Waves work independently (no barriers); a wave stops as soon as a break at or before its tile is
+// known, so an unordered push costs one tile of reads.
+template <bool MAT>
+__global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict__ keys,
+                                                          const int32_t* __restrict__ cols, i64 n,
+                                                          PartDesc part, LaunchCtl* ctl, u32 ntiles) {
   typedef typename AddrT<MAT>::T A;
-  __shared__ int s_b[8];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const i64 n = a.n;
-
-  // a ticket is "dead" when a break before it is already resolved: it and every later ticket stay
-  // unapplied (push_scatter takes them). Decided by thread 0 and broadcast (block-uniform).
-  auto dead_ticket = [&](u32 tt) {
-    const u32 brk = ld_relaxed(&a.ctl->brk_enc);
-    return brk != 0u && a.ntiles - brk < tt;
-  };
-
-  // pending tile (checked, not yet applied)
-  u32 tp = 0xFFFFFFFFu;
-  bool p_ok = false;  // its local check
-  A pa0[kSeqPPT], pa1[kSeqPPT];
-  unsigned pmask = 0;  // bit 2j: record 2p valid, bit 2j+1: record 2p+1 valid
-
-  if (tid == 0) {
-    const u32 tt = atomicAdd(&a.ctl->ticket, 1u);
-    s_b[0] = (int)tt;
-    s_b[1] = dead_ticket(tt);
-  }
-  __syncthreads();
-  u32 t = (u32)s_b[0];
-  bool dead = s_b[1] != 0;
-  __syncthreads();
-
-  for (;;) {
-    const bool have_cur = t < a.ntiles && !dead;
-    if (t < a.ntiles && dead && tid == 0) st_relaxed(a.status + t, ST_P_BAD);  // nobody waits on it
-    const bool have_pend = tp != 0xFFFFFFFFu;
-    if (!have_cur && !have_pend) break;
-
-    u32 t_next = 0xFFFFFFFFu;
-    if (have_cur && tid == 0) t_next = atomicAdd(&a.ctl->ticket, 1u);
-
-    // ---- issue every load of this iteration -----------------------------------------------------
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  constexpr int kWavePairs = kSeqPPT * 64;  // pairs one wave checks per tile slice
+  for (u32 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const u32 brk = __builtin_amdgcn_readfirstlane(ld_relaxed(&ctl->brk_enc));
+    if (brk != 0u && ntiles - brk < t) return;  // an earlier break is already known
+    const i64 pbase = (i64)t * (kSeqTile / 2) + (i64)wid * kWavePairs;
     K2 k[kSeqPPT];
     C2 c[kSeqPPT];
+#pragma unroll
+    for (int j = 0; j < kSeqPPT; ++j) {
+      const i64 p = pbase + lane + (i64)j * 64;
+      const i64 r = 2 * p;
+      if (r + 1 < n) {
+        k[j] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p);
+        if (MAT) c[j] = __builtin_nontemporal_load(reinterpret_cast<const C2*>(cols) + p);
+      } else if (r < n) {
+        k[j] = K2{keys[r], 0};
+        if (MAT) c[j] = C2{cols[r], 0};
+      } else {
+        k[j] = K2{0, 0};
+        if (MAT) c[j] = C2{0, 0};
+      }
+    }
+    // the record before this wave's slice (another wave's or the previous tile's last record)
+    A before = 0;
+    const i64 r_first = 2 * pbase;
+    if (r_first > 0 && r_first < n) rec_addr_t<MAT>(part, keys[r_first - 1], MAT ? cols[r_first - 1] : 0, before);
+    bool mono = true;
+    A last_of_prev_step = before;
+#pragma unroll
+    for (int j = 0; j < kSeqPPT; ++j) {
+      const i64 r = 2 * (pbase + lane + (i64)j * 64);
+      const bool h0 = r < n, h1 = r + 1 < n;
+      A a0, a1;
+      rec_addr_t<MAT>(part, k[j].x, MAT ? c[j].x : 0, a0);
+      rec_addr_t<MAT>(part, k[j].y, MAT ? c[j].y : 0, a1);
+      if (h1) mono = mono && (a1 > a0);
+      A prev = __shfl_up(a1, 1);
+      if (lane == 0) prev = last_of_prev_step;
+      if (h0 && r > 0) mono = mono && (a0 > prev);
+      last_of_prev_step = __shfl(a1, 63);
+    }
+    if (__any(!mono) && lane == 0) atomicMax(&ctl->brk_enc, ntiles - t);
+  }
+}
+
+// push_apply: tiles before the break, plain read-modify-write. Their addresses are strictly
+// increasing across the whole prefix, hence unique, so no two lanes touch one element. Pairs of
+// records that hit two adjacent, 16-B aligned elements move as one 16-B access.
+template <typename V, bool MAT>
+__global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a) {
+  typedef typename Vec2<V>::T V2;
+  typedef typename AddrT<MAT>::T A;
+  const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
+  const u32 tiles = brk == 0u ? a.ntiles : a.ntiles - brk;
+  const int tid = threadIdx.x;
+  const i64 n = a.n;
+  for (u32 t = blockIdx.x; t < tiles; t += gridDim.x) {
     const i64 pbase = (i64)t * (kSeqTile / 2);
-    if (have_cur) {
+    K2 k[kSeqPPT];
+    C2 c[kSeqPPT];
+    V2 v[kSeqPPT];
 #pragma unroll
-      for (int j = 0; j < kSeqPPT; ++j) {
-        const i64 p = pbase + tid + (i64)j * kTPB;
-        const i64 r = 2 * p;
-        if (r + 1 < n) {
-          k[j] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(a.keys) + p);
-          if (MAT) c[j] = __builtin_nontemporal_load(reinterpret_cast<const C2*>(a.cols) + p);
-        } else if (r < n) {
-          k[j] = K2{a.keys[r], 0};
-          if (MAT) c[j] = C2{a.cols[r], 0};
-        } else {
-          k[j] = K2{0, 0};
-          if (MAT) c[j] = C2{0, 0};
-        }
+    for (int j = 0; j < kSeqPPT; ++j) {
+      const i64 p = pbase + tid + (i64)j * kTPB;
+      const i64 r = 2 * p;
+      if (r + 1 < n) {
+        k[j] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(a.keys) + p);
+        if (MAT) c[j] = __builtin_nontemporal_load(reinterpret_cast<const C2*>(a.cols) + p);
+        v[j] = __builtin_nontemporal_load(reinterpret_cast<const V2*>(a.vals) + p);
+      } else if (r < n) {
+        k[j] = K2{a.keys[r], 0};
+        if (MAT) c[j] = C2{a.cols[r], 0};
+        v[j] = as2<V>(a.vals[r], V(0));
+      } else {
+        k[j] = K2{0, 0};
+        if (MAT) c[j] = C2{0, 0};
+        v[j] = as2<V>(V(0), V(0));
       }
     }
-    V2 v[kSeqPPT], d[kSeqPPT];
-    if (have_pend && p_ok) {
-      const i64 qbase = (i64)tp * (kSeqTile / 2);
 #pragma unroll
-      for (int j = 0; j < kSeqPPT; ++j) {
-        const i64 p = qbase + tid + (i64)j * kTPB;
-        const i64 r = 2 * p;
-        if (r + 1 < n) v[j] = __builtin_nontemporal_load(reinterpret_cast<const V2*>(a.vals) + p);
-        else if (r < n) v[j] = as2<V>(a.vals[r], V(0));
-        else v[j] = as2<V>(V(0), V(0));
-      }
-#pragma unroll
-      for (int j = 0; j < kSeqPPT; ++j) {
-        const bool o0 = (pmask >> (2 * j)) & 1u, o1 = (pmask >> (2 * j + 1)) & 1u;
-        if (o0 && o1 && pa1[j] == pa0[j] + 1 && (pa0[j] & 1) == 0) {
-          d[j] = *reinterpret_cast<const V2*>(a.data + pa0[j]);
-        } else {
-          d[j] = as2<V>(o0 ? a.data[pa0[j]] : V(0), o1 ? a.data[pa1[j]] : V(0));
-        }
+    for (int j = 0; j < kSeqPPT; ++j) {
+      const i64 r = 2 * (pbase + tid + (i64)j * kTPB);
+      A a0, a1;
+      const bool o0 = rec_addr_t<MAT>(a.part, k[j].x, MAT ? c[j].x : 0, a0) && r < n;
+      const bool o1 = rec_addr_t<MAT>(a.part, k[j].y, MAT ? c[j].y : 0, a1) && r + 1 < n;
+      if (r < n && !o0) record_error(a.err, r);
+      if (r + 1 < n && !o1) record_error(a.err, r + 1);
+      if (o0 && o1 && a1 == a0 + 1 && (a0 & 1) == 0) {
+        V2* dp = reinterpret_cast<V2*>(a.data + a0);
+        const V2 d = *dp;
+        *dp = as2<V>(vadd((V)d.x, (V)v[j].x), vadd((V)d.y, (V)v[j].y));
+      } else {
+        if (o0) a.data[a0] = vadd(a.data[a0], (V)v[j].x);
+        if (o1) a.data[a1] = vadd(a.data[a1], (V)v[j].y);
       }
     }
-
-    // ---- APPLY(pending): look-back overlaps the loads above -----------------------------------
-    if (have_pend) {
-      const bool pre = p_ok ? lookback(a, tp, tid, s_b + 4) : false;
-      if (tid == 0) {
-        st_relaxed(a.status + tp, pre ? ST_P_OK : ST_P_BAD);
-        if (!pre) atomicMax(&a.ctl->brk_enc, a.ntiles - tp);
-      }
-      if (pre) {
-#pragma unroll
-        for (int j = 0; j < kSeqPPT; ++j) {
-          const bool o0 = (pmask >> (2 * j)) & 1u, o1 = (pmask >> (2 * j + 1)) & 1u;
-          const V x = vadd((V)d[j].x, (V)v[j].x);
-          const V y = vadd((V)d[j].y, (V)v[j].y);
-          if (o0 && o1 && pa1[j] == pa0[j] + 1 && (pa0[j] & 1) == 0) {
-            *reinterpret_cast<V2*>(a.data + pa0[j]) = as2<V>(x, y);
-          } else {
-            if (o0) a.data[pa0[j]] = x;
-            if (o1) a.data[pa1[j]] = y;
-          }
-        }
-      }
-      tp = 0xFFFFFFFFu;
-    }
-
-    // ---- CHECK(current): addresses, validity, strictly increasing --------------------------------
-    if (have_cur) {
-      bool mono = true;
-      unsigned mask = 0;
-#pragma unroll
-      for (int j = 0; j < kSeqPPT; ++j) {
-        const i64 p = pbase + tid + (i64)j * kTPB;
-        const i64 r = 2 * p;
-        const bool h0 = r < n, h1 = r + 1 < n;
-        const bool o0 = rec_addr_t<MAT>(a.part, k[j].x, MAT ? c[j].x : 0, pa0[j]) && h0;
-        const bool o1 = rec_addr_t<MAT>(a.part, k[j].y, MAT ? c[j].y : 0, pa1[j]) && h1;
-        mask |= (o0 ? 1u : 0u) << (2 * j);
-        mask |= (o1 ? 1u : 0u) << (2 * j + 1);
-        if (h1) mono = mono && (pa1[j] > pa0[j]);
-        // predecessor of record r is record r-1: the previous lane's second record, or, for lane 0,
-        // a record of another wave / tile read straight from memory (L2-resident)
-        A prev = __shfl_up(pa1[j], 1);
-        if (lane == 0 && r > 0 && h0) {
-          const i64 kp = a.keys[r - 1];
-          const int32_t cp = MAT ? a.cols[r - 1] : 0;
-          rec_addr_t<MAT>(a.part, kp, cp, prev);
-        }
-        if (h0 && r > 0) mono = mono && (pa0[j] > prev);
-        if (h0 && !o0) record_error(a.err, r);
-        if (h1 && !o1) record_error(a.err, r + 1);
-      }
-      pmask = mask;
-      const int ok = __syncthreads_and(mono ? 1 : 0);
-      if (tid == 0) {
-        st_relaxed(a.status + t, ok ? ST_A_OK : ST_A_BAD);
-        if (!ok) atomicMax(&a.ctl->bad_enc, a.ntiles - t);
-      }
-      tp = t;
-      p_ok = ok != 0;
-    }
-
-    // ---- next ticket ----------------------------------------------------------------------------
-    if (tid == 0) {
-      s_b[0] = (int)t_next;
-      s_b[1] = have_cur ? dead_ticket(t_next) : 1;
-    }
-    __syncthreads();
-    t = have_cur ? (u32)s_b[0] : 0xFFFFFFFFu;
-    dead = s_b[1] != 0;
-    __syncthreads();
   }
 }
 
@@ -327,7 +222,7 @@ template <typename V, bool MAT>
 __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int force_all) {
   i64 r0 = 0;
   if (!force_all) {
-    const u32 brk = a.ctl->brk_enc;  // written by push_seq; ordered by the kernel boundary
+    const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
     if (brk == 0u) return;
     r0 = (i64)(a.ntiles - brk) * kSeqTile;
   }
@@ -344,9 +239,6 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
 
   for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const i64 cbase = r0 + ch * kScatterChunk;
-    // a chunk lies inside one push_seq tile (kSeqTile % kScatterChunk == 0); a tile push_seq
-    // applied (P_OK) is skipped, every other tile is applied here -- each record exactly once
-    if (!force_all && a.status[cbase / kSeqTile] == ST_P_OK) continue;
 #pragma unroll 2
     for (int q = tid; q < kScatterChunk; q += kTPB) {
       const i64 i = cbase + q;
@@ -512,7 +404,7 @@ struct glint_shard {
   void* data = nullptr;
   hipStream_t stream = nullptr;
   int cus = 256;
-  // per-launch control region: [LaunchCtl (16 B)][status u32 x cap_tiles]
+  // per-launch control words (LaunchCtl), zeroed before each ordered push
   void* d_ctl = nullptr;
   size_t ctl_bytes = 0;
   ErrState* d_err = nullptr;
@@ -554,7 +446,6 @@ struct DeviceGuard {
   } while (0)
 
 size_t dtype_size(int dt) { return (dt == GLINT_I32 || dt == GLINT_F32) ? 4 : 8; }
-size_t pad16(size_t b) { return (b + 15) & ~(size_t)15; }
 size_t pad256(size_t b) { return (b + 255) & ~(size_t)255; }
 bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
@@ -622,6 +513,20 @@ unsigned grid_for(i64 units, i64 per_block, i64 cap) {
   return (unsigned)g;
 }
 
+// resident blocks per CU for a kernel (occupancy query), capped; GLINT_BLOCKS_PER_CU overrides
+template <typename K>
+int blocks_per_cu(K kernel, int cap) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kTPB, 0) != hipSuccess || b < 1) {
+    (void)hipGetLastError();
+    b = 2;
+  }
+  b = std::min(b, cap);
+  const char* env = getenv("GLINT_BLOCKS_PER_CU");  // tuning override
+  if (env && atoi(env) > 0) b = atoi(env);
+  return b;
+}
+
 // ---- push -------------------------------------------------------------------------------------
 template <typename V, bool MAT>
 int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
@@ -680,27 +585,21 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.ntiles = (u32)ntiles;
   const bool vec_ok = aligned(keys, 16) && aligned(vals, 2 * sizeof(V)) && (!MAT || aligned(cols, 8));
   const bool det = (flags & GLINT_PUSH_DETERMINISTIC) && (s->dtype == GLINT_F32 || s->dtype == GLINT_F64);
-  const size_t ctl_need = sizeof(LaunchCtl) + pad16((size_t)ntiles * 4);
+  const size_t ctl_need = sizeof(LaunchCtl);
   int rc = grow(&s->d_ctl, &s->ctl_bytes, ctl_need);
   if (rc) return rc;
   a.ctl = (LaunchCtl*)s->d_ctl;
-  a.status = (u32*)((char*)s->d_ctl + sizeof(LaunchCtl));
   if (vec_ok) {
-    HIPCHK(hipMemsetAsync(s->d_ctl, 0, ctl_need, st));
-    static int per_cu = 0;  // resident blocks per CU of this instantiation (occupancy query, once)
-    if (per_cu == 0) {
-      int b = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, push_seq_kernel<V, MAT>, kTPB, 0) != hipSuccess || b < 1) {
-        (void)hipGetLastError();
-        b = 2;
-      }
-      const char* env = getenv("GLINT_SEQ_BLOCKS_PER_CU");
-      if (env && atoi(env) > 0) b = atoi(env);
-      per_cu = b;
+    HIPCHK(hipMemsetAsync(s->d_ctl, 0, sizeof(LaunchCtl), st));
+    {
+      const unsigned gc = grid_for(ntiles, 1, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT>, 4));
+      ProfScope pc(s, GLINT_K_PUSH_CHECK, st);
+      push_check_kernel<MAT><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, a.ntiles);
+      HIPCHK(hipGetLastError());
     }
-    const unsigned g = grid_for(ntiles, 1, (i64)s->cus * per_cu);
-    ProfScope ps(s, GLINT_K_PUSH_SEQ, st);
-    push_seq_kernel<V, MAT><<<g, kTPB, 0, st>>>(a);
+    const unsigned ga = grid_for(ntiles, 1, (i64)s->cus * blocks_per_cu(push_apply_kernel<V, MAT>, 4));
+    ProfScope ps(s, GLINT_K_PUSH_APPLY, st);
+    push_apply_kernel<V, MAT><<<ga, kTPB, 0, st>>>(a);
     HIPCHK(hipGetLastError());
   }
   if (det) return push_det_tail<V, MAT>(s, a, vec_ok, st);

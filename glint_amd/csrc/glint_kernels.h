@@ -12,18 +12,18 @@
 // A record is rejected (GLINT_EOUTOFRANGE) exactly when the JVM would throw
 // ArrayIndexOutOfBoundsException: local index outside [0, size) or col outside [0, cols).
 //
-// Push = two stream-ordered kernels:
-//   push_seq      persistent, ticketed tiles; a decoupled look-back computes, per tile, whether
-//                 every record address from the start of the call up to the end of the tile is
-//                 strictly increasing. Such a prefix has unique addresses, so those tiles apply
-//                 their records with PLAIN coalesced read-modify-write (16-B accesses when two
-//                 consecutive records hit adjacent elements). The first tile whose prefix is not
-//                 increasing records itself as the break point and is NOT applied; neither is any
-//                 later tile.
-//   push_scatter  applies records [break*TILE, n) -- nothing when the whole call was increasing --
-//                 by LDS hash aggregation (duplicate addresses within a chunk are summed in LDS)
-//                 followed by one device-scope atomic add per distinct address.
-// The kernel boundary between the two orders every plain store before every atomic.
+// Push = up to three stream-ordered kernels:
+//   push_check    reads the keys once and finds the first 4096-record tile whose record addresses
+//                 stop being strictly increasing (within the tile or across its left edge).
+//   push_apply    every tile before that break: the prefix's addresses are strictly increasing,
+//                 hence unique, so records are applied with PLAIN coalesced read-modify-write
+//                 (16-B accesses when two consecutive records hit adjacent elements) -- bit-exact
+//                 with the reference's sequential loop.
+//   push_scatter  records [break*TILE, n) -- nothing when the whole call was increasing -- by LDS
+//                 hash aggregation (duplicate addresses within a chunk summed in LDS) followed by one
+//                 device-scope atomic add per distinct address; or, in deterministic mode, a stable
+//                 sort by address and an in-order fold per address.
+// Kernel boundaries order check -> apply -> scatter: every plain store precedes every atomic.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,22 +35,15 @@ typedef unsigned long long u64;
 typedef unsigned int u32;
 
 constexpr int kTPB = 256;          // threads per block (4 waves)
-constexpr int kSeqPPT = 8;         // record pairs per thread in push_seq
+constexpr int kSeqPPT = 8;         // record pairs per thread per tile in push_check / push_apply
 constexpr int kSeqTile = kTPB * kSeqPPT * 2;  // 4096 records per tile
 constexpr int kHashSlots = 4096;   // LDS hash table slots in push_scatter (64 KiB for 8-B V)
 constexpr int kScatterChunk = 2048;  // records per block iteration in push_scatter (load <= 0.5)
-static_assert(kSeqTile % kScatterChunk == 0, "a scatter chunk must lie inside one push_seq tile");
 
-// tile status words (published with agent-scope relaxed atomics; the word IS the payload)
-constexpr u32 ST_EMPTY = 0, ST_A_OK = 1, ST_A_BAD = 2, ST_P_OK = 3, ST_P_BAD = 4;
-constexpr u32 kLookbackSpinLimit = 1u << 22;
-
-// per-launch control words, zeroed by one hipMemsetAsync together with the status array
+// per-launch control words, zeroed by one hipMemsetAsync before push_check
 struct LaunchCtl {
-  u32 ticket;    // next tile ticket
-  u32 brk_enc;   // max over prefix-bad tiles of (ntiles - t); 0 = whole call increasing
-  u32 bad_enc;   // max over locally-bad tiles of (ntiles - t)
-  u32 timeouts;  // look-back spins that hit the limit (treated as a break: conservative)
+  u32 brk_enc;  // max over tiles that break the increasing order of (ntiles - t); 0 = none
+  u32 pad_[3];
 };
 
 // persistent error state, cleared by glint_shard_sync / host-pointer calls
@@ -84,7 +77,6 @@ struct PushArgs {
   V* data;
   PartDesc part;
   LaunchCtl* ctl;
-  u32* status;
   u32 ntiles;
   ErrState* err;
 };
