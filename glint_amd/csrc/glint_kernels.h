@@ -13,8 +13,10 @@
 // ArrayIndexOutOfBoundsException: local index outside [0, size) or col outside [0, cols).
 //
 // Push = up to three stream-ordered kernels:
-//   push_check    reads the keys once and finds the first 4096-record tile whose record addresses
-//                 stop being strictly increasing (within the tile or across its left edge).
+//   push_check    reads the keys once; finds the first 1024-record wave tile whose record addresses
+//                 stop being strictly increasing (within the tile or across its left edge), and
+//                 marks AFFINE tiles (record r hits element base + r), whose addresses push_apply
+//                 then knows without reading the keys again.
 //   push_apply    every tile before that break: the prefix's addresses are strictly increasing,
 //                 hence unique, so records are applied with PLAIN coalesced read-modify-write
 //                 (16-B accesses when two consecutive records hit adjacent elements) -- bit-exact
@@ -35,15 +37,18 @@ typedef unsigned long long u64;
 typedef unsigned int u32;
 
 constexpr int kTPB = 256;          // threads per block (4 waves)
-constexpr int kSeqPPT = 8;         // record pairs per thread per tile in push_check / push_apply
-constexpr int kSeqTile = kTPB * kSeqPPT * 2;  // 4096 records per tile
+constexpr int kPPT = 8;            // record pairs per lane per wave tile (push_check / push_apply)
+constexpr int kTile = 64 * kPPT * 2;  // 1024 records per wave tile
+constexpr int kStreamPPL = 4;      // record pairs per lane per push_stream step (default)
+constexpr i64 kNotAffine = (i64)0x8000000000000000ll;  // tile descriptor: addresses not base + r
 constexpr int kHashSlots = 4096;   // LDS hash table slots in push_scatter (64 KiB for 8-B V)
 constexpr int kScatterChunk = 2048;  // records per block iteration in push_scatter (load <= 0.5)
 
 // per-launch control words, zeroed by one hipMemsetAsync before push_check
 struct LaunchCtl {
-  u32 brk_enc;  // max over tiles that break the increasing order of (ntiles - t); 0 = none
-  u32 pad_[3];
+  u32 brk_enc;   // max over tiles that break the increasing order of (ntiles - t); 0 = none
+  u32 unsorted;  // push_stream: some tile is not increasing (or not linked to its predecessor)
+  u32 pad_[2];
 };
 
 // persistent error state, cleared by glint_shard_sync / host-pointer calls
@@ -75,6 +80,7 @@ struct PushArgs {
   const V* vals;
   i64 n;
   V* data;
+  i64 elems;  // elements allocated in the shard (bounds push_stream's speculative reads)
   PartDesc part;
   LaunchCtl* ctl;
   u32 ntiles;

@@ -29,6 +29,41 @@ __global__ __launch_bounds__(256) void k_stream4(const K2* __restrict__ keys, co
   }
 }
 
+// stream3: values + shard RMW only (the affine apply: no keys read)
+__global__ __launch_bounds__(256) void k_stream3(const D2* __restrict__ vals, D2* __restrict__ data, i64 n2) {
+  const i64 stride = (i64)gridDim.x * 256;
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n2; i += stride) {
+    const D2 v = __builtin_nontemporal_load(&vals[i]);
+    D2 d = data[i];
+    d += v;
+    data[i] = d;
+  }
+}
+// stream3 with two pairs per iteration (the product's apply_stream)
+__global__ __launch_bounds__(256) void k_stream3x2(const D2* __restrict__ vals, D2* __restrict__ data, i64 n2) {
+  const i64 stride = (i64)gridDim.x * 256;
+  i64 p = (i64)blockIdx.x * 256 + threadIdx.x;
+  for (; p + stride < n2; p += 2 * stride) {
+    const D2 v0 = __builtin_nontemporal_load(&vals[p]);
+    const D2 v1 = __builtin_nontemporal_load(&vals[p + stride]);
+    const D2 d0 = data[p];
+    const D2 d1 = data[p + stride];
+    data[p] = d0 + v0;
+    data[p + stride] = d1 + v1;
+  }
+  for (; p < n2; p += stride) data[p] = data[p] + __builtin_nontemporal_load(&vals[p]);
+}
+// pure read of one stream (push_check's traffic)
+__global__ __launch_bounds__(256) void k_read1(const K2* __restrict__ keys, i64 n2, i64* sink) {
+  const i64 stride = (i64)gridDim.x * 256;
+  i64 acc = 0;
+  for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n2; i += stride) {
+    const K2 k = __builtin_nontemporal_load(&keys[i]);
+    acc += k.x ^ k.y;
+  }
+  if (acc == 42) sink[0] = acc;
+}
+
 // grid-stride, PPT pairs per thread per iteration, dependent shard access
 template <int PPT, bool NTST>
 __global__ __launch_bounds__(256) void k_rmw(const K2* __restrict__ keys, const D2* __restrict__ vals,
@@ -127,6 +162,14 @@ int main(int argc, char** argv) {
   const D2* Vv = (const D2*)vals;
   for (int g : {512, 1024, 2048}) {
     rep("stream4", g, timeit([&] { k_stream4<<<g, 256>>>(K, Vv, (D2*)data, n2); }, reps));
+  }
+  for (int g : {256, 512, 1024, 2048}) {
+    const float ms = timeit([&] { k_stream3<<<g, 256>>>(Vv, (D2*)data, n2); }, reps);
+    printf("%-14s grid %6d  %8.3f ms  %7.0f GB/s actual (24B/rec)\n", "stream3", g, ms, 24.0 * n / ms / 1e6);
+    const float ms2 = timeit([&] { k_stream3x2<<<g, 256>>>(Vv, (D2*)data, n2); }, reps);
+    printf("%-14s grid %6d  %8.3f ms  %7.0f GB/s actual (24B/rec)\n", "stream3x2", g, ms2, 24.0 * n / ms2 / 1e6);
+    const float ms3 = timeit([&] { k_read1<<<g, 256>>>(K, n2, keys); }, reps);
+    printf("%-14s grid %6d  %8.3f ms  %7.0f GB/s actual (8B/rec)\n", "read1", g, ms3, 8.0 * n / ms3 / 1e6);
   }
   for (int g : {512, 1024, 2048, 4096}) {
     rep("rmw_p1", g, timeit([&] { k_rmw<1, false><<<g, 256>>>(K, Vv, data, n2); }, reps));
