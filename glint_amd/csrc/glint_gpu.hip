@@ -156,8 +156,15 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   const bool any_bad = __any(!mono);  // wave-wide votes, outside any lane-divergent branch
   const bool all_affine = __all(affine);
   if (lane == 0) {
-    if (any_bad) atomicMax(&ctl->brk_enc, ntiles - t);
-    else desc[t] = all_affine ? (i64)a_first : kNotAffine;
+    if (any_bad) {
+      atomicMax(&ctl->brk_enc, ntiles - t);
+    } else {
+      desc[t] = all_affine ? (i64)a_first : kNotAffine;
+      // the push is ONE affine run iff every tile is affine and continues its predecessor; only a
+      // tile that breaks the run writes the shared flag (after a relaxed read: it flips once)
+      const bool linked = all_affine && (r_first == 0 || (i64)a_first == (i64)before + 1);
+      if (!linked && ld_relaxed(&ctl->nonaffine) == 0u) atomicOr(&ctl->nonaffine, 1u);
+    }
   }
   return true;
 }
@@ -232,9 +239,8 @@ __device__ __forceinline__ void apply_affine(const PushArgs<V>& a, i64 pbase, i6
   }
 }
 
-template <typename V, bool MAT, bool FULL, bool MASK = false>
-__device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, int lane, u64 skip_steps = 0,
-                                              int step = kTile) {
+template <typename V, bool MAT, bool FULL>
+__device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, int lane) {
   typedef typename Vec2<V>::T V2;
   typedef typename AddrT<MAT>::T A;
   const i64 n = a.n;
@@ -258,10 +264,8 @@ __device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, i
 #pragma unroll
   for (int j = 0; j < kPPT; ++j) {
     const i64 r = 2 * (pbase + lane + (i64)j * 64);
-    // MASK: records of steps push_stream already applied are skipped (a pair never straddles steps)
-    const bool live = !MASK || !((skip_steps >> ((r - 2 * pbase) / step)) & 1ull);
     A a0, a1;
-    const bool h0 = (FULL || r < n) && live, h1 = (FULL || r + 1 < n) && live;
+    const bool h0 = FULL || r < n, h1 = FULL || r + 1 < n;
     const bool o0 = rec_addr_t<MAT>(a.part, k[j].x, MAT ? c[j].x : 0, a0) && h0;
     const bool o1 = rec_addr_t<MAT>(a.part, k[j].y, MAT ? c[j].y : 0, a1) && h1;
     if (h0 && !o0) record_error(a.err, r);
@@ -277,9 +281,43 @@ __device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, i
   }
 }
 
+// The whole push is one affine run (element = record + delta): a grid-stride sweep over record
+// pairs, so the grid reads one compact window of the value and shard streams at a time and no
+// load depends on another (the keys were read once, by push_check).
+template <typename V, bool EVEN>
+__device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta) {
+  typedef typename Vec2<V>::T V2;
+  const i64 npairs = a.n >> 1;
+  const i64 stride = (i64)gridDim.x * kTPB;
+  const V2* vp = reinterpret_cast<const V2*>(a.vals);
+  for (i64 p = (i64)blockIdx.x * kTPB + threadIdx.x; p < npairs; p += stride) {
+    const V2 v = __builtin_nontemporal_load(vp + p);
+    const i64 e = 2 * p + delta;
+    if (EVEN) {
+      V2* dp = reinterpret_cast<V2*>(a.data + e);
+      const V2 d = *dp;
+      *dp = as2<V>(vadd((V)d.x, (V)v.x), vadd((V)d.y, (V)v.y));
+    } else {
+      const V d0 = a.data[e], d1 = a.data[e + 1];
+      a.data[e] = vadd(d0, (V)v.x);
+      a.data[e + 1] = vadd(d1, (V)v.y);
+    }
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const i64 e = a.n - 1 + delta;
+    a.data[e] = vadd(a.data[e], a.vals[a.n - 1]);
+  }
+}
+
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i64* __restrict__ desc) {
   const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
+  if (brk == 0u && a.ctl->nonaffine == 0u) {
+    const i64 delta = desc[0];  // tile 0 starts the run at record 0
+    if ((delta & 1) == 0) apply_sweep<V, true>(a, delta);
+    else apply_sweep<V, false>(a, delta);
+    return;
+  }
   const u32 tiles = brk == 0u ? a.ntiles : a.ntiles - brk;
   const int lane = threadIdx.x & 63;
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
@@ -304,177 +342,6 @@ __global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i
 }
 
 // ------------------------------------------------------------------------------------------------
-// push (default mode): push_stream + push_rest_plain / push_scatter
-// ------------------------------------------------------------------------------------------------
-// push_stream speculates that the push is one AFFINE run -- record r hits element r + delta, with
-// delta taken from record 0 -- the shape of a dense contiguous push. The grid sweeps the push in
-// steps of 128 x SPP records per wave (SPP record pairs per lane), so at any moment the chip reads
-// one compact window of each stream (keys, values, shard), which HBM serves near its peak. Per step
-// the key, value and PREDICTED shard loads are issued together (no load waits on another); then
-// every record is verified against the prediction. A conforming step is applied with plain stores
-// and marked in `status`; any other step is left for the second kernel.
-// Correct for ANY input: conforming records hit pairwise distinct elements (r -> r + delta is
-// injective), so plain read-modify-write needs no atomics, and every other record is applied after
-// this kernel. The keys are read once, so a dense push moves exactly its algorithmic 32 B/record.
-// The same pass checks whether the push's addresses are strictly increasing; once a step shows
-// they are not, waves stop (the rest of the push goes to push_scatter).
-template <typename V, bool EVEN>
-__device__ __forceinline__ typename Vec2<V>::T load_pair(const V* data, i64 e) {
-  if (EVEN) return *reinterpret_cast<const typename Vec2<V>::T*>(data + e);
-  return as2<V>(data[e], data[e + 1]);
-}
-template <typename V, bool EVEN>
-__device__ __forceinline__ void store_pair(V* data, i64 e, typename Vec2<V>::T x) {
-  if (EVEN) *reinterpret_cast<typename Vec2<V>::T*>(data + e) = x;
-  else { data[e] = (V)x.x; data[e + 1] = (V)x.y; }
-}
-
-template <typename V, bool MAT, bool EVEN, bool FULL, int SPP>
-__device__ __forceinline__ bool stream_step(const PushArgs<V>& a, i64 delta, u32* __restrict__ status, u32 epoch,
-                                           u32 t, int lane, bool spec, bool poll, bool& stop) {
-  typedef typename Vec2<V>::T V2;
-  typedef typename AddrT<MAT>::T A;
-  constexpr int STEP = 128 * SPP;  // records per wave step: SPP pairs per lane, 1 KB per load instruction
-  const i64 n = a.n;
-  const i64 r_first = (i64)t * STEP;
-  const i64 pbase = r_first / 2;
-  // speculate only where the predicted elements exist
-  spec = spec && r_first + delta >= 0 && r_first + STEP + delta <= a.elems;
-  K2 k[SPP];
-  C2 c[SPP];
-  V2 v[SPP], d[SPP];
-#pragma unroll
-  for (int j = 0; j < SPP; ++j) {
-    const i64 p = pbase + lane + 64 * j;
-    const i64 r = 2 * p;
-    c[j] = C2{0, 0};
-    if (FULL || r + 1 < n) {
-      k[j] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(a.keys) + p);
-      if (MAT) c[j] = __builtin_nontemporal_load(reinterpret_cast<const C2*>(a.cols) + p);
-    } else {
-      k[j] = K2{r < n ? a.keys[r] : 0, 0};
-      if (MAT) c[j] = C2{r < n ? a.cols[r] : 0, 0};
-    }
-  }
-  if (spec) {
-#pragma unroll
-    for (int j = 0; j < SPP; ++j) {
-      const i64 p = pbase + lane + 64 * j;
-      const i64 r = 2 * p;
-      if (FULL || r + 1 < n) {
-        v[j] = __builtin_nontemporal_load(reinterpret_cast<const V2*>(a.vals) + p);
-        d[j] = load_pair<V, EVEN>(a.data, r + delta);
-      }
-    }
-  }
-  const i64 kb = r_first > 0 ? a.keys[r_first - 1] : 0;  // the record before this step
-  const int32_t cb = (MAT && r_first > 0) ? a.cols[r_first - 1] : 0;
-  if (poll) stop = __builtin_amdgcn_readfirstlane(ld_relaxed(&a.ctl->unsorted)) != 0u;
-
-  A before = 0;
-  if (r_first > 0) rec_addr_t<MAT>(a.part, kb, cb, before);
-  bool mono = true, conf = true;
-  A last = before;
-#pragma unroll
-  for (int j = 0; j < SPP; ++j) {
-    const i64 r = 2 * (pbase + lane + 64 * j);
-    const bool h0 = FULL || r < n, h1 = FULL || r + 1 < n;
-    A a0, a1;
-    const bool o0 = rec_addr_t<MAT>(a.part, k[j].x, MAT ? c[j].x : 0, a0);
-    const bool o1 = rec_addr_t<MAT>(a.part, k[j].y, MAT ? c[j].y : 0, a1);
-    if (h1) mono = mono && (a1 > a0);
-    A prev = __shfl_up(a1, 1);
-    if (lane == 0) prev = last;
-    if (h0 && r > 0) mono = mono && (a0 > prev);
-    last = __shfl(a1, 63);
-    conf = conf && (!h0 || (o0 && (i64)a0 == r + delta)) && (!h1 || (o1 && (i64)a1 == r + 1 + delta));
-  }
-  const bool all_conf = __all(conf);  // wave-wide votes, outside any lane-divergent branch
-  const bool any_unsorted = __any(!mono);
-  if (any_unsorted && lane == 0 && !stop) atomicOr(&a.ctl->unsorted, 1u);
-  if (!all_conf) return false;
-  if (!spec) {  // conforms although not speculated: load what was not (still no dependent address)
-#pragma unroll
-    for (int j = 0; j < SPP; ++j) {
-      const i64 p = pbase + lane + 64 * j;
-      const i64 r = 2 * p;
-      if (FULL || r + 1 < n) {
-        v[j] = __builtin_nontemporal_load(reinterpret_cast<const V2*>(a.vals) + p);
-        d[j] = load_pair<V, EVEN>(a.data, r + delta);
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < SPP; ++j) {
-    const i64 r = 2 * (pbase + lane + 64 * j);
-    if (FULL || r + 1 < n) {
-      store_pair<V, EVEN>(a.data, r + delta, as2<V>(vadd((V)d[j].x, (V)v[j].x), vadd((V)d[j].y, (V)v[j].y)));
-    } else if (r < n) {
-      a.data[r + delta] = vadd(a.data[r + delta], a.vals[r]);
-    }
-  }
-  if (lane == 0) status[t] = epoch;
-  return true;
-}
-
-template <typename V, bool MAT, bool EVEN, int SPP>
-__device__ __forceinline__ void stream_loop(const PushArgs<V>& a, i64 delta, u32* status, u32 epoch) {
-  constexpr int STEP = 128 * SPP;
-  const int lane = threadIdx.x & 63;
-  const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
-  const u32 nw = gridDim.x * (kTPB / 64);
-  const u32 nsteps = (u32)((a.n + STEP - 1) / STEP);
-  bool spec = true;
-  for (u32 t = w0, it = 0; t < nsteps; t += nw, ++it) {
-    bool stop = false;
-    const bool poll = (it & 3) == 0;  // look at the shared "unordered" flag every 4 steps
-    const bool full = (i64)(t + 1) * STEP <= a.n;
-    spec = full ? stream_step<V, MAT, EVEN, true, SPP>(a, delta, status, epoch, t, lane, spec, poll, stop)
-                : stream_step<V, MAT, EVEN, false, SPP>(a, delta, status, epoch, t, lane, spec, poll, stop);
-    if (stop) return;  // unordered push: push_scatter takes every step not applied yet
-  }
-}
-
-template <typename V, bool MAT, int SPP>
-__global__ __launch_bounds__(kTPB) void push_stream_kernel(PushArgs<V> a, u32* __restrict__ status, u32 epoch) {
-  typedef typename AddrT<MAT>::T A;
-  A a0 = 0;
-  rec_addr_t<MAT>(a.part, a.keys[0], MAT ? a.cols[0] : 0, a0);  // any delta is correct; record 0's is useful
-  const i64 delta = (i64)a0;
-  if ((delta & 1) == 0) stream_loop<V, MAT, true, SPP>(a, delta, status, epoch);
-  else stream_loop<V, MAT, false, SPP>(a, delta, status, epoch);
-}
-
-// push_rest_plain: after push_stream, when the whole push is strictly increasing (hence every
-// address unique): the steps push_stream did not apply, plain dependent read-modify-write, one
-// wave tile (kTile records = kTile / step steps) per wave iteration.
-template <typename V, bool MAT>
-__global__ __launch_bounds__(kTPB) void push_rest_plain_kernel(PushArgs<V> a, const u32* __restrict__ status,
-                                                               u32 epoch, int step) {
-  if (a.ctl->unsorted) return;  // ordered by the kernel boundary
-  const int lane = threadIdx.x & 63;
-  const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
-  const u32 nw = gridDim.x * (kTPB / 64);
-  const int kStepsPerTile = kTile / step;  // 1..8 status words per wave tile
-  for (u32 t = w0; t < a.ntiles; t += nw) {
-    const i64 s0 = (i64)t * kStepsPerTile;
-    const i64 nsteps = (a.n + step - 1) / step;
-    const bool mine = lane < kStepsPerTile && s0 + lane < nsteps;
-    const u32 st = mine ? status[s0 + lane] : epoch;
-    if (__all(st == epoch)) continue;  // the whole tile was applied by push_stream
-    const i64 pbase = (i64)t * (kTile / 2);
-    if (__all(st != epoch || !mine)) {  // none of it applied
-      if (2 * pbase + kTile <= a.n) apply_general<V, MAT, true>(a, pbase, lane);
-      else apply_general<V, MAT, false>(a, pbase, lane);
-      continue;
-    }
-    // mixed tile: records of applied steps are masked out
-    const u64 applied = __ballot(mine && st == epoch);
-    apply_general<V, MAT, false, true>(a, pbase, lane, applied, step);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // push_scatter: LDS-binned aggregation + device atomics for records [break*TILE, n)
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void lds_add(double* p, double v) { unsafeAtomicAdd(p, v); }
@@ -484,21 +351,15 @@ __device__ __forceinline__ void lds_add(int* p, int v) { atomicAdd((u32*)p, (u32
 
 constexpr u64 kEmpty = ~0ull;
 
-// mode: kScatterAll -- every record (unaligned inputs); kScatterAfterBreak -- records from the
-// break push_check found; kScatterUnapplied -- when push_stream saw an unordered push, every wave
-// tile it did not apply (status != epoch).
-enum { kScatterAll = 0, kScatterAfterBreak = 1, kScatterUnapplied = 2 };
-
+// force_all: every record (unaligned caller pointers, no push_check ran); otherwise the records
+// from the first non-increasing tile push_check found (none when the push was increasing).
 template <typename V, bool MAT>
-__global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int mode, const u32* __restrict__ status,
-                                                            u32 epoch, int step) {
+__global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int force_all) {
   i64 r0 = 0;
-  if (mode == kScatterAfterBreak) {
+  if (!force_all) {
     const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
     if (brk == 0u) return;
     r0 = (i64)(a.ntiles - brk) * kTile;
-  } else if (mode == kScatterUnapplied) {
-    if (!a.ctl->unsorted) return;  // ordered push: push_rest_plain handles the rest
   }
   if (r0 >= a.n) return;
   const i64 rem = a.n - r0;
@@ -517,7 +378,6 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int m
     for (int q = tid; q < kScatterChunk; q += kTPB) {
       const i64 i = cbase + q;
       if (i >= a.n) break;
-      if (mode == kScatterUnapplied && status[i / step] == epoch) continue;  // push_stream applied it
       const i64 key = a.keys[i];
       const int32_t col = MAT ? a.cols[i] : 0;
       const V val = a.vals[i];
@@ -689,7 +549,6 @@ struct glint_shard {
   void* d_det = nullptr;
   size_t det_bytes = 0;
   i64 last_bad = -1;
-  u32 epoch = 0;  // push_stream's tile-status generation
   // kernel timing (glint_prof_*): HIP event pairs recorded on the launch stream, summed lazily
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[GLINT_K_COUNT];
@@ -789,16 +648,17 @@ unsigned grid_for(i64 units, i64 per_block, i64 cap) {
   return (unsigned)g;
 }
 
-// resident blocks per CU for a kernel (occupancy query), capped; GLINT_BLOCKS_PER_CU overrides
+// resident blocks per CU for a kernel (occupancy query), capped at the measured best; the
+// environment variable `knob` (e.g. GLINT_CHECK_BPC) overrides it for tuning sweeps
 template <typename K>
-int blocks_per_cu(K kernel, int cap) {
+int blocks_per_cu(K kernel, int cap, const char* knob = nullptr) {
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kTPB, 0) != hipSuccess || b < 1) {
     (void)hipGetLastError();
     b = 2;
   }
   b = std::min(b, cap);
-  const char* env = getenv("GLINT_BLOCKS_PER_CU");  // tuning override
+  const char* env = knob ? getenv(knob) : nullptr;
   if (env && atoi(env) > 0) b = atoi(env);
   return b;
 }
@@ -862,81 +722,41 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.ntiles = (u32)ntiles;
   const bool vec_ok = aligned(keys, 16) && aligned(vals, 2 * sizeof(V)) && (!MAT || aligned(cols, 8));
   const bool det = (flags & GLINT_PUSH_DETERMINISTIC) && (s->dtype == GLINT_F32 || s->dtype == GLINT_F64);
-  // control region: [LaunchCtl | pad to 256][status u32 x ntiles | pad][descriptors i64 x ntiles]
-  const int spp = [] {  // record pairs per lane per push_stream step (tuning knob)
-    const char* e = getenv("GLINT_STREAM_PPL");
-    const int v = e ? atoi(e) : kStreamPPL;
-    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : kStreamPPL;
-  }();
-  const int step = 128 * spp;
-  const i64 nsteps = (n + step - 1) / step;
-  const size_t st_bytes = pad256((size_t)nsteps * sizeof(u32));
-  const size_t ctl_need = 256 + st_bytes + (size_t)ntiles * sizeof(i64);
-  const size_t old_cap = s->ctl_bytes;
+  // control region: [LaunchCtl | pad to 256][tile descriptors i64 x ntiles]
+  const size_t ctl_need = 256 + (size_t)ntiles * sizeof(i64);
   int rc = grow(&s->d_ctl, &s->ctl_bytes, ctl_need);
   if (rc) return rc;
-  if (s->ctl_bytes != old_cap) HIPCHK(hipMemsetAsync(s->d_ctl, 0, s->ctl_bytes, st));  // fresh status words
   a.ctl = (LaunchCtl*)s->d_ctl;
-  u32* status = (u32*)((char*)s->d_ctl + 256);
-  i64* desc = (i64*)((char*)s->d_ctl + 256 + st_bytes);
+  i64* desc = (i64*)((char*)s->d_ctl + 256);
 
   if (!vec_ok) {  // unaligned caller pointers: the scalar-load scatter for everything
     if (det) return push_det_tail<V, MAT>(s, a, false, st);
     const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
     ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
-    push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, kScatterAll, status, 0, kTile);
+    push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, 1);
     HIPCHK(hipGetLastError());
     return GLINT_OK;
   }
   HIPCHK(hipMemsetAsync(s->d_ctl, 0, sizeof(LaunchCtl), st));
-  if (det) {
-    // strict sequential order: the increasing prefix (push_check + push_apply, bit-exact) and the
-    // rest by a stable sort + in-order fold
-    {
-      const unsigned gc = grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT>, 4));
-      ProfScope pc(s, GLINT_K_PUSH_CHECK, st);
-      push_check_kernel<MAT><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
-      HIPCHK(hipGetLastError());
-    }
-    {
-      const unsigned ga = grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_apply_kernel<V, MAT>, 4));
-      ProfScope ps(s, GLINT_K_PUSH_APPLY, st);
-      push_apply_kernel<V, MAT><<<ga, kTPB, 0, st>>>(a, desc);
-      HIPCHK(hipGetLastError());
-    }
-    return push_det_tail<V, MAT>(s, a, true, st);
-  }
-  // default: speculative affine stream, then the remainder (plain if ordered, else LDS scatter)
-  if (++s->epoch == 0u) {
-    HIPCHK(hipMemsetAsync(status, 0, st_bytes, st));
-    s->epoch = 1u;
-  }
   {
-    ProfScope ps(s, GLINT_K_PUSH_STREAM, st);
-    auto go = [&](auto kernel) {
-      const unsigned g = grid_for(nsteps, kTPB / 64, (i64)s->cus * blocks_per_cu(kernel, 2));
-      kernel<<<g, kTPB, 0, st>>>(a, status, s->epoch);
-    };
-    switch (spp) {
-      case 1: go(push_stream_kernel<V, MAT, 1>); break;
-      case 2: go(push_stream_kernel<V, MAT, 2>); break;
-      case 4: go(push_stream_kernel<V, MAT, 4>); break;
-      default: go(push_stream_kernel<V, MAT, 8>); break;
-    }
+    const unsigned gc =
+        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT>, 8, "GLINT_CHECK_BPC"));
+    ProfScope pc(s, GLINT_K_PUSH_CHECK, st);
+    push_check_kernel<MAT><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
     HIPCHK(hipGetLastError());
   }
   {
-    const unsigned g = grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_rest_plain_kernel<V, MAT>, 4));
+    const unsigned ga =
+        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_apply_kernel<V, MAT>, 2, "GLINT_APPLY_BPC"));
     ProfScope ps(s, GLINT_K_PUSH_APPLY, st);
-    push_rest_plain_kernel<V, MAT><<<g, kTPB, 0, st>>>(a, status, s->epoch, step);
+    push_apply_kernel<V, MAT><<<ga, kTPB, 0, st>>>(a, desc);
     HIPCHK(hipGetLastError());
   }
-  {
-    const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
-    ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
-    push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, kScatterUnapplied, status, s->epoch, step);
-    HIPCHK(hipGetLastError());
-  }
+  if (det) return push_det_tail<V, MAT>(s, a, true, st);
+  const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
+  ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
+  push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, 0);
+  HIPCHK(hipGetLastError());
   return GLINT_OK;
 }
 

@@ -39,15 +39,14 @@ typedef unsigned int u32;
 constexpr int kTPB = 256;          // threads per block (4 waves)
 constexpr int kPPT = 8;            // record pairs per lane per wave tile (push_check / push_apply)
 constexpr int kTile = 64 * kPPT * 2;  // 1024 records per wave tile
-constexpr int kStreamPPL = 4;      // record pairs per lane per push_stream step (default)
 constexpr i64 kNotAffine = (i64)0x8000000000000000ll;  // tile descriptor: addresses not base + r
 constexpr int kHashSlots = 4096;   // LDS hash table slots in push_scatter (64 KiB for 8-B V)
 constexpr int kScatterChunk = 2048;  // records per block iteration in push_scatter (load <= 0.5)
 
 // per-launch control words, zeroed by one hipMemsetAsync before push_check
 struct LaunchCtl {
-  u32 brk_enc;   // max over tiles that break the increasing order of (ntiles - t); 0 = none
-  u32 unsorted;  // push_stream: some tile is not increasing (or not linked to its predecessor)
+  u32 brk_enc;    // max over tiles that break the increasing order of (ntiles - t); 0 = none
+  u32 nonaffine;  // some tile is not affine or does not continue its predecessor's affine run
   u32 pad_[2];
 };
 
@@ -80,7 +79,7 @@ struct PushArgs {
   const V* vals;
   i64 n;
   V* data;
-  i64 elems;  // elements allocated in the shard (bounds push_stream's speculative reads)
+  i64 elems;  // elements allocated in the shard
   PartDesc part;
   LaunchCtl* ctl;
   u32 ntiles;

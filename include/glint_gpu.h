@@ -145,14 +145,13 @@ int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uin
  * stream it is launched on; glint_prof_read waits for them and returns the summed device time and
  * launch count of one kernel kind since the last reset. Used by bench.py for the roofline figure. */
 enum glint_kernel_id {
-  GLINT_K_PUSH_APPLY = 0,   /* plain-RMW push of ordered, non-affine records */
-  GLINT_K_PUSH_SCATTER = 1, /* LDS-aggregated atomic push of unordered records */
+  GLINT_K_PUSH_APPLY = 0,   /* plain-RMW push of the increasing prefix (the dense hot path) */
+  GLINT_K_PUSH_SCATTER = 1, /* LDS-aggregated atomic push of the unordered tail */
   GLINT_K_VEC_PULL = 2,
   GLINT_K_MAT_PULL = 3,
   GLINT_K_MAT_PULL_ROWS = 4,
-  GLINT_K_PUSH_CHECK = 5,   /* order check (deterministic mode) */
-  GLINT_K_PUSH_STREAM = 6,  /* speculative affine stream: the dense push hot path */
-  GLINT_K_COUNT = 7
+  GLINT_K_PUSH_CHECK = 5,   /* order / affinity check over the keys in front of push_apply */
+  GLINT_K_COUNT = 6
 };
 int glint_prof_enable(glint_shard_t shard, int on);
 int glint_prof_read(glint_shard_t shard, int kernel_id, double* total_ms, int64_t* launches);

@@ -1,5 +1,6 @@
-"""Tuning sweep for the push kernels (run on the GPU box): times glint_vec_push_dev on a dense
-2^28 push for every (GLINT_STREAM_PPL, GLINT_BLOCKS_PER_CU) pair, in one process."""
+"""Tuning sweep for the push kernels (run on the GPU box): times glint_vec_push_dev on a 2^lg push
+for blocks-per-CU values of one kernel (knob GLINT_CHECK_BPC or GLINT_APPLY_BPC), in one process.
+Usage: sweep_push.py [lg] [dense|sorted_sparse] [knob]"""
 import ctypes as C
 import os
 import sys
@@ -22,24 +23,29 @@ if pattern == "sorted_sparse":
     keys = torch.arange(0, n, 2, dtype=torch.int64, device=dev)
 vals = torch.rand(keys.numel(), dtype=torch.float64, device=dev)
 stream = torch.cuda.current_stream(dev).cuda_stream
-for ppl in (1, 2, 4, 8):
-    for bpc in (1, 2, 3, 4, 8):
-        os.environ["GLINT_STREAM_PPL"] = str(ppl)
-        os.environ["GLINT_BLOCKS_PER_CU"] = str(bpc)
-        for _ in range(2):
-            lib.glint_vec_push_dev(sh.handle, keys.data_ptr(), vals.data_ptr(), keys.numel(), 0, stream)
-        torch.cuda.synchronize()
-        lib.glint_prof_reset(sh.handle)
-        lib.glint_prof_enable(sh.handle, 1)
-        t0 = time.perf_counter()
-        for _ in range(10):
-            lib.glint_vec_push_dev(sh.handle, keys.data_ptr(), vals.data_ptr(), keys.numel(), 0, stream)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 10
-        lib.glint_prof_enable(sh.handle, 0)
-        ms, cnt = C.c_double(), C.c_int64()
-        lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_STREAM, C.byref(ms), C.byref(cnt))
-        k = ms.value / max(cnt.value, 1)
-        gbs = 32.0 * keys.numel() / dt / 1e9
-        print(f"ppl {ppl} bpc {bpc}: step {dt*1e3:.3f} ms  {gbs:7.0f} GB/s   push_stream {k:.3f} ms", flush=True)
+
+
+def kms(kid):
+    ms, cnt = C.c_double(), C.c_int64()
+    lib.glint_prof_read(sh.handle, kid, C.byref(ms), C.byref(cnt))
+    return ms.value / max(cnt.value, 1)
+
+
+knob = sys.argv[3] if len(sys.argv) > 3 else "GLINT_APPLY_BPC"
+for bpc in (1, 2, 3, 4, 6, 8):
+    os.environ[knob] = str(bpc)
+    for _ in range(2):
+        lib.glint_vec_push_dev(sh.handle, keys.data_ptr(), vals.data_ptr(), keys.numel(), 0, stream)
+    torch.cuda.synchronize()
+    lib.glint_prof_reset(sh.handle)
+    lib.glint_prof_enable(sh.handle, 1)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        lib.glint_vec_push_dev(sh.handle, keys.data_ptr(), vals.data_ptr(), keys.numel(), 0, stream)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 10
+    lib.glint_prof_enable(sh.handle, 0)
+    gbs = 32.0 * keys.numel() / dt / 1e9
+    print(f"{pattern} {knob}={bpc}: step {dt*1e3:.3f} ms  {gbs:7.0f} GB/s   check {kms(N.GLINT_K_PUSH_CHECK):.3f} "
+          f"apply {kms(N.GLINT_K_PUSH_APPLY):.3f} scatter {kms(N.GLINT_K_PUSH_SCATTER):.3f} ms", flush=True)
 sh.sync(stream)
