@@ -413,29 +413,80 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
 // deterministic tail: stable sort by address, then an in-order fold per address starting from the
 // shard's current value -- the reference's sequential `+=` order, bit for bit
 // ------------------------------------------------------------------------------------------------
-template <bool MAT>
-__global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, const int32_t* cols, i64 r0, i64 m,
-                                                           PartDesc part, u64 sentinel, u64* addr, u32* idx,
+template <typename V, bool MAT>
+__global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, const int32_t* cols, const V* vals, i64 r0,
+                                                           i64 m, PartDesc part, u64 sentinel, u64* addr, V* val,
                                                            ErrState* err) {
   for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
     i64 ad;
     const bool ok = rec_addr<MAT>(part, keys[r0 + i], MAT ? cols[r0 + i] : 0, ad);
     if (!ok) record_error(err, r0 + i);
     addr[i] = ok ? (u64)ad : sentinel;
-    idx[i] = (u32)i;
+    val[i] = vals[r0 + i];
   }
 }
 
+// After the stable sort by address, each run of equal addresses holds that element's values in
+// push order. A run is folded into the shard strictly left to right, starting from the shard's
+// current value -- the reference's `data(k) += v` sequence, rounding for rounding.
+constexpr int kDetShort = 64;  // runs up to this length: one thread; longer: one wave
+
 template <typename V>
-__global__ __launch_bounds__(kTPB) void det_fold_kernel(const u64* addr, const u32* idx, i64 m, const V* vals,
-                                                        i64 r0, u64 sentinel, V* data) {
+__global__ __launch_bounds__(kTPB) void det_fold_short_kernel(const u64* addr, const V* val, i64 m, u64 sentinel,
+                                                              V* data, u32* long_count, u32* long_list) {
   for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
     const u64 ad = addr[i];
     if (ad == sentinel) continue;
     if (i > 0 && addr[i - 1] == ad) continue;  // not the head of its run
+    i64 j = i;
+    while (j < m && j - i < kDetShort && addr[j] == ad) ++j;
+    if (j < m && j - i == kDetShort && addr[j] == ad) {  // a long run: leave it to a whole wave
+      long_list[atomicAdd(long_count, 1u)] = (u32)i;
+      continue;
+    }
     V acc = data[ad];
-    for (i64 j = i; j < m && addr[j] == ad; ++j) acc = vadd(acc, vals[r0 + idx[j]]);
+    for (i64 q = i; q < j; ++q) acc = vadd(acc, val[q]);
     data[ad] = acc;
+  }
+}
+
+// value of lane l (wave-uniform l) through v_readlane -> SGPR: no LDS round trip per element
+__device__ __forceinline__ double lane_value(double x, int l) {
+  const u64 b = __double_as_longlong(x);
+  const u32 lo = __builtin_amdgcn_readlane((u32)b, l), hi = __builtin_amdgcn_readlane((u32)(b >> 32), l);
+  return __longlong_as_double((long long)(((u64)hi << 32) | lo));
+}
+__device__ __forceinline__ float lane_value(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+__device__ __forceinline__ long long lane_value(long long x, int l) {
+  const u64 b = (u64)x;
+  return (long long)(((u64)__builtin_amdgcn_readlane((u32)(b >> 32), l) << 32) | __builtin_amdgcn_readlane((u32)b, l));
+}
+__device__ __forceinline__ int lane_value(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+
+template <typename V>
+__global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, const V* val, i64 m,
+                                                             const u32* long_count, const u32* long_list, V* data) {
+  const int lane = threadIdx.x & 63;
+  const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
+  const u32 nw = gridDim.x * (kTPB / 64);
+  const u32 cnt = *long_count;
+  for (u32 w = w0; w < cnt; w += nw) {
+    const i64 i = long_list[w];
+    const u64 ad = addr[i];
+    V acc = data[ad];
+    for (i64 base = i;; base += 64) {
+      // 64 consecutive values per load (coalesced); the adds stay strictly sequential
+      const i64 q = base + lane;
+      const bool in = q < m && addr[q] == ad;
+      const V x = in ? val[q] : V(0);
+      const u64 msk = __ballot(in);
+      const int len = msk == ~0ull ? 64 : __ffsll((long long)~msk) - 1;  // the run is contiguous
+      for (int l = 0; l < len; ++l) acc = vadd(acc, lane_value(x, l));
+      if (len < 64) break;
+    }
+    if (lane == 0) data[ad] = acc;
   }
 }
 
@@ -682,23 +733,31 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
   while (end_bit < 64 && ((u64)1 << end_bit) <= sentinel) ++end_bit;
   size_t tmp_bytes = 0;
   u64* nul64 = nullptr;
-  u32* nul32 = nullptr;
-  HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, nul64, nul64, nul32, nul32, (size_t)m, 0, end_bit, st));
-  const size_t b_addr = pad256((size_t)m * 8), b_idx = pad256((size_t)m * 4);
-  const size_t need = 2 * b_addr + 2 * b_idx + pad256(tmp_bytes);
+  V* nulv = nullptr;
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, nul64, nul64, nulv, nulv, (size_t)m, 0, end_bit, st));
+  const size_t b_addr = pad256((size_t)m * 8), b_val = pad256((size_t)m * sizeof(V));
+  const size_t b_list = pad256(((size_t)m / kDetShort + 2) * 4);
+  const size_t need = 2 * b_addr + 2 * b_val + b_list + pad256(tmp_bytes);
   int rc = grow(&s->d_det, &s->det_bytes, need);
   if (rc) return rc;
   char* base = (char*)s->d_det;
   u64* addr_in = (u64*)base;
   u64* addr_out = (u64*)(base + b_addr);
-  u32* idx_in = (u32*)(base + 2 * b_addr);
-  u32* idx_out = (u32*)(base + 2 * b_addr + b_idx);
-  void* tmp = base + 2 * b_addr + 2 * b_idx;
+  V* val_in = (V*)(base + 2 * b_addr);
+  V* val_out = (V*)(base + 2 * b_addr + b_val);
+  u32* long_count = (u32*)(base + 2 * b_addr + 2 * b_val);
+  u32* long_list = long_count + 1;
+  void* tmp = base + 2 * b_addr + 2 * b_val + b_list;
   const unsigned g = grid_for(m, kTPB, (i64)s->cus * 8);
-  det_prepare_kernel<MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, r0, m, a.part, sentinel, addr_in, idx_in, a.err);
+  det_prepare_kernel<V, MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, a.vals, r0, m, a.part, sentinel, addr_in, val_in,
+                                                 a.err);
   HIPCHK(hipGetLastError());
-  HIPCHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, addr_in, addr_out, idx_in, idx_out, (size_t)m, 0, end_bit, st));
-  det_fold_kernel<V><<<g, kTPB, 0, st>>>(addr_out, idx_out, m, a.vals, r0, sentinel, a.data);
+  // stable LSD radix sort: equal addresses keep their push order
+  HIPCHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, addr_in, addr_out, val_in, val_out, (size_t)m, 0, end_bit, st));
+  HIPCHK(hipMemsetAsync(long_count, 0, 4, st));
+  det_fold_short_kernel<V><<<g, kTPB, 0, st>>>(addr_out, val_out, m, sentinel, a.data, long_count, long_list);
+  HIPCHK(hipGetLastError());
+  det_fold_long_kernel<V><<<(unsigned)s->cus * 2, kTPB, 0, st>>>(addr_out, val_out, m, long_count, long_list, a.data);
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }

@@ -1,4 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python tools/sweep_push.py 28 dense GLINT_CHECK_BPC > gpurun_out/sweep28c.txt 2>&1 || exit 1
-timeout -k 10 300 python tools/sweep_push.py 28 dense GLINT_APPLY_BPC > gpurun_out/sweep28a.txt 2>&1 || exit 1
-timeout -k 10 150 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/bench_28.txt 2>&1 || exit 1
+timeout -k 10 500 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.txt 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.txt
+timeout -k 10 600 python tools/measure_paths.py > gpurun_out/paths.jsonl 2> gpurun_out/paths.err
