@@ -17,6 +17,7 @@ GLINT_OK, GLINT_EOUTOFRANGE, GLINT_EDEVICE, GLINT_EINVAL, GLINT_ENOMEM = 0, 1, 2
 GLINT_PUSH_DEFAULT, GLINT_PUSH_DETERMINISTIC = 0, 1
 GLINT_K_PUSH_APPLY, GLINT_K_PUSH_SCATTER, GLINT_K_VEC_PULL, GLINT_K_MAT_PULL, GLINT_K_MAT_PULL_ROWS = 0, 1, 2, 3, 4
 GLINT_K_PUSH_CHECK = 5
+GLINT_ROUTE_RANGE, GLINT_ROUTE_CYCLIC = 0, 1
 
 # every symbol include/glint_gpu.h declares, with its C signature
 _P = C.c_void_p
@@ -46,6 +47,7 @@ SIGNATURES = {
     "glint_shard_pitch": (_I, [_P, C.POINTER(_I64)]),
     "glint_push_wire": (_I, [_P, _P, _SZ, C.POINTER(_I32), _I]),
     "glint_pull_wire": (_I, [_P, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
+    "glint_route_dev": (_I, [_P, _I64, _I, _I32, _I64, _P, _P, C.POINTER(_I64), _P]),
     "glint_prof_enable": (_I, [_P, _I]),
     "glint_prof_read": (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(_I64)]),
     "glint_prof_reset": (_I, [_P]),

@@ -22,7 +22,7 @@ LIB = LIB_DIR / "libglint_gpu.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "build" / "libglint_oracle.so"
 
-HIP_SOURCES = [PKG / "csrc" / "glint_gpu.hip"]
+HIP_SOURCES = [PKG / "csrc" / "glint_gpu.hip", PKG / "csrc" / "glint_route.hip"]
 HIP_DEPS = HIP_SOURCES + [PKG / "csrc" / "glint_kernels.h", ROOT / "include" / "glint_gpu.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "glint_oracle.c"]
 

@@ -140,6 +140,20 @@ int glint_push_wire(glint_shard_t shard, const uint8_t* payload, size_t len, int
 int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uint8_t* response,
                     size_t cap, size_t* out_len);
 
+/* ---- client routing (device) -------------------------------------------------------------- *
+ * Replaces the client-side grouping in AsyncBigVector/AsyncBigMatrix.mapPartitions
+ * (src/main/scala/glint/models/client/async/AsyncBigVector.scala:96-98, AsyncBigMatrix.scala:
+ * 150-152): a stable counting sort of the n device-resident keys by owning partition under
+ * RangePartitioner.apply(nparts, nkeys) (RangePartitioner.scala:27-84) or
+ * CyclicPartitioner.apply(nparts, nkeys) (CyclicPartitioner.scala:19-22, 41-50). On return (the
+ * call synchronises `stream`): order[0..n) holds the record indices grouped by partition, each
+ * group in the caller's order; counts[0..nparts) (device) the group sizes. Out-of-range keys
+ * (IndexOutOfBoundsException in partition()) -> GLINT_EOUTOFRANGE with the first bad record index
+ * in *first_bad (host), else *first_bad = -1. nparts <= 8192, n < 2^32. */
+enum glint_route_kind { GLINT_ROUTE_RANGE = 0, GLINT_ROUTE_CYCLIC = 1 };
+int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys,
+                    int64_t* counts, int64_t* order, int64_t* first_bad, void* stream);
+
 /* ---- kernel timing ------------------------------------------------------------------------- *
  * With profiling on, every kernel launch of the shard is bracketed by HIP events recorded on the
  * stream it is launched on; glint_prof_read waits for them and returns the summed device time and

@@ -1,0 +1,159 @@
+"""Worker bodies for the multi-process tests (test_dist_cpu.py, test_gpu_parity.py::test_dist_*).
+
+Each rank pushes / pulls its own seeded batch through glint_amd.dist; every rank regenerates all
+ranks' batches and checks its answers against one sequential oracle replay of the whole job:
+shards apply records in source-rank order, each source's records in its caller's order, so the
+replay -- rank 0's batch, then rank 1's, ... -- is bit-exact also for Double sums.
+"""
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from glint_amd.errors import IndexOutOfBoundsException  # noqa: E402
+from glint_amd.partitioning import CyclicPartitioner, RangePartition, RangePartitioner  # noqa: E402
+from glint_amd.shard import resolve_dtype  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+class OracleShard:
+    """Test double with the PartialVector / PartialMatrix call surface over the CPU oracle, so the
+    routing and exchange layers can be exercised on CPU-only ranks (gloo)."""
+
+    def __init__(self, kind, partition, cols, dtype, device):
+        self.code, self.np_dtype = resolve_dtype(dtype)
+        if isinstance(partition, RangePartition):
+            part = O.part_range(partition.start, partition.end)
+        else:
+            part = O.part_cyclic(partition.index, partition.numberOfPartitions, partition.numberOfKeys)
+        self.o = O.OracleVector(part, self.code) if kind == "vector" else O.OracleMatrix(part, cols, self.code)
+
+    def update(self, *args, deterministic=False):
+        assert self.o.update(*[a.cpu().numpy() for a in args]) == -1
+
+    def get(self, *args):
+        out, bad = self.o.get(*[a.cpu().numpy() for a in args])
+        assert bad == -1
+        return torch.from_numpy(out)
+
+    def getRows(self, rows):
+        out, bad = self.o.get_rows(rows.cpu().numpy())
+        assert bad == -1
+        return torch.from_numpy(out)
+
+    def destroy(self):
+        pass
+
+
+def _oracle_factory(kind, partition, cols, dtype, device):
+    return OracleShard(kind, partition, cols, dtype, device)
+
+
+def _batch(seed, n, nkeys, np_dtype):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, nkeys, n).astype(np.int64)
+    k[: n // 4] = k[n // 2: n // 2 + n // 4]  # duplicates inside the batch
+    if np.dtype(np_dtype).kind == "f":
+        v = rng.uniform(-1, 1, n).astype(np_dtype)
+    else:
+        v = rng.integers(-1000, 1000, n).astype(np_dtype)
+    return k, v
+
+
+def _init(rank, world, port, backend):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+
+
+def run_case(rank, world, port, backend, case, use_gpu):
+    _init(rank, world, port, backend)
+    try:
+        if use_gpu:
+            torch.cuda.set_device(0)
+            dev = torch.device("cuda", 0)
+            from glint_amd.dist import DistributedClient
+            client = DistributedClient(device=dev)
+        else:
+            dev = torch.device("cpu")
+            from glint_amd.dist import DistributedClient
+            client = DistributedClient(device=dev, shard_factory=_oracle_factory)
+        CASES[case](client, rank, world, dev)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _vector_case(nkeys, mps, partitioner, dtype, n=3000):
+    def body(client, rank, world, dev):
+        _, np_dtype = resolve_dtype(dtype)
+        vec = client.vector(nkeys, dtype, modelsPerServer=mps, createPartitioner=partitioner)
+        for step in range(2):
+            k, v = _batch(1000 * step + rank, n + 37 * rank, nkeys, np_dtype)
+            vec.push(torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev))
+        # oracle replay: all ranks' batches in rank order, step by step
+        ref = O.OracleVector(O.part_range(0, nkeys), resolve_dtype(dtype)[0])
+        for step in range(2):
+            for r in range(world):
+                k, v = _batch(1000 * step + r, n + 37 * r, nkeys, np_dtype)
+                assert ref.update(k, v) == -1
+        q = np.random.default_rng(77 + rank).integers(0, nkeys, 1500 + rank).astype(np.int64)
+        got = vec.pull(torch.from_numpy(q).to(dev)).cpu().numpy()
+        want, _ = ref.get(q)
+        np.testing.assert_array_equal(got, want)
+        # out-of-range key: raised on every rank before any exchange, the model is untouched
+        bad = np.array([0, nkeys], dtype=np.int64)
+        try:
+            vec.push(torch.from_numpy(bad).to(dev), torch.from_numpy(np.zeros(2, np_dtype)).to(dev))
+            raise AssertionError("out-of-range key accepted")
+        except IndexOutOfBoundsException:
+            pass
+        got2 = vec.pull(torch.from_numpy(q).to(dev)).cpu().numpy()
+        np.testing.assert_array_equal(got2, want)
+        # an empty batch still takes part in the exchange
+        vec.push(torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.float64, device=dev))
+        assert vec.pull(torch.zeros(0, dtype=torch.int64, device=dev)).numel() == 0
+        vec.destroy()
+    return body
+
+
+def _matrix_case(nrows, ncols, mps, dtype="double", n=2500):
+    def body(client, rank, world, dev):
+        _, np_dtype = resolve_dtype(dtype)
+        mat = client.matrix(nrows, ncols, dtype, modelsPerServer=mps)
+        ref = O.OracleMatrix(O.part_range(0, nrows), ncols, resolve_dtype(dtype)[0])
+        for r in range(world):
+            rng = np.random.default_rng(500 + r)
+            rows = rng.integers(0, nrows, n).astype(np.int64)
+            cols = rng.integers(0, ncols, n).astype(np.int32)
+            vals = rng.uniform(-1, 1, n).astype(np_dtype)
+            if r == rank:
+                mat.push(torch.from_numpy(rows).to(dev), torch.from_numpy(cols).to(dev),
+                         torch.from_numpy(vals).to(dev))
+            assert ref.update(rows, cols, vals) == -1
+        rng = np.random.default_rng(900 + rank)
+        qr = rng.integers(0, nrows, 700).astype(np.int64)
+        qc = rng.integers(0, ncols, 700).astype(np.int32)
+        got = mat.pull(torch.from_numpy(qr).to(dev), torch.from_numpy(qc).to(dev)).cpu().numpy()
+        np.testing.assert_array_equal(got, ref.get(qr, qc)[0])
+        rows_got = mat.pull(torch.from_numpy(qr[:50]).to(dev)).cpu().numpy()
+        np.testing.assert_array_equal(rows_got, ref.get_rows(qr[:50])[0])
+        mat.destroy()
+    return body
+
+
+CASES = {
+    "vec_range": _vector_case(10_007, 1, RangePartitioner.apply, "double"),
+    "vec_range_mps3": _vector_case(10_007, 3, RangePartitioner.apply, "double"),
+    "vec_cyclic_mps2": _vector_case(9_001, 2, CyclicPartitioner.apply, "double"),
+    "vec_long_few_keys": _vector_case(5, 2, RangePartitioner.apply, "long", n=200),
+    "mat_range": _matrix_case(1_003, 17, 1),
+    "mat_range_mps2": _matrix_case(1_003, 17, 2),
+}

@@ -324,3 +324,86 @@ def test_large_dense_push_property(gpu):
         sh.update(keys, vals)
         out = sh.get(keys)
         assert torch.equal(out, vals * 2)
+
+
+# ---- client routing on the device (glint_route_dev) against the oracle's bucketing -------------------
+def route_dev(keys_np, kind, nparts, nkeys, dev=0):
+    import ctypes as C
+    import torch
+    lib = N.load()
+    keys = torch.from_numpy(keys_np).to(torch.device("cuda", dev))
+    counts = torch.full((nparts,), -7, dtype=torch.int64, device=keys.device)
+    order = torch.full((max(keys.numel(), 1),), -7, dtype=torch.int64, device=keys.device)
+    bad = C.c_int64(-2)
+    rc = lib.glint_route_dev(keys.data_ptr(), keys.numel(), kind, nparts, nkeys, counts.data_ptr(),
+                             order.data_ptr(), C.byref(bad), torch.cuda.current_stream(keys.device).cuda_stream)
+    return rc, bad.value, counts.cpu().numpy(), order[:keys.numel()].cpu().numpy()
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 7, 64, 1000, 8192])
+@pytest.mark.parametrize("n", [0, 1, 4095, 4096, 4097, 100_003, 1 << 22])
+def test_route_range_matches_oracle(gpu, nparts, n):
+    nkeys = 1_000_003
+    if nparts > nkeys:
+        pytest.skip("more partitions than keys")
+    rng = np.random.default_rng(n + nparts)
+    keys = rng.integers(0, nkeys, n).astype(np.int64)
+    if n > 100:
+        keys[: n // 3] = np.sort(keys[: n // 3])  # ordered runs next to random ones
+    rc, bad, counts, order = route_dev(keys, N.GLINT_ROUTE_RANGE, nparts, nkeys, gpu)
+    assert rc == N.GLINT_OK and bad == -1
+    c_ref, _, o_ref = O.bucket_range(keys, nparts, nkeys)
+    np.testing.assert_array_equal(counts, c_ref)
+    np.testing.assert_array_equal(order, o_ref)  # stable: identical permutation
+
+
+@pytest.mark.parametrize("nparts", [1, 3, 8, 4096])
+def test_route_cyclic_matches_host(gpu, nparts):
+    from glint_amd.partitioning import CyclicPartitioner
+    nkeys = (1 << 31) + 11  # keys beyond Int range: Long modulo, as CyclicPartitioner.partition
+    rng = np.random.default_rng(nparts)
+    keys = rng.integers(0, nkeys, 300_001).astype(np.int64)
+    rc, bad, counts, order = route_dev(keys, N.GLINT_ROUTE_CYCLIC, nparts, nkeys, gpu)
+    assert rc == N.GLINT_OK and bad == -1
+    owner = CyclicPartitioner.apply(nparts, nkeys).partition_indices(keys)
+    np.testing.assert_array_equal(counts, np.bincount(owner, minlength=nparts))
+    np.testing.assert_array_equal(order, np.argsort(owner, kind="stable"))
+
+
+def test_route_range_odd_partitioner_sizes(gpu):
+    """Large and small partitions (RangePartitioner.apply with N % P != 0) and P > N/2."""
+    for nparts, nkeys in [(7, 100), (60, 100), (100, 100), (3, 1 << 32)]:
+        rng = np.random.default_rng(nkeys)
+        keys = rng.integers(0, nkeys, 50_000).astype(np.int64)
+        keys[:nparts] = np.arange(nparts) * (nkeys // nparts)
+        rc, bad, counts, order = route_dev(keys, N.GLINT_ROUTE_RANGE, nparts, nkeys, gpu)
+        assert rc == N.GLINT_OK
+        c_ref, _, o_ref = O.bucket_range(keys, nparts, nkeys)
+        np.testing.assert_array_equal(counts, c_ref)
+        np.testing.assert_array_equal(order, o_ref)
+
+
+def test_route_out_of_range_reports_first_bad(gpu):
+    keys = np.arange(20_000, dtype=np.int64)
+    keys[12_345] = 20_000
+    keys[15_000] = -1
+    rc, bad, _, _ = route_dev(keys, N.GLINT_ROUTE_RANGE, 4, 20_000, gpu)
+    assert rc == N.GLINT_EOUTOFRANGE and bad == 12_345
+    rc, bad, _, _ = route_dev(keys, N.GLINT_ROUTE_CYCLIC, 4, 20_000, gpu)
+    assert rc == N.GLINT_EOUTOFRANGE and bad == 12_345
+    assert route_dev(keys, N.GLINT_ROUTE_RANGE, 8193, 20_000, gpu)[0] == N.GLINT_EINVAL
+
+
+# ---- the exchange layer with HBM shards: gloo world 2 (both ranks on this GPU), nccl world 1 --------
+@pytest.mark.parametrize("backend,world,case", [
+    ("gloo", 2, "vec_range"), ("gloo", 2, "vec_range_mps3"), ("gloo", 2, "vec_cyclic_mps2"),
+    ("gloo", 2, "vec_long_few_keys"), ("gloo", 2, "mat_range_mps2"),
+    ("nccl", 1, "vec_range_mps3"), ("nccl", 1, "mat_range")])
+def test_dist_exchange_on_gpu(gpu, backend, world, case):
+    import socket
+    import torch.multiprocessing as mp
+    import dist_workers
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(dist_workers.run_case, args=(world, port, backend, case, True), nprocs=world, join=True)

@@ -107,6 +107,25 @@ def main():
     sh.destroy()
     del keys, vals, out, rkeys
 
+    # ---- client routing: stable grouping of a 2^26-record batch by owning partition ----------------
+    m = 1 << 26
+    rkeys = torch.randint(0, 1 << 30, (m,), dtype=torch.int64, device=dev)
+    counts = torch.empty(4096, dtype=torch.int64, device=dev)
+    order = torch.empty(m, dtype=torch.int64, device=dev)
+    bad = C.c_int64()
+    for nparts in (8, 64, 4096):
+        fn = lambda: lib.glint_route_dev(rkeys.data_ptr(), m, N.GLINT_ROUTE_RANGE, nparts, 1 << 30,  # noqa: E731
+                                         counts.data_ptr(), order.data_ptr(), C.byref(bad), stream)
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            assert fn() == 0
+        dt = (time.perf_counter() - t0) / 5
+        emit(op="route_dev", nparts=nparts, records=m, ms=dt * 1e3, Grecords_per_s=m / dt / 1e9,
+             algorithmic_GBps=(8.0 * 2 + 8.0) * m / dt / 1e9,
+             note="keys read twice (histogram, scatter) + 8 B index written; includes the D2H status sync")
+    del rkeys, order
+
     # ---- cfg3: Zipf(1.1) sparse push with duplicates into a 2^28 shard -----------------------------
     sh = glint_amd.PartialVector(glint_amd.RangePartition(0, 0, n), "double", 0)
     h = sh.handle
