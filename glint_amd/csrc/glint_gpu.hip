@@ -465,6 +465,36 @@ __device__ __forceinline__ long long lane_value(long long x, int l) {
 }
 __device__ __forceinline__ int lane_value(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
+// End (exclusive) of the run of `ad` that starts at i in the sorted addresses: a 64-way gallop,
+// then 64-way refinement -- O(log64 len) dependent probe rounds instead of a compare per element.
+__device__ __forceinline__ i64 run_end(const u64* addr, i64 m, i64 i, u64 ad, int lane) {
+  i64 lo = i, hi;  // addr[lo] == ad; the end lies in (lo, hi]
+  for (i64 step = 1;; step *= 64) {
+    const i64 p = lo + (i64)(lane + 1) * step;
+    const int c = __popcll(__ballot(p < m && addr[p] == ad));  // equal probes form a prefix
+    if (c < 64) {
+      hi = lo + (i64)(c + 1) * step;
+      lo += (i64)c * step;
+      break;
+    }
+    lo += 64 * step;
+  }
+  if (hi > m) hi = m;
+  while (hi - lo > 1) {
+    const i64 step = (hi - lo + 63) / 64;
+    const i64 p = lo + (i64)(lane + 1) * step;
+    const int c = __popcll(__ballot(p < hi && addr[p] == ad));
+    const i64 nh = lo + (i64)(c + 1) * step;
+    lo += (i64)c * step;
+    if (nh < hi) hi = nh;
+  }
+  return lo + 1;
+}
+
+// One wave per long run: the value loads run kDetBatch x 64 elements ahead of the strictly
+// sequential add chain (a dependent v_add per element, operands from v_readlane), so the fold is
+// bound by the add latency, not by HBM latency.
+constexpr int kDetBatch = 8;
 template <typename V>
 __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, const V* val, i64 m,
                                                              const u32* long_count, const u32* long_list, V* data) {
@@ -475,16 +505,34 @@ __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, co
   for (u32 w = w0; w < cnt; w += nw) {
     const i64 i = long_list[w];
     const u64 ad = addr[i];
+    const i64 e = run_end(addr, m, i, ad, lane);
     V acc = data[ad];
-    for (i64 base = i;; base += 64) {
-      // 64 consecutive values per load (coalesced); the adds stay strictly sequential
-      const i64 q = base + lane;
-      const bool in = q < m && addr[q] == ad;
-      const V x = in ? val[q] : V(0);
-      const u64 msk = __ballot(in);
-      const int len = msk == ~0ull ? 64 : __ffsll((long long)~msk) - 1;  // the run is contiguous
-      for (int l = 0; l < len; ++l) acc = vadd(acc, lane_value(x, l));
-      if (len < 64) break;
+    V x[kDetBatch];
+#pragma unroll
+    for (int j = 0; j < kDetBatch; ++j) {
+      const i64 q = i + j * 64 + lane;
+      x[j] = q < e ? val[q] : V(0);
+    }
+    for (i64 base = i; base < e; base += kDetBatch * 64) {
+      V y[kDetBatch];
+      const i64 nb = base + kDetBatch * 64;
+#pragma unroll
+      for (int j = 0; j < kDetBatch; ++j) {  // next batch in flight while this one is folded
+        const i64 q = nb + j * 64 + lane;
+        y[j] = q < e ? val[q] : V(0);
+      }
+#pragma unroll
+      for (int j = 0; j < kDetBatch; ++j) {
+        const i64 left = e - (base + j * 64);
+        if (left >= 64) {
+#pragma unroll
+          for (int l = 0; l < 64; ++l) acc = vadd(acc, lane_value(x[j], l));
+        } else {
+          for (int l = 0; l < (int)left; ++l) acc = vadd(acc, lane_value(x[j], l));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kDetBatch; ++j) x[j] = y[j];
     }
     if (lane == 0) data[ad] = acc;
   }

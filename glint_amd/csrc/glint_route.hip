@@ -9,8 +9,9 @@
 //                  partition-major so that one exclusive scan yields every (partition, block) offset;
 //   (rocPRIM exclusive scan over the histogram)
 //   route_scatter  each block writes its record indices to their partition's range, in order: a
-//                  wave ranks its 64 records per owner with ballots, waves and 256-record rounds are
-//                  chained through per-owner counters in LDS -- the result is stable.
+//                  wave finds its same-owner lanes with one ballot per owner bit, the waves of a
+//                  256-record round then claim slots in wave order from per-owner LDS counters --
+//                  the result is stable.
 // Out-of-range keys (IndexOutOfBoundsException in the reference, :30-32) are reported as the first
 // bad record index; the routing of the other records is unaffected.
 #include <hip/hip_runtime.h>
@@ -26,10 +27,9 @@ typedef int64_t i64;
 typedef uint64_t u64;
 typedef unsigned int u32;
 
-constexpr int kRT = 256;                // threads per block
-constexpr int kRPerThread = 16;         // records per thread per block chunk
-constexpr int kRChunk = kRT * kRPerThread;  // 4096 records per block
-constexpr int kMaxParts = 8192;         // LDS counters (32 KiB)
+constexpr int kRT = 256;         // threads per block
+constexpr int kMinRounds = 16;   // a block's chunk: >= 16 rounds of 256 records (4096)
+constexpr int kMaxParts = 8192;  // LDS counters (32 KiB)
 
 struct RangeDesc {
   i64 nkeys;      // RangePartitioner.size / CyclicPartitioner.keys
@@ -52,81 +52,74 @@ __device__ __forceinline__ int32_t owner_of(const RangeDesc& d, i64 key) {
   return o < d.nparts ? o : -1;
 }
 
-__global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, i64 n, RangeDesc d,
-                                                  u32* __restrict__ hist, i64 nblocks, u64* __restrict__ bad) {
+// Lanes of the wave whose owner equals this lane's: one ballot per owner bit (owners < 2^nbits,
+// the sentinel `nparts` included) instead of a loop over the distinct owners of the wave.
+__device__ __forceinline__ u64 match_owner(int32_t o, int nbits) {
+  u64 m = ~0ull;
+  for (int k = 0; k < nbits; ++k) {
+    const bool bit = (o >> k) & 1;
+    const u64 b = __ballot(bit);
+    m &= bit ? b : ~b;
+  }
+  return m;
+}
+
+// The block's chunk is `rounds` x 256 consecutive records; owners outside [0, nparts) count as bad.
+__global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, i64 n, RangeDesc d, int nbits,
+                                                  int rounds, u32* __restrict__ hist, i64 nblocks,
+                                                  u64* __restrict__ bad) {
   __shared__ u32 h[kMaxParts];
+  const int lane = threadIdx.x & 63;
   for (int p = threadIdx.x; p < d.nparts; p += kRT) h[p] = 0;
   __syncthreads();
-  const i64 base = (i64)blockIdx.x * kRChunk;
-  for (int q = threadIdx.x; q < kRChunk; q += kRT) {
-    const i64 i = base + q;
-    if (i >= n) break;
-    const int32_t o = owner_of(d, keys[i]);
-    if (o < 0) { atomicMax(bad, ~(u64)i); continue; }
-    atomicAdd(&h[o], 1u);
+  const i64 base = (i64)blockIdx.x * rounds * kRT;
+  for (int r = 0; r < rounds; ++r) {
+    const i64 i = base + (i64)r * kRT + threadIdx.x;
+    int32_t o = d.nparts;  // sentinel: past the end
+    if (i < n) {
+      o = owner_of(d, keys[i]);
+      if (o < 0) { atomicMax(bad, ~(u64)i); o = d.nparts; }
+    }
+    const u64 m = match_owner(o, nbits);
+    // the group's lowest lane adds the group size: one LDS atomic per distinct owner per wave
+    if (o < d.nparts && (m & ((1ull << lane) - 1)) == 0) atomicAdd(&h[o], (u32)__popcll(m));
   }
   __syncthreads();
   for (int p = threadIdx.x; p < d.nparts; p += kRT) hist[(i64)p * nblocks + blockIdx.x] = h[p];  // partition-major
 }
 
-__global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ keys, i64 n, RangeDesc d,
-                                                     const u32* __restrict__ offs, i64 nblocks,
+__global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ keys, i64 n, RangeDesc d, int nbits,
+                                                     int rounds, const u32* __restrict__ offs, i64 nblocks,
                                                      i64* __restrict__ order) {
-  __shared__ u32 cnt[kMaxParts];       // records of each owner already placed by this block
-  __shared__ u32 wave_cnt[4][64];      // per round: per wave, count of each of its (<= 64) owners
-  __shared__ int32_t wave_own[4][64];  // the owners each wave saw this round
-  __shared__ int wave_n[4];
+  __shared__ u32 cnt[kMaxParts];  // records of each owner this block has placed so far
+  __shared__ u32 grp_base[kRT];   // per group leader: the group's first slot within its owner
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int p = threadIdx.x; p < d.nparts; p += kRT) cnt[p] = 0;
   __syncthreads();
-  const i64 base = (i64)blockIdx.x * kRChunk;
-  for (int round = 0; round < kRPerThread; ++round) {
-    const i64 i = base + (i64)round * kRT + threadIdx.x;  // 256 consecutive records per round
-    const int32_t o = i < n ? owner_of(d, keys[i]) : -1;
-    // rank among the same-owner lanes of this wave, lane order = record order
-    u64 pending = __ballot(o >= 0);
-    int my_rank = 0, nslots = 0;
-    while (pending) {
-      const int leader = __ffsll((long long)pending) - 1;
-      const int32_t lo = __shfl(o, leader);
-      const u64 m = __ballot(o == lo);
-      if (o == lo) {
-        my_rank = __popcll(m & ((1ull << lane) - 1));
+  const i64 base = (i64)blockIdx.x * rounds * kRT;
+  for (int r = 0; r < rounds; ++r) {
+    const i64 i = base + (i64)r * kRT + threadIdx.x;  // 256 consecutive records per round
+    int32_t o = d.nparts;
+    if (i < n) {
+      o = owner_of(d, keys[i]);
+      if (o < 0) o = d.nparts;
+    }
+    const u64 m = match_owner(o, nbits);
+    const u64 below = m & ((1ull << lane) - 1);
+    const bool leader = below == 0 && o < d.nparts;
+    // waves claim their slots in order (wave 0 holds the round's earliest records): stable
+    for (int w = 0; w < kRT / 64; ++w) {
+      if (wid == w && leader) {
+        grp_base[threadIdx.x] = cnt[o];
+        cnt[o] += (u32)__popcll(m);
       }
-      if (lane == 0) { wave_own[wid][nslots] = lo; wave_cnt[wid][nslots] = (u32)__popcll(m); }
-      ++nslots;
-      pending &= ~m;
+      __syncthreads();
     }
-    if (lane == 0) wave_n[wid] = nslots;
-    __syncthreads();
-    if (o >= 0) {
-      // earlier waves' records of the same owner in this round come first
-      u32 before = cnt[o];
-      for (int w = 0; w < wid; ++w)
-        for (int s = 0; s < wave_n[w]; ++s)
-          if (wave_own[w][s] == o) before += wave_cnt[w][s];
-      order[(i64)offs[(i64)o * nblocks + blockIdx.x] + before + my_rank] = i;
+    if (o < d.nparts) {
+      const int lead = __ffsll((long long)m) - 1;
+      order[(i64)offs[(i64)o * nblocks + blockIdx.x] + grp_base[wid * 64 + lead] + __popcll(below)] = i;
     }
-    __syncthreads();
-    // advance the block's per-owner counters by this round's totals (one writer per owner)
-    if (threadIdx.x < 64 * 4) {
-      const int w = threadIdx.x >> 6, s = threadIdx.x & 63;
-      if (s < wave_n[w]) {
-        const int32_t ow = wave_own[w][s];
-        bool first = true;  // the first wave that saw this owner sums every wave's count
-        for (int w2 = 0; w2 < w; ++w2)
-          for (int s2 = 0; s2 < wave_n[w2]; ++s2)
-            if (wave_own[w2][s2] == ow) first = false;
-        if (first) {
-          u32 tot = 0;
-          for (int w2 = w; w2 < 4; ++w2)
-            for (int s2 = 0; s2 < wave_n[w2]; ++s2)
-              if (wave_own[w2][s2] == ow) tot += wave_cnt[w2][s2];
-          cnt[ow] += tot;
-        }
-      }
-    }
-    __syncthreads();
+    __syncthreads();  // grp_base is rewritten next round
   }
 }
 
@@ -163,7 +156,12 @@ extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t
   d.nkeys = nkeys;
   d.nparts = nparts;
   d.cyclic = kind == GLINT_ROUTE_CYCLIC;
-  const i64 nblocks = std::max<i64>(1, (n + kRChunk - 1) / kRChunk);
+  // chunk per block grows with nparts so the (partition x block) histogram stays <= n/4 entries
+  const int rounds = std::max<int>(kMinRounds, (4 * nparts + kRT - 1) / kRT);
+  const i64 chunk = (i64)rounds * kRT;
+  const i64 nblocks = std::max<i64>(1, (n + chunk - 1) / chunk);
+  int nbits = 1;
+  while ((1 << nbits) <= nparts) ++nbits;  // owners and the sentinel nparts fit in nbits
   std::lock_guard<std::mutex> lk(g_route_mu);
   const size_t hist_bytes = (size_t)nparts * nblocks * 4;
   size_t scan_bytes = 0;
@@ -187,11 +185,11 @@ extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t
   if (n == 0) {
     if (hipMemsetAsync(counts, 0, (size_t)nparts * 8, st) != hipSuccess) return GLINT_EDEVICE;
   } else {
-    route_hist<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, hist, nblocks, bad);
+    route_hist<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, nbits, rounds, hist, nblocks, bad);
     if (rocprim::exclusive_scan(scan_tmp, scan_bytes, hist, offs, 0u, (size_t)nparts * nblocks,
                                 rocprim::plus<u32>(), st) != hipSuccess)
       return GLINT_EDEVICE;
-    route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, offs, nblocks, order);
+    route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, nbits, rounds, offs, nblocks, order);
     route_counts<<<(unsigned)((nparts + 255) / 256), 256, 0, st>>>(offs, hist, nblocks, nparts, counts);
   }
   // first bad record: enc = ~index (0 = none); returned through the host word *first_bad

@@ -97,7 +97,7 @@ def _vector_case(nkeys, mps, partitioner, dtype, n=3000):
         vec = client.vector(nkeys, dtype, modelsPerServer=mps, createPartitioner=partitioner)
         for step in range(2):
             k, v = _batch(1000 * step + rank, n + 37 * rank, nkeys, np_dtype)
-            vec.push(torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev))
+            vec.push(torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev), deterministic=True)
         # oracle replay: all ranks' batches in rank order, step by step
         ref = O.OracleVector(O.part_range(0, nkeys), resolve_dtype(dtype)[0])
         for step in range(2):
@@ -136,7 +136,7 @@ def _matrix_case(nrows, ncols, mps, dtype="double", n=2500):
             vals = rng.uniform(-1, 1, n).astype(np_dtype)
             if r == rank:
                 mat.push(torch.from_numpy(rows).to(dev), torch.from_numpy(cols).to(dev),
-                         torch.from_numpy(vals).to(dev))
+                         torch.from_numpy(vals).to(dev), deterministic=True)
             assert ref.update(rows, cols, vals) == -1
         rng = np.random.default_rng(900 + rank)
         qr = rng.integers(0, nrows, 700).astype(np.int64)
