@@ -491,10 +491,38 @@ __device__ __forceinline__ i64 run_end(const u64* addr, i64 m, i64 i, u64 ad, in
   return lo + 1;
 }
 
-// One wave per long run: the value loads run kDetBatch x 64 elements ahead of the strictly
-// sequential add chain (a dependent v_add per element, operands from v_readlane), so the fold is
-// bound by the add latency, not by HBM latency.
-constexpr int kDetBatch = 8;
+// One wave per long run. The fold is one strictly sequential chain of adds, so its speed is the
+// dependent v_add latency: the values are loaded *transposed* -- lane L holds kDetK consecutive
+// values of the run in VGPRs -- and lane L alone (exec = one lane) folds them into the running sum
+// with register operands, then hands the sum to lane L+1 (v_readlane). Two buffers alternate so
+// the next 64 x kDetK values are in flight while the current ones are folded. Padding is -0.0, the
+// exact identity of IEEE addition (x + -0.0 == x for every x, signed zeros included).
+constexpr int kDetK = 32;
+template <typename V>
+__device__ __forceinline__ void det_load(V (&x)[kDetK], const V* val, i64 start, i64 e, int lane) {
+  const i64 q0 = start + (i64)lane * kDetK;
+#pragma unroll
+  for (int j = 0; j < kDetK; ++j) {
+    const i64 q = q0 + j;
+    const V v = val[q < e ? q : e - 1];  // clamped, branch-free: all loads issue back to back
+    x[j] = q < e ? v : V(-0.0);
+  }
+}
+template <typename V>
+__device__ __forceinline__ V det_fold(const V (&x)[kDetK], V acc, i64 start, i64 e, int lane) {
+  if (start >= e) return acc;
+  const i64 left = e - start;
+  const int nl = left >= 64 * kDetK ? 64 : (int)((left + kDetK - 1) / kDetK);
+  for (int L = 0; L < nl; ++L) {
+    if (lane == L) {
+#pragma unroll
+      for (int j = 0; j < kDetK; ++j) acc = vadd(acc, x[j]);
+    }
+    acc = lane_value(acc, L);
+  }
+  return acc;
+}
+
 template <typename V>
 __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, const V* val, i64 m,
                                                              const u32* long_count, const u32* long_list, V* data) {
@@ -502,37 +530,19 @@ __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, co
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const u32 nw = gridDim.x * (kTPB / 64);
   const u32 cnt = *long_count;
+  constexpr i64 kB = 64 * kDetK;
   for (u32 w = w0; w < cnt; w += nw) {
     const i64 i = long_list[w];
     const u64 ad = addr[i];
     const i64 e = run_end(addr, m, i, ad, lane);
     V acc = data[ad];
-    V x[kDetBatch];
-#pragma unroll
-    for (int j = 0; j < kDetBatch; ++j) {
-      const i64 q = i + j * 64 + lane;
-      x[j] = q < e ? val[q] : V(0);
-    }
-    for (i64 base = i; base < e; base += kDetBatch * 64) {
-      V y[kDetBatch];
-      const i64 nb = base + kDetBatch * 64;
-#pragma unroll
-      for (int j = 0; j < kDetBatch; ++j) {  // next batch in flight while this one is folded
-        const i64 q = nb + j * 64 + lane;
-        y[j] = q < e ? val[q] : V(0);
-      }
-#pragma unroll
-      for (int j = 0; j < kDetBatch; ++j) {
-        const i64 left = e - (base + j * 64);
-        if (left >= 64) {
-#pragma unroll
-          for (int l = 0; l < 64; ++l) acc = vadd(acc, lane_value(x[j], l));
-        } else {
-          for (int l = 0; l < (int)left; ++l) acc = vadd(acc, lane_value(x[j], l));
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kDetBatch; ++j) x[j] = y[j];
+    V A[kDetK], B[kDetK];
+    det_load(A, val, i, e, lane);
+    for (i64 base = i; base < e; base += 2 * kB) {
+      det_load(B, val, base + kB, e, lane);
+      acc = det_fold(A, acc, base, e, lane);
+      det_load(A, val, base + 2 * kB, e, lane);
+      acc = det_fold(B, acc, base + kB, e, lane);
     }
     if (lane == 0) data[ad] = acc;
   }
