@@ -13,6 +13,7 @@
 #include "../../include/glint_gpu.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <mutex>
 #include <vector>
@@ -312,6 +313,9 @@ __device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta) {
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i64* __restrict__ desc) {
   const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.hint)  // for the host's next push: how unordered was this one?
+    __hip_atomic_store(a.hint, brk == 0u ? 0ull : (u64)(a.n - (i64)(a.ntiles - brk) * kTile), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   if (brk == 0u && a.ctl->nonaffine == 0u) {
     const i64 delta = desc[0];  // tile 0 starts the run at record 0
     if ((delta & 1) == 0) apply_sweep<V, true>(a, delta);
@@ -404,6 +408,140 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
         hk[s] = kEmpty;
         hv[s] = V(0);
       }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// binned push: the unordered tail of a large push, without per-record global atomics
+// ------------------------------------------------------------------------------------------------
+// Element-granular device atomics run at ~17 G/s here (each lane's add is its own 64-B memory-side
+// request). A large unordered tail is instead binned by shard slab -- a stable rocPRIM radix sort of
+// (u32 element address, value) on the address bits above kSlabBits -- and each slab's records are
+// summed in LDS (ds_add) and written back with one coalesced read-modify-write of the slab's touched
+// element pairs. Slabs with more than kBinItem records are split into several work items, which
+// then flush with device atomics, so a hot slab never serialises on one workgroup.
+constexpr int kSlabBits = 13;
+constexpr int kSlab = 1 << kSlabBits;  // elements accumulated in LDS per work item (64 KiB of Double)
+constexpr i64 kBinItem = 16384;        // records per work item at most
+constexpr u32 kBinSentinel = 0xFFFFFFFFu;
+
+// u32 element address of every record from r0 on (records before r0 and rejected ones: sentinel);
+// from_break: r0 is the start of push_check's unordered tail, otherwise 0
+template <bool MAT>
+__global__ __launch_bounds__(kTPB) void bin_prepare_kernel(const i64* keys, const int32_t* cols, i64 n, PartDesc part,
+                                                           const LaunchCtl* ctl, u32 ntiles, int from_break,
+                                                           u32* __restrict__ addr, ErrState* err) {
+  i64 r0 = 0;
+  if (from_break) {
+    const u32 brk = ctl->brk_enc;
+    r0 = brk == 0u ? n : (i64)(ntiles - brk) * kTile;
+  }
+  for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += (i64)gridDim.x * kTPB) {
+    u32 out = kBinSentinel;
+    if (i >= r0) {
+      i64 ad;
+      if (rec_addr<MAT>(part, keys[i], MAT ? cols[i] : 0, ad)) out = (u32)ad;
+      else record_error(err, i);
+    }
+    addr[i] = out;
+  }
+}
+
+__device__ __forceinline__ u32 slab_of(u32 a, u32 mask) { return (a >> kSlabBits) & mask; }
+
+// per slab s < nslabs: start[s] = first sorted record of slab s, items[s] = its work items;
+// start[nslabs] = n, items[nslabs] = 0 (so that an exclusive scan of items ends in the total)
+__global__ void bin_bounds_kernel(const u32* __restrict__ addr, i64 n, u32 nslabs, u32 mask, i64* __restrict__ start,
+                                  u32* __restrict__ items) {
+  for (i64 s = (i64)blockIdx.x * blockDim.x + threadIdx.x; s <= (i64)nslabs; s += (i64)gridDim.x * blockDim.x) {
+    i64 lo = 0, hi = n;  // first record with slab_of >= s
+    while (lo < hi) {
+      const i64 mid = (lo + hi) >> 1;
+      if (slab_of(addr[mid], mask) < (u32)s) lo = mid + 1;
+      else hi = mid;
+    }
+    start[s] = lo;
+    if (s == (i64)nslabs) {
+      items[s] = 0;
+    } else {
+      i64 lo2 = lo, hi2 = n;  // first record with slab_of > s
+      while (lo2 < hi2) {
+        const i64 mid = (lo2 + hi2) >> 1;
+        if (slab_of(addr[mid], mask) <= (u32)s) lo2 = mid + 1;
+        else hi2 = mid;
+      }
+      items[s] = (u32)((lo2 - lo + kBinItem - 1) / kBinItem);
+    }
+  }
+}
+
+template <typename V>
+__global__ __launch_bounds__(kTPB) void bin_apply_kernel(const u32* __restrict__ addr, const V* __restrict__ val,
+                                                         const i64* __restrict__ start,
+                                                         const u32* __restrict__ item_off, u32 nslabs, i64 elems,
+                                                         V* __restrict__ data) {
+  typedef typename Vec2<V>::T V2;
+  __shared__ V acc[kSlab];
+  __shared__ u32 bits[kSlab / 32];
+  constexpr int kPairsPerThread = kSlab / 2 / kTPB;
+  const int tid = threadIdx.x;
+  const u32 total = item_off[nslabs];
+  for (u32 it = blockIdx.x; it < total; it += gridDim.x) {
+    u32 lo = 0, hi = nslabs;  // the slab whose items cover `it`: item_off[lo] <= it < item_off[lo + 1]
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) >> 1;
+      if (item_off[mid] <= it) lo = mid;
+      else hi = mid;
+    }
+    const u32 slab = lo;
+    const u32 k = it - item_off[slab];
+    const bool exclusive = item_off[slab + 1] - item_off[slab] == 1u;
+    const i64 r_lo = start[slab] + (i64)k * kBinItem;
+    const i64 r_hi = min(start[slab + 1], r_lo + kBinItem);
+    for (int e = tid; e < kSlab; e += kTPB) acc[e] = V(0);
+    for (int w = tid; w < kSlab / 32; w += kTPB) bits[w] = 0u;
+    __syncthreads();
+    for (i64 j = r_lo + tid; j < r_hi; j += kTPB) {
+      const u32 ad = addr[j];
+      if (ad == kBinSentinel) continue;
+      const u32 e = ad & (kSlab - 1);
+      lds_add(&acc[e], val[j]);
+      atomicOr(&bits[e >> 5], 1u << (e & 31));
+    }
+    __syncthreads();
+    V* const sbase = data + (i64)slab * kSlab;
+    if (exclusive) {
+      // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair
+      // instead (one cached line), so all loads issue back to back without a branch
+      V2 d[kPairsPerThread];
+      u32 t[kPairsPerThread];
+#pragma unroll
+      for (int q = 0; q < kPairsPerThread; ++q) {
+        const int e0 = 2 * (tid + q * kTPB);
+        const i64 g = (i64)slab * kSlab + e0;
+        t[q] = (bits[e0 >> 5] >> (e0 & 31)) & 3u;
+        const bool vec = t[q] != 0u && g + 1 < elems;
+        d[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
+      }
+#pragma unroll
+      for (int q = 0; q < kPairsPerThread; ++q) {
+        if (t[q] == 0u) continue;
+        const int e0 = 2 * (tid + q * kTPB);
+        const i64 g = (i64)slab * kSlab + e0;
+        if (g + 1 < elems) {
+          V2 r = d[q];
+          if (t[q] & 1u) r.x = vadd(r.x, acc[e0]);
+          if (t[q] & 2u) r.y = vadd(r.y, acc[e0 + 1]);
+          *reinterpret_cast<V2*>(sbase + e0) = r;
+        } else {  // the shard's last element, odd count
+          sbase[e0] = vadd(sbase[e0], acc[e0]);
+        }
+      }
+    } else {
+      for (int e = tid; e < kSlab; e += kTPB)
+        if ((bits[e >> 5] >> (e & 31)) & 1u) gadd(sbase + e, acc[e]);
     }
     __syncthreads();
   }
@@ -657,6 +795,10 @@ struct glint_shard {
   size_t scratch_bytes = 0;
   void* d_det = nullptr;
   size_t det_bytes = 0;
+  void* d_bin = nullptr;  // binned-push scratch
+  size_t bin_bytes = 0;
+  u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
+  u64* d_hint = nullptr;
   i64 last_bad = -1;
   // kernel timing (glint_prof_*): HIP event pairs recorded on the launch stream, summed lazily
   bool prof = false;
@@ -820,6 +962,62 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
   return GLINT_OK;
 }
 
+// The binned tail pipeline over the whole push (records before push_check's break are masked on
+// the device, so no host round trip is needed): prepare -> radix sort by slab -> bounds -> item
+// scan -> LDS slab apply.
+template <typename V, bool MAT>
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
+  const i64 n = a.n;
+  if (n >= ((i64)1 << 32) || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
+  int end_bit = kSlabBits + 1;
+  while (end_bit < 32 && ((i64)1 << end_bit) < s->elems) ++end_bit;
+  const u32 nslabs = 1u << (end_bit - kSlabBits);
+  const u32 mask = nslabs - 1u;
+  size_t sort_bytes = 0, scan_bytes = 0;
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, sort_bytes, (u32*)nullptr, (u32*)nullptr, (const V*)nullptr, (V*)nullptr,
+                                   (size_t)n, kSlabBits, end_bit, st));
+  HIPCHK(rocprim::exclusive_scan(nullptr, scan_bytes, (u32*)nullptr, (u32*)nullptr, 0u, (size_t)nslabs + 1,
+                                 rocprim::plus<u32>(), st));
+  const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(V));
+  const size_t b_s = pad256(((size_t)nslabs + 1) * 8), b_i = pad256(((size_t)nslabs + 1) * 4);
+  const size_t need = 2 * b_a + b_v + b_s + 2 * b_i + pad256(sort_bytes) + pad256(scan_bytes);
+  int rc = grow(&s->d_bin, &s->bin_bytes, need);
+  if (rc) return rc;
+  char* p = (char*)s->d_bin;
+  u32* addr_in = (u32*)p;
+  u32* addr_out = (u32*)(p + b_a);
+  V* val_out = (V*)(p + 2 * b_a);
+  i64* start = (i64*)(p + 2 * b_a + b_v);
+  u32* items = (u32*)(p + 2 * b_a + b_v + b_s);
+  u32* item_off = (u32*)(p + 2 * b_a + b_v + b_s + b_i);
+  void* sort_tmp = p + 2 * b_a + b_v + b_s + 2 * b_i;
+  void* scan_tmp = (char*)sort_tmp + pad256(sort_bytes);
+  ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
+  bin_prepare_kernel<MAT><<<grid_for(n, kTPB, (i64)s->cus * 8), kTPB, 0, st>>>(
+      a.keys, a.cols, n, a.part, a.ctl, a.ntiles, from_break ? 1 : 0, addr_in, a.err);
+  HIPCHK(hipGetLastError());
+  HIPCHK(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, addr_in, addr_out, a.vals, val_out, (size_t)n, kSlabBits,
+                                   end_bit, st));
+  bin_bounds_kernel<<<grid_for((i64)nslabs + 1, 256, 4096), 256, 0, st>>>(addr_out, n, nslabs, mask, start, items);
+  HIPCHK(hipGetLastError());
+  HIPCHK(rocprim::exclusive_scan(scan_tmp, scan_bytes, items, item_off, 0u, (size_t)nslabs + 1, rocprim::plus<u32>(),
+                                 st));
+  const i64 max_items = (i64)nslabs + (n + kBinItem - 1) / kBinItem;
+  bin_apply_kernel<V><<<(unsigned)std::min<i64>(max_items, (i64)s->cus * 8), kTPB, 0, st>>>(
+      addr_out, val_out, start, item_off, nslabs, s->elems, a.data);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
+// GLINT_BINNED: 0 = never bin, 1 = bin every large push, unset = bin when the previous push on the
+// shard left a large unordered tail (read from the host-mapped word push_apply writes)
+int binned_mode() {
+  const char* e = getenv("GLINT_BINNED");
+  if (!e || !*e) return -1;
+  return atoi(e) != 0 ? 1 : 0;
+}
+constexpr i64 kBinMin = (i64)1 << 20;  // records: below this the LDS-hash scatter wins
+
 template <typename V, bool MAT>
 int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void* vals, i64 n, int flags,
                 hipStream_t st) {
@@ -834,6 +1032,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.part = s->part;
   a.err = s->d_err;
   a.elems = s->elems;
+  a.hint = s->d_hint;
   const i64 ntiles = (n + kTile - 1) / kTile;
   if (ntiles >= (i64)0xFFFFFFF0ll) return GLINT_EINVAL;
   a.ntiles = (u32)ntiles;
@@ -846,6 +1045,12 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.ctl = (LaunchCtl*)s->d_ctl;
   i64* desc = (i64*)((char*)s->d_ctl + 256);
 
+  const int bmode = binned_mode();
+  const bool unordered = (flags & GLINT_PUSH_UNORDERED) != 0;
+  const i64 last_tail = s->h_hint ? (i64)__atomic_load_n(s->h_hint, __ATOMIC_RELAXED) : 0;
+  const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
+                      (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
+  if (binned && unordered) return push_binned<V, MAT>(s, a, false, st);
   if (!vec_ok) {  // unaligned caller pointers: the scalar-load scatter for everything
     if (det) return push_det_tail<V, MAT>(s, a, false, st);
     const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
@@ -870,6 +1075,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     HIPCHK(hipGetLastError());
   }
   if (det) return push_det_tail<V, MAT>(s, a, true, st);
+  if (binned) return push_binned<V, MAT>(s, a, true, st);
   const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
   ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
   push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, 0);
@@ -976,7 +1182,8 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     s->cus = prop.multiProcessorCount;
   HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  const size_t bytes = std::max<size_t>((size_t)s->elems * s->vsize, 16);
+  // +16 B: a slab-wide pair load may touch one element past an odd-sized shard's end
+  const size_t bytes = (size_t)s->elems * s->vsize + 16;
   if (hipMalloc(&s->data, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return GLINT_ENOMEM;
@@ -985,6 +1192,14 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
     (void)hipGetLastError();
     return GLINT_ENOMEM;
   }
+  if (hipHostMalloc((void**)&s->h_hint, 64, hipHostMallocMapped) == hipSuccess) {
+    *s->h_hint = 0;
+    if (hipHostGetDevicePointer((void**)&s->d_hint, s->h_hint, 0) != hipSuccess) s->d_hint = nullptr;
+  } else {
+    s->h_hint = nullptr;
+  }
+  (void)hipGetLastError();
+  if (!s->d_hint && s->h_hint) { (void)hipHostFree(s->h_hint); s->h_hint = nullptr; }
   HIPCHK(hipMemsetAsync(s->data, 0, bytes, s->stream));  // new Array[V](size) is zeroed
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
@@ -1002,6 +1217,8 @@ void free_shard(glint_shard* s) {
     if (s->d_ctl) (void)hipFree(s->d_ctl);
     if (s->d_scratch) (void)hipFree(s->d_scratch);
     if (s->d_det) (void)hipFree(s->d_det);
+    if (s->d_bin) (void)hipFree(s->d_bin);
+    if (s->h_hint) (void)hipHostFree(s->h_hint);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     (void)hipGetLastError();
   }

@@ -84,6 +84,7 @@ struct PushArgs {
   LaunchCtl* ctl;
   u32 ntiles;
   ErrState* err;
+  u64* hint;  // host-mapped word: the unordered-tail size push_apply saw (binned-path heuristic)
 };
 
 }  // namespace glint

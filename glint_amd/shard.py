@@ -60,6 +60,10 @@ def check(rc: int, handle=None) -> None:
     raise ValueError(N.strerror(rc))
 
 
+def _flags(deterministic: bool, unordered: bool) -> int:
+    return (N.GLINT_PUSH_DETERMINISTIC if deterministic else 0) | (N.GLINT_PUSH_UNORDERED if unordered else 0)
+
+
 def _is_torch_cuda(x) -> bool:
     return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
 
@@ -152,9 +156,10 @@ class PartialVector(_Shard):
     def __init__(self, partition: Partition, dtype="double", device: int = 0):
         super().__init__(partition, dtype, 0, device)
 
-    def update(self, keys, values, deterministic: bool = False, sync: bool = True) -> bool:
-        """PartialVector.update (PartialVector.scala:35-43): data(globalToLocal(k)) += v."""
-        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+    def update(self, keys, values, deterministic: bool = False, sync: bool = True, unordered: bool = False) -> bool:
+        """PartialVector.update (PartialVector.scala:35-43): data(globalToLocal(k)) += v.
+        ``unordered`` is a performance hint (GLINT_PUSH_UNORDERED): skip the order check, bin by slab."""
+        flags = _flags(deterministic, unordered)
         if _is_torch_cuda(keys):
             import torch
             self._check_dev(keys, values)
@@ -222,9 +227,10 @@ class PartialMatrix(_Shard):
         super().__init__(partition, dtype, int(cols), device)
         self.rows = self.size
 
-    def update(self, rows, cols, values, deterministic: bool = False, sync: bool = True) -> bool:
+    def update(self, rows, cols, values, deterministic: bool = False, sync: bool = True,
+               unordered: bool = False) -> bool:
         """PartialMatrix.update (PartialMatrix.scala:74-83)."""
-        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+        flags = _flags(deterministic, unordered)
         if _is_torch_cuda(rows):
             self._check_dev(rows, cols, values)
             rc = self.lib.glint_mat_push_dev(self.handle, rows.data_ptr(), cols.data_ptr(), values.data_ptr(),

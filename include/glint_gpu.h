@@ -47,7 +47,13 @@ enum glint_push_flags {
    * Float/Double even when keys repeat (PartialVector.scala:37-41). Without it, repeated keys in
    * a push are summed by device atomics in arbitrary order (<= 1e-6 relative for Double; Int and
    * Long are exact either way). Unique-key pushes are bit-exact in both modes. */
-  GLINT_PUSH_DETERMINISTIC = 1
+  GLINT_PUSH_DETERMINISTIC = 1,
+  /* Hint: the keys are in no particular order. The push skips the order check and sums the records
+   * per shard slab in LDS (radix binning + one read-modify-write per touched element pair)
+   * instead of per-record device atomics. Results as GLINT_PUSH_DEFAULT. Without the hint, a
+   * large push takes this path by itself when the shard's previous push was unordered
+   * (environment GLINT_BINNED=0 disables that, =1 forces it for pushes >= 2^20 records). */
+  GLINT_PUSH_UNORDERED = 2
 };
 
 typedef struct glint_shard* glint_shard_t;
@@ -165,7 +171,8 @@ enum glint_kernel_id {
   GLINT_K_MAT_PULL = 3,
   GLINT_K_MAT_PULL_ROWS = 4,
   GLINT_K_PUSH_CHECK = 5,   /* order / affinity check over the keys in front of push_apply */
-  GLINT_K_COUNT = 6
+  GLINT_K_PUSH_BINNED = 6,  /* the binned unordered-push pipeline (prepare, sort, bounds, scan, apply) */
+  GLINT_K_COUNT = 7
 };
 int glint_prof_enable(glint_shard_t shard, int on);
 int glint_prof_read(glint_shard_t shard, int kernel_id, double* total_ms, int64_t* launches);

@@ -407,3 +407,107 @@ def test_dist_exchange_on_gpu(gpu, backend, world, case):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(dist_workers.run_case, args=(world, port, backend, case, True), nprocs=world, join=True)
+
+
+# ---- binned unordered push (GLINT_PUSH_UNORDERED, and the adaptive switch) ----------------------------
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("pattern", ["permutation", "uniform", "zipf", "hot_slab", "with_prefix"])
+def test_binned_push(gpu, dtype, pattern):
+    rng = np.random.default_rng(zlib.crc32(f"binned/{dtype}/{pattern}".encode()))
+    start, size = 5_000_000, 1_000_003  # 123 slabs, the last one partial (odd element count)
+    part = RangePartition(1, start, start + size)
+    if pattern == "permutation":
+        keys = rng.permutation(size).astype(np.int64)
+    elif pattern == "uniform":
+        keys = rng.integers(0, size, 700_000).astype(np.int64)
+    elif pattern == "zipf":
+        keys = np.minimum(rng.zipf(1.2, 600_000) - 1, size - 1).astype(np.int64)
+        keys = rng.permutation(size)[keys].astype(np.int64)
+    elif pattern == "hot_slab":  # one slab with > kBinItem records: split items flush with atomics
+        keys = np.concatenate([rng.integers(0, 8192, 100_000), rng.integers(0, size, 50_000)]).astype(np.int64)
+        keys = rng.permutation(keys)
+    else:  # an increasing prefix then an unordered tail (adaptive path masks the prefix on the device)
+        keys = np.concatenate([np.arange(0, size, 3), rng.integers(0, size, 300_000)]).astype(np.int64)
+    keys += start
+    keys[-1] = size - 1 + start  # the shard's last element (odd-count edge)
+    vals = rand_vals(rng, dtype, keys.size)
+    ref = oracle_vec(part, dtype)
+    with PartialVector(part, dtype, gpu) as sh:
+        lib = N.load()
+        lib.glint_prof_enable(sh.handle, 1)
+        for _ in range(2):
+            sh.update(keys, vals, unordered=True)
+            assert ref.update(keys, vals) == -1
+        import ctypes as C
+        ms, cnt = C.c_double(), C.c_int64()
+        lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
+        assert cnt.value == 2, "the unordered hint must take the binned path"
+        got = sh.to_numpy()
+        if dtype in ("long", "int") or pattern == "permutation":
+            np.testing.assert_array_equal(got, ref.data)  # unique keys: 0 + v is exact, then one add
+        else:
+            np.testing.assert_allclose(got, ref.data, rtol=1e-6 if dtype == "double" else 1e-4,
+                                       atol=1e-9 if dtype == "double" else 2e-3)
+
+
+def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
+    import ctypes as C
+    lib = N.load()
+    start, size = 0, 1 << 22
+    part = RangePartition(0, start, start + size)
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, size, 1 << 21).astype(np.int64)
+    vals = rng.integers(-5, 5, keys.size).astype(np.int64)
+    ref = oracle_vec(part, "long")
+    monkeypatch.delenv("GLINT_BINNED", raising=False)
+    with PartialVector(part, "long", gpu) as sh:
+        lib.glint_prof_enable(sh.handle, 1)
+        counts = []
+        for _ in range(3):
+            sh.update(keys, vals)
+            assert ref.update(keys, vals) == -1
+            ms, cnt = C.c_double(), C.c_int64()
+            lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
+            counts.append(cnt.value)
+        # push 1: no history -> LDS-hash scatter; pushes 2, 3: the previous tail was large -> binned
+        assert counts == [0, 1, 2]
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+        # a sorted dense push afterwards is still exact (the prefix is masked on the device)
+        dense = np.arange(size, dtype=np.int64)
+        sh.update(dense, np.ones(size, np.int64))
+        assert ref.update(dense, np.ones(size, np.int64)) == -1
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+        # an out-of-range record in a binned push is reported; the other records are not corrupted
+        bad = keys.copy()
+        bad[1234] = size + 7
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.update(bad, vals, unordered=True)
+        assert ei.value.record == 1234
+    monkeypatch.setenv("GLINT_BINNED", "0")
+    with PartialVector(part, "long", gpu) as sh:
+        lib.glint_prof_enable(sh.handle, 1)
+        for _ in range(2):
+            sh.update(keys, vals)
+        ms, cnt = C.c_double(), C.c_int64()
+        lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
+        assert cnt.value == 0
+
+
+@pytest.mark.parametrize("dtype", ["double", "int"])
+def test_binned_matrix_push(gpu, dtype):
+    rng = np.random.default_rng(11)
+    rows_n, cols_n = 20_011, 301  # pitch 302 (double) / 304 (int): the row padding stays untouched
+    part = RangePartition(0, 0, rows_n)
+    r = rng.integers(0, rows_n, 800_000).astype(np.int64)
+    c = rng.integers(0, cols_n, r.size).astype(np.int32)
+    v = rand_vals(rng, dtype, r.size)
+    code = O.CODE[dtype]
+    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, code)
+    assert ref.update(r, c, v) == -1
+    with PartialMatrix(part, cols_n, dtype, gpu) as sh:
+        sh.update(r, c, v, unordered=True)
+        got = sh.to_numpy()
+        if dtype == "int":
+            np.testing.assert_array_equal(got, ref.data)
+        else:
+            np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9)

@@ -7,6 +7,7 @@ the JNI shim sees. One JSON line per measurement on stdout.
 """
 import ctypes as C
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -134,19 +135,25 @@ def main():
     U = int(np.unique(zk).size)
     zkeys = torch.from_numpy(zk).to(dev)
     zvals = torch.rand(zk.size, dtype=torch.float64, device=dev)
-    dt = timed(lambda: lib.glint_vec_push_dev(h, zkeys.data_ptr(), zvals.data_ptr(), zk.size, 0, stream), 5, h)
-    k = kernel_ms(h, N.GLINT_K_PUSH_SCATTER)
-    emit(op="vec_push_dev", pattern="zipf1.1", records=int(zk.size), distinct=U,
-         dup_ratio=1 - U / zk.size, ms=dt * 1e3, scatter_kernel_ms=k,
-         algorithmic_GBps=(16.0 * zk.size + 16.0 * U) / dt / 1e9, Grecords_per_s=zk.size / dt / 1e9)
+    uk = torch.randint(0, n, (nz,), dtype=torch.int64, device=dev)
+    for pat, kt, Uk in (("zipf1.1", zkeys, U), ("uniform random", uk, None)):
+        for mode, flags, env in (("atomic", 0, "0"), ("binned (UNORDERED hint)", N.GLINT_PUSH_UNORDERED, ""),
+                                 ("adaptive (no hint)", 0, "")):
+            os.environ["GLINT_BINNED"] = env
+            dt = timed(lambda: lib.glint_vec_push_dev(h, kt.data_ptr(), zvals.data_ptr(), nz, flags, stream), 5, h)
+            rec = dict(op="vec_push_dev", pattern=pat, path=mode, records=nz, ms=dt * 1e3,
+                       Grecords_per_s=nz / dt / 1e9,
+                       scatter_kernel_ms=kernel_ms(h, N.GLINT_K_PUSH_SCATTER),
+                       binned_pipeline_ms=kernel_ms(h, N.GLINT_K_PUSH_BINNED))
+            if Uk is not None:
+                rec.update(distinct=Uk, dup_ratio=1 - Uk / nz, algorithmic_GBps=(16.0 * nz + 16.0 * Uk) / dt / 1e9)
+            else:
+                rec.update(algorithmic_GBps=32.0 * nz / dt / 1e9)
+            emit(**rec)
+        os.environ["GLINT_BINNED"] = ""
     dt = timed(lambda: lib.glint_vec_push_dev(h, zkeys.data_ptr(), zvals.data_ptr(), zk.size, 1, stream), 2, h)
     emit(op="vec_push_dev", mode="deterministic", pattern="zipf1.1", records=int(zk.size), ms=dt * 1e3,
          algorithmic_GBps=(16.0 * zk.size + 16.0 * U) / dt / 1e9)
-    # uniform random keys (cfg4b's per-GPU shape: every key distinct-ish, unordered)
-    uk = torch.randint(0, n, (nz,), dtype=torch.int64, device=dev)
-    dt = timed(lambda: lib.glint_vec_push_dev(h, uk.data_ptr(), zvals.data_ptr(), nz, 0, stream), 5, h)
-    emit(op="vec_push_dev", pattern="uniform random", records=nz, ms=dt * 1e3,
-         algorithmic_GBps=32.0 * nz / dt / 1e9, Grecords_per_s=nz / dt / 1e9)
     sh.destroy()
     del zkeys, zvals, uk
 
@@ -167,6 +174,13 @@ def main():
     emit(op="mat_push_dev", pattern="zipf1.0 rows x uniform cols", shape=[shard_rows, cols], records=int(r.size),
          distinct=U, ms=dt * 1e3, algorithmic_GBps=(20.0 * r.size + 16.0 * U) / dt / 1e9,
          Grecords_per_s=r.size / dt / 1e9)
+    for mode, flags, env in (("atomic", 0, "0"), ("binned (UNORDERED hint)", N.GLINT_PUSH_UNORDERED, "")):
+        os.environ["GLINT_BINNED"] = env
+        dt = timed(lambda: lib.glint_mat_push_dev(h, mr.data_ptr(), mc.data_ptr(), mv.data_ptr(), r.size, flags,
+                                                  stream), 5, h)
+        emit(op="mat_push_dev", pattern="zipf1.0 rows x uniform cols", path=mode, records=int(r.size), distinct=U,
+             ms=dt * 1e3, algorithmic_GBps=(20.0 * r.size + 16.0 * U) / dt / 1e9, Grecords_per_s=r.size / dt / 1e9)
+    os.environ["GLINT_BINNED"] = ""
     nrow = (1 << 16) // 8
     qr = torch.from_numpy(zipf_keys(rng, shard_rows, nrow, 1.0)).to(dev)
     rout = torch.empty((qr.numel(), cols), dtype=torch.float64, device=dev)
