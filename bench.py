@@ -172,6 +172,9 @@ def main():
     apply_ms, apply_n = kernel_avg(N.GLINT_K_PUSH_APPLY)
     check_ms, _ = kernel_avg(N.GLINT_K_PUSH_CHECK)
     scat_ms, _ = kernel_avg(N.GLINT_K_PUSH_SCATTER)
+    bin_ms, bin_n = kernel_avg(N.GLINT_K_PUSH_BINNED)
+    if apply_n:
+        bin_ms = bin_ms * bin_n / apply_n  # per push (the binned pipeline may skip the warm-up pushes)
 
     # post-run check: the shard must hold (W+K) sequential additions of each value (bit-exact for
     # the ordered path); for zipf, a sample checked against the oracle would need the CPU: skip
@@ -189,10 +192,11 @@ def main():
     bytes_per_step = 16.0 * nrec + 16.0 * uniq  # n(8+8) + U(8+8)
     value = world * bytes_per_step * args.steps / dt / 1e9
     # The push is push_check (reads the keys: 8 B/record) + push_apply (values and shard: 24 B/record
-    # for a dense push) + push_scatter (unordered records). Together they move the algorithmic bytes
-    # once, so the roofline is taken over their summed device time (each kernel's share below).
-    kern = "push_check+push_apply+push_scatter"
-    kern_ms = check_ms + apply_ms + scat_ms
+    # for a dense push) + the unordered tail (push_scatter, or the binned pipeline for large tails).
+    # Together they move the algorithmic bytes once, so the roofline is taken over their summed
+    # device time (each kernel's share below).
+    kern = "push_check+push_apply+push_scatter+push_binned"
+    kern_ms = check_ms + apply_ms + scat_ms + bin_ms
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(tag)
     out = {
@@ -218,7 +222,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_step,
                      "launches_timed": apply_n,
                      "push_kernels_ms": {"push_check": round(check_ms, 4), "push_apply": round(apply_ms, 4),
-                                         "push_scatter": round(scat_ms, 4)}},
+                                         "push_scatter": round(scat_ms, 4), "push_binned": round(bin_ms, 4)}},
         "check": ok,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -417,20 +417,25 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
 // binned push: the unordered tail of a large push, without per-record global atomics
 // ------------------------------------------------------------------------------------------------
 // Element-granular device atomics run at ~17 G/s here (each lane's add is its own 64-B memory-side
-// request). A large unordered tail is instead binned by shard slab -- a stable rocPRIM radix sort of
-// (u32 element address, value) on the address bits above kSlabBits -- and each slab's records are
-// summed in LDS (ds_add) and written back with one coalesced read-modify-write of the slab's touched
-// element pairs. Slabs with more than kBinItem records are split into several work items, which
-// then flush with device atomics, so a hot slab never serialises on one workgroup.
-constexpr int kSlabBits = 13;
-constexpr int kSlab = 1 << kSlabBits;  // elements accumulated in LDS per work item (64 KiB of Double)
-constexpr i64 kBinItem = 16384;        // records per work item at most
+// request). A large unordered tail is instead binned by shard slab -- a rocPRIM radix sort of
+// (u32 element address, value) on the address bits above kSlabBits (two 8-bit passes for a 2^28
+// shard) -- and each slab's records are summed in LDS (ds_add) and written back with one coalesced
+// read-modify-write of the slab's touched element pairs. Slabs with more than kBinItem records are
+// split into several work items, which then flush with device atomics, so a hot slab never
+// serialises on one workgroup. (A single-pass counting sort into the 32768 slabs measured slower:
+// 1.4-2.1 ms for 2^26 records against 1.2 ms here -- its per-record writes scatter over too many
+// output segments for L2 to merge.)
+constexpr int kSlabBits = 12;
+constexpr int kSlab = 1 << kSlabBits;  // elements accumulated in LDS per work item (32 KiB of Double:
+                                       // 4 workgroups per CU keep enough item phases overlapping)
+constexpr i64 kBinItem = 16384;        // records per apply work item at most
 constexpr u32 kBinSentinel = 0xFFFFFFFFu;
 
-// u32 element address of every record from r0 on (records before r0 and rejected ones: sentinel);
-// from_break: r0 is the start of push_check's unordered tail, otherwise 0
+// u32 element address of every record from the tail start on (records before it and rejected
+// ones: the sentinel); from_break: the tail starts at push_check's break, otherwise at 0
 template <bool MAT>
-__global__ __launch_bounds__(kTPB) void bin_prepare_kernel(const i64* keys, const int32_t* cols, i64 n, PartDesc part,
+__global__ __launch_bounds__(kTPB) void bin_prepare_kernel(const i64* __restrict__ keys,
+                                                           const int32_t* __restrict__ cols, i64 n, PartDesc part,
                                                            const LaunchCtl* ctl, u32 ntiles, int from_break,
                                                            u32* __restrict__ addr, ErrState* err) {
   i64 r0 = 0;
@@ -451,9 +456,10 @@ __global__ __launch_bounds__(kTPB) void bin_prepare_kernel(const i64* keys, cons
 
 __device__ __forceinline__ u32 slab_of(u32 a, u32 mask) { return (a >> kSlabBits) & mask; }
 
-// per slab s < nslabs: start[s] = first sorted record of slab s, items[s] = its work items;
-// start[nslabs] = n, items[nslabs] = 0 (so that an exclusive scan of items ends in the total)
-__global__ void bin_bounds_kernel(const u32* __restrict__ addr, i64 n, u32 nslabs, u32 mask, i64* __restrict__ start,
+// per slab s < nslabs: start[s] = first sorted record of slab s (the sort orders by slab_of, so the
+// sentinels share the all-ones slab with its real records), items[s] = its apply work items;
+// start[nslabs] = n, items[nslabs] = 0 (an exclusive scan of items then ends in the total)
+__global__ void bin_bounds_kernel(const u32* __restrict__ addr, i64 n, u32 nslabs, u32 mask, u32* __restrict__ start,
                                   u32* __restrict__ items) {
   for (i64 s = (i64)blockIdx.x * blockDim.x + threadIdx.x; s <= (i64)nslabs; s += (i64)gridDim.x * blockDim.x) {
     i64 lo = 0, hi = n;  // first record with slab_of >= s
@@ -462,9 +468,9 @@ __global__ void bin_bounds_kernel(const u32* __restrict__ addr, i64 n, u32 nslab
       if (slab_of(addr[mid], mask) < (u32)s) lo = mid + 1;
       else hi = mid;
     }
-    start[s] = lo;
+    start[s] = (u32)lo;
     if (s == (i64)nslabs) {
-      items[s] = 0;
+      items[s] = 0u;
     } else {
       i64 lo2 = lo, hi2 = n;  // first record with slab_of > s
       while (lo2 < hi2) {
@@ -477,41 +483,64 @@ __global__ void bin_bounds_kernel(const u32* __restrict__ addr, i64 n, u32 nslab
   }
 }
 
+// One descriptor per apply work item {slab, first record, end record, exclusive}: an apply
+// workgroup finds its work with one 16-B load instead of a search
+__global__ void bin_item_map_kernel(const u32* __restrict__ start, const u32* __restrict__ items,
+                                    const u32* __restrict__ item_off, u32 nslabs, uint4* __restrict__ item_desc) {
+  for (u32 s = blockIdx.x * blockDim.x + threadIdx.x; s < nslabs; s += gridDim.x * blockDim.x) {
+    const u32 o = item_off[s], m = items[s], r0 = start[s], r1 = start[s + 1];
+    for (u32 k = 0; k < m; ++k) {
+      const u32 lo = r0 + k * (u32)kBinItem;
+      item_desc[o + k] = make_uint4(s, lo, min(r1, lo + (u32)kBinItem), m == 1u ? 1u : 0u);
+    }
+  }
+}
+
+constexpr int kBinTPB = 256;  // 4 waves share one LDS slab
+constexpr int kBinRB = 4;     // records per thread per batch: loads issue together, then the LDS adds
+
+// One work item = up to kBinItem records of one slab
 template <typename V>
-__global__ __launch_bounds__(kTPB) void bin_apply_kernel(const u32* __restrict__ addr, const V* __restrict__ val,
-                                                         const i64* __restrict__ start,
-                                                         const u32* __restrict__ item_off, u32 nslabs, i64 elems,
-                                                         V* __restrict__ data) {
+__global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restrict__ addr, const V* __restrict__ val,
+                                                            const uint4* __restrict__ item_desc,
+                                                            const u32* __restrict__ item_off, u32 nslabs,
+                                                            i64 elems, V* __restrict__ data) {
   typedef typename Vec2<V>::T V2;
   __shared__ V acc[kSlab];
-  __shared__ u32 bits[kSlab / 32];
-  constexpr int kPairsPerThread = kSlab / 2 / kTPB;
+  __shared__ uint8_t touched[kSlab];  // plain byte stores: no atomic serialisation on hot elements
+  constexpr int kPairsPerThread = kSlab / 2 / kBinTPB;
   const int tid = threadIdx.x;
   const u32 total = item_off[nslabs];
   for (u32 it = blockIdx.x; it < total; it += gridDim.x) {
-    u32 lo = 0, hi = nslabs;  // the slab whose items cover `it`: item_off[lo] <= it < item_off[lo + 1]
-    while (hi - lo > 1) {
-      const u32 mid = (lo + hi) >> 1;
-      if (item_off[mid] <= it) lo = mid;
-      else hi = mid;
-    }
-    const u32 slab = lo;
-    const u32 k = it - item_off[slab];
-    const bool exclusive = item_off[slab + 1] - item_off[slab] == 1u;
-    const i64 r_lo = start[slab] + (i64)k * kBinItem;
-    const i64 r_hi = min(start[slab + 1], r_lo + kBinItem);
-    for (int e = tid; e < kSlab; e += kTPB) acc[e] = V(0);
-    for (int w = tid; w < kSlab / 32; w += kTPB) bits[w] = 0u;
+    const uint4 d4 = item_desc[it];
+    const u32 slab = d4.x;
+    const bool exclusive = d4.w != 0u;
+    const i64 r_lo = d4.y, r_hi = d4.z;
+    const i64 sbase_g = (i64)slab << kSlabBits;
+    for (int e = tid; e < kSlab; e += kBinTPB) acc[e] = V(0);
+    for (int w = tid; w < kSlab / 16; w += kBinTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    for (i64 j = r_lo + tid; j < r_hi; j += kTPB) {
-      const u32 ad = addr[j];
-      if (ad == kBinSentinel) continue;
-      const u32 e = ad & (kSlab - 1);
-      lds_add(&acc[e], val[j]);
-      atomicOr(&bits[e >> 5], 1u << (e & 31));
+    for (i64 j0 = r_lo; j0 < r_hi; j0 += (i64)kBinTPB * kBinRB) {
+      u32 ad[kBinRB];
+      V v[kBinRB];
+#pragma unroll
+      for (int q = 0; q < kBinRB; ++q) {  // clamped, branch-free loads
+        const i64 j = j0 + q * kBinTPB + tid;
+        const i64 jj = j < r_hi ? j : r_hi - 1;
+        ad[q] = addr[jj];
+        v[q] = val[jj];
+        if (j >= r_hi) ad[q] = kBinSentinel;
+      }
+#pragma unroll
+      for (int q = 0; q < kBinRB; ++q) {
+        if (ad[q] == kBinSentinel) continue;
+        const u32 e = ad[q] & (kSlab - 1);
+        lds_add(&acc[e], v[q]);
+        touched[e] = 1;
+      }
     }
     __syncthreads();
-    V* const sbase = data + (i64)slab * kSlab;
+    V* const sbase = data + sbase_g;
     if (exclusive) {
       // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair
       // instead (one cached line), so all loads issue back to back without a branch
@@ -519,18 +548,16 @@ __global__ __launch_bounds__(kTPB) void bin_apply_kernel(const u32* __restrict__
       u32 t[kPairsPerThread];
 #pragma unroll
       for (int q = 0; q < kPairsPerThread; ++q) {
-        const int e0 = 2 * (tid + q * kTPB);
-        const i64 g = (i64)slab * kSlab + e0;
-        t[q] = (bits[e0 >> 5] >> (e0 & 31)) & 3u;
-        const bool vec = t[q] != 0u && g + 1 < elems;
+        const int e0 = 2 * (tid + q * kBinTPB);
+        t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
+        const bool vec = t[q] != 0u && sbase_g + e0 + 1 < elems;
         d[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
       }
 #pragma unroll
       for (int q = 0; q < kPairsPerThread; ++q) {
         if (t[q] == 0u) continue;
-        const int e0 = 2 * (tid + q * kTPB);
-        const i64 g = (i64)slab * kSlab + e0;
-        if (g + 1 < elems) {
+        const int e0 = 2 * (tid + q * kBinTPB);
+        if (sbase_g + e0 + 1 < elems) {
           V2 r = d[q];
           if (t[q] & 1u) r.x = vadd(r.x, acc[e0]);
           if (t[q] & 2u) r.y = vadd(r.y, acc[e0 + 1]);
@@ -540,8 +567,8 @@ __global__ __launch_bounds__(kTPB) void bin_apply_kernel(const u32* __restrict__
         }
       }
     } else {
-      for (int e = tid; e < kSlab; e += kTPB)
-        if ((bits[e >> 5] >> (e & 31)) & 1u) gadd(sbase + e, acc[e]);
+      for (int e = tid; e < kSlab; e += kBinTPB)
+        if (touched[e]) gadd(sbase + e, acc[e]);
     }
     __syncthreads();
   }
@@ -963,8 +990,8 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
 }
 
 // The binned tail pipeline over the whole push (records before push_check's break are masked on
-// the device, so no host round trip is needed): prepare -> radix sort by slab -> bounds -> item
-// scan -> LDS slab apply.
+// the device, so no host round trip is needed): prepare -> radix sort by slab -> slab bounds ->
+// item scan -> item map -> LDS slab apply.
 template <typename V, bool MAT>
 int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
   const i64 n = a.n;
@@ -978,33 +1005,37 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
                                    (size_t)n, kSlabBits, end_bit, st));
   HIPCHK(rocprim::exclusive_scan(nullptr, scan_bytes, (u32*)nullptr, (u32*)nullptr, 0u, (size_t)nslabs + 1,
                                  rocprim::plus<u32>(), st));
+  const i64 max_items = (i64)nslabs + (n + kBinItem - 1) / kBinItem;
   const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(V));
-  const size_t b_s = pad256(((size_t)nslabs + 1) * 8), b_i = pad256(((size_t)nslabs + 1) * 4);
-  const size_t need = 2 * b_a + b_v + b_s + 2 * b_i + pad256(sort_bytes) + pad256(scan_bytes);
+  const size_t b_s = pad256(((size_t)nslabs + 1) * 4), b_m = pad256((size_t)max_items * 16);
+  const size_t need = 2 * b_a + b_v + 3 * b_s + b_m + pad256(sort_bytes) + pad256(scan_bytes);
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   char* p = (char*)s->d_bin;
   u32* addr_in = (u32*)p;
   u32* addr_out = (u32*)(p + b_a);
   V* val_out = (V*)(p + 2 * b_a);
-  i64* start = (i64*)(p + 2 * b_a + b_v);
+  u32* start = (u32*)(p + 2 * b_a + b_v);
   u32* items = (u32*)(p + 2 * b_a + b_v + b_s);
-  u32* item_off = (u32*)(p + 2 * b_a + b_v + b_s + b_i);
-  void* sort_tmp = p + 2 * b_a + b_v + b_s + 2 * b_i;
+  u32* item_off = (u32*)(p + 2 * b_a + b_v + 2 * b_s);
+  uint4* item_desc = (uint4*)(p + 2 * b_a + b_v + 3 * b_s);
+  void* sort_tmp = p + 2 * b_a + b_v + 3 * b_s + b_m;
   void* scan_tmp = (char*)sort_tmp + pad256(sort_bytes);
+  const unsigned gs = grid_for((i64)nslabs + 1, 256, 8192);
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   bin_prepare_kernel<MAT><<<grid_for(n, kTPB, (i64)s->cus * 8), kTPB, 0, st>>>(
       a.keys, a.cols, n, a.part, a.ctl, a.ntiles, from_break ? 1 : 0, addr_in, a.err);
   HIPCHK(hipGetLastError());
   HIPCHK(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, addr_in, addr_out, a.vals, val_out, (size_t)n, kSlabBits,
                                    end_bit, st));
-  bin_bounds_kernel<<<grid_for((i64)nslabs + 1, 256, 4096), 256, 0, st>>>(addr_out, n, nslabs, mask, start, items);
+  bin_bounds_kernel<<<gs, 256, 0, st>>>(addr_out, n, nslabs, mask, start, items);
   HIPCHK(hipGetLastError());
   HIPCHK(rocprim::exclusive_scan(scan_tmp, scan_bytes, items, item_off, 0u, (size_t)nslabs + 1, rocprim::plus<u32>(),
                                  st));
-  const i64 max_items = (i64)nslabs + (n + kBinItem - 1) / kBinItem;
-  bin_apply_kernel<V><<<(unsigned)std::min<i64>(max_items, (i64)s->cus * 8), kTPB, 0, st>>>(
-      addr_out, val_out, start, item_off, nslabs, s->elems, a.data);
+  bin_item_map_kernel<<<gs, 256, 0, st>>>(start, items, item_off, nslabs, item_desc);
+  HIPCHK(hipGetLastError());
+  bin_apply_kernel<V><<<(unsigned)std::min<i64>(max_items, (i64)s->cus * 8), kBinTPB, 0, st>>>(
+      addr_out, val_out, item_desc, item_off, nslabs, s->elems, a.data);
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }
