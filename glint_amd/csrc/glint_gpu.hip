@@ -454,6 +454,101 @@ __global__ __launch_bounds__(kTPB) void bin_prepare_kernel(const i64* __restrict
   }
 }
 
+// Duplicate-heavy tails: each workgroup first sums its chunk's records per element in an LDS hash
+// table and emits one (address, sum) per distinct element, so the sort and the apply see only
+// those. Output order is arbitrary (the default mode's contract); the count goes to *m_out.
+constexpr int kDedupSlots = 4096;   // u32 keys + V sums: 48 KiB for Double
+constexpr int kDedupChunk = 2048;   // records per table fill (load factor <= 0.5)
+template <typename V, bool MAT>
+__global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
+                                                         const V* __restrict__ vals, i64 n, PartDesc part,
+                                                         const LaunchCtl* ctl, u32 ntiles, int from_break,
+                                                         u32* __restrict__ addr_out, V* __restrict__ val_out,
+                                                         u32* __restrict__ m_out, ErrState* err) {
+  __shared__ u32 hk[kDedupSlots];
+  __shared__ V hv[kDedupSlots];
+  __shared__ u32 wsum[kTPB / 64];
+  __shared__ u32 obase;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  i64 r0 = 0;
+  if (from_break) {
+    const u32 brk = ctl->brk_enc;
+    r0 = brk == 0u ? n : (i64)(ntiles - brk) * kTile;
+  }
+  if (blockIdx.x == 0 && tid == 0) m_out[1] = (u32)(n - r0);  // the tail size, for the host's ratio
+  for (int sl = tid; sl < kDedupSlots; sl += kTPB) { hk[sl] = kBinSentinel; hv[sl] = V(0); }
+  __syncthreads();
+  const i64 nchunks = (n - r0 + kDedupChunk - 1) / kDedupChunk;
+  for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const i64 c0 = r0 + ch * kDedupChunk, c1 = min(n, c0 + kDedupChunk);
+    constexpr int kPer = kDedupChunk / kTPB;
+    i64 k[kPer];
+    int32_t cl[kPer];
+    V v[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {  // clamped, branch-free loads
+      const i64 i = c0 + q * kTPB + tid;
+      const i64 ii = i < c1 ? i : c1 - 1;
+      k[q] = keys[ii];
+      cl[q] = MAT ? cols[ii] : 0;
+      v[q] = vals[ii];
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const i64 i = c0 + q * kTPB + tid;
+      if (i >= c1) continue;
+      i64 ad64;
+      if (!rec_addr<MAT>(part, k[q], cl[q], ad64)) { record_error(err, i); continue; }
+      const u32 ad = (u32)ad64;
+      u32 h = (ad * 0x9E3779B1u) >> (32 - 12);
+      for (;;) {
+        const u32 cur = hk[h];
+        if (cur == ad) break;
+        if (cur == kBinSentinel) {
+          const u32 prev = atomicCAS(&hk[h], kBinSentinel, ad);
+          if (prev == kBinSentinel || prev == ad) break;
+        }
+        h = (h + 1) & (kDedupSlots - 1);
+      }
+      lds_add(&hv[h], v[q]);
+    }
+    __syncthreads();
+    // compact: count this thread's occupied slots, scan across the block, reserve, write
+    constexpr int kSlotsPer = kDedupSlots / kTPB;
+    u32 cnt = 0;
+#pragma unroll
+    for (int q = 0; q < kSlotsPer; ++q) cnt += hk[tid * kSlotsPer + q] != kBinSentinel;
+    u32 incl = cnt;  // wave-inclusive scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      u32 t = 0;
+      for (int w = 0; w < kTPB / 64; ++w) { const u32 x = wsum[w]; wsum[w] = t; t += x; }
+      obase = atomicAdd(m_out, t);
+    }
+    __syncthreads();
+    u32 pos = obase + wsum[wid] + incl - cnt;
+#pragma unroll
+    for (int q = 0; q < kSlotsPer; ++q) {
+      const int sl = tid * kSlotsPer + q;
+      const u32 key = hk[sl];
+      if (key != kBinSentinel) {
+        addr_out[pos] = key;
+        val_out[pos] = hv[sl];
+        ++pos;
+        hk[sl] = kBinSentinel;
+        hv[sl] = V(0);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ u32 slab_of(u32 a, u32 mask) { return (a >> kSlabBits) & mask; }
 
 // per slab s < nslabs: start[s] = first sorted record of slab s (the sort orders by slab_of, so the
@@ -824,6 +919,8 @@ struct glint_shard {
   size_t det_bytes = 0;
   void* d_bin = nullptr;  // binned-push scratch
   size_t bin_bytes = 0;
+  double bin_dedup_ratio = 0.0;  // distinct/records of the last deduplicating binned push
+  uint32_t bin_pushes = 0;
   u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
   u64* d_hint = nullptr;
   i64 last_bad = -1;
@@ -1000,6 +1097,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   while (end_bit < 32 && ((i64)1 << end_bit) < s->elems) ++end_bit;
   const u32 nslabs = 1u << (end_bit - kSlabBits);
   const u32 mask = nslabs - 1u;
+  // dedup when the last probe found < 60 % distinct records per chunk; re-probe every 16 pushes
+  const bool dedup = s->bin_dedup_ratio < 0.6 || (++s->bin_pushes & 15) == 0;
   size_t sort_bytes = 0, scan_bytes = 0;
   HIPCHK(rocprim::radix_sort_pairs(nullptr, sort_bytes, (u32*)nullptr, (u32*)nullptr, (const V*)nullptr, (V*)nullptr,
                                    (size_t)n, kSlabBits, end_bit, st));
@@ -1008,33 +1107,52 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const i64 max_items = (i64)nslabs + (n + kBinItem - 1) / kBinItem;
   const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(V));
   const size_t b_s = pad256(((size_t)nslabs + 1) * 4), b_m = pad256((size_t)max_items * 16);
-  const size_t need = 2 * b_a + b_v + 3 * b_s + b_m + pad256(sort_bytes) + pad256(scan_bytes);
+  const size_t need = 2 * b_a + 2 * b_v + 3 * b_s + b_m + 256 + pad256(sort_bytes) + pad256(scan_bytes);
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   char* p = (char*)s->d_bin;
   u32* addr_in = (u32*)p;
   u32* addr_out = (u32*)(p + b_a);
-  V* val_out = (V*)(p + 2 * b_a);
-  u32* start = (u32*)(p + 2 * b_a + b_v);
-  u32* items = (u32*)(p + 2 * b_a + b_v + b_s);
-  u32* item_off = (u32*)(p + 2 * b_a + b_v + 2 * b_s);
-  uint4* item_desc = (uint4*)(p + 2 * b_a + b_v + 3 * b_s);
-  void* sort_tmp = p + 2 * b_a + b_v + 3 * b_s + b_m;
+  V* val_in = (V*)(p + 2 * b_a);
+  V* val_out = (V*)(p + 2 * b_a + b_v);
+  u32* start = (u32*)(p + 2 * b_a + 2 * b_v);
+  u32* items = (u32*)(p + 2 * b_a + 2 * b_v + b_s);
+  u32* item_off = (u32*)(p + 2 * b_a + 2 * b_v + 2 * b_s);
+  uint4* item_desc = (uint4*)(p + 2 * b_a + 2 * b_v + 3 * b_s);
+  u32* m_dev = (u32*)(p + 2 * b_a + 2 * b_v + 3 * b_s + b_m);
+  void* sort_tmp = p + 2 * b_a + 2 * b_v + 3 * b_s + b_m + 256;
   void* scan_tmp = (char*)sort_tmp + pad256(sort_bytes);
   const unsigned gs = grid_for((i64)nslabs + 1, 256, 8192);
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
-  bin_prepare_kernel<MAT><<<grid_for(n, kTPB, (i64)s->cus * 8), kTPB, 0, st>>>(
-      a.keys, a.cols, n, a.part, a.ctl, a.ntiles, from_break ? 1 : 0, addr_in, a.err);
-  HIPCHK(hipGetLastError());
-  HIPCHK(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, addr_in, addr_out, a.vals, val_out, (size_t)n, kSlabBits,
+  i64 m = n;
+  const V* sort_vals = a.vals;
+  if (dedup) {
+    HIPCHK(hipMemsetAsync(m_dev, 0, 8, st));
+    bin_dedup_kernel<V, MAT><<<grid_for(n, kDedupChunk, (i64)s->cus * 3), kTPB, 0, st>>>(
+        a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, from_break ? 1 : 0, addr_in, val_in, m_dev, a.err);
+    HIPCHK(hipGetLastError());
+    u32 mh[2] = {0, 0};  // the sort needs its size on the host: one round trip, only on this path
+    HIPCHK(hipMemcpyAsync(mh, m_dev, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    m = mh[0];
+    sort_vals = val_in;
+    if (mh[1] > 0) s->bin_dedup_ratio = (double)mh[0] / (double)mh[1];
+    if (m == 0) return GLINT_OK;
+  } else {
+    bin_prepare_kernel<MAT><<<grid_for(n, kTPB, (i64)s->cus * 8), kTPB, 0, st>>>(
+        a.keys, a.cols, n, a.part, a.ctl, a.ntiles, from_break ? 1 : 0, addr_in, a.err);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, addr_in, addr_out, sort_vals, val_out, (size_t)m, kSlabBits,
                                    end_bit, st));
-  bin_bounds_kernel<<<gs, 256, 0, st>>>(addr_out, n, nslabs, mask, start, items);
+  bin_bounds_kernel<<<gs, 256, 0, st>>>(addr_out, m, nslabs, mask, start, items);
   HIPCHK(hipGetLastError());
   HIPCHK(rocprim::exclusive_scan(scan_tmp, scan_bytes, items, item_off, 0u, (size_t)nslabs + 1, rocprim::plus<u32>(),
                                  st));
   bin_item_map_kernel<<<gs, 256, 0, st>>>(start, items, item_off, nslabs, item_desc);
   HIPCHK(hipGetLastError());
-  bin_apply_kernel<V><<<(unsigned)std::min<i64>(max_items, (i64)s->cus * 8), kBinTPB, 0, st>>>(
+  const i64 mi = (i64)nslabs + (m + kBinItem - 1) / kBinItem;
+  bin_apply_kernel<V><<<(unsigned)std::min<i64>(mi, (i64)s->cus * 8), kBinTPB, 0, st>>>(
       addr_out, val_out, item_desc, item_off, nslabs, s->elems, a.data);
   HIPCHK(hipGetLastError());
   return GLINT_OK;

@@ -511,3 +511,20 @@ def test_binned_matrix_push(gpu, dtype):
             np.testing.assert_array_equal(got, ref.data)
         else:
             np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9)
+
+
+def test_binned_dedup_policy(gpu):
+    """Duplicate-heavy unordered pushes are summed per chunk in LDS before binning; unique-key
+    pushes stop paying for that after one probe. Both stay correct across the switch."""
+    rng = np.random.default_rng(3)
+    size = 1 << 20
+    part = RangePartition(0, 0, size)
+    hot = rng.integers(0, 5000, 1 << 20).astype(np.int64)            # ~0.5 % distinct per chunk
+    uniq = rng.permutation(size).astype(np.int64)                     # 100 % distinct
+    ref = oracle_vec(part, "long")
+    with PartialVector(part, "long", gpu) as sh:
+        for keys in (hot, uniq, uniq, hot, uniq, hot):
+            vals = rng.integers(-9, 9, keys.size).astype(np.int64)
+            sh.update(keys, vals, unordered=True)
+            assert ref.update(keys, vals) == -1
+            np.testing.assert_array_equal(sh.to_numpy(), ref.data)
