@@ -78,9 +78,41 @@ def cpu_baseline(log2_keys: int, seconds: float):
         if el >= seconds:
             break
     gbs = 32.0 * n * passes / el / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{passes} x PartialVector[Double].update of 2^{min(log2_keys, 26)} dense records "
-                      f"(oracle/glint_oracle.c scalar loop, 1 thread = 1 actor), {el:.1f} s"}
+    out = {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": f"{passes} x PartialVector[Double].update of 2^{min(log2_keys, 26)} dense records "
+                     f"(oracle/glint_oracle.c scalar loop, 1 thread = 1 actor), {el:.1f} s"}
+    # the same sample as P = 8 range shards (cfg4's partition count), one actor thread per shard on
+    # min(P, host cores) threads
+    P = 8
+    threads = max(1, min(P, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    q = n // P
+    starts, ends = [i * q for i in range(P)], [(i + 1) * q for i in range(P)]
+    datas = [data[i * q:(i + 1) * q] for i in range(P)]
+    ks = [keys[i * q:(i + 1) * q] for i in range(P)]
+    vs = [vals[i * q:(i + 1) * q] for i in range(P)]
+    O.vec_update_f64_parallel(starts, ends, datas, ks, vs, threads)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        O.vec_update_f64_parallel(starts, ends, datas, ks, vs, threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds / 2:
+            break
+    # BASELINE.json configs[0]: 1 client + 2 loopback servers, 1M-key Double vector, dense push in
+    # <= 1000-record messages with the exactly-once protocol, then a pull of every key
+    # (tools/loopback/glint_loopback.c with the oracle's server loop as the shard)
+    try:
+        import subprocess
+        from glint_amd.build import LOOPBACK_BIN, ORACLE_LIB
+        r = subprocess.run([str(LOOPBACK_BIN), "--backend", "oracle", "--lib", str(ORACLE_LIB)],
+                           capture_output=True, text=True, timeout=120)
+        out["cfg1_loopback"] = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # the baseline is reported, never required
+        out["cfg1_loopback"] = {"error": str(e)[:200]}
+    out["parallel"] = {"value": round(32.0 * q * P * passes / el / 1e9, 3), "unit": "GB/s", "cores": threads,
+                       "sample": f"{passes} x 2^{min(log2_keys, 26)} dense records over {P} shards, "
+                                 f"one thread per shard on {threads} threads, {el:.1f} s"}
+    return out
 
 
 def main():

@@ -25,6 +25,8 @@ ORACLE_LIB = ORACLE_DIR / "build" / "libglint_oracle.so"
 HIP_SOURCES = [PKG / "csrc" / "glint_gpu.hip", PKG / "csrc" / "glint_route.hip"]
 HIP_DEPS = HIP_SOURCES + [PKG / "csrc" / "glint_kernels.h", ROOT / "include" / "glint_gpu.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "glint_oracle.c"]
+LOOPBACK_SRC = ROOT / "tools" / "loopback" / "glint_loopback.c"
+LOOPBACK_BIN = ROOT / "tools" / "loopback" / "build" / "glint_loopback"
 
 
 def _hipcc() -> str:
@@ -75,12 +77,30 @@ def build_oracle(force: bool = False, verbose: bool = False) -> Path:
     return ORACLE_LIB
 
 
+def build_loopback(force: bool = False, verbose: bool = False) -> Path:
+    """The loopback-TCP client/server harness (BASELINE.json configs[0]); it dlopens its shard
+    backend at run time and links neither library."""
+    if not force and not _stale(LOOPBACK_BIN, [LOOPBACK_SRC]):
+        return LOOPBACK_BIN
+    LOOPBACK_BIN.parent.mkdir(parents=True, exist_ok=True)
+    tmp = LOOPBACK_BIN.with_suffix(".tmp")
+    cc = shutil.which("gcc") or "cc"
+    cmd = [cc, "-O2", "-std=c11", "-Wall", "-pthread", "-o", str(tmp), str(LOOPBACK_SRC), "-ldl"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=str(ROOT))
+    os.replace(tmp, LOOPBACK_BIN)
+    return LOOPBACK_BIN
+
+
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_gpu_lib(force=force, verbose=verbose)
     build_oracle(force=force, verbose=verbose)
+    build_loopback(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv, verbose=True)
     print(LIB)
     print(ORACLE_LIB)
+    print(LOOPBACK_BIN)

@@ -234,6 +234,17 @@ static void* job_main(void* arg) {
 /* Runs `nshards` independent PartialVector[Double].update loops on `nthreads` POSIX threads
  * (nthreads == nshards or 1). Shard s: range [starts[s], ends[s]), its own data array and its own
  * record stream. Returns the number of failed shards. */
+typedef struct {
+  oracle_job* jobs;
+  int32_t first, step, count;
+} oracle_worker;
+
+static void* worker_main(void* arg) {
+  oracle_worker* w = (oracle_worker*)arg;
+  for (int32_t s = w->first; s < w->count; s += w->step) job_main(&w->jobs[s]);
+  return NULL;
+}
+
 int oracle_vec_update_f64_parallel(int32_t nshards, const int64_t* starts, const int64_t* ends,
                                    double** datas, const int64_t** keys, const double** vals,
                                    const int64_t* ns, int32_t nthreads) {
@@ -246,10 +257,17 @@ int oracle_vec_update_f64_parallel(int32_t nshards, const int64_t* starts, const
   if (nthreads <= 1) {
     for (int32_t s = 0; s < nshards; ++s) job_main(&jobs[s]);
   } else {
-    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nshards);
-    for (int32_t s = 0; s < nshards; ++s) pthread_create(&th[s], NULL, job_main, &jobs[s]);
-    for (int32_t s = 0; s < nshards; ++s) pthread_join(th[s], NULL);
+    /* nthreads workers; worker w runs the actors (shards) w, w + nthreads, ... one after another */
+    if (nthreads > nshards) nthreads = nshards;
+    oracle_worker* ws = (oracle_worker*)calloc((size_t)nthreads, sizeof(oracle_worker));
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    for (int32_t w = 0; w < nthreads; ++w) {
+      ws[w].jobs = jobs; ws[w].first = w; ws[w].step = nthreads; ws[w].count = nshards;
+      pthread_create(&th[w], NULL, worker_main, &ws[w]);
+    }
+    for (int32_t w = 0; w < nthreads; ++w) pthread_join(th[w], NULL);
     free(th);
+    free(ws);
   }
   int bad = 0;
   for (int32_t s = 0; s < nshards; ++s) bad += jobs[s].rc >= 0;

@@ -528,3 +528,16 @@ def test_binned_dedup_policy(gpu):
             sh.update(keys, vals, unordered=True)
             assert ref.update(keys, vals) == -1
             np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+def test_loopback_harness_gpu_backend(gpu):
+    """configs[0] over loopback TCP with HBM shards fed the raw wire images (glint_push_wire /
+    glint_pull_wire): pulled values equal the pushed ones bit for bit."""
+    import json
+    import subprocess
+    from glint_amd.build import LIB, LOOPBACK_BIN
+    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--device", str(gpu)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["check"] is True and d["push_messages"] == 1000

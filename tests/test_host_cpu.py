@@ -105,3 +105,23 @@ def test_client_bucketing_matches_reference_groupby():
     counts, ooff, oorder = O.bucket_range(keys, P, Nk)
     np.testing.assert_array_equal(off, ooff)
     np.testing.assert_array_equal(order, oorder)
+
+
+def test_loopback_harness_cpu_backend():
+    """configs[0] restated over loopback TCP (tools/loopback/glint_loopback.c) with the oracle's
+    server loop: the exactly-once push protocol, ragged partitions and message sizes, and the
+    GranularBigVectorSpec values (java.util.Random(42))."""
+    import json
+    import subprocess
+    from glint_amd.build import LOOPBACK_BIN, ORACLE_LIB, build_loopback
+    build_loopback()
+    for servers, keys, msg in [(2, 100_000, 1000), (3, 10_007, 77), (5, 3, 1)]:
+        r = subprocess.run([str(LOOPBACK_BIN), "--backend", "oracle", "--lib", str(ORACLE_LIB), "--servers",
+                            str(servers), "--keys", str(keys), "--msg", str(msg)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        d = json.loads(r.stdout)
+        assert d["check"] is True and d["resends"] == 0
+        assert d["push_messages"] >= -(-keys // msg)
+        first = O.JavaRandom(42).nextDoubles(3)
+        assert d["first_values"][:min(3, keys)] == list(first[:min(3, keys)])

@@ -198,6 +198,15 @@ def main():
          algorithmic_GBps=36.0 * dr.numel() / dt / 1e9, note="36 B/record: row 8 + col 4 + value 8 + shard 16")
     msh.destroy()
 
+    # ---- configs[0] end to end over loopback TCP: HBM shards behind the wire ingest ----------------
+    import subprocess
+    from glint_amd.build import LIB, LOOPBACK_BIN
+    for servers, keys, msg in ((2, 1_000_000, 1000), (2, 1 << 24, 79_999)):
+        r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--servers", str(servers),
+                            "--keys", str(keys), "--msg", str(msg)], capture_output=True, text=True, timeout=300)
+        rec = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-300:]}
+        emit(op="loopback_tcp", **rec)
+
 
 if __name__ == "__main__":
     main()
