@@ -284,21 +284,41 @@ __device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, i
 
 // The whole push is one affine run (element = record + delta): a grid-stride sweep over record
 // pairs, so the grid reads one compact window of the value and shard streams at a time and no
-// load depends on another (the keys were read once, by push_check).
+// load depends on another (the keys were read once, by push_check). Only the first
+// a.sweep_blocks blocks take part (about one per CU): this 2-read + 1-write stream runs fastest
+// with ~16 KiB of loads in flight per CU and every access non-temporal (tools/microbench_stream.hip:
+// 6.2 TB/s, against 5.7 TB/s at twice the waves with cached shard accesses).
+constexpr int kSweepU = 2;  // record pairs per lane per iteration
 template <typename V, bool EVEN>
 __device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta) {
   typedef typename Vec2<V>::T V2;
+  if (blockIdx.x >= a.sweep_blocks) return;
   const i64 npairs = a.n >> 1;
-  const i64 stride = (i64)gridDim.x * kTPB;
+  const i64 stride = (i64)a.sweep_blocks * kTPB;
   const V2* vp = reinterpret_cast<const V2*>(a.vals);
-  for (i64 p = (i64)blockIdx.x * kTPB + threadIdx.x; p < npairs; p += stride) {
-    const V2 v = __builtin_nontemporal_load(vp + p);
-    const i64 e = 2 * p + delta;
-    if (EVEN) {
-      V2* dp = reinterpret_cast<V2*>(a.data + e);
-      const V2 d = *dp;
-      *dp = as2<V>(vadd((V)d.x, (V)v.x), vadd((V)d.y, (V)v.y));
-    } else {
+  i64 p = (i64)blockIdx.x * kTPB + threadIdx.x;
+  if (EVEN) {
+    V2* dp = reinterpret_cast<V2*>(a.data + delta);  // pair p -> element pair delta + 2p
+    for (; p + (kSweepU - 1) * stride < npairs; p += kSweepU * stride) {
+      V2 v[kSweepU], d[kSweepU];
+#pragma unroll
+      for (int j = 0; j < kSweepU; ++j) {
+        v[j] = __builtin_nontemporal_load(vp + p + j * stride);
+        d[j] = __builtin_nontemporal_load(dp + p + j * stride);
+      }
+#pragma unroll
+      for (int j = 0; j < kSweepU; ++j)
+        __builtin_nontemporal_store(as2<V>(vadd((V)d[j].x, (V)v[j].x), vadd((V)d[j].y, (V)v[j].y)), dp + p + j * stride);
+    }
+    for (; p < npairs; p += stride) {
+      const V2 v = __builtin_nontemporal_load(vp + p);
+      const V2 d = __builtin_nontemporal_load(dp + p);
+      __builtin_nontemporal_store(as2<V>(vadd((V)d.x, (V)v.x), vadd((V)d.y, (V)v.y)), dp + p);
+    }
+  } else {
+    for (; p < npairs; p += stride) {
+      const V2 v = __builtin_nontemporal_load(vp + p);
+      const i64 e = 2 * p + delta;
       const V d0 = a.data[e], d1 = a.data[e + 1];
       a.data[e] = vadd(d0, (V)v.x);
       a.data[e + 1] = vadd(d1, (V)v.y);
@@ -828,13 +848,14 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
         const bool o1 = rec_addr<false>(part, k.y, 0, l1);
         V2 o;
         if (o0 && o1 && l1 == l0 + 1 && (l0 & 1) == 0) {
-          o = *reinterpret_cast<const V2*>(data + l0);
+          // adjacent pair: a streamed (dense) pull -- non-temporal, like the push sweep
+          o = __builtin_nontemporal_load(reinterpret_cast<const V2*>(data + l0));
         } else {
           if (!o0) record_error(err, r);
           if (!o1) record_error(err, r + 1);
           o = as2<V>(o0 ? data[l0] : V(0), o1 ? data[l1] : V(0));
         }
-        *reinterpret_cast<V2*>(out + r) = o;
+        __builtin_nontemporal_store(o, reinterpret_cast<V2*>(out + r));
       } else {
         i64 l0;
         const bool o0 = rec_addr<false>(part, keys[r], 0, l0);
@@ -1158,6 +1179,15 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   return GLINT_OK;
 }
 
+// blocks per CU in the affine sweep (GLINT_SWEEP_BPC overrides; 1 measured best on MI355X)
+int sweep_blocks_per_cu() {
+  static const int v = [] {
+    const char* e = getenv("GLINT_SWEEP_BPC");
+    return (e && atoi(e) > 0) ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // GLINT_BINNED: 0 = never bin, 1 = bin every large push, unset = bin when the previous push on the
 // shard left a large unordered tail (read from the host-mapped word push_apply writes)
 int binned_mode() {
@@ -1182,6 +1212,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.err = s->d_err;
   a.elems = s->elems;
   a.hint = s->d_hint;
+  a.sweep_blocks = 0;
   const i64 ntiles = (n + kTile - 1) / kTile;
   if (ntiles >= (i64)0xFFFFFFF0ll) return GLINT_EINVAL;
   a.ntiles = (u32)ntiles;
@@ -1211,7 +1242,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   HIPCHK(hipMemsetAsync(s->d_ctl, 0, sizeof(LaunchCtl), st));
   {
     const unsigned gc =
-        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT>, 8, "GLINT_CHECK_BPC"));
+        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT>, 2, "GLINT_CHECK_BPC"));
     ProfScope pc(s, GLINT_K_PUSH_CHECK, st);
     push_check_kernel<MAT><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
     HIPCHK(hipGetLastError());
@@ -1219,6 +1250,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   {
     const unsigned ga =
         grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_apply_kernel<V, MAT>, 2, "GLINT_APPLY_BPC"));
+    a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * sweep_blocks_per_cu()));
     ProfScope ps(s, GLINT_K_PUSH_APPLY, st);
     push_apply_kernel<V, MAT><<<ga, kTPB, 0, st>>>(a, desc);
     HIPCHK(hipGetLastError());
@@ -1240,7 +1272,8 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
   ProfScope ps(s, GLINT_K_VEC_PULL, st);
   if (pairs) {
-    const unsigned g = grid_for((n + 1) / 2, kTPB, (i64)s->cus * 8);
+    // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5)
+    const unsigned g = grid_for((n + 1) / 2, kTPB, (i64)s->cus * 4);
     vec_pull_kernel<V, true><<<g, kTPB, 0, st>>>(keys, n, (const V*)s->data, s->part, (V*)out, s->d_err);
   } else {
     const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);

@@ -84,6 +84,7 @@ struct PushArgs {
   LaunchCtl* ctl;
   u32 ntiles;
   ErrState* err;
+  u32 sweep_blocks;  // blocks of push_apply that take part in the affine sweep (<= grid)
   u64* hint;  // host-mapped word: the unordered-tail size push_apply saw (binned-path heuristic)
 };
 

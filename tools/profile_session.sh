@@ -11,3 +11,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 --no-check > $OUT/bench_write.txt 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ztrace -o run -- python3 bench.py --no-cpu-baseline --pattern zipf > $OUT/bench_zipf_traced.txt 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py > $OUT/bench_default.txt 2>&1 || exit 1
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --log2-keys 30 --steps 10 > $OUT/bench_2p30.txt 2>&1 || exit 1
