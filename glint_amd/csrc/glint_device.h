@@ -1,0 +1,72 @@
+// glint_device.h -- device helpers shared by the push/pull kernels (glint_gpu.hip) and the
+// sort-based push tails (glint_sort.hip): paired vector types, the reference's `+` on JVM
+// primitives, device/LDS atomics and the record -> element address map with its range test.
+#pragma once
+#include "glint_kernels.h"
+
+namespace glint {
+
+// ------------------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------------------
+template <typename V> struct Vec2;
+template <> struct Vec2<double> { typedef __attribute__((ext_vector_type(2))) double T; };
+template <> struct Vec2<float> { typedef __attribute__((ext_vector_type(2))) float T; };
+template <> struct Vec2<long long> { typedef __attribute__((ext_vector_type(2))) unsigned long long T; };
+template <> struct Vec2<int> { typedef __attribute__((ext_vector_type(2))) unsigned int T; };
+
+typedef __attribute__((ext_vector_type(2))) long long K2;
+typedef __attribute__((ext_vector_type(2))) int C2;
+
+// Semiring `+` of spire on JVM primitives: IEEE round-to-nearest for Float/Double, two's-complement
+// wrap for Int/Long (PartialVector.scala:39 `data(key) += values(i)`).
+__device__ __forceinline__ double vadd(double a, double b) { return a + b; }
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ long long vadd(long long a, long long b) { return (long long)((u64)a + (u64)b); }
+__device__ __forceinline__ int vadd(int a, int b) { return (int)((u32)a + (u32)b); }
+
+template <typename V> __device__ __forceinline__ typename Vec2<V>::T as2(V x, V y);
+template <> __device__ __forceinline__ Vec2<double>::T as2(double x, double y) { return {x, y}; }
+template <> __device__ __forceinline__ Vec2<float>::T as2(float x, float y) { return {x, y}; }
+template <> __device__ __forceinline__ Vec2<long long>::T as2(long long x, long long y) { return {(u64)x, (u64)y}; }
+template <> __device__ __forceinline__ Vec2<int>::T as2(int x, int y) { return {(u32)x, (u32)y}; }
+
+// device-scope atomic add, no return (global_atomic_add_f64 / _f32 / _x2 / plain)
+__device__ __forceinline__ void gadd(double* p, double v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void gadd(float* p, float v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void gadd(long long* p, long long v) { atomicAdd((u64*)p, (u64)v); }
+__device__ __forceinline__ void gadd(int* p, int v) { atomicAdd((u32*)p, (u32)v); }
+
+__device__ __forceinline__ u32 ld_relaxed(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(u32* p, u32 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void record_error(ErrState* e, i64 idx) {
+  atomicMax(&e->min_bad_enc, ~(u64)idx);
+  atomicAdd(&e->count, 1ull);
+}
+
+// address of a record; false when the JVM would throw ArrayIndexOutOfBoundsException
+template <bool MAT>
+__device__ __forceinline__ bool rec_addr(const PartDesc& p, i64 key, int32_t col, i64& addr) {
+  const int32_t l = g2l(p, key);
+  bool ok = l >= 0 && l < p.size;
+  if (MAT) {
+    ok = ok && col >= 0 && col < p.cols;
+    addr = (i64)l * p.pitch + (i64)col;
+  } else {
+    addr = (i64)l;
+  }
+  return ok;
+}
+
+
+__device__ __forceinline__ void lds_add(double* p, double v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void lds_add(float* p, float v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void lds_add(long long* p, long long v) { atomicAdd((u64*)p, (u64)v); }
+__device__ __forceinline__ void lds_add(int* p, int v) { atomicAdd((u32*)p, (u32)v); }
+
+}  // namespace glint

@@ -1,0 +1,163 @@
+// glint_host.h -- host-side state of a shard (the handle behind glint_shard_t) and the helpers
+// shared by the C ABI (glint_gpu.hip) and the sort-based push tails (glint_sort.hip).
+#pragma once
+#include "glint_kernels.h"
+#include "../../include/glint_gpu.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+using namespace glint;
+
+struct glint_shard {
+  int device = 0;
+  int dtype = 0;
+  size_t vsize = 0;
+  PartDesc part{};
+  i64 elems = 0;  // allocated elements (size * pitch for matrices)
+  void* data = nullptr;
+  hipStream_t stream = nullptr;
+  int cus = 256;
+  // per-launch control words (LaunchCtl), zeroed before each ordered push
+  void* d_ctl = nullptr;
+  size_t ctl_bytes = 0;
+  ErrState* d_err = nullptr;
+  // grow-only device scratch for host-pointer calls and the deterministic path
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* d_det = nullptr;
+  size_t det_bytes = 0;
+  void* d_bin = nullptr;  // binned-push scratch
+  size_t bin_bytes = 0;
+  double bin_dedup_ratio = 0.0;  // distinct/records of the last deduplicating binned push
+  uint32_t bin_pushes = 0;
+  u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
+  u64* d_hint = nullptr;
+  i64 last_bad = -1;
+  // kernel timing (glint_prof_*): HIP event pairs recorded on the launch stream, summed lazily
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[GLINT_K_COUNT];
+  double prof_ms[GLINT_K_COUNT] = {0};
+  int64_t prof_n[GLINT_K_COUNT] = {0};
+  std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+#define HIPCHK(x)                                   \
+  do {                                              \
+    hipError_t e_ = (x);                            \
+    if (e_ != hipSuccess) {                         \
+      (void)hipGetLastError();                      \
+      return GLINT_EDEVICE;                         \
+    }                                               \
+  } while (0)
+
+inline size_t dtype_size(int dt) { return (dt == GLINT_I32 || dt == GLINT_F32) ? 4 : 8; }
+inline size_t pad256(size_t b) { return (b + 255) & ~(size_t)255; }
+inline bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+inline int grow(void** buf, size_t* cap, size_t need) {
+  if (*cap >= need) return GLINT_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  size_t sz = std::max(need, (size_t)1 << 20);
+  if (hipMalloc(buf, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    *buf = nullptr;
+    return GLINT_ENOMEM;
+  }
+  *cap = sz;
+  return GLINT_OK;
+}
+
+// device-resident calls run on the caller's stream exactly as given (NULL = the HIP null stream,
+// as in every HIP API), so they order with the caller's producers and consumers of the buffers
+inline hipStream_t pick(glint_shard*, void* stream) { return (hipStream_t)stream; }
+
+// Brackets one kernel launch with events on its stream when profiling is on.
+struct ProfScope {
+  glint_shard* s;
+  int id;
+  hipStream_t st;
+  hipEvent_t b = nullptr, e = nullptr;
+  ProfScope(glint_shard* s_, int id_, hipStream_t st_) : s(s_), id(id_), st(st_) {
+    if (!s->prof) return;
+    if (hipEventCreate(&b) != hipSuccess || hipEventCreate(&e) != hipSuccess) {
+      (void)hipGetLastError();
+      b = e = nullptr;
+      return;
+    }
+    (void)hipEventRecord(b, st);
+  }
+  ~ProfScope() {
+    if (!b) return;
+    (void)hipEventRecord(e, st);
+    s->prof_ev[id].emplace_back(b, e);
+  }
+};
+
+inline void prof_drain(glint_shard* s) {
+  for (int k = 0; k < GLINT_K_COUNT; ++k) {
+    for (auto& pr : s->prof_ev[k]) {
+      float ms = 0.f;
+      if (hipEventSynchronize(pr.second) == hipSuccess && hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+        s->prof_ms[k] += ms;
+        s->prof_n[k] += 1;
+      }
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    s->prof_ev[k].clear();
+  }
+  (void)hipGetLastError();
+}
+
+inline unsigned grid_for(i64 units, i64 per_block, i64 cap) {
+  i64 g = (units + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// resident blocks per CU for a kernel (occupancy query), capped at the measured best; the
+// environment variable `knob` (e.g. GLINT_CHECK_BPC) overrides it for tuning sweeps
+template <typename K>
+inline int blocks_per_cu(K kernel, int cap, const char* knob = nullptr) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kTPB, 0) != hipSuccess || b < 1) {
+    (void)hipGetLastError();
+    b = 2;
+  }
+  b = std::min(b, cap);
+  const char* env = knob ? getenv(knob) : nullptr;
+  if (env && atoi(env) > 0) b = atoi(env);
+  return b;
+}
+
+}  // namespace
+
+namespace glint {
+// sort-based tails of a push (glint_sort.hip), instantiated for V in {int, long long, float, double}
+// and MAT in {false, true}
+template <typename V, bool MAT>
+int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
+template <typename V, bool MAT>
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
+}  // namespace glint
