@@ -50,9 +50,9 @@ __device__ __forceinline__ void record_error(ErrState* e, i64 idx) {
 }
 
 // address of a record; false when the JVM would throw ArrayIndexOutOfBoundsException
-template <bool MAT>
+template <bool MAT, int KIND = -1>
 __device__ __forceinline__ bool rec_addr(const PartDesc& p, i64 key, int32_t col, i64& addr) {
-  const int32_t l = g2l(p, key);
+  const int32_t l = g2l<KIND>(p, key);
   bool ok = l >= 0 && l < p.size;
   if (MAT) {
     ok = ok && col >= 0 && col < p.cols;

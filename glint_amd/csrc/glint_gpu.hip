@@ -32,10 +32,10 @@ namespace glint {
 template <bool MAT> struct AddrT { typedef int32_t T; };
 template <> struct AddrT<true> { typedef i64 T; };
 
-template <bool MAT>
+template <bool MAT, int KIND = -1>
 __device__ __forceinline__ bool rec_addr_t(const PartDesc& p, i64 key, int32_t col, typename AddrT<MAT>::T& addr) {
   i64 ad;
-  const bool ok = rec_addr<MAT>(p, key, col, ad);
+  const bool ok = rec_addr<MAT, KIND>(p, key, col, ad);
   addr = (typename AddrT<MAT>::T)ad;
   return ok;
 }
@@ -48,7 +48,7 @@ __device__ __forceinline__ bool rec_addr_t(const PartDesc& p, i64 key, int32_t c
 // Waves work independently (no barriers) and stop once a break before their tile is known, so an
 // unordered push costs about one wave tile of reads per wave. Full tiles take a branch-free path
 // (a per-element bounds test would make hipcc wait for each load before issuing the next).
-template <bool MAT, bool FULL>
+template <bool MAT, bool FULL, int KIND>
 __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const int32_t* __restrict__ cols, i64 n,
                                            const PartDesc& part, LaunchCtl* ctl, i64* __restrict__ desc,
                                            u32 ntiles, u32 t, int lane) {
@@ -75,7 +75,7 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   const u32 brk = __builtin_amdgcn_readfirstlane(ld_relaxed(&ctl->brk_enc));
   if (brk != 0u && ntiles - brk < t) return false;
   A before = 0;
-  if (r_first > 0) rec_addr_t<MAT>(part, kb, cb, before);
+  if (r_first > 0) rec_addr_t<MAT, KIND>(part, kb, cb, before);
   bool mono = true, affine = true;
   A a_first = 0;
   A last = before;
@@ -84,8 +84,8 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
     const i64 r = 2 * (pbase + lane + (i64)j * 64);
     const bool h0 = FULL || r < n, h1 = FULL || r + 1 < n;
     A a0, a1;
-    const bool o0 = rec_addr_t<MAT>(part, k[j].x, MAT ? c[j].x : 0, a0);
-    const bool o1 = rec_addr_t<MAT>(part, k[j].y, MAT ? c[j].y : 0, a1);
+    const bool o0 = rec_addr_t<MAT, KIND>(part, k[j].x, MAT ? c[j].x : 0, a0);
+    const bool o1 = rec_addr_t<MAT, KIND>(part, k[j].y, MAT ? c[j].y : 0, a1);
     if (j == 0) a_first = __shfl(a0, 0);
     if (h1) mono = mono && (a1 > a0);
     A prev = __shfl_up(a1, 1);
@@ -111,7 +111,7 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   return true;
 }
 
-template <bool MAT>
+template <bool MAT, int KIND>
 __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict__ keys,
                                                           const int32_t* __restrict__ cols, i64 n,
                                                           PartDesc part, LaunchCtl* ctl, i64* __restrict__ desc,
@@ -121,8 +121,8 @@ __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict_
   const u32 nw = gridDim.x * (kTPB / 64);
   for (u32 t = w0; t < ntiles; t += nw) {
     const bool full = 2 * ((i64)t * (kTile / 2)) + kTile <= n;
-    const bool go = full ? check_tile<MAT, true>(keys, cols, n, part, ctl, desc, ntiles, t, lane)
-                         : check_tile<MAT, false>(keys, cols, n, part, ctl, desc, ntiles, t, lane);
+    const bool go = full ? check_tile<MAT, true, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane)
+                         : check_tile<MAT, false, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane);
     if (!go) return;
   }
 }
@@ -530,9 +530,10 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   HIPCHK(hipMemsetAsync(s->d_ctl, 0, sizeof(LaunchCtl), st));
   {
     const unsigned gc =
-        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT>, 2, "GLINT_CHECK_BPC"));
+        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT, 0>, 2, "GLINT_CHECK_BPC"));
     ProfScope pc(s, GLINT_K_PUSH_CHECK, st);
-    push_check_kernel<MAT><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
+    if (a.part.kind == 0) push_check_kernel<MAT, 0><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
+    else push_check_kernel<MAT, 1><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
     HIPCHK(hipGetLastError());
   }
   {

@@ -68,8 +68,12 @@ struct PartDesc {
   int64_t pitch;  // elements per row (matrix)
 };
 
+// KIND: 0 range, 1 cyclic (a kernel specialised per layout keeps the cyclic 64-bit division out of
+// the range hot path), -1 = read p.kind at run time
+template <int KIND = -1>
 __device__ __forceinline__ int32_t g2l(const PartDesc& p, i64 key) {
-  return p.kind == 0 ? (int32_t)(key - p.start) : (int32_t)((key - (i64)p.cidx) / (i64)p.cparts);
+  if (KIND == 0 || (KIND < 0 && p.kind == 0)) return (int32_t)(key - p.start);
+  return (int32_t)((key - (i64)p.cidx) / (i64)p.cparts);
 }
 
 template <typename V>
