@@ -114,9 +114,13 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
 template <bool MAT, int KIND>
 __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict__ keys,
                                                           const int32_t* __restrict__ cols, i64 n,
-                                                          PartDesc part, LaunchCtl* ctl, i64* __restrict__ desc,
-                                                          u32 ntiles) {
+                                                          PartDesc part, LaunchCtl* ctl, LaunchCtl* next,
+                                                          i64* __restrict__ desc, u32 ntiles) {
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next push's control words (no kernel of this push reads them)
+    next->brk_enc = 0u;
+    next->nonaffine = 0u;
+  }
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const u32 nw = gridDim.x * (kTPB / 64);
   for (u32 t = w0; t < ntiles; t += nw) {
@@ -506,11 +510,19 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.ntiles = (u32)ntiles;
   const bool vec_ok = aligned(keys, 16) && aligned(vals, 2 * sizeof(V)) && (!MAT || aligned(cols, 8));
   const bool det = (flags & GLINT_PUSH_DETERMINISTIC) && (s->dtype == GLINT_F32 || s->dtype == GLINT_F64);
-  // control region: [LaunchCtl | pad to 256][tile descriptors i64 x ntiles]
+  // control region: [LaunchCtl slot 0 | slot 1 | pad to 256][tile descriptors i64 x ntiles]. An
+  // ordered push uses one slot while its push_check zeroes the other for the next push, so no
+  // memset runs per push (pushes on one shard are stream-ordered, as the actor's messages are).
   const size_t ctl_need = 256 + (size_t)ntiles * sizeof(i64);
+  const void* ctl_old = s->d_ctl;
   int rc = grow(&s->d_ctl, &s->ctl_bytes, ctl_need);
   if (rc) return rc;
-  a.ctl = (LaunchCtl*)s->d_ctl;
+  if (s->d_ctl != ctl_old) {  // fresh region: both slots zero
+    HIPCHK(hipMemsetAsync(s->d_ctl, 0, 2 * sizeof(LaunchCtl), st));
+    s->ctl_par = 0;
+  }
+  LaunchCtl* const slots = (LaunchCtl*)s->d_ctl;
+  a.ctl = slots + s->ctl_par;
   i64* desc = (i64*)((char*)s->d_ctl + 256);
 
   const int bmode = binned_mode();
@@ -522,34 +534,29 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   if (!vec_ok) {  // unaligned caller pointers: the scalar-load scatter for everything
     if (det) return push_det_tail<V, MAT>(s, a, false, st);
     const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
-    ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
-    push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, 1);
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 1));
     return GLINT_OK;
   }
-  HIPCHK(hipMemsetAsync(s->d_ctl, 0, sizeof(LaunchCtl), st));
   {
+    LaunchCtl* const next = slots + (s->ctl_par ^ 1);
+    s->ctl_par ^= 1;
     const unsigned gc =
         grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT, 0>, 2, "GLINT_CHECK_BPC"));
-    ProfScope pc(s, GLINT_K_PUSH_CHECK, st);
-    if (a.part.kind == 0) push_check_kernel<MAT, 0><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
-    else push_check_kernel<MAT, 1><<<gc, kTPB, 0, st>>>(keys, cols, n, a.part, a.ctl, desc, a.ntiles);
-    HIPCHK(hipGetLastError());
+    HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
+                                       a.part, a.ctl, next, desc, a.ntiles)
+                            : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
+                                       a.part, a.ctl, next, desc, a.ntiles));
   }
   {
     const unsigned ga =
         grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_apply_kernel<V, MAT>, 2, "GLINT_APPLY_BPC"));
     a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * sweep_blocks_per_cu()));
-    ProfScope ps(s, GLINT_K_PUSH_APPLY, st);
-    push_apply_kernel<V, MAT><<<ga, kTPB, 0, st>>>(a, desc);
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch_k(s, GLINT_K_PUSH_APPLY, push_apply_kernel<V, MAT>, ga, kTPB, st, a, (const i64*)desc));
   }
   if (det) return push_det_tail<V, MAT>(s, a, true, st);
   if (binned) return push_binned<V, MAT>(s, a, true, st);
   const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
-  ProfScope ps(s, GLINT_K_PUSH_SCATTER, st);
-  push_scatter_kernel<V, MAT><<<g2, kTPB, 0, st>>>(a, 0);
-  HIPCHK(hipGetLastError());
+  HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 0));
   return GLINT_OK;
 }
 
@@ -559,16 +566,16 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   if (n <= 0) return GLINT_OK;
   if (!keys || !out) return GLINT_EINVAL;
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
-  ProfScope ps(s, GLINT_K_VEC_PULL, st);
   if (pairs) {
     // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5)
     const unsigned g = grid_for((n + 1) / 2, kTPB, (i64)s->cus * 4);
-    vec_pull_kernel<V, true><<<g, kTPB, 0, st>>>(keys, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+    HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, true>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
+                    (V*)out, s->d_err));
   } else {
     const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);
-    vec_pull_kernel<V, false><<<g, kTPB, 0, st>>>(keys, n, (const V*)s->data, s->part, (V*)out, s->d_err);
+    HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, false>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
+                    (V*)out, s->d_err));
   }
-  HIPCHK(hipGetLastError());
   return GLINT_OK;
 }
 
@@ -577,9 +584,8 @@ int launch_mat_pull(glint_shard* s, const i64* rows, const int32_t* cols, void* 
   if (n <= 0) return GLINT_OK;
   if (!rows || !cols || !out) return GLINT_EINVAL;
   const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);
-  ProfScope ps(s, GLINT_K_MAT_PULL, st);
-  mat_pull_kernel<V><<<g, kTPB, 0, st>>>(rows, cols, n, (const V*)s->data, s->part, (V*)out, s->d_err);
-  HIPCHK(hipGetLastError());
+  HIPCHK(launch_k(s, GLINT_K_MAT_PULL, mat_pull_kernel<V>, g, kTPB, st, rows, cols, n, (const V*)s->data, s->part,
+                  (V*)out, s->d_err));
   return GLINT_OK;
 }
 
@@ -589,12 +595,8 @@ int launch_mat_pull_rows(glint_shard* s, const i64* rows, void* out, i64 n, hipS
   if (!rows || !out) return GLINT_EINVAL;
   const bool v16 = ((i64)s->part.cols * (i64)sizeof(V)) % 16 == 0 && aligned(out, 16);
   const unsigned g = grid_for(n, kTPB / 64, (i64)s->cus * 8);
-  ProfScope ps(s, GLINT_K_MAT_PULL_ROWS, st);
-  if (v16)
-    mat_pull_rows_kernel<V, true><<<g, kTPB, 0, st>>>(rows, n, (const V*)s->data, s->part, (V*)out, s->d_err);
-  else
-    mat_pull_rows_kernel<V, false><<<g, kTPB, 0, st>>>(rows, n, (const V*)s->data, s->part, (V*)out, s->d_err);
-  HIPCHK(hipGetLastError());
+  HIPCHK(launch_k(s, GLINT_K_MAT_PULL_ROWS, v16 ? mat_pull_rows_kernel<V, true> : mat_pull_rows_kernel<V, false>, g,
+                  kTPB, st, rows, n, (const V*)s->data, s->part, (V*)out, s->d_err));
   return GLINT_OK;
 }
 

@@ -4,6 +4,8 @@
 #include "glint_kernels.h"
 #include "../../include/glint_gpu.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
@@ -24,6 +26,7 @@ struct glint_shard {
   // per-launch control words (LaunchCtl), zeroed before each ordered push
   void* d_ctl = nullptr;
   size_t ctl_bytes = 0;
+  int ctl_par = 0;  // which of the two LaunchCtl slots the next ordered push uses
   ErrState* d_err = nullptr;
   // grow-only device scratch for host-pointer calls and the deterministic path
   void* d_scratch = nullptr;
@@ -112,6 +115,23 @@ struct ProfScope {
     s->prof_ev[id].emplace_back(b, e);
   }
 };
+
+// Launches one kernel. With profiling on, its start/stop events ride on the kernel's own dispatch
+// packet (hipExtLaunchKernel), so timing adds no marker packets and no gaps to the stream; a
+// bracketing hipEventRecord pair costs ~8 us of stream time per kernel here.
+template <typename... KArgs, typename... Args>
+inline hipError_t launch_k(glint_shard* s, int id, void (*kernel)(KArgs...), unsigned grid, unsigned block,
+                           hipStream_t st, Args... args) {
+  hipEvent_t b = nullptr, e = nullptr;
+  if (s->prof && (hipEventCreate(&b) != hipSuccess || hipEventCreate(&e) != hipSuccess)) {
+    (void)hipGetLastError();
+    b = e = nullptr;
+  }
+  hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, st, b, e, 0, static_cast<KArgs>(args)...);
+  const hipError_t err = hipGetLastError();
+  if (b) s->prof_ev[id].emplace_back(b, e);
+  return err;
+}
 
 inline void prof_drain(glint_shard* s) {
   for (int k = 0; k < GLINT_K_COUNT; ++k) {

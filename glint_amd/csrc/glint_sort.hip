@@ -415,7 +415,7 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
   i64 r0 = 0;
   if (from_break) {
     LaunchCtl h{};
-    HIPCHK(hipMemcpyAsync(&h, s->d_ctl, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (h.brk_enc == 0u) return GLINT_OK;
     r0 = (i64)(a.ntiles - h.brk_enc) * kTile;
