@@ -11,6 +11,8 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
+#include <cstring>
+
 namespace glint {
 
 // ------------------------------------------------------------------------------------------------
@@ -467,8 +469,13 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   while (end_bit < 32 && ((i64)1 << end_bit) < s->elems) ++end_bit;
   const u32 nslabs = 1u << (end_bit - kSlabBits);
   const u32 mask = nslabs - 1u;
-  // dedup when the last probe found < 60 % distinct records per chunk; re-probe every 16 pushes
-  const bool dedup = s->bin_dedup_ratio < 0.6 || (++s->bin_pushes & 15) == 0;
+  // dedup when the last probe found < 60 % distinct records per chunk; re-probe every 16 pushes.
+  // GLINT_BIN_FRONT = dedup | prep forces one front end (tests, tuning).
+  bool dedup = s->bin_dedup_ratio < 0.6 || (++s->bin_pushes & 15) == 0;
+  if (const char* e = getenv("GLINT_BIN_FRONT")) {
+    if (!strcmp(e, "dedup")) dedup = true;
+    else if (!strcmp(e, "prep")) dedup = false;
+  }
   size_t sort_bytes = 0, scan_bytes = 0;
   HIPCHK(rocprim::radix_sort_pairs(nullptr, sort_bytes, (u32*)nullptr, (u32*)nullptr, (const V*)nullptr, (V*)nullptr,
                                    (size_t)n, kSlabBits, end_bit, st));

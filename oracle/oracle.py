@@ -41,11 +41,12 @@ _lib = None
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
-        if not LIB_PATH.exists():
-            import sys
-            sys.path.insert(0, str(HERE.parent))
-            from glint_amd.build import build_oracle  # builds only the oracle (gcc), not the product
-            build_oracle()
+        if not LIB_PATH.exists():  # build only the oracle (gcc), not the product; the build module is
+            import importlib.util  # loaded by path (the glint_amd package needs the built product)
+            spec = importlib.util.spec_from_file_location("_glint_build", HERE.parent / "glint_amd" / "build.py")
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            mod.build_oracle()
         L = C.CDLL(str(LIB_PATH))
         P, I64, I32 = C.c_void_p, C.c_int64, C.c_int32
         L.oracle_range_partitioner.argtypes = [I32, I64, P, P, P, P]

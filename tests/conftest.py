@@ -17,8 +17,12 @@ if str(ROOT) not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")
     config.addinivalue_line("markers", "slow: long-running")
-    from glint_amd.build import build_all
-    build_all()
+    # by path: importing the glint_amd package loads libglint_gpu.so, which a fresh checkout lacks
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_glint_build", ROOT / "glint_amd" / "build.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.build_all()
 
 
 @pytest.fixture(scope="session")

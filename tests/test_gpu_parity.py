@@ -530,6 +530,66 @@ def test_binned_dedup_policy(gpu):
             np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
+@pytest.mark.parametrize("front", ["dedup", "prep"])
+@pytest.mark.parametrize("dtype", ["double", "long"])
+@pytest.mark.parametrize("pattern", ["zipf", "hot_slab", "uniform", "with_prefix", "one_key"])
+def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
+    """Both front ends of the binned tail (GLINT_BIN_FRONT: per-chunk LDS dedup, plain address
+    prepare) against the oracle, on skewed and flat tails; Long is bit-exact."""
+    monkeypatch.setenv("GLINT_BIN_FRONT", front)
+    rng = np.random.default_rng(zlib.crc32(f"fronts/{front}/{dtype}/{pattern}".encode()))
+    start, size = 1 << 33, 2_000_003
+    part = RangePartition(2, start, start + size)
+    n = 1_500_000
+    if pattern == "zipf":
+        keys = rng.permutation(size)[np.minimum(rng.zipf(1.1, n) - 1, size - 1)]
+    elif pattern == "hot_slab":  # a few hundred hot elements inside one slab, plus a uniform tail
+        keys = np.concatenate([rng.integers(4096, 4096 + 300, n // 2), rng.integers(0, size, n - n // 2)])
+        keys = rng.permutation(keys)
+    elif pattern == "uniform":
+        keys = rng.integers(0, size, n)
+    elif pattern == "with_prefix":  # ordered prefix (plain path), then a skewed unordered tail
+        keys = np.concatenate([np.arange(0, size, 2), rng.permutation(size)[np.minimum(rng.zipf(1.3, n) - 1,
+                                                                                       size - 1)]])
+    else:  # every record on one element: the whole tail is one hot key
+        keys = np.full(n, size - 1)
+    keys = keys.astype(np.int64) + start
+    vals = rand_vals(rng, dtype, keys.size) if dtype == "double" else rng.integers(-1 << 40, 1 << 40, keys.size)
+    ref = oracle_vec(part, dtype)
+    with PartialVector(part, dtype, gpu) as sh:
+        for _ in range(2):
+            sh.update(keys, vals, unordered=(pattern != "with_prefix"))
+            assert ref.update(keys, vals) == -1
+        got = sh.to_numpy()
+        if dtype == "long":
+            np.testing.assert_array_equal(got, ref.data)
+        else:
+            np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9)
+        # an out-of-range record is reported (first bad index) and nothing else is corrupted
+        bad = keys.copy()
+        bad[777] = start + size + 5
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.update(bad, vals, unordered=True)
+        assert ei.value.record == 777
+
+
+@pytest.mark.parametrize("front", ["dedup", "prep"])
+def test_binned_fronts_matrix(gpu, monkeypatch, front):
+    monkeypatch.setenv("GLINT_BIN_FRONT", front)
+    rng = np.random.default_rng(23)
+    rows_n, cols_n = 30_011, 129  # pitch 130: row padding stays untouched
+    part = RangePartition(0, 0, rows_n)
+    r = np.minimum(rng.zipf(1.05, 1_200_000) - 1, rows_n - 1).astype(np.int64)
+    c = rng.integers(0, cols_n, r.size).astype(np.int32)
+    c[::3] = 7  # hot columns of hot rows
+    v = rng.integers(-1000, 1000, r.size).astype(np.int64)
+    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE["long"])
+    assert ref.update(r, c, v) == -1
+    with PartialMatrix(part, cols_n, "long", gpu) as sh:
+        sh.update(r, c, v, unordered=True)
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
 def test_loopback_harness_gpu_backend(gpu):
     """configs[0] over loopback TCP with HBM shards fed the raw wire images (glint_push_wire /
     glint_pull_wire): pulled values equal the pushed ones bit for bit."""
