@@ -175,7 +175,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+        # one push at a time: the adaptive tail switch reads the previous push's hint (written by
+        # its push_apply) at launch, so its one-time scratch allocation lands in the warm-up
+        torch.cuda.synchronize(dev)
     shard.sync(stream)
     lib.glint_prof_reset(h)
     lib.glint_prof_enable(h, 1)

@@ -12,3 +12,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ztrace -o run -- python3 bench.py --no-cpu-baseline --pattern zipf > $OUT/bench_zipf_traced.txt 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py > $OUT/bench_default.txt 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --log2-keys 30 --steps 10 > $OUT/bench_2p30.txt 2>&1 || exit 1
+timeout -k 10 400 python3 tools/measure_paths.py > $OUT/measure_paths.jsonl 2> $OUT/measure_paths.err || exit 1
+timeout -k 10 200 python3 tools/binned_probe.py > $OUT/binned_probe.jsonl 2>&1 || exit 1
