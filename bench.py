@@ -129,10 +129,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # rehearsal hooks (not used by the driver): GLINT_BENCH_DEVICE pins every rank to one GPU and
+    # GLINT_BENCH_BACKEND=gloo replaces RCCL, so the N > 1 path can run on a one-GPU box
+    local = int(os.environ.get("GLINT_BENCH_DEVICE", local))
+    backend = os.environ.get("GLINT_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     lib = N.load()
     per = 1 << args.log2_keys
@@ -194,7 +201,7 @@ def main():
     lib.glint_prof_enable(h, 0)
     shard.sync(stream)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
