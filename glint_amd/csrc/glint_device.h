@@ -69,4 +69,18 @@ __device__ __forceinline__ void lds_add(float* p, float v) { unsafeAtomicAdd(p, 
 __device__ __forceinline__ void lds_add(long long* p, long long v) { atomicAdd((u64*)p, (u64)v); }
 __device__ __forceinline__ void lds_add(int* p, int v) { atomicAdd((u32*)p, (u32)v); }
 
+// Type of an LDS partial sum of V. Float shards accumulate in double: ds_add_f32 runs ~20x slower
+// than ds_add_f64 on gfx950 (2.6 vs 0.12 cycles per lane per CU, tools/microbench_lds.hip,
+// profiles/r01/mb_lds.txt), and a single record's sum stays exact, so a key pushed once still
+// gets data + value rounded once, as PartialVector.scala:39 does.
+template <typename V> struct LdsAcc { typedef V T; };
+template <> struct LdsAcc<float> { typedef double T; };
+
+// d + (LDS partial sum a), rounded once: float((double)d + a) equals the float sum d + v when a
+// holds one float v (double carries > 2*24+2 bits, so the double rounding is innocuous)
+__device__ __forceinline__ double acc_add(double d, double a) { return d + a; }
+__device__ __forceinline__ float acc_add(float d, double a) { return (float)((double)d + a); }
+__device__ __forceinline__ long long acc_add(long long d, long long a) { return vadd(d, a); }
+__device__ __forceinline__ int acc_add(int d, int a) { return vadd(d, a); }
+
 }  // namespace glint

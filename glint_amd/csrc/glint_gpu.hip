@@ -331,10 +331,11 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
   const i64 nchunks = (rem + kScatterChunk - 1) / kScatterChunk;
   if ((i64)blockIdx.x >= nchunks) return;
 
+  typedef typename LdsAcc<V>::T A;
   __shared__ u64 hk[kHashSlots];
-  __shared__ V hv[kHashSlots];
+  __shared__ A hv[kHashSlots];
   const int tid = threadIdx.x;
-  for (int s = tid; s < kHashSlots; s += kTPB) { hk[s] = kEmpty; hv[s] = V(0); }
+  for (int s = tid; s < kHashSlots; s += kTPB) { hk[s] = kEmpty; hv[s] = A(0); }
   __syncthreads();
 
   for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
@@ -359,15 +360,15 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
         }
         h = (h + 1) & (kHashSlots - 1);
       }
-      lds_add(&hv[h], val);
+      lds_add(&hv[h], (A)val);
     }
     __syncthreads();
     for (int s = tid; s < kHashSlots; s += kTPB) {
       const u64 key = hk[s];
       if (key != kEmpty) {
-        gadd(a.data + key, hv[s]);
+        gadd(a.data + key, (V)hv[s]);
         hk[s] = kEmpty;
-        hv[s] = V(0);
+        hv[s] = A(0);
       }
     }
     __syncthreads();

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kTPB) void bin_prepare_kernel(const i64* __restrict
 // Duplicate-heavy tails: each workgroup first sums its chunk's records per element in an LDS hash
 // table and emits one (address, sum) per distinct element, so the sort and the apply see only
 // those. Output order is arbitrary (the default mode's contract); the count goes to *m_out.
-constexpr int kDedupSlots = 4096;   // u32 keys + V sums: 48 KiB for Double
+constexpr int kDedupSlots = 4096;   // u32 keys + 64-bit sums (LdsAcc): 48 KiB
 constexpr int kDedupChunk = 2048;   // records per table fill (load factor <= 0.5)
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
@@ -67,8 +67,9 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
                                                          const LaunchCtl* ctl, u32 ntiles, int from_break,
                                                          u32* __restrict__ addr_out, V* __restrict__ val_out,
                                                          u32* __restrict__ m_out, ErrState* err) {
+  typedef typename LdsAcc<V>::T A;
   __shared__ u32 hk[kDedupSlots];
-  __shared__ V hv[kDedupSlots];
+  __shared__ A hv[kDedupSlots];
   __shared__ u32 wsum[kTPB / 64];
   __shared__ u32 obase;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
     r0 = brk == 0u ? n : (i64)(ntiles - brk) * kTile;
   }
   if (blockIdx.x == 0 && tid == 0) m_out[1] = (u32)(n - r0);  // the tail size, for the host's ratio
-  for (int sl = tid; sl < kDedupSlots; sl += kTPB) { hk[sl] = kBinSentinel; hv[sl] = V(0); }
+  for (int sl = tid; sl < kDedupSlots; sl += kTPB) { hk[sl] = kBinSentinel; hv[sl] = A(0); }
   __syncthreads();
   const i64 nchunks = (n - r0 + kDedupChunk - 1) / kDedupChunk;
   for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
         }
         h = (h + 1) & (kDedupSlots - 1);
       }
-      lds_add(&hv[h], v[q]);
+      lds_add(&hv[h], (A)v[q]);
     }
     __syncthreads();
     // compact: count this thread's occupied slots, scan across the block, reserve, write
@@ -141,10 +142,10 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
       const u32 key = hk[sl];
       if (key != kBinSentinel) {
         addr_out[pos] = key;
-        val_out[pos] = hv[sl];
+        val_out[pos] = (V)hv[sl];
         ++pos;
         hk[sl] = kBinSentinel;
-        hv[sl] = V(0);
+        hv[sl] = A(0);
       }
     }
     __syncthreads();
@@ -203,7 +204,8 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
                                                             const u32* __restrict__ item_off, u32 nslabs,
                                                             i64 elems, V* __restrict__ data) {
   typedef typename Vec2<V>::T V2;
-  __shared__ V acc[kSlab];
+  typedef typename LdsAcc<V>::T A;
+  __shared__ A acc[kSlab];
   __shared__ uint8_t touched[kSlab];  // plain byte stores: no atomic serialisation on hot elements
   constexpr int kPairsPerThread = kSlab / 2 / kBinTPB;
   const int tid = threadIdx.x;
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
     const bool exclusive = d4.w != 0u;
     const i64 r_lo = d4.y, r_hi = d4.z;
     const i64 sbase_g = (i64)slab << kSlabBits;
-    for (int e = tid; e < kSlab; e += kBinTPB) acc[e] = V(0);
+    for (int e = tid; e < kSlab; e += kBinTPB) acc[e] = A(0);
     for (int w = tid; w < kSlab / 16; w += kBinTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     for (i64 j0 = r_lo; j0 < r_hi; j0 += (i64)kBinTPB * kBinRB) {
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
       for (int q = 0; q < kBinRB; ++q) {
         if (ad[q] == kBinSentinel) continue;
         const u32 e = ad[q] & (kSlab - 1);
-        lds_add(&acc[e], v[q]);
+        lds_add(&acc[e], (A)v[q]);
         touched[e] = 1;
       }
     }
@@ -256,16 +258,16 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
         const int e0 = 2 * (tid + q * kBinTPB);
         if (sbase_g + e0 + 1 < elems) {
           V2 r = d[q];
-          if (t[q] & 1u) r.x = vadd(r.x, acc[e0]);
-          if (t[q] & 2u) r.y = vadd(r.y, acc[e0 + 1]);
+          if (t[q] & 1u) r.x = acc_add(r.x, acc[e0]);
+          if (t[q] & 2u) r.y = acc_add(r.y, acc[e0 + 1]);
           *reinterpret_cast<V2*>(sbase + e0) = r;
         } else {  // the shard's last element, odd count
-          sbase[e0] = vadd(sbase[e0], acc[e0]);
+          sbase[e0] = acc_add(sbase[e0], acc[e0]);
         }
       }
     } else {
       for (int e = tid; e < kSlab; e += kBinTPB)
-        if (touched[e]) gadd(sbase + e, acc[e]);
+        if (touched[e]) gadd(sbase + e, (V)acc[e]);
     }
     __syncthreads();
   }

@@ -531,11 +531,14 @@ def test_binned_dedup_policy(gpu):
 
 
 @pytest.mark.parametrize("front", ["dedup", "prep"])
-@pytest.mark.parametrize("dtype", ["double", "long"])
-@pytest.mark.parametrize("pattern", ["zipf", "hot_slab", "uniform", "with_prefix", "one_key"])
+@pytest.mark.parametrize("dtype", ["double", "float", "long"])
+@pytest.mark.parametrize("pattern", ["zipf", "hot_slab", "uniform", "with_prefix", "one_key", "unique"])
 def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
     """Both front ends of the binned tail (GLINT_BIN_FRONT: per-chunk LDS dedup, plain address
-    prepare) against the oracle, on skewed and flat tails; Long is bit-exact."""
+    prepare) against the oracle, on skewed and flat tails; Long is bit-exact, and so is Float when
+    every key occurs once per push (its LDS partial sums are double, LdsAcc in glint_device.h).
+    Float sums over duplicates are checked against the exact (float64) sum within 1e-6 of the sum
+    of magnitudes per element -- the reference's sequential float order is one rounding of many."""
     monkeypatch.setenv("GLINT_BIN_FRONT", front)
     rng = np.random.default_rng(zlib.crc32(f"fronts/{front}/{dtype}/{pattern}".encode()))
     start, size = 1 << 33, 2_000_003
@@ -551,20 +554,31 @@ def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
     elif pattern == "with_prefix":  # ordered prefix (plain path), then a skewed unordered tail
         keys = np.concatenate([np.arange(0, size, 2), rng.permutation(size)[np.minimum(rng.zipf(1.3, n) - 1,
                                                                                        size - 1)]])
+    elif pattern == "unique":  # every key at most once per push, in random order
+        keys = rng.permutation(size)[:n]
     else:  # every record on one element: the whole tail is one hot key
         keys = np.full(n, size - 1)
     keys = keys.astype(np.int64) + start
-    vals = rand_vals(rng, dtype, keys.size) if dtype == "double" else rng.integers(-1 << 40, 1 << 40, keys.size)
+    if dtype == "long":
+        vals = rng.integers(-1 << 40, 1 << 40, keys.size)
+    else:
+        vals = rand_vals(rng, dtype, keys.size)
     ref = oracle_vec(part, dtype)
     with PartialVector(part, dtype, gpu) as sh:
         for _ in range(2):
             sh.update(keys, vals, unordered=(pattern != "with_prefix"))
             assert ref.update(keys, vals) == -1
         got = sh.to_numpy()
-        if dtype == "long":
+        if dtype == "long" or (dtype == "float" and pattern == "unique"):
             np.testing.assert_array_equal(got, ref.data)
-        else:
+        elif dtype == "double":
             np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9)
+        else:
+            exact = np.zeros(size)
+            mag = np.zeros(size)
+            np.add.at(exact, keys - start, 2 * vals.astype(np.float64))
+            np.add.at(mag, keys - start, 2 * np.abs(vals.astype(np.float64)))
+            assert np.all(np.abs(got.astype(np.float64) - exact) <= 1e-6 * mag + 1e-30)
         # an out-of-range record is reported (first bad index) and nothing else is corrupted
         bad = keys.copy()
         bad[777] = start + size + 5

@@ -27,8 +27,9 @@ def zipf_keys(rng, n_keys, n, s):
 n = 1 << 28
 rng = np.random.default_rng(42)
 dev = torch.device("cuda", 0)
-sh = glint_amd.PartialVector(glint_amd.RangePartition(0, 0, n), "double", 0)
-vals = torch.rand(n // 4, dtype=torch.float64, device=dev)
+dtype = os.environ.get("GLINT_PROBE_DTYPE", "double")  # double | float
+sh = glint_amd.PartialVector(glint_amd.RangePartition(0, 0, n), dtype, 0)
+vals = torch.rand(n // 4, dtype=torch.float64 if dtype == "double" else torch.float32, device=dev)
 fronts = sys.argv[1:] or ["dedup", "prep"]
 for name, keys in (("zipf1.1", torch.from_numpy(zipf_keys(rng, n, n // 4, 1.1)).to(dev)),
                    ("uniform", torch.randint(0, n, (n // 4,), dtype=torch.int64, device=dev))):
@@ -41,6 +42,6 @@ for name, keys in (("zipf1.1", torch.from_numpy(zipf_keys(rng, n, n // 4, 1.1)).
             sh.update(keys, vals, unordered=True)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        print(json.dumps({"pattern": name, "front": front, "records": int(keys.numel()),
+        print(json.dumps({"dtype": dtype, "pattern": name, "front": front, "records": int(keys.numel()),
                           "push_ms": [round(t, 3) for t in ts], "best_ms": round(min(ts[1:]), 3)}), flush=True)
 sh.destroy()
