@@ -489,6 +489,15 @@ int binned_mode() {
   return atoi(e) != 0 ? 1 : 0;
 }
 constexpr i64 kBinMin = (i64)1 << 20;  // records: below this the LDS-hash scatter wins
+// records: up to this many, a (non-deterministic) push is the single scatter launch.
+// GLINT_SMALL_PUSH overrides it (0 = always check + apply).
+i64 small_push_max() {
+  static const i64 v = [] {
+    const char* e = std::getenv("GLINT_SMALL_PUSH");
+    return e ? (i64)std::strtoll(e, nullptr, 10) : (i64)4096;
+  }();
+  return v;
+}
 
 template <typename V, bool MAT>
 int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void* vals, i64 n, int flags,
@@ -532,7 +541,12 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
   if (binned && unordered) return push_binned<V, MAT>(s, a, false, st);
-  if (!vec_ok) {  // unaligned caller pointers: the scalar-load scatter for everything
+  // Small pushes (an Akka message is ~1000 records, GranularBigVectorSpec.scala:21) are one launch:
+  // the scatter handles every record, instead of check + apply + scatter. Launch latency is the
+  // whole cost at this size, so two fewer launches is the win; results are those of the scatter
+  // path (bit-exact for unique keys and for Int/Long, unordered sums otherwise).
+  const bool small = !det && n <= small_push_max();
+  if (!vec_ok || small) {  // unaligned caller pointers or a small push: the scatter for everything
     if (det) return push_det_tail<V, MAT>(s, a, false, st);
     const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
     HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 1));
@@ -674,6 +688,10 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   }
   (void)hipGetLastError();
   if (!s->d_hint && s->h_hint) { (void)hipHostFree(s->h_hint); s->h_hint = nullptr; }
+  if (hipHostMalloc((void**)&s->h_err, sizeof(ErrState), hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    s->h_err = nullptr;  // host calls then read the error state with a pageable copy
+  }
   HIPCHK(hipMemsetAsync(s->data, 0, bytes, s->stream));  // new Array[V](size) is zeroed
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
@@ -693,6 +711,8 @@ void free_shard(glint_shard* s) {
     if (s->d_det) (void)hipFree(s->d_det);
     if (s->d_bin) (void)hipFree(s->d_bin);
     if (s->h_hint) (void)hipHostFree(s->h_hint);
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
+    if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     (void)hipGetLastError();
   }
@@ -920,31 +940,68 @@ int glint_mat_pull_rows_dev(glint_shard_t s, const int64_t* rows, void* out, int
 // ---- host-pointer entry points --------------------------------------------------------------------
 namespace {
 
-// stage host arrays into the shard's device scratch: returns device pointers to each section
+// Host arrays up to this size are staged through the shard's pinned buffer: one CPU memcpy per
+// section, then ONE DMA for the whole message (a pageable hipMemcpy costs a driver-side bounce and a
+// fence per section, which dominated small Akka-sized messages: ~1000 records per push,
+// GranularBigVectorSpec.scala:21). Larger arrays go straight from pageable memory at PCIe rate.
+// GLINT_PINNED_STAGE_MAX (bytes) overrides the crossover; tools/host_latency.py measures it.
+size_t pinned_stage_max() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLINT_PINNED_STAGE_MAX");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : ((size_t)2 << 20);
+  }();
+  return v;
+}
+
+// stage host arrays into the shard's device scratch: returns device pointers to each section and,
+// when the call is small enough, the pinned host block that mirrors the scratch (pinned = true)
 struct Staged {
   char* p[3] = {nullptr, nullptr, nullptr};
+  bool pinned = false;
+  size_t in_bytes = 0;  // bytes of the staged input sections (the pinned block's first part)
 };
 
 int stage(glint_shard* s, const void* const* src, const size_t* bytes, int count, Staged& out, size_t extra,
           char** extra_ptr) {
   size_t need = 0;
   for (int i = 0; i < count; ++i) need += pad256(bytes[i]);
+  out.in_bytes = need;
   need += pad256(extra);
   int rc = grow(&s->d_scratch, &s->scratch_bytes, need);
   if (rc) return rc;
+  out.pinned = need <= pinned_stage_max() && grow_pinned(&s->h_stage, &s->h_stage_bytes, need) == GLINT_OK;
   char* b = (char*)s->d_scratch;
+  char* h = (char*)s->h_stage;
   for (int i = 0; i < count; ++i) {
     out.p[i] = b;
-    if (bytes[i]) HIPCHK(hipMemcpyAsync(b, src[i], bytes[i], hipMemcpyHostToDevice, s->stream));
+    if (bytes[i]) {
+      if (out.pinned) std::memcpy(h, src[i], bytes[i]);
+      else HIPCHK(hipMemcpyAsync(b, src[i], bytes[i], hipMemcpyHostToDevice, s->stream));
+    }
     b += pad256(bytes[i]);
+    h += pad256(bytes[i]);
+  }
+  if (out.pinned && out.in_bytes) {
+    HIPCHK(hipMemcpyAsync(s->d_scratch, s->h_stage, out.in_bytes, hipMemcpyHostToDevice, s->stream));
   }
   if (extra_ptr) *extra_ptr = b;
   return GLINT_OK;
 }
 
+// Ends a host call: the device error state rides back with the call's last copy (pinned, async),
+// so a clean call costs one stream synchronisation.
 int finish(glint_shard* s) {
+  if (!s->h_err) {
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return collect_errors(s, s->stream, nullptr);
+  }
+  HIPCHK(hipMemcpyAsync(s->h_err, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
-  return collect_errors(s, s->stream, nullptr);
+  if (s->h_err->min_bad_enc == 0) return GLINT_OK;
+  s->last_bad = (i64)~s->h_err->min_bad_enc;
+  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return GLINT_EOUTOFRANGE;
 }
 
 int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols, const void* vals, int64_t n,
@@ -969,7 +1026,10 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
       GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)st.p[0], nullptr, st.p[1], n, flags, s->stream);
     }();
   }
-  if (rc) return rc;
+  if (rc) {
+    (void)hipStreamSynchronize(s->stream);  // the staging buffers stay busy until the stream drains
+    return rc;
+  }
   return finish(s);
 }
 
@@ -999,7 +1059,17 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
       GLINT_DISPATCH(s->dtype, launch_mat_pull_rows, s, (const i64*)st.p[0], d_out, n, s->stream);
     }();
   }
-  if (rc) return rc;
+  if (rc) {
+    (void)hipStreamSynchronize(s->stream);
+    return rc;
+  }
+  if (st.pinned) {  // answer into the pinned block behind the inputs, then one CPU copy out
+    char* h_out = (char*)s->h_stage + st.in_bytes;
+    HIPCHK(hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, s->stream));
+    rc = finish(s);
+    if (rc == GLINT_OK) std::memcpy(out, h_out, out_bytes);
+    return rc;
+  }
   HIPCHK(hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s->stream));
   return finish(s);
 }

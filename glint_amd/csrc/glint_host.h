@@ -37,6 +37,11 @@ struct glint_shard {
   size_t bin_bytes = 0;
   double bin_dedup_ratio = 0.0;  // distinct/records of the last deduplicating binned push
   uint32_t bin_pushes = 0;
+  // pinned host staging for host-pointer calls (grow-only, <= pinned_stage_max()): the caller's
+  // arrays are memcpy'd in and cross PCIe in one DMA; pull answers come back the same way
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
+  ErrState* h_err = nullptr;  // pinned: the device error state lands here with the push's last copy
   u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
   u64* d_hint = nullptr;
   i64 last_bad = -1;
@@ -82,6 +87,23 @@ inline int grow(void** buf, size_t* cap, size_t need) {
   *cap = 0;
   size_t sz = std::max(need, (size_t)1 << 20);
   if (hipMalloc(buf, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    *buf = nullptr;
+    return GLINT_ENOMEM;
+  }
+  *cap = sz;
+  return GLINT_OK;
+}
+
+// pinned host buffer, grow-only (hipHostFree of the old one after the caller's stream sync)
+inline int grow_pinned(void** buf, size_t* cap, size_t need) {
+  if (*cap >= need) return GLINT_OK;
+  if (*buf) (void)hipHostFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  size_t sz = (size_t)1 << 20;
+  while (sz < need) sz <<= 1;
+  if (hipHostMalloc(buf, sz, hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     *buf = nullptr;
     return GLINT_ENOMEM;

@@ -220,6 +220,42 @@ def test_out_of_range_raises(gpu):
         assert sh.get([107])[0] == 5
 
 
+# ---- small pushes: the one-launch path (<= 4096 records, the Akka message sizes) ------------------
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,pattern", [(1000, "dense"), (1000, "duplicates"), (4096, "permutation"),
+                                       (4097, "permutation"), (4096, "duplicates"), (3, "single_bad")])
+def test_small_push(gpu, dtype, n, pattern):
+    """Akka-sized messages (GranularBigVectorSpec.scala:21 slices 1000 records per push), replayed
+    many times onto one shard as a server sees them; 4096/4097 straddle the single-launch bound."""
+    rng = np.random.default_rng(zlib.crc32(f"small/{dtype}/{n}/{pattern}".encode()))
+    start, size = 77, 10_000
+    part = RangePartition(0, start, start + size)
+    ref = oracle_vec(part, dtype)
+    with PartialVector(part, dtype, gpu) as sh:
+        if pattern == "single_bad":  # record 1 is out of range: the others are applied, as in the reference
+            with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+                sh.update([start, start + size, start + 5], rand_vals(rng, dtype, 3))
+            assert ei.value.record == 1
+            return
+        for m in range(20):
+            if pattern == "dense":
+                keys = (np.arange(n, dtype=np.int64) + m * n // 4) % size + start
+            elif pattern == "permutation":
+                keys = rng.permutation(size)[:n].astype(np.int64) + start
+            else:
+                keys = rng.integers(0, 64, n).astype(np.int64) + start
+            vals = rand_vals(rng, dtype, n)
+            assert sh.update(keys, vals)
+            assert ref.update(keys, vals) == -1
+        got = sh.to_numpy()
+        if dtype in ("long", "int") or pattern != "duplicates":
+            np.testing.assert_array_equal(got, ref.data)
+        else:
+            np.testing.assert_allclose(got, ref.data, rtol=1e-6 if dtype == "double" else 1e-4,
+                                       atol=1e-9 if dtype == "double" else 2e-3)
+        np.testing.assert_array_equal(sh.get(keys), got[keys - start])
+
+
 # ---- matrix ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("cols", [512, 300, 7, 1])
