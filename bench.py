@@ -15,7 +15,12 @@ Algorithmic bytes per record: 8 (key) + 8 (value) + 8 + 8 (shar
 The roofline figure uses the push kernel's own device time from HIP events recorded around each
 launch on its stream (glint_prof_*); PMC HBM traffic comes from profiles/ when present.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--log2-keys 28] [--pattern dense|zipf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log2-keys 28] [--pattern dense|zipf|matrix]
+
+--pattern matrix is BASELINE.json configs[4] per GPU (weak scaling): a 2^17-row x 512-col Double
+shard of RangePartitioner(N, N * 2^17) rows (8 x 2^17 = the 2^20-row matrix at N = 8), pushed
+2^23 triplets (2^26 / 8) with rows Zipf(1.0) and cols uniform: PartialMatrix.update
+(PartialMatrix.scala:74-83) through glint_mat_push_dev. Algorithmic bytes n(8+4+8) + 16U.
 """
 from __future__ import annotations
 
@@ -40,7 +45,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2-keys", type=int, default=28, help="keys per GPU shard (cfg2: 28, north star: 30)")
-    ap.add_argument("--pattern", choices=["dense", "zipf"], default="dense")
+    ap.add_argument("--pattern", choices=["dense", "zipf", "matrix"], default="dense",
+                    help="dense: cfg2/cfg4a; zipf: cfg3; matrix: cfg5 per GPU (2^17 x 512 Double rows, "
+                         "2^23 Zipf(1.0)-row x uniform-col triplets)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run shard check")
@@ -121,7 +128,7 @@ def main():
     import torch
     import torch.distributed as dist
     import glint_amd
-    from glint_amd import PartialVector, RangePartitioner
+    from glint_amd import PartialMatrix, PartialVector, RangePartitioner
     from glint_amd import _native as N
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,15 +149,32 @@ def main():
             dist.init_process_group(backend)
 
     lib = N.load()
-    per = 1 << args.log2_keys
+    mat = args.pattern == "matrix"
+    per = (1 << 17) if mat else (1 << args.log2_keys)
     partitioner = RangePartitioner.apply(world, world * per)
     part = partitioner.all()[rank]
-    shard = PartialVector(part, "double", device=local)
+    cols_n = 512
+    shard = PartialMatrix(part, cols_n, "double", device=local) if mat else PartialVector(part, "double", device=local)
     n = part.size
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
-    vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
-    if args.pattern == "dense":
+    vals = torch.rand(n if not mat else 1 << 23, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+    cols = None
+    if mat:
+        # cfg5: rows Zipf(1.0) (word frequency; inverse CDF of the 1/k law) through a seeded
+        # permutation of the shard's rows, cols uniform [0, 512), seed 42 + rank
+        rng = np.random.default_rng(42 + rank)
+        nrec = 1 << 23
+        ranks = np.minimum(np.floor(np.power(float(n), rng.random(nrec))).astype(np.int64) - 1, n - 1)
+        r = rng.permutation(n)[ranks].astype(np.int64)
+        c = rng.integers(0, cols_n, nrec).astype(np.int32)
+        uniq = int(np.unique(r * cols_n + c).size)
+        keys = torch.from_numpy(r + part.start).to(dev)
+        cols = torch.from_numpy(c).to(dev)
+        tag = "matrix_2p17x512"
+        workload = (f"cfg5 per GPU: {nrec} Zipf(1.0)-row x uniform-col triplets into a 2^17 x 512 Double "
+                    f"matrix shard of RangePartitioner({world}, {world}x2^17) rows")
+    elif args.pattern == "dense":
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
         nrec, uniq = n, n
         tag = f"dense_2p{args.log2_keys}"
@@ -176,7 +200,10 @@ def main():
     h = shard.handle
 
     def step():
-        rc = lib.glint_vec_push_dev(h, keys.data_ptr(), vals.data_ptr(), nrec, 0, stream)
+        if mat:
+            rc = lib.glint_mat_push_dev(h, keys.data_ptr(), cols.data_ptr(), vals.data_ptr(), nrec, 0, stream)
+        else:
+            rc = lib.glint_vec_push_dev(h, keys.data_ptr(), vals.data_ptr(), nrec, 0, stream)
         if rc:
             raise RuntimeError(N.strerror(rc))
 
@@ -217,20 +244,40 @@ def main():
     if apply_n:
         bin_ms = bin_ms * bin_n / apply_n  # per push (the binned pipeline may skip the warm-up pushes)
 
-    # post-run check: the shard must hold (W+K) sequential additions of each value (bit-exact for
-    # the ordered path); for zipf, a sample checked against the oracle would need the CPU: skip
+    # post-run check: the shard must hold (W+K) additions of each record. Dense: bit-exact (each key
+    # once per push, the ordered path). Zipf / matrix: repeated keys sum in an unordered way, so the
+    # check is a torch fp64 index_add of one push times (W+K), within the north star's 1e-6 relative.
     ok = None
-    if not args.no_check and args.pattern == "dense":
-        acc = torch.zeros_like(vals)
-        for _ in range(args.warmup + args.steps):
-            acc += vals
-        got = shard.get(keys)
-        ok = bool(torch.equal(got, acc))
-        del acc, got
+    if not args.no_check:
+        reps = args.warmup + args.steps
+        if args.pattern == "dense":
+            acc = torch.zeros_like(vals)
+            for _ in range(reps):
+                acc += vals
+            got = shard.get(keys)
+            ok = bool(torch.equal(got, acc))
+            del acc
+        else:
+            if mat:
+                addr = (keys - part.start) * cols_n + cols.to(torch.int64)
+                got = shard.getRows(torch.arange(part.start, part.end, dtype=torch.int64, device=dev)).reshape(-1)
+            else:
+                addr = keys - part.start
+                got = shard.get(torch.arange(part.start, part.end, dtype=torch.int64, device=dev))
+            # segment sums over the sorted addresses (an atomic index_add_ serialises on Zipf's hot key)
+            a, order = torch.sort(addr)
+            uq, counts = torch.unique_consecutive(a, return_counts=True)
+            sums = torch.segment_reduce(vals[order], "sum", lengths=counts) * reps
+            ok = bool(torch.allclose(got[uq], sums, rtol=1e-6, atol=1e-9 * reps))
+            got[uq] = 0
+            ok = ok and not bool(got.any())  # nothing outside the pushed addresses
+            del a, order, uq, counts, sums, addr
+        del got
         if not ok:
             raise SystemExit("post-run shard check FAILED")
 
-    bytes_per_step = 16.0 * nrec + 16.0 * uniq  # n(8+8) + U(8+8)
+    # vector n(8+8) + U(8+8); matrix n(8+4+8) + U(8+8)
+    bytes_per_step = (20.0 if mat else 16.0) * nrec + 16.0 * uniq
     value = world * bytes_per_step * args.steps / dt / 1e9
     # The push is push_check (reads the keys: 8 B/record) + push_apply (values and shard: 24 B/record
     # for a dense push) + the unordered tail (push_scatter, or the binned pipeline for large tails).
@@ -253,7 +300,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (keys per BASELINE.md config, values U[-1,1) seed 42+rank), resident in HBM",
-        "config": {"workload": workload, "keys_per_gpu": n, "records_per_step_per_gpu": nrec,
+        "config": {"workload": workload, "keys_per_gpu": n * (cols_n if mat else 1), "records_per_step_per_gpu": nrec,
                    "distinct_keys_per_step_per_gpu": uniq, "key_dtype": "i64", "value_dtype": "f64",
                    "parallelism": f"range-sharded x{world}, no exchange"},
         "pct_hbm_peak_per_gpu": round(100.0 * value / world / HBM_PEAK_GBS, 2),
