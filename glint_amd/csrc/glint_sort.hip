@@ -70,9 +70,11 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
   typedef typename LdsAcc<V>::T A;
   __shared__ u32 hk[kDedupSlots];
   __shared__ A hv[kDedupSlots];
-  __shared__ u32 wsum[kTPB / 64];
-  __shared__ u32 obase;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // slots claimed in this chunk, in claim order: the compaction walks only these (distinct <=
+  // kDedupChunk) instead of scanning and re-zeroing the whole table
+  __shared__ uint16_t used[kDedupChunk];
+  __shared__ u32 nused, obase, olen;
+  const int tid = threadIdx.x, lane = tid & 63;
   i64 r0 = 0;
   if (from_break) {
     const u32 brk = ctl->brk_enc;
@@ -80,7 +82,9 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
   }
   if (blockIdx.x == 0 && tid == 0) m_out[1] = (u32)(n - r0);  // the tail size, for the host's ratio
   for (int sl = tid; sl < kDedupSlots; sl += kTPB) { hk[sl] = kBinSentinel; hv[sl] = A(0); }
+  if (tid == 0) nused = 0;
   __syncthreads();
+  const u64 below = (1ull << lane) - 1ull;
   const i64 nchunks = (n - r0 + kDedupChunk - 1) / kDedupChunk;
   for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const i64 c0 = r0 + ch * kDedupChunk, c1 = min(n, c0 + kDedupChunk);
@@ -99,54 +103,51 @@ __global__ __launch_bounds__(kTPB) void bin_dedup_kernel(const i64* __restrict__
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const i64 i = c0 + q * kTPB + tid;
-      if (i >= c1) continue;
-      i64 ad64;
-      if (!rec_addr<MAT>(part, k[q], cl[q], ad64)) { record_error(err, i); continue; }
-      const u32 ad = (u32)ad64;
-      u32 h = (ad * 0x9E3779B1u) >> (32 - 12);
-      for (;;) {
-        const u32 cur = hk[h];
-        if (cur == ad) break;
-        if (cur == kBinSentinel) {
-          const u32 prev = atomicCAS(&hk[h], kBinSentinel, ad);
-          if (prev == kBinSentinel || prev == ad) break;
+      bool claimed = false;
+      u32 h = 0;
+      if (i < c1) {
+        i64 ad64;
+        if (!rec_addr<MAT>(part, k[q], cl[q], ad64)) {
+          record_error(err, i);
+        } else {
+          const u32 ad = (u32)ad64;
+          h = (ad * 0x9E3779B1u) >> (32 - 12);
+          for (;;) {
+            const u32 cur = hk[h];
+            if (cur == ad) break;
+            if (cur == kBinSentinel) {
+              const u32 prev = atomicCAS(&hk[h], kBinSentinel, ad);
+              if (prev == kBinSentinel) { claimed = true; break; }
+              if (prev == ad) break;
+            }
+            h = (h + 1) & (kDedupSlots - 1);
+          }
+          lds_add(&hv[h], (A)v[q]);
         }
-        h = (h + 1) & (kDedupSlots - 1);
       }
-      lds_add(&hv[h], (A)v[q]);
+      // the wave's new slots join the list with one LDS atomic (every lane reaches the ballot)
+      const u64 b = __ballot(claimed);
+      if (b) {
+        u32 base = 0;
+        if (lane == 0) base = atomicAdd(&nused, (u32)__popcll(b));
+        base = __shfl(base, 0);
+        if (claimed) used[base + (u32)__popcll(b & below)] = (uint16_t)h;
+      }
     }
-    __syncthreads();
-    // compact: count this thread's occupied slots, scan across the block, reserve, write
-    constexpr int kSlotsPer = kDedupSlots / kTPB;
-    u32 cnt = 0;
-#pragma unroll
-    for (int q = 0; q < kSlotsPer; ++q) cnt += hk[tid * kSlotsPer + q] != kBinSentinel;
-    u32 incl = cnt;  // wave-inclusive scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const u32 y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
-    if (lane == 63) wsum[wid] = incl;
     __syncthreads();
     if (tid == 0) {
-      u32 t = 0;
-      for (int w = 0; w < kTPB / 64; ++w) { const u32 x = wsum[w]; wsum[w] = t; t += x; }
-      obase = atomicAdd(m_out, t);
+      olen = nused;
+      obase = atomicAdd(m_out, olen);
+      nused = 0;
     }
     __syncthreads();
-    u32 pos = obase + wsum[wid] + incl - cnt;
-#pragma unroll
-    for (int q = 0; q < kSlotsPer; ++q) {
-      const int sl = tid * kSlotsPer + q;
-      const u32 key = hk[sl];
-      if (key != kBinSentinel) {
-        addr_out[pos] = key;
-        val_out[pos] = (V)hv[sl];
-        ++pos;
-        hk[sl] = kBinSentinel;
-        hv[sl] = A(0);
-      }
+    const u32 len = olen, ob = obase;
+    for (u32 j = tid; j < len; j += kTPB) {  // contiguous, coalesced output of the chunk's sums
+      const u32 sl = used[j];
+      addr_out[ob + j] = hk[sl];
+      val_out[ob + j] = (V)hv[sl];
+      hk[sl] = kBinSentinel;
+      hv[sl] = A(0);
     }
     __syncthreads();
   }
