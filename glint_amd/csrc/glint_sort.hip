@@ -532,7 +532,11 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   bin_item_map_kernel<<<gs, 256, 0, st>>>(start, items, item_off, nslabs, item_desc);
   HIPCHK(hipGetLastError());
   const i64 mi = (i64)nslabs + (m + kBinItem - 1) / kBinItem;
-  bin_apply_kernel<V><<<(unsigned)std::min<i64>(mi, (i64)s->cus * 8), kBinTPB, 0, st>>>(
+  static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
+    const char* e = getenv("GLINT_BIN_APPLY_BPC");
+    return (e && atoi(e) > 0) ? atoi(e) : 64;  // swept 4..all: 32-128 best (profiles/r01/bin_apply_bpc.txt)
+  }();
+  bin_apply_kernel<V><<<(unsigned)std::min<i64>(mi, (i64)s->cus * apply_bpc), kBinTPB, 0, st>>>(
       addr_out, val_out, item_desc, item_off, nslabs, s->elems, a.data);
   HIPCHK(hipGetLastError());
   return GLINT_OK;
