@@ -203,7 +203,7 @@ template <typename V>
 __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restrict__ addr, const V* __restrict__ val,
                                                             const uint4* __restrict__ item_desc,
                                                             const u32* __restrict__ item_off, u32 nslabs,
-                                                            i64 elems, V* __restrict__ data) {
+                                                            i64 elems, V* __restrict__ data, u32 pre_min) {
   typedef typename Vec2<V>::T V2;
   typedef typename LdsAcc<V>::T A;
   __shared__ A acc[kSlab];
@@ -217,6 +217,18 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
     const bool exclusive = d4.w != 0u;
     const i64 r_lo = d4.y, r_hi = d4.z;
     const i64 sbase_g = (i64)slab << kSlabBits;
+    V* const sbase = data + sbase_g;
+    // A slab item with many records touches most of its lines: pull the slab into L2 now (one
+    // dword per 128-B line), so the fetch overlaps the record phase and the RMW's loads below hit
+    // in cache. Into registers it would cost the kernel its occupancy (246 VGPRs, measured).
+    const bool pre = exclusive && (u32)(r_hi - r_lo) >= pre_min;
+    u32 warm = 0;
+    if (pre) {
+      constexpr int kLines = kSlab * (int)sizeof(V) / 128;
+      constexpr int kPerLine = 128 / (int)sizeof(V);
+      for (int l = tid; l < kLines; l += kBinTPB)
+        if (sbase_g + (i64)l * kPerLine < elems) warm ^= *reinterpret_cast<const u32*>(sbase + (i64)l * kPerLine);
+    }
     for (int e = tid; e < kSlab; e += kBinTPB) acc[e] = A(0);
     for (int w = tid; w < kSlab / 16; w += kBinTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
     __syncthreads();
@@ -239,8 +251,8 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
         touched[e] = 1;
       }
     }
+    asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
     __syncthreads();
-    V* const sbase = data + sbase_g;
     if (exclusive) {
       // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair
       // instead (one cached line), so all loads issue back to back without a branch
@@ -461,6 +473,16 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
   return GLINT_OK;
 }
 
+// records per slab item from which bin_apply prefetches the whole slab (GLINT_BIN_PREFETCH_MIN;
+// 0xFFFFFFFF disables)
+u32 bin_prefetch_min() {
+  static const u32 v = [] {
+    const char* e = getenv("GLINT_BIN_PREFETCH_MIN");
+    return e ? (u32)strtoul(e, nullptr, 10) : (u32)(kSlab / 4);
+  }();
+  return v;
+}
+
 // The binned tail pipeline over the whole push (records before push_check's break are masked on
 // the device, so no host round trip is needed): prepare -> radix sort by slab -> slab bounds ->
 // item scan -> item map -> LDS slab apply.
@@ -537,7 +559,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     return (e && atoi(e) > 0) ? atoi(e) : 64;  // swept 4..all: 32-128 best (profiles/r01/bin_apply_bpc.txt)
   }();
   bin_apply_kernel<V><<<(unsigned)std::min<i64>(mi, (i64)s->cus * apply_bpc), kBinTPB, 0, st>>>(
-      addr_out, val_out, item_desc, item_off, nslabs, s->elems, a.data);
+      addr_out, val_out, item_desc, item_off, nslabs, s->elems, a.data, bin_prefetch_min());
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }
