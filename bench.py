@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2-keys", type=int, default=28, help="keys per GPU shard (cfg2: 28, north star: 30)")
-    ap.add_argument("--pattern", choices=["dense", "zipf", "matrix"], default="dense",
+    ap.add_argument("--pattern", choices=["dense", "zipf", "matrix", "exchange"], default="dense",
                     help="dense: cfg2/cfg4a; zipf: cfg3; matrix: cfg5 per GPU (2^17 x 512 Double rows, "
                          "2^23 Zipf(1.0)-row x uniform-col triplets)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
@@ -142,7 +142,13 @@ def main():
     backend = os.environ.get("GLINT_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    exch = args.pattern == "exchange"
+    if world > 1 or exch:
+        if world == 1:  # the exchange path needs a process group even alone (RCCL world 1)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29561")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -174,6 +180,21 @@ def main():
         tag = "matrix_2p17x512"
         workload = (f"cfg5 per GPU: {nrec} Zipf(1.0)-row x uniform-col triplets into a 2^17 x 512 Double "
                     f"matrix shard of RangePartitioner({world}, {world}x2^17) rows")
+    elif exch:
+        # cfg4b: every rank's batch holds keys of every rank's range (uniform over the whole key
+        # space), so each push is route (glint_route_dev) + all_to_all_single + the local push
+        from glint_amd.dist import DistributedBigVector
+        dv = DistributedBigVector(partitioner, [shard], world * per, np.float64, None, dev)
+        nrec = 1 << 26
+        kg = torch.Generator(device=dev)
+        kg.manual_seed(1042 + rank)
+        keys = torch.randint(0, world * per, (nrec,), dtype=torch.int64, device=dev, generator=kg)
+        vals = vals[:nrec].contiguous()
+        # distinct elements a rank receives per push (uniform, ~nrec records into per keys): expected value
+        uniq = int(per * (1.0 - np.exp(-nrec / per)))
+        tag = f"exchange_2p{args.log2_keys}"
+        workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({world}, "
+                    f"{world}x2^{args.log2_keys}); route + RCCL all-to-all + local push (U estimated)")
     elif args.pattern == "dense":
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
         nrec, uniq = n, n
@@ -200,6 +221,9 @@ def main():
     h = shard.handle
 
     def step():
+        if exch:
+            dv.push(keys, vals)
+            return
         if mat:
             rc = lib.glint_mat_push_dev(h, keys.data_ptr(), cols.data_ptr(), vals.data_ptr(), nrec, 0, stream)
         else:
@@ -248,7 +272,7 @@ def main():
     # once per push, the ordered path). Zipf / matrix: repeated keys sum in an unordered way, so the
     # check is a torch fp64 index_add of one push times (W+K), within the north star's 1e-6 relative.
     ok = None
-    if not args.no_check:
+    if not args.no_check and not exch:  # the exchange layer's parity lives in tests/ (dist_workers)
         reps = args.warmup + args.steps
         if args.pattern == "dense":
             acc = torch.zeros_like(vals)
@@ -302,7 +326,7 @@ def main():
         "data": "synthetic (keys per BASELINE.md config, values U[-1,1) seed 42+rank), resident in HBM",
         "config": {"workload": workload, "keys_per_gpu": n * (cols_n if mat else 1), "records_per_step_per_gpu": nrec,
                    "distinct_keys_per_step_per_gpu": uniq, "key_dtype": "i64", "value_dtype": "f64",
-                   "parallelism": f"range-sharded x{world}, no exchange"},
+                   "parallelism": f"range-sharded x{world}, " + ("route + all-to-all exchange" if exch else "no exchange")},
         "pct_hbm_peak_per_gpu": round(100.0 * value / world / HBM_PEAK_GBS, 2),
         "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -318,7 +342,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     shard.destroy()
-    if world > 1:
+    if world > 1 or exch:
         dist.destroy_process_group()
 
 
