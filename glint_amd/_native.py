@@ -18,6 +18,7 @@ GLINT_PUSH_DEFAULT, GLINT_PUSH_DETERMINISTIC, GLINT_PUSH_UNORDERED = 0, 1, 2
 GLINT_K_PUSH_APPLY, GLINT_K_PUSH_SCATTER, GLINT_K_VEC_PULL, GLINT_K_MAT_PULL, GLINT_K_MAT_PULL_ROWS = 0, 1, 2, 3, 4
 GLINT_K_PUSH_CHECK = 5
 GLINT_K_PUSH_BINNED = 6
+GLINT_K_PUSH_ORDERED = 7
 GLINT_ROUTE_RANGE, GLINT_ROUTE_CYCLIC = 0, 1
 
 # every symbol include/glint_gpu.h declares, with its C signature

@@ -519,7 +519,14 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   if (ntiles >= (i64)0xFFFFFFF0ll) return GLINT_EINVAL;
   a.ntiles = (u32)ntiles;
   const bool vec_ok = aligned(keys, 16) && aligned(vals, 2 * sizeof(V)) && (!MAT || aligned(cols, 8));
-  const bool det = (flags & GLINT_PUSH_DETERMINISTIC) && (s->dtype == GLINT_F32 || s->dtype == GLINT_F64);
+  const bool fp = s->dtype == GLINT_F32 || s->dtype == GLINT_F64;
+  const bool det = (flags & GLINT_PUSH_DETERMINISTIC) && fp;
+  const bool unordered = (flags & GLINT_PUSH_UNORDERED) != 0;
+  // Message-sized Float/Double pushes that must keep the reference's summation order -- every
+  // deterministic one, and host-pointer / wire pushes unless the caller said UNORDERED -- are one
+  // launch of the order-preserving fold (glint_ordered.hip). Int/Long sums are exact in any order.
+  const bool seq = det || (fp && (flags & kPushHostSequential) && !unordered);
+  if (seq && n <= kOrderedMax && s->elems < ((i64)1 << 32)) return push_ordered<V, MAT>(s, a, st);
   // control region: [LaunchCtl slot 0 | slot 1 | pad to 256][tile descriptors i64 x ntiles]. An
   // ordered push uses one slot while its push_check zeroes the other for the next push, so no
   // memset runs per push (pushes on one shard are stream-ordered, as the actor's messages are).
@@ -536,7 +543,6 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   i64* desc = (i64*)((char*)s->d_ctl + 256);
 
   const int bmode = binned_mode();
-  const bool unordered = (flags & GLINT_PUSH_UNORDERED) != 0;
   const i64 last_tail = s->h_hint ? (i64)__atomic_load_n(s->h_hint, __ATOMIC_RELAXED) : 0;
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
@@ -554,13 +560,13 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   }
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
-    s->ctl_par ^= 1;
     const unsigned gc =
         grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT, 0>, 2, "GLINT_CHECK_BPC"));
     HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
                                        a.part, a.ctl, next, desc, a.ntiles)
                             : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
                                        a.part, a.ctl, next, desc, a.ntiles));
+    s->ctl_par ^= 1;  // only once the check that zeroes the other slot is on the stream
   }
   {
     const unsigned ga =
@@ -714,6 +720,7 @@ void free_shard(glint_shard* s) {
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->order_ev) (void)hipEventDestroy(s->order_ev);
     (void)hipGetLastError();
   }
   delete s;
@@ -824,6 +831,8 @@ int glint_shard_zero(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  int rc = order_after_dev(s);
+  if (rc) return rc;
   HIPCHK(hipMemsetAsync(s->data, 0, (size_t)s->elems * s->vsize, s->stream));
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
@@ -887,8 +896,9 @@ int glint_shard_sync(glint_shard_t s, void* stream, int64_t* first_bad) {
   if (!s) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
-  hipStream_t st = pick(s, stream);
+  hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(st));
+  if (st == s->last_dev_stream) s->dev_dirty = false;  // everything enqueued there has completed
   return collect_errors(s, st, first_bad);
 }
 
@@ -1011,19 +1021,22 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
   if (n == 0) return GLINT_OK;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  int rc = order_after_dev(s);
+  if (rc) return rc;
   Staged st;
   const void* src[3] = {keys, mat ? (const void*)cols : vals, vals};
   size_t bytes[3] = {(size_t)n * 8, mat ? (size_t)n * 4 : (size_t)n * s->vsize, (size_t)n * s->vsize};
-  int rc = stage(s, src, bytes, mat ? 3 : 2, st, 0, nullptr);
+  rc = stage(s, src, bytes, mat ? 3 : 2, st, 0, nullptr);
   if (rc) return rc;
+  const int hflags = flags | kPushHostSequential;  // the actor's update: message order by default
   if (mat) {
     rc = [&]() -> int {
-      GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)st.p[0], (const int32_t*)st.p[1], st.p[2], n, flags,
+      GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)st.p[0], (const int32_t*)st.p[1], st.p[2], n, hflags,
                      s->stream);
     }();
   } else {
     rc = [&]() -> int {
-      GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)st.p[0], nullptr, st.p[1], n, flags, s->stream);
+      GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)st.p[0], nullptr, st.p[1], n, hflags, s->stream);
     }();
   }
   if (rc) {
@@ -1040,12 +1053,14 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   if (n == 0) return GLINT_OK;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  int rc = order_after_dev(s);
+  if (rc) return rc;
   const size_t out_bytes = (size_t)n * s->vsize * (kind == 2 ? (size_t)s->part.cols : 1);
   Staged st;
   const void* src[2] = {keys, cols};
   size_t bytes[2] = {(size_t)n * 8, kind == 1 ? (size_t)n * 4 : 0};
   char* d_out = nullptr;
-  int rc = stage(s, src, bytes, kind == 1 ? 2 : 1, st, out_bytes, &d_out);
+  rc = stage(s, src, bytes, kind == 1 ? 2 : 1, st, out_bytes, &d_out);
   if (rc) return rc;
   if (kind == 0) {
     rc = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)st.p[0], d_out, n, s->stream); }();

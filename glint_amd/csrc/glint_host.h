@@ -45,6 +45,11 @@ struct glint_shard {
   u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
   u64* d_hint = nullptr;
   i64 last_bad = -1;
+  // ordering of host-pointer calls (private stream) after device-resident calls (caller's stream):
+  // the last stream a *_dev call used; a host call records an event there and waits on it
+  hipStream_t last_dev_stream = nullptr;
+  bool dev_dirty = false;
+  hipEvent_t order_ev = nullptr;
   // kernel timing (glint_prof_*): HIP event pairs recorded on the launch stream, summed lazily
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[GLINT_K_COUNT];
@@ -114,7 +119,29 @@ inline int grow_pinned(void** buf, size_t* cap, size_t need) {
 
 // device-resident calls run on the caller's stream exactly as given (NULL = the HIP null stream,
 // as in every HIP API), so they order with the caller's producers and consumers of the buffers
-inline hipStream_t pick(glint_shard*, void* stream) { return (hipStream_t)stream; }
+inline hipStream_t pick(glint_shard* s, void* stream) {
+  s->last_dev_stream = (hipStream_t)stream;
+  s->dev_dirty = true;
+  return (hipStream_t)stream;
+}
+
+// A host-pointer call runs on the shard's private stream: it first waits for everything the
+// caller has enqueued on the last device-resident call's stream (that call's kernels share the
+// shard's data, control words and error state with this one).
+inline int order_after_dev(glint_shard* s) {
+  if (!s->dev_dirty) return GLINT_OK;
+  if (!s->order_ev && hipEventCreateWithFlags(&s->order_ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    return GLINT_EDEVICE;
+  }
+  if (hipEventRecord(s->order_ev, s->last_dev_stream) != hipSuccess ||
+      hipStreamWaitEvent(s->stream, s->order_ev, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return GLINT_EDEVICE;
+  }
+  s->dev_dirty = false;
+  return GLINT_OK;
+}
 
 // Brackets one kernel launch with events on its stream when profiling is on.
 struct ProfScope {
@@ -202,4 +229,7 @@ template <typename V, bool MAT>
 int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
 template <typename V, bool MAT>
 int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
+// one-launch order-preserving push (glint_ordered.hip): n <= kOrderedMax, elems < 2^32
+template <typename V, bool MAT>
+int push_ordered(glint_shard* s, const PushArgs<V>& a, hipStream_t st);
 }  // namespace glint

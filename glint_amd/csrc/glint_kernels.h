@@ -42,6 +42,12 @@ constexpr int kTile = 64 * kPPT * 2;  // 1024 records per wave tile
 constexpr i64 kNotAffine = (i64)0x8000000000000000ll;  // tile descriptor: addresses not base + r
 constexpr int kHashSlots = 4096;   // LDS hash table slots in push_scatter (64 KiB for 8-B V)
 constexpr int kScatterChunk = 2048;  // records per block iteration in push_scatter (load <= 0.5)
+// pushes of up to this many records can take the one-launch order-preserving fold (glint_ordered.hip):
+// above the reference's frame cap of 79 999 Double records per message (glint.conf:143)
+constexpr i64 kOrderedMax = (i64)1 << 17;
+// internal push flag (not in the ABI): the call comes from a host-pointer / wire entry point, i.e.
+// from the actor's update(), and keeps the message's summation order unless GLINT_PUSH_UNORDERED
+constexpr int kPushHostSequential = 1 << 16;
 
 // per-launch control words, zeroed by one hipMemsetAsync before push_check
 struct LaunchCtl {

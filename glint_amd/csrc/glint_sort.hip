@@ -290,16 +290,27 @@ __global__ __launch_bounds__(kBinTPB) void bin_apply_kernel(const u32* __restric
 // deterministic tail: stable sort by address, then an in-order fold per address starting from the
 // shard's current value -- the reference's sequential `+=` order, bit for bit
 // ------------------------------------------------------------------------------------------------
+// Records before the tail start (push_check's break, read here on the device: no host round trip)
+// and rejected records get the sentinel address, which sorts behind every element and is skipped.
 template <typename V, bool MAT>
-__global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, const int32_t* cols, const V* vals, i64 r0,
-                                                           i64 m, PartDesc part, u64 sentinel, u64* addr, V* val,
+__global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, const int32_t* cols, const V* vals, i64 m,
+                                                           const LaunchCtl* ctl, u32 ntiles, int from_break,
+                                                           PartDesc part, u64 sentinel, u64* addr, V* val,
                                                            ErrState* err) {
+  i64 r0 = 0;
+  if (from_break) {
+    const u32 brk = ctl->brk_enc;
+    r0 = brk == 0u ? m : (i64)(ntiles - brk) * kTile;
+  }
   for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
-    i64 ad;
-    const bool ok = rec_addr<MAT>(part, keys[r0 + i], MAT ? cols[r0 + i] : 0, ad);
-    if (!ok) record_error(err, r0 + i);
-    addr[i] = ok ? (u64)ad : sentinel;
-    val[i] = vals[r0 + i];
+    u64 out = sentinel;
+    if (i >= r0) {
+      i64 ad;
+      if (rec_addr<MAT>(part, keys[i], MAT ? cols[i] : 0, ad)) out = (u64)ad;
+      else record_error(err, i);
+    }
+    addr[i] = out;
+    val[i] = vals[i];
   }
 }
 
@@ -428,17 +439,9 @@ __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, co
 // ---- host side ----------------------------------------------------------------------------------
 template <typename V, bool MAT>
 int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
-  // where does the non-increasing tail start? (a host round trip: this is the strict-order path)
-  i64 r0 = 0;
-  if (from_break) {
-    LaunchCtl h{};
-    HIPCHK(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (h.brk_enc == 0u) return GLINT_OK;
-    r0 = (i64)(a.ntiles - h.brk_enc) * kTile;
-  }
-  if (r0 >= a.n) return GLINT_OK;
-  const i64 m = a.n - r0;
+  // the whole push is sorted; records before push_check's break are masked on the device, so the
+  // call stays stream-ordered with no host synchronisation
+  const i64 m = a.n;
   const u64 sentinel = (u64)s->elems;
   int end_bit = 1;
   while (end_bit < 64 && ((u64)1 << end_bit) <= sentinel) ++end_bit;
@@ -460,8 +463,8 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
   u32* long_list = long_count + 1;
   void* tmp = base + 2 * b_addr + 2 * b_val + b_list;
   const unsigned g = grid_for(m, kTPB, (i64)s->cus * 8);
-  det_prepare_kernel<V, MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, a.vals, r0, m, a.part, sentinel, addr_in, val_in,
-                                                 a.err);
+  det_prepare_kernel<V, MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, a.vals, m, a.ctl, a.ntiles, from_break ? 1 : 0,
+                                                 a.part, sentinel, addr_in, val_in, a.err);
   HIPCHK(hipGetLastError());
   // stable LSD radix sort: equal addresses keep their push order
   HIPCHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, addr_in, addr_out, val_in, val_out, (size_t)m, 0, end_bit, st));

@@ -142,12 +142,45 @@ class _Shard:
         import torch
         return torch.cuda.current_stream(t.device).cuda_stream
 
-    def _check_dev(self, *tensors) -> None:
-        for t in tensors:
+    @property
+    def torch_dtype(self):
+        import torch
+        return getattr(torch, np.dtype(self.np_dtype).name)
+
+    def _check_dev(self, n: int, keys, cols=None, values=None, out=None, out_elems=None) -> None:
+        """Device-resident arguments: every tensor on the shard's GPU, contiguous, of the dtype the
+        kernels read (keys/rows int64, cols int32, values/out the shard's type) and long enough --
+        the kernels take raw pointers, so a mismatch would read or write past a buffer."""
+        import torch
+        spec = [("keys", keys, torch.int64, n)]
+        if cols is not None:
+            spec.append(("cols", cols, torch.int32, n))
+        if values is not None:
+            spec.append(("values", values, self.torch_dtype, n))
+        if out is not None:
+            spec.append(("out", out, self.torch_dtype, n if out_elems is None else out_elems))
+        for name, t, dt, want in spec:
+            if not _is_torch_cuda(t):
+                raise TypeError(f"{name}: expected a CUDA tensor (mixing host arrays and device tensors)")
             if t.device.index != self.device:
-                raise ValueError(f"tensor on cuda:{t.device.index}, shard on cuda:{self.device}")
+                raise ValueError(f"{name} on cuda:{t.device.index}, shard on cuda:{self.device}")
             if not t.is_contiguous():
-                raise ValueError("device tensors must be contiguous")
+                raise ValueError(f"{name}: device tensors must be contiguous")
+            if t.dtype != dt:
+                raise TypeError(f"{name}: dtype {t.dtype}, expected {dt}")
+            if t.numel() != want:
+                raise ValueError(f"{name}: {t.numel()} elements, expected {want}")
+
+    def _host_out(self, out, shape) -> np.ndarray:
+        """A caller-provided host result buffer must be a writable C-contiguous array of the shard's
+        type and exact shape (the library writes n x sizeof(V) bytes into it)."""
+        if out is None:
+            return np.empty(shape, dtype=self.np_dtype)
+        if not isinstance(out, np.ndarray) or out.dtype != self.np_dtype or out.shape != tuple(shape) \
+                or not out.flags.c_contiguous or not out.flags.writeable:
+            raise ValueError(f"out must be a writable C-contiguous {np.dtype(self.np_dtype).name} array of shape "
+                             f"{tuple(shape)}")
+        return out
 
 
 class PartialVector(_Shard):
@@ -161,9 +194,7 @@ class PartialVector(_Shard):
         ``unordered`` is a performance hint (GLINT_PUSH_UNORDERED): skip the order check, bin by slab."""
         flags = _flags(deterministic, unordered)
         if _is_torch_cuda(keys):
-            import torch
-            self._check_dev(keys, values)
-            assert keys.dtype == torch.int64 and values.numel() == keys.numel()
+            self._check_dev(keys.numel(), keys, values=values)
             rc = self.lib.glint_vec_push_dev(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(), flags,
                                              self._stream_of(keys))
             check(rc, self.handle)
@@ -181,10 +212,9 @@ class PartialVector(_Shard):
         """PartialVector.get (PartialVector.scala:51-60): a new array of data(globalToLocal(k))."""
         if _is_torch_cuda(keys):
             import torch
-            self._check_dev(keys)
             if out is None:
-                out = torch.empty(keys.numel(), dtype=getattr(torch, np.dtype(self.np_dtype).name),
-                                  device=keys.device)
+                out = torch.empty(keys.numel(), dtype=self.torch_dtype, device=keys.device)
+            self._check_dev(keys.numel(), keys, out=out)
             rc = self.lib.glint_vec_pull_dev(self.handle, keys.data_ptr(), out.data_ptr(), keys.numel(),
                                              self._stream_of(keys))
             check(rc, self.handle)
@@ -192,7 +222,7 @@ class PartialVector(_Shard):
                 self.sync(self._stream_of(keys))
             return out
         k = _host(keys, np.int64)
-        res = np.empty(k.shape, dtype=self.np_dtype) if out is None else out
+        res = self._host_out(out, k.shape)
         check(self.lib.glint_vec_pull(self.handle, k.ctypes.data, res.ctypes.data, k.size), self.handle)
         return res
 
@@ -232,7 +262,7 @@ class PartialMatrix(_Shard):
         """PartialMatrix.update (PartialMatrix.scala:74-83)."""
         flags = _flags(deterministic, unordered)
         if _is_torch_cuda(rows):
-            self._check_dev(rows, cols, values)
+            self._check_dev(rows.numel(), rows, cols=cols, values=values)
             rc = self.lib.glint_mat_push_dev(self.handle, rows.data_ptr(), cols.data_ptr(), values.data_ptr(),
                                              rows.numel(), flags, self._stream_of(rows))
             check(rc, self.handle)
@@ -252,10 +282,9 @@ class PartialMatrix(_Shard):
         """PartialMatrix.get (PartialMatrix.scala:55-65)."""
         if _is_torch_cuda(rows):
             import torch
-            self._check_dev(rows, cols)
             if out is None:
-                out = torch.empty(rows.numel(), dtype=getattr(torch, np.dtype(self.np_dtype).name),
-                                  device=rows.device)
+                out = torch.empty(rows.numel(), dtype=self.torch_dtype, device=rows.device)
+            self._check_dev(rows.numel(), rows, cols=cols, out=out)
             rc = self.lib.glint_mat_pull_dev(self.handle, rows.data_ptr(), cols.data_ptr(), out.data_ptr(),
                                              rows.numel(), self._stream_of(rows))
             check(rc, self.handle)
@@ -264,7 +293,9 @@ class PartialMatrix(_Shard):
             return out
         r = _host(rows, np.int64)
         c = _host(cols, np.int32)
-        res = np.empty(r.shape, dtype=self.np_dtype) if out is None else out
+        if r.shape != c.shape:
+            raise ValueError("rows and cols differ in length")
+        res = self._host_out(out, r.shape)
         check(self.lib.glint_mat_pull(self.handle, r.ctypes.data, c.ctypes.data, res.ctypes.data, r.size),
               self.handle)
         return res
@@ -274,18 +305,17 @@ class PartialMatrix(_Shard):
         row-major image ResponseSerializer sends (ResponseSerializer.scala:52-61)."""
         if _is_torch_cuda(rows):
             import torch
-            self._check_dev(rows)
             if out is None:
-                out = torch.empty((rows.numel(), self.cols), dtype=getattr(torch, np.dtype(self.np_dtype).name),
-                                  device=rows.device)
+                out = torch.empty((rows.numel(), self.cols), dtype=self.torch_dtype, device=rows.device)
+            self._check_dev(rows.numel(), rows, out=out, out_elems=rows.numel() * self.cols)
             rc = self.lib.glint_mat_pull_rows_dev(self.handle, rows.data_ptr(), out.data_ptr(), rows.numel(),
                                                   self._stream_of(rows))
             check(rc, self.handle)
             if sync:
                 self.sync(self._stream_of(rows))
             return out
-        r = _host(rows, np.int64)
-        res = np.empty((r.size, self.cols), dtype=self.np_dtype) if out is None else out
+        r = _host(rows, np.int64).reshape(-1)
+        res = self._host_out(out, (r.size, self.cols))
         check(self.lib.glint_mat_pull_rows(self.handle, r.ctypes.data, res.ctypes.data, r.size), self.handle)
         return res
 

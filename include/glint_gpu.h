@@ -45,14 +45,20 @@ enum glint_push_flags {
   GLINT_PUSH_DEFAULT = 0,
   /* Bit-exact reproduction of the reference's strictly sequential `data(k) += v` order for
    * Float/Double even when keys repeat (PartialVector.scala:37-41). Without it, repeated keys in
-   * a push are summed by device atomics in arbitrary order (<= 1e-6 relative for Double; Int and
-   * Long are exact either way). Unique-key pushes are bit-exact in both modes. */
+   * a device-resident push are summed in arbitrary order (<= 1e-6 relative for Double; Int and
+   * Long are exact either way). Unique-key pushes are bit-exact in both modes.
+   * Host-pointer and wire pushes (glint_vec_push, glint_mat_push, glint_push_wire: what the actor's
+   * update() calls) of up to 131 072 records -- above the 79 999-record frame cap, glint.conf:143 --
+   * keep the message's order WITHOUT this flag too (one launch, glint_ordered.hip), unless
+   * GLINT_PUSH_UNORDERED is given. */
   GLINT_PUSH_DETERMINISTIC = 1,
-  /* Hint: the keys are in no particular order. The push skips the order check and sums the records
-   * per shard slab in LDS (radix binning + one read-modify-write per touched element pair)
-   * instead of per-record device atomics. Results as GLINT_PUSH_DEFAULT. Without the hint, a
-   * large push takes this path by itself when the shard's previous push was unordered
-   * (environment GLINT_BINNED=0 disables that, =1 forces it for pushes >= 2^20 records). */
+  /* Hint: the keys are in no particular order and the caller does not need the reference's
+   * summation order. A large push skips the order check and sums the records per shard slab in
+   * LDS (partition by slab + one read-modify-write per touched element pair) instead of per-record
+   * device atomics; a host-pointer push takes the unordered LDS-hash scatter instead of the
+   * order-preserving fold. Without the hint, a large push takes the binned path by itself when the
+   * shard's previous push was unordered (environment GLINT_BINNED=0 disables that, =1 forces it
+   * for pushes >= 2^20 records). */
   GLINT_PUSH_UNORDERED = 2
 };
 
@@ -171,8 +177,9 @@ enum glint_kernel_id {
   GLINT_K_MAT_PULL = 3,
   GLINT_K_MAT_PULL_ROWS = 4,
   GLINT_K_PUSH_CHECK = 5,   /* order / affinity check over the keys in front of push_apply */
-  GLINT_K_PUSH_BINNED = 6,  /* the binned unordered-push pipeline (prepare, sort, bounds, scan, apply) */
-  GLINT_K_COUNT = 7
+  GLINT_K_PUSH_BINNED = 6,  /* the binned unordered-push pipeline (count, partition, apply) */
+  GLINT_K_PUSH_ORDERED = 7, /* the order-preserving push of message-sized pushes (one launch) */
+  GLINT_K_COUNT = 8
 };
 int glint_prof_enable(glint_shard_t shard, int on);
 int glint_prof_read(glint_shard_t shard, int kernel_id, double* total_ms, int64_t* launches);
