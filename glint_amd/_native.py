@@ -50,6 +50,7 @@ SIGNATURES = {
     "glint_push_wire": (_I, [_P, _P, _SZ, C.POINTER(_I32), _I]),
     "glint_pull_wire": (_I, [_P, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     "glint_route_dev": (_I, [_P, _I64, _I, _I32, _I64, _P, _P, C.POINTER(_I64), _P]),
+    "glint_route_gather_dev": (_I, [_P, _P, _P, _I, _I64, _I, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "glint_prof_enable": (_I, [_P, _I]),
     "glint_prof_read": (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(_I64)]),
     "glint_prof_reset": (_I, [_P]),

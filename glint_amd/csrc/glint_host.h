@@ -37,6 +37,7 @@ struct glint_shard {
   size_t bin_bytes = 0;
   double bin_dedup_ratio = 0.0;  // distinct/records of the last deduplicating binned push
   uint32_t bin_pushes = 0;
+  bool bin_last_dedup = false;   // whether the last binned push ran the dedup front end
   // pinned host staging for host-pointer calls (grow-only, <= pinned_stage_max()): the caller's
   // arrays are memcpy'd in and cross PCIe in one DMA; pull answers come back the same way
   void* h_stage = nullptr;

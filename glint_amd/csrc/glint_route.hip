@@ -64,10 +64,18 @@ __device__ __forceinline__ u64 match_owner(int32_t o, int nbits) {
   return m;
 }
 
+// Group ("slot") of a record: its owning partition, or slot_of[partition] when the caller orders
+// the partitions differently (e.g. by hosting rank); nparts (the sentinel) for a bad key.
+__device__ __forceinline__ int32_t slot_of_key(const RangeDesc& d, const int32_t* slot_of, i64 key) {
+  const int32_t o = owner_of(d, key);
+  if (o < 0) return -1;
+  return slot_of ? slot_of[o] : o;
+}
+
 // The block's chunk is `rounds` x 256 consecutive records; owners outside [0, nparts) count as bad.
-__global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, i64 n, RangeDesc d, int nbits,
-                                                  int rounds, u32* __restrict__ hist, i64 nblocks,
-                                                  u64* __restrict__ bad) {
+__global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, i64 n, RangeDesc d,
+                                                  const int32_t* __restrict__ slot_of, int nbits, int rounds,
+                                                  u32* __restrict__ hist, i64 nblocks, u64* __restrict__ bad) {
   __shared__ u32 h[kMaxParts];
   const int lane = threadIdx.x & 63;
   for (int p = threadIdx.x; p < d.nparts; p += kRT) h[p] = 0;
@@ -77,7 +85,7 @@ __global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, 
     const i64 i = base + (i64)r * kRT + threadIdx.x;
     int32_t o = d.nparts;  // sentinel: past the end
     if (i < n) {
-      o = owner_of(d, keys[i]);
+      o = slot_of_key(d, slot_of, keys[i]);
       if (o < 0) { atomicMax(bad, ~(u64)i); o = d.nparts; }
     }
     const u64 m = match_owner(o, nbits);
@@ -88,9 +96,21 @@ __global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, 
   for (int p = threadIdx.x; p < d.nparts; p += kRT) hist[(i64)p * nblocks + blockIdx.x] = h[p];  // partition-major
 }
 
-__global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ keys, i64 n, RangeDesc d, int nbits,
-                                                     int rounds, const u32* __restrict__ offs, i64 nblocks,
-                                                     i64* __restrict__ order) {
+// Send-order outputs of the fused route (each may be null): the record indices (order) and the
+// records themselves -- keys, cols, and values of vsize bytes -- so no separate gather pass runs.
+struct RouteOut {
+  i64* order;
+  i64* keys;
+  int32_t* cols;
+  void* vals;
+  const int32_t* in_cols;
+  const void* in_vals;
+  int vsize;  // 4 or 8
+};
+
+__global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ keys, i64 n, RangeDesc d,
+                                                     const int32_t* __restrict__ slot_of, int nbits, int rounds,
+                                                     const u32* __restrict__ offs, i64 nblocks, RouteOut out) {
   __shared__ u32 cnt[kMaxParts];  // records of each owner this block has placed so far
   __shared__ u32 grp_base[kRT];   // per group leader: the group's first slot within its owner
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -100,8 +120,10 @@ __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ key
   for (int r = 0; r < rounds; ++r) {
     const i64 i = base + (i64)r * kRT + threadIdx.x;  // 256 consecutive records per round
     int32_t o = d.nparts;
+    i64 key = 0;
     if (i < n) {
-      o = owner_of(d, keys[i]);
+      key = keys[i];
+      o = slot_of_key(d, slot_of, key);
       if (o < 0) o = d.nparts;
     }
     const u64 m = match_owner(o, nbits);
@@ -117,7 +139,14 @@ __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ key
     }
     if (o < d.nparts) {
       const int lead = __ffsll((long long)m) - 1;
-      order[(i64)offs[(i64)o * nblocks + blockIdx.x] + grp_base[wid * 64 + lead] + __popcll(below)] = i;
+      const i64 pos = (i64)offs[(i64)o * nblocks + blockIdx.x] + grp_base[wid * 64 + lead] + __popcll(below);
+      if (out.order) out.order[pos] = i;
+      if (out.keys) out.keys[pos] = key;
+      if (out.cols) out.cols[pos] = out.in_cols[i];
+      if (out.vals) {
+        if (out.vsize == 8) reinterpret_cast<u64*>(out.vals)[pos] = reinterpret_cast<const u64*>(out.in_vals)[i];
+        else reinterpret_cast<u32*>(out.vals)[pos] = reinterpret_cast<const u32*>(out.in_vals)[i];
+      }
     }
     __syncthreads();  // grp_base is rewritten next round
   }
@@ -134,19 +163,45 @@ __global__ void route_counts(const u32* __restrict__ offs, const u32* __restrict
   }
 }
 
-std::mutex g_route_mu;
-void* g_tmp = nullptr;
-size_t g_tmp_bytes = 0;
+// route scratch, one per device (a process may route on several GPUs at once)
+constexpr int kMaxDevices = 64;
+struct RouteScratch {
+  std::mutex mu;
+  void* tmp = nullptr;
+  size_t bytes = 0;
+};
+RouteScratch g_scratch[kMaxDevices];
 
-}  // namespace
+struct DevGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
-extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys,
-                               int64_t* counts, int64_t* order, int64_t* first_bad, void* stream) {
+// Launches the route (histogram, scan, scatter, counts) on `st`; the first bad record (~index, 0 =
+// none) lands in the device word *bad_dev. No host synchronisation.
+int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of,
+                 int64_t* counts, const RouteOut& out, uint64_t* bad_dev, hipStream_t st) {
   if (kind != GLINT_ROUTE_RANGE && kind != GLINT_ROUTE_CYCLIC) return GLINT_EINVAL;
-  if (nparts <= 0 || nparts > kMaxParts || n < 0 || nkeys < 0 || !counts || !first_bad) return GLINT_EINVAL;
-  if (n > 0 && (!keys || !order)) return GLINT_EINVAL;
+  if (nparts <= 0 || nparts > kMaxParts || n < 0 || nkeys < 0 || !counts || !bad_dev) return GLINT_EINVAL;
+  if (n > 0 && !keys) return GLINT_EINVAL;
   if (n >= ((i64)1 << 32)) return GLINT_EINVAL;  // 32-bit offsets
-  hipStream_t st = (hipStream_t)stream;
+  if (out.vals && out.vsize != 4 && out.vsize != 8) return GLINT_EINVAL;
+  if ((out.vals && !out.in_vals) || (out.cols && !out.in_cols)) return GLINT_EINVAL;
+  int dev = 0;
+  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return GLINT_EDEVICE;
+  }
+  if (dev < 0 || dev >= kMaxDevices) return GLINT_EDEVICE;
+  DevGuard guard(dev);
+  if (!guard.ok) return GLINT_EDEVICE;
   // RangePartitioner.apply (RangePartitioner.scala:62-84) -- same Int truncation of the sizes
   RangeDesc d{};
   const int32_t n_large = (int32_t)(nkeys % nparts);
@@ -162,41 +217,93 @@ extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t
   const i64 nblocks = std::max<i64>(1, (n + chunk - 1) / chunk);
   int nbits = 1;
   while ((1 << nbits) <= nparts) ++nbits;  // owners and the sentinel nparts fit in nbits
-  std::lock_guard<std::mutex> lk(g_route_mu);
+  RouteScratch& sc = g_scratch[dev];
+  std::lock_guard<std::mutex> lk(sc.mu);
   const size_t hist_bytes = (size_t)nparts * nblocks * 4;
   size_t scan_bytes = 0;
   if (rocprim::exclusive_scan(nullptr, scan_bytes, (u32*)nullptr, (u32*)nullptr, 0u, (size_t)nparts * nblocks,
                               rocprim::plus<u32>(), st) != hipSuccess)
     return GLINT_EDEVICE;
-  const size_t need = 2 * ((hist_bytes + 255) & ~(size_t)255) + 256 + scan_bytes;
-  if (g_tmp_bytes < need) {
-    if (g_tmp) (void)hipFree(g_tmp);
-    g_tmp = nullptr;
-    g_tmp_bytes = 0;
-    if (hipMalloc(&g_tmp, need) != hipSuccess) { (void)hipGetLastError(); return GLINT_ENOMEM; }
-    g_tmp_bytes = need;
+  const size_t need = 2 * ((hist_bytes + 255) & ~(size_t)255) + scan_bytes;
+  if (sc.bytes < need) {
+    // the old buffer may still be read by kernels queued on another stream of this device
+    if (sc.tmp) { (void)hipDeviceSynchronize(); (void)hipFree(sc.tmp); }
+    sc.tmp = nullptr;
+    sc.bytes = 0;
+    if (hipMalloc(&sc.tmp, need) != hipSuccess) { (void)hipGetLastError(); return GLINT_ENOMEM; }
+    sc.bytes = need;
   }
-  char* b = (char*)g_tmp;
+  char* b = (char*)sc.tmp;
   u32* hist = (u32*)b;
   u32* offs = (u32*)(b + ((hist_bytes + 255) & ~(size_t)255));
-  u64* bad = (u64*)(b + 2 * ((hist_bytes + 255) & ~(size_t)255));
-  void* scan_tmp = b + 2 * ((hist_bytes + 255) & ~(size_t)255) + 256;
-  if (hipMemsetAsync(bad, 0, 8, st) != hipSuccess) return GLINT_EDEVICE;
+  void* scan_tmp = b + 2 * ((hist_bytes + 255) & ~(size_t)255);
+  if (hipMemsetAsync(bad_dev, 0, 8, st) != hipSuccess) return GLINT_EDEVICE;
   if (n == 0) {
     if (hipMemsetAsync(counts, 0, (size_t)nparts * 8, st) != hipSuccess) return GLINT_EDEVICE;
   } else {
-    route_hist<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, nbits, rounds, hist, nblocks, bad);
+    route_hist<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, hist, nblocks, bad_dev);
     if (rocprim::exclusive_scan(scan_tmp, scan_bytes, hist, offs, 0u, (size_t)nparts * nblocks,
                                 rocprim::plus<u32>(), st) != hipSuccess)
       return GLINT_EDEVICE;
-    route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, nbits, rounds, offs, nblocks, order);
+    route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, offs, nblocks, out);
     route_counts<<<(unsigned)((nparts + 255) / 256), 256, 0, st>>>(offs, hist, nblocks, nparts, counts);
   }
-  // first bad record: enc = ~index (0 = none); returned through the host word *first_bad
-  u64 enc = 0;
-  if (hipMemcpyAsync(&enc, bad, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return GLINT_EDEVICE;
+  if (hipGetLastError() != hipSuccess) return GLINT_EDEVICE;
+  return GLINT_OK;
+}
+
+}  // namespace
+
+extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys,
+                               int64_t* counts, int64_t* order, int64_t* first_bad, void* stream) {
+  if (!first_bad || (n > 0 && !order)) return GLINT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  RouteOut out{};
+  out.order = order;
+  // a per-device status word in device memory (read back with the call's synchronisation)
+  static std::mutex mu;
+  static uint64_t* bad_words[kMaxDevices] = {};
+  int dev = 0;
+  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return GLINT_EDEVICE;
+  }
+  if (dev < 0 || dev >= kMaxDevices) return GLINT_EDEVICE;
+  uint64_t* bad_dev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!bad_words[dev]) {
+      DevGuard guard(dev);
+      // one word per 256 B so concurrent callers on one device do not share it
+      if (!guard.ok || hipMalloc((void**)&bad_words[dev], 256 * 64) != hipSuccess) {
+        (void)hipGetLastError();
+        bad_words[dev] = nullptr;
+        return GLINT_ENOMEM;
+      }
+    }
+    static int next_slot = 0;
+    bad_dev = bad_words[dev] + 32 * (next_slot++ & 63);
+  }
+  int rc = route_launch(keys, n, kind, nparts, nkeys, nullptr, counts, out, bad_dev, st);
+  if (rc) return rc;
+  uint64_t enc = 0;
+  if (hipMemcpyAsync(&enc, bad_dev, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return GLINT_EDEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return GLINT_EDEVICE;
   *first_bad = enc ? (int64_t)~enc : -1;
-  if (hipGetLastError() != hipSuccess) return GLINT_EDEVICE;
   return enc ? GLINT_EOUTOFRANGE : GLINT_OK;
+}
+
+extern "C" int glint_route_gather_dev(const int64_t* keys, const int32_t* cols, const void* vals, int vsize, int64_t n,
+                                      int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of, int64_t* counts,
+                                      int64_t* order, int64_t* out_keys, int32_t* out_cols, void* out_vals,
+                                      uint64_t* bad_dev, void* stream) {
+  RouteOut out{};
+  out.order = order;
+  out.keys = out_keys;
+  out.cols = out_cols;
+  out.vals = out_vals;
+  out.in_cols = cols;
+  out.in_vals = vals;
+  out.vsize = vsize;
+  return route_launch(keys, n, kind, nparts, nkeys, slot_of, counts, out, bad_dev, (hipStream_t)stream);
 }

@@ -166,6 +166,19 @@ enum glint_route_kind { GLINT_ROUTE_RANGE = 0, GLINT_ROUTE_CYCLIC = 1 };
 int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys,
                     int64_t* counts, int64_t* order, int64_t* first_bad, void* stream);
 
+/* The exchange's send buffers in one pass, with no host synchronisation (AsyncBigVector.scala:96-116,
+ * AsyncBigMatrix.scala:141-156): records grouped as glint_route_dev groups them -- by partition, or
+ * by slot_of[partition] (device array of nparts group indices, e.g. partitions ordered by hosting
+ * rank; NULL = identity) -- each group in the caller's order, and written in that order into every
+ * non-NULL output: order (record indices), out_keys, out_cols (from cols), out_vals (vsize = 4 or 8
+ * bytes per value, from vals). counts[0..nparts) (device) receives the group sizes. The first bad
+ * record is left in the device word *bad_dev as ~index (0 = none); bad records are in no group.
+ * Stream-ordered on `stream`; the caller reads counts and *bad_dev when it needs them. */
+int glint_route_gather_dev(const int64_t* keys, const int32_t* cols, const void* vals, int vsize, int64_t n,
+                           int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of, int64_t* counts,
+                           int64_t* order, int64_t* out_keys, int32_t* out_cols, void* out_vals,
+                           uint64_t* bad_dev, void* stream);
+
 /* ---- kernel timing ------------------------------------------------------------------------- *
  * With profiling on, every kernel launch of the shard is bracketed by HIP events recorded on the
  * stream it is launched on; glint_prof_read waits for them and returns the summed device time and
