@@ -16,16 +16,17 @@ is both a client and a server driving one GPU:
 4. answer  -- (pull) values travel back along the reversed splits and are scattered to the
               caller's order (AsyncBigVector.scala:61-79).
 
-Out-of-range keys raise ``IndexOutOfBoundsException`` on the calling rank before anything is sent
--- the reference throws inside ``mapPartitions`` before any message leaves -- so a caller that
-catches it must not enter the collective (every rank of the group takes part in every exchange).
+Out-of-range keys raise ``IndexOutOfBoundsException`` on the calling rank, and nothing of that
+rank's batch is applied -- the reference throws inside ``mapPartitions`` before any message leaves.
+For device batches the bad rank still joins the call's collectives (with nothing to send, so the
+other ranks' pushes and pulls complete) and raises after them; host (CPU) batches raise before the
+exchange, so there a caller that catches it must not enter the collective.
 
 The bench's weak-scaling line does not come through here: there every rank pushes the records of
 the partition it hosts, which needs no exchange.
 """
 from __future__ import annotations
 
-import ctypes as C
 from typing import Callable, List, Optional
 
 import numpy as np
@@ -60,28 +61,56 @@ class Router:
         self.perm = [p for r in range(self.world) for p in self.rank_parts[r]]
         self.maxp = max(len(p) for p in self.rank_parts)
         self.identity = self.perm == list(range(self.nparts))
+        # group ("slot") of partition p in send order, and the slot's cell in the (rank, j) count matrix
+        slot_of = np.empty(self.nparts, np.int32)
+        slot_of[self.perm] = np.arange(self.nparts, dtype=np.int32)
+        self.slot_of = slot_of
+        self.slot_cell = np.array([r * self.maxp + j for r in range(self.world)
+                                   for j in range(len(self.rank_parts[r]))], np.int64)
+        self._dev = {}
+
+    def _device_tables(self, device):
+        t = self._dev.get(device)
+        if t is None:
+            slot_of = None if self.identity else torch.from_numpy(self.slot_of).to(device)
+            t = (slot_of, torch.from_numpy(self.slot_cell).to(device))
+            self._dev[device] = t
+        return t
+
+    def route(self, keys: torch.Tensor, cols=None, vals=None, want_order: bool = False):
+        """Device batch -> records in send order, in ONE kernel pass (glint_route_gather_dev) with no
+        host synchronisation: (counts, order, keys, cols, vals, bad), all device tensors; counts in
+        slot (send) order, bad = ~first bad record index or 0."""
+        n = keys.numel()
+        dev = keys.device
+        slot_of, _ = self._device_tables(dev)
+        counts = torch.empty(self.nparts, dtype=torch.int64, device=dev)
+        bad = torch.empty(1, dtype=torch.int64, device=dev)
+        order = torch.empty(n, dtype=torch.int64, device=dev) if want_order else None
+        sk = torch.empty(n, dtype=torch.int64, device=dev)
+        sc = torch.empty(n, dtype=torch.int32, device=dev) if cols is not None else None
+        sv = torch.empty(n, dtype=vals.dtype, device=dev) if vals is not None else None
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        rc = N.load().glint_route_gather_dev(
+            keys.data_ptr(), ptr(cols), ptr(vals), vals.element_size() if vals is not None else 0, n, self.kind,
+            self.nparts, self.nkeys, ptr(slot_of), counts.data_ptr(), ptr(order), sk.data_ptr(), ptr(sc), ptr(sv),
+            bad.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        check(rc)
+        return counts, order, sk, sc, sv, bad
 
     def group(self, keys: torch.Tensor):
         """-> (order, counts): order = record indices grouped by partition in ``perm`` order (each
         group in the caller's order), counts = host int64 array of the group sizes (perm order)."""
-        n = keys.numel()
         if keys.is_cuda:
-            lib = N.load()
-            counts_d = torch.empty(self.nparts, dtype=torch.int64, device=keys.device)
-            order = torch.empty(n, dtype=torch.int64, device=keys.device)
-            bad = C.c_int64(-1)
-            stream = torch.cuda.current_stream(keys.device).cuda_stream
-            rc = lib.glint_route_dev(keys.data_ptr(), n, self.kind, self.nparts, self.nkeys, counts_d.data_ptr(),
-                                     order.data_ptr(), C.byref(bad), stream)
-            if rc == N.GLINT_EOUTOFRANGE:
-                i = bad.value
+            counts, order, _, _, _, bad = self.route(keys, want_order=True)
+            host = torch.cat([counts, bad]).cpu().numpy()
+            if host[-1] != 0:
+                i = int(~host[-1])
                 raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.nkeys})")
-            check(rc)
-            counts = counts_d.cpu().numpy()
-        else:
-            owner = self.partitioner.partition_indices(keys.numpy())  # raises IndexOutOfBoundsException
-            o, off = bucket(owner, self.nparts)
-            order, counts = torch.from_numpy(o), np.diff(off)
+            return order, host[:-1]
+        owner = self.partitioner.partition_indices(keys.numpy())  # raises IndexOutOfBoundsException
+        o, off = bucket(owner, self.nparts)
+        order, counts = torch.from_numpy(o), np.diff(off)
         if not self.identity:
             off = np.zeros(self.nparts + 1, dtype=np.int64)
             np.cumsum(counts, out=off[1:])
@@ -91,33 +120,72 @@ class Router:
 
 
 class _Exchange:
-    """The all-to-all legs of one routed call (send splits, receive splits, local layout)."""
+    """The all-to-all legs of one routed call (send splits, receive splits, local layout).
 
-    def __init__(self, router: Router, rank: int, counts: np.ndarray, group, device):
+    Device batches over RCCL: the (rank, partition) count matrix is built and exchanged on the
+    device, and the host reads it ONCE together with the route's status word; that single read gives
+    both the send and the receive splits. A batch with an out-of-range key sends nothing (every rank
+    still joins the collectives) and raises after them, so the other ranks' pushes complete."""
+
+    def __init__(self, router: Router, rank: int, counts, group, device, bad=None):
         W, maxp = router.world, router.maxp
-        self.group, self.device = group, device
-        send = np.zeros((W, maxp), dtype=np.int64)
-        i = 0
-        for r in range(W):
-            k = len(router.rank_parts[r])
-            send[r, :k] = counts[i:i + k]
-            i += k
-        recv = torch.empty((W, maxp), dtype=torch.int64, device=device)
-        dist.all_to_all_single(recv, torch.from_numpy(send).to(device), group=group)
-        self.recv_counts = recv.cpu().numpy()  # [source rank, local partition j]
-        self.in_splits = send.sum(axis=1).tolist()
-        self.out_splits = self.recv_counts.sum(axis=1).tolist()
+        self.group, self.device, self.world = group, device, W
+        self.bad = -1
+        self.bad_exc = None
+        if isinstance(counts, torch.Tensor) and device.type == "cuda":
+            _, cell = router._device_tables(counts.device)
+            send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
+            send[cell] = counts
+            if bad is not None:
+                send = torch.where(bad == 0, send, torch.zeros_like(send))
+            recv = torch.empty_like(send)
+            if W > 1:
+                dist.all_to_all_single(recv, send, group=group)
+            else:
+                recv = send
+            parts = [send, recv] + ([bad] if bad is not None else [])
+            host = torch.cat(parts).cpu().numpy()  # the call's one host synchronisation
+            send_h, recv_h = host[:W * maxp].reshape(W, maxp), host[W * maxp:2 * W * maxp].reshape(W, maxp)
+            if bad is not None and host[-1] != 0:
+                self.bad = int(~host[-1])
+        else:
+            if isinstance(counts, torch.Tensor):  # device route, host (gloo) exchange
+                host = torch.cat([counts] + ([bad] if bad is not None else [])).cpu().numpy()
+                if bad is not None and host[-1] != 0:
+                    self.bad = int(~host[-1])
+                counts = host[:router.nparts]
+            send_h = np.zeros((W, maxp), dtype=np.int64)
+            if self.bad < 0:
+                send_h.reshape(-1)[router.slot_cell] = counts
+            recv = torch.empty((W, maxp), dtype=torch.int64, device=device)
+            dist.all_to_all_single(recv, torch.from_numpy(send_h).to(device), group=group)
+            recv_h = recv.cpu().numpy()
+        self.recv_counts = recv_h  # [source rank, local partition j]
+        self.in_splits = send_h.sum(axis=1).tolist()
+        self.out_splits = recv_h.sum(axis=1).tolist()
         self.nlocal = len(router.rank_parts[rank])
 
     def forward(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:  # a world of one exchanges with itself: the send buffer is the receive buffer
+            return t[:self.out_splits[0]]
         out = torch.empty((sum(self.out_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_to_all_single(out, t.contiguous(), self.out_splits, self.in_splits, group=self.group)
+        dist.all_to_all_single(out, t[:sum(self.in_splits)].contiguous(), self.out_splits, self.in_splits,
+                               group=self.group)
         return out
 
     def backward(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
         out = torch.empty((sum(self.in_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_to_all_single(out, t.contiguous(), self.in_splits, self.out_splits, group=self.group)
         return out
+
+    def raise_if_bad(self, keys: torch.Tensor, nkeys: int):
+        if self.bad_exc is not None:
+            raise self.bad_exc
+        if self.bad >= 0:
+            i = self.bad
+            raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {nkeys})")
 
     def local_index(self, j: int) -> Optional[torch.Tensor]:
         """Positions in the received buffer of local partition j's records (source-rank order);
@@ -152,10 +220,30 @@ class _Distributed:
             return t.cpu()
         return t
 
+    def _nccl(self, keys: torch.Tensor) -> bool:
+        return keys.is_cuda and dist.get_backend(self.group) != "gloo"
+
     def _begin(self, keys: torch.Tensor):
-        order, counts = self.router.group(keys)
+        """Host path (CPU tensors, or gloo): order + host counts, records gathered by index. A batch
+        with an out-of-range key sends nothing and raises after the collectives (raise_if_bad)."""
+        exc = None
+        try:
+            order, counts = self.router.group(keys)
+        except IndexOutOfBoundsException as e:
+            exc = e
+            order = torch.zeros(0, dtype=torch.int64, device=keys.device)
+            counts = np.zeros(self.router.nparts, dtype=np.int64)
         comm = torch.device("cpu") if dist.get_backend(self.group) == "gloo" else keys.device
-        return order, _Exchange(self.router, self.rank, counts, self.group, comm)
+        ex = _Exchange(self.router, self.rank, counts, self.group, comm)
+        ex.bad_exc = exc
+        return order, ex
+
+    def _begin_fused(self, keys, cols=None, vals=None, want_order=False):
+        """Device path: the fused route writes the send buffers; one host read for the splits."""
+        counts, order, sk, sc, sv, bad = self.router.route(keys, cols, vals, want_order)
+        comm = keys.device if self._nccl(keys) else torch.device("cpu")
+        ex = _Exchange(self.router, self.rank, counts, self.group, comm, bad)
+        return ex, order, sk, sc, sv
 
     def _to_shard(self, t: torch.Tensor) -> torch.Tensor:
         return t.to(self.device) if t.device != self.device else t
@@ -184,18 +272,27 @@ class DistributedBigVector(_Distributed):
         values = values.reshape(-1).to(self.dtype)
         if keys.numel() != values.numel():
             raise ValueError("keys and values differ in length")
-        order, ex = self._begin(keys)
-        rk = ex.forward(self._comm_device(keys.index_select(0, order)))
-        rv = ex.forward(self._comm_device(values.index_select(0, order.to(values.device))))
+        if keys.is_cuda and values.device == keys.device:
+            ex, _, sk, _, sv = self._begin_fused(keys, vals=values.contiguous())
+            rk, rv = ex.forward(self._comm_device(sk)), ex.forward(self._comm_device(sv))
+        else:
+            order, ex = self._begin(keys)
+            rk = ex.forward(self._comm_device(keys.index_select(0, order)))
+            rv = ex.forward(self._comm_device(values.index_select(0, order.to(values.device))))
         for _, sh, (k, v) in self._split(ex, rk, rv):
             if k.numel():
                 sh.update(self._to_shard(k), self._to_shard(v), deterministic=deterministic)
+        ex.raise_if_bad(keys, self.router.nkeys)
         return True
 
     def pull(self, keys: torch.Tensor) -> torch.Tensor:
         keys = keys.reshape(-1).to(torch.int64)
-        order, ex = self._begin(keys)
-        rk = ex.forward(self._comm_device(keys.index_select(0, order)))
+        if keys.is_cuda:
+            ex, order, sk, _, _ = self._begin_fused(keys, want_order=True)
+            rk = ex.forward(self._comm_device(sk))
+        else:
+            order, ex = self._begin(keys)
+            rk = ex.forward(self._comm_device(keys.index_select(0, order)))
         resp = torch.empty(rk.numel(), dtype=self.dtype, device=rk.device)
         for j, sh, (k,) in self._split(ex, rk):
             if k.numel():
@@ -206,6 +303,7 @@ class DistributedBigVector(_Distributed):
                 else:
                     resp.index_copy_(0, idx.to(resp.device), got)
         back = ex.backward(resp).to(keys.device)
+        ex.raise_if_bad(keys, self.router.nkeys)  # after the collectives: this rank asked for nothing
         out = torch.empty(keys.numel(), dtype=self.dtype, device=keys.device)
         out.index_copy_(0, order.to(keys.device), back)
         return out
@@ -226,27 +324,39 @@ class DistributedBigMatrix(_Distributed):
         values = values.reshape(-1).to(self.dtype)
         if not rows.numel() == cols.numel() == values.numel():
             raise ValueError("rows, cols and values differ in length")
-        order, ex = self._begin(rows)
-        rr = ex.forward(self._comm_device(rows.index_select(0, order)))
-        rc = ex.forward(self._comm_device(cols.index_select(0, order.to(cols.device))))
-        rv = ex.forward(self._comm_device(values.index_select(0, order.to(values.device))))
+        if rows.is_cuda and cols.device == rows.device and values.device == rows.device:
+            ex, _, sr, sc, sv = self._begin_fused(rows, cols=cols.contiguous(), vals=values.contiguous())
+            rr, rc, rv = (ex.forward(self._comm_device(t)) for t in (sr, sc, sv))
+        else:
+            order, ex = self._begin(rows)
+            rr = ex.forward(self._comm_device(rows.index_select(0, order)))
+            rc = ex.forward(self._comm_device(cols.index_select(0, order.to(cols.device))))
+            rv = ex.forward(self._comm_device(values.index_select(0, order.to(values.device))))
         for _, sh, (r, c, v) in self._split(ex, rr, rc, rv):
             if r.numel():
                 sh.update(self._to_shard(r), self._to_shard(c), self._to_shard(v), deterministic=deterministic)
+        ex.raise_if_bad(rows, self.router.nkeys)
         return True
 
     def pull(self, rows: torch.Tensor, cols: Optional[torch.Tensor] = None) -> torch.Tensor:
         """pull(rows, cols): elements (AsyncBigMatrix.scala:96-130); pull(rows): whole rows as an
         (n, cols) tensor (AsyncBigMatrix.scala:53-86)."""
         rows = rows.reshape(-1).to(torch.int64)
-        order, ex = self._begin(rows)
-        rr = ex.forward(self._comm_device(rows.index_select(0, order)))
+        if cols is not None:
+            cols = cols.reshape(-1).to(torch.int32)
+        if rows.is_cuda and (cols is None or cols.device == rows.device):
+            ex, order, sr, sc, _ = self._begin_fused(rows, cols=None if cols is None else cols.contiguous(),
+                                                     want_order=True)
+            rr = ex.forward(self._comm_device(sr))
+            rc = None if cols is None else ex.forward(self._comm_device(sc))
+        else:
+            order, ex = self._begin(rows)
+            rr = ex.forward(self._comm_device(rows.index_select(0, order)))
+            rc = None if cols is None else ex.forward(self._comm_device(cols.index_select(0, order.to(cols.device))))
         if cols is None:
             shape = (rr.numel(), self.cols)
             bufs = (rr,)
         else:
-            cols = cols.reshape(-1).to(torch.int32)
-            rc = ex.forward(self._comm_device(cols.index_select(0, order.to(cols.device))))
             shape = (rr.numel(),)
             bufs = (rr, rc)
         resp = torch.empty(shape, dtype=self.dtype, device=rr.device)
@@ -261,6 +371,7 @@ class DistributedBigMatrix(_Distributed):
                 else:
                     resp.index_copy_(0, idx.to(resp.device), got)
         back = ex.backward(resp).to(rows.device)
+        ex.raise_if_bad(rows, self.router.nkeys)
         out = torch.empty((rows.numel(),) + shape[1:], dtype=self.dtype, device=rows.device)
         out.index_copy_(0, order.to(rows.device), back)
         return out

@@ -117,6 +117,27 @@ def _vector_case(nkeys, mps, partitioner, dtype, n=3000):
             pass
         got2 = vec.pull(torch.from_numpy(q).to(dev)).cpu().numpy()
         np.testing.assert_array_equal(got2, want)
+        # only rank 0's batch is bad: it raises after the collectives, the other ranks' pushes land
+        k1 = np.array([3], np.int64) if rank else np.array([1, nkeys + 5], np.int64)
+        try:
+            vec.push(torch.from_numpy(k1).to(dev), torch.from_numpy(np.ones(k1.size, np_dtype)).to(dev))
+            assert rank != 0, "out-of-range key accepted"
+        except IndexOutOfBoundsException:
+            assert rank == 0
+        for _ in range(world - 1):
+            assert ref.update(np.array([3], np.int64), np.ones(1, np_dtype)) == -1
+        want, _ = ref.get(q)
+        np.testing.assert_array_equal(vec.pull(torch.from_numpy(q).to(dev)).cpu().numpy(), want)
+        # a bad pull on rank 0 only: the others are answered
+        qb = q.copy()
+        if rank == 0:
+            qb[3] = -1
+        try:
+            got3 = vec.pull(torch.from_numpy(qb).to(dev)).cpu().numpy()
+            assert rank != 0, "out-of-range pull accepted"
+            np.testing.assert_array_equal(got3, want)
+        except IndexOutOfBoundsException:
+            assert rank == 0
         # an empty batch still takes part in the exchange
         vec.push(torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.float64, device=dev))
         assert vec.pull(torch.zeros(0, dtype=torch.int64, device=dev)).numel() == 0

@@ -1,0 +1,120 @@
+"""The exchange step on the device: glint_route_gather_dev (client bucketing + send-buffer gather in
+one pass, AsyncBigVector.scala:96-116 / AsyncBigMatrix.scala:141-156) against the oracle's stable
+bucketing, and the self-launching multi-rank bench (one process per rank, gloo rehearsal on one GPU).
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from glint_amd import _native as N
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def route_gather(keys, nparts, nkeys, slot_of=None, cols=None, vals=None, dev=0):
+    import torch
+    d = torch.device("cuda", dev)
+    lib = N.load()
+    k = torch.from_numpy(keys).to(d)
+    c = None if cols is None else torch.from_numpy(cols).to(d)
+    v = None if vals is None else torch.from_numpy(vals).to(d)
+    so = None if slot_of is None else torch.from_numpy(np.asarray(slot_of, np.int32)).to(d)
+    n = keys.size
+    counts = torch.full((nparts,), -7, dtype=torch.int64, device=d)
+    order = torch.full((max(n, 1),), -7, dtype=torch.int64, device=d)
+    ok = torch.full((max(n, 1),), -7, dtype=torch.int64, device=d)
+    oc = torch.full((max(n, 1),), -7, dtype=torch.int32, device=d)
+    ov = torch.full((max(n, 1),), -7, dtype=v.dtype if v is not None else torch.float64, device=d)
+    bad = torch.full((1,), -7, dtype=torch.int64, device=d)
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    rc = lib.glint_route_gather_dev(k.data_ptr(), p(c), p(v), v.element_size() if v is not None else 0, n,
+                                    N.GLINT_ROUTE_RANGE, nparts, nkeys, p(so), counts.data_ptr(), order.data_ptr(),
+                                    ok.data_ptr(), p(oc) if c is not None else None,
+                                    p(ov) if v is not None else None, bad.data_ptr(),
+                                    torch.cuda.current_stream(d).cuda_stream)
+    torch.cuda.synchronize(d)
+    return rc, counts.cpu().numpy(), order.cpu().numpy()[:n], ok.cpu().numpy()[:n], oc.cpu().numpy()[:n], \
+        ov.cpu().numpy()[:n], int(bad.item())
+
+
+@pytest.mark.parametrize("nparts", [1, 3, 8, 64, 1000])
+@pytest.mark.parametrize("n", [0, 1, 4097, 300_001])
+def test_route_gather_matches_oracle(gpu, nparts, n):
+    nkeys = 1_000_003
+    rng = np.random.default_rng(nparts * 7 + n)
+    keys = rng.integers(0, nkeys, n).astype(np.int64)
+    cols = rng.integers(0, 512, n).astype(np.int32)
+    vals = rng.uniform(-1, 1, n)
+    c_ref, off, o_ref = O.bucket_range(keys, nparts, nkeys)
+    rc, counts, order, ok, oc, ov, bad = route_gather(keys, nparts, nkeys, cols=cols, vals=vals, dev=gpu)
+    assert rc == N.GLINT_OK and bad == 0
+    np.testing.assert_array_equal(counts, c_ref)
+    np.testing.assert_array_equal(order, o_ref)         # stable: the oracle's exact permutation
+    np.testing.assert_array_equal(ok, keys[o_ref])       # send buffers in send order
+    np.testing.assert_array_equal(oc, cols[o_ref])
+    np.testing.assert_array_equal(ov, vals[o_ref])
+
+
+def test_route_gather_slot_order_and_float_values(gpu):
+    """Partitions ordered by hosting rank (rank r hosts r, r + W, ...: Client.scala:75-84), 4-byte values."""
+    nparts, world, nkeys = 6, 4, 50_000
+    perm = [p for r in range(world) for p in range(r, nparts, world)]
+    slot_of = np.empty(nparts, np.int32)
+    slot_of[perm] = np.arange(nparts)
+    rng = np.random.default_rng(1)
+    keys = rng.integers(0, nkeys, 77_777).astype(np.int64)
+    vals = rng.uniform(-1, 1, keys.size).astype(np.float32)
+    c_ref, off, o_ref = O.bucket_range(keys, nparts, nkeys)
+    want = np.concatenate([o_ref[off[p]:off[p + 1]] for p in perm])
+    rc, counts, order, ok, _, ov, bad = route_gather(keys, nparts, nkeys, slot_of=slot_of, vals=vals, dev=gpu)
+    assert rc == N.GLINT_OK and bad == 0
+    np.testing.assert_array_equal(counts, c_ref[perm])
+    np.testing.assert_array_equal(order, want)
+    np.testing.assert_array_equal(ok, keys[want])
+    np.testing.assert_array_equal(ov, vals[want])
+
+
+def test_route_gather_bad_key_word(gpu):
+    keys = np.arange(10_000, dtype=np.int64)
+    keys[7_777] = 10_000
+    keys[9_000] = -5
+    rc, counts, *_, bad = route_gather(keys, 4, 10_000, dev=gpu)
+    assert rc == N.GLINT_OK  # no synchronisation: the status stays on the device
+    assert bad != 0 and ~bad == 7_777
+    assert counts.sum() == keys.size - 2  # bad records are in no group
+
+
+def _bench(args, **env):
+    e = dict(os.environ, **env)
+    e.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, env=e, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("pattern", ["dense", "exchange"])
+def test_bench_self_launches_ranks(gpu, pattern):
+    """`python bench.py --gpus 2` with no launcher: two rank processes (here both on this GPU over
+    gloo -- the rehearsal hooks), one JSON line with n_gpus 2."""
+    d = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--log2-keys", "22", "--pattern", pattern,
+                "--no-cpu-baseline"], GLINT_BENCH_DEVICE=str(gpu), GLINT_BENCH_BACKEND="gloo")
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    if pattern == "dense":
+        assert d["check"] is True
+
+
+@pytest.mark.parametrize("args", [["--pattern", "pull"], ["--pattern", "rowpull"],
+                                  ["--scaling", "strong", "--log2-keys", "24"]])
+def test_bench_patterns(gpu, args):
+    d = _bench(args + ["--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
+    assert d["check"] is True and d["value"] > 0 and d["roofline"]["achieved"] > 0
