@@ -29,7 +29,10 @@
 
 namespace glint {
 
-constexpr int kSlabBits = 12;
+#ifndef GLINT_SLAB_BITS
+#define GLINT_SLAB_BITS 12
+#endif
+constexpr int kSlabBits = GLINT_SLAB_BITS;  // (a build-time experiment knob; 12 = 32 KiB of Double per slab)
 constexpr int kSlab = 1 << kSlabBits;
 constexpr int kMaxDigit = 1024;        // coarse buckets and fine slabs per bucket, at most
 constexpr int kATPB = 1024;            // partition workgroups: 16 waves
@@ -37,9 +40,10 @@ constexpr int kAChunk = 4096;          // records per partition chunk (and dedup
 constexpr int kAPer = kAChunk / kATPB;
 constexpr int kASlots = 8192;          // dedup hash slots (load <= 0.5)
 constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments per bucket)
-constexpr int kFTPB = 256;             // fine partition: one workgroup per coarse bucket
+constexpr int kFTPB = 256;             // fine partition workgroups
 constexpr int kFTile = 2048;           // records staged per fine-partition step
 constexpr int kFPer = kFTile / kFTPB;
+constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
 constexpr int kCTPB = 256;
 constexpr u32 kCItem = 16384;          // records per apply item at most
 constexpr u32 kEmptySlot = 0xFFFFFFFFu;
@@ -57,8 +61,8 @@ __device__ __forceinline__ u32 fine_of(u32 a, const BinGeom& g) { return (a >> k
 struct BinCtl {
   u32 m;       // records the partition emitted (after dedup)
   u32 tail;    // valid records in the tail
-  u32 nslots;  // apply item slots written by bin_fpart (the last bucket's workgroup knows the total)
-  u32 pad_;
+  u32 nslots;  // apply item slots written by bin_fpart (the last bucket's first item knows the total)
+  u32 nfitems; // fine-partition items (written by bin_part's workgroup 0)
 };
 
 // ---- block-level helpers ------------------------------------------------------------------------
@@ -240,21 +244,34 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
 }
 
 // Workgroup w's bucket ranges: cur[b] = chunk_base(w) * kAChunk + exclusive scan of R[w][*], also
-// published as segoff[w][b] for bin_fpart.
+// published bucket-major as segoff[b][w] for the fine partition.
 __device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks, const u32* __restrict__ R,
                                            u32* __restrict__ segoff, u32* cur, u32* dcnt) {
   const u32 base = chunk_base(w, gridDim.x, nchunks) * (u32)kAChunk;
   block_scan<kATPB, 1>(g.nb, [&](u32 b) { return R[w * g.nb + b]; },
                        [&](u32 b, u32 excl) {
                          cur[b] = base + excl;
-                         segoff[w * g.nb + b] = base + excl;
+                         segoff[b * gridDim.x + w] = base + excl;  // bucket-major: bin_fpart reads a row
                          dcnt[b] = 0;
                        });
 }
 
+// Workgroup 0 of bin_part: the fine-partition items -- bucket b gets max(1, ceil(T[b] / kFItem))
+// of them ({b, j}: its records [j * kFItem, (j + 1) * kFItem) in segment order).
+__device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
+                                           BinCtl* bc) {
+  const u32 tot = block_scan<kATPB, 1>(
+      g.nb, [&](u32 b) { return max(1u, (T[b] + kFItem - 1) / kFItem); },
+      [&](u32 b, u32 excl) {
+        const u32 J = max(1u, (T[b] + kFItem - 1) / kFItem);
+        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
+      });
+  if (threadIdx.x == 0) bc->nfitems = tot;
+}
+
 __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
                                             u32* __restrict__ seglen, u32 emitted, BinCtl* bc) {
-  for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[w * g.nb + b] = cur[b] - segoff[w * g.nb + b];
+  for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[b * gridDim.x + w] = cur[b] - segoff[b * gridDim.x + w];
   if (threadIdx.x == 0 && emitted) atomicAdd(&bc->m, emitted);
 }
 
@@ -266,7 +283,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
                                                          const u32* __restrict__ R, u32* __restrict__ segoff,
                                                          u32* __restrict__ seglen, u32* __restrict__ addr_out,
                                                          typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
-                                                         BinCtl* bc) {
+                                                         BinCtl* bc, const u32* __restrict__ T,
+                                                         uint2* __restrict__ fitems) {
   typedef typename LdsAcc<V>::T A;
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
   __shared__ u32 st_a[kAChunk];
@@ -275,6 +293,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   const u32 w = blockIdx.x;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
+  if (w == 0) part_items(g, T, fitems, bc);
   part_setup(g, w, nchunks, R, segoff, cur, dcnt);
   i64 k[kAPer];
   int32_t cl[kAPer];
@@ -317,7 +336,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     const i64* __restrict__ keys, const int32_t* __restrict__ cols, const V* __restrict__ vals, i64 n, PartDesc part,
     const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, const u32* __restrict__ R,
     u32* __restrict__ segoff, u32* __restrict__ seglen, u32* __restrict__ addr_out,
-    typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc) {
+    typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc, const u32* __restrict__ T,
+    uint2* __restrict__ fitems) {
   typedef typename LdsAcc<V>::T A;
   static_assert(kAChunk * (4 + sizeof(A)) <= kASlots * sizeof(A), "staging must fit the value table");
   __shared__ u32 hk[kASlots];
@@ -337,6 +357,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     hv[sl] = A(0);
   }
   if (tid == 0) nused = 0;
+  if (w == 0) part_items(g, T, fitems, bc);
   part_setup(g, w, nchunks, R, segoff, cur, dcnt);
   const u64 below = (1ull << lane) - 1ull;
   i64 k[kAPer];
@@ -413,92 +434,146 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
 }
 
-// ---- bin_fpart: one workgroup per coarse bucket ------------------------------------------------------
-// Record v of the bucket (0 <= v < M, segments in workgroup order) lives at segst[s] + v - segpre[s].
-// Each thread visits increasing v, so it walks the segment list with a cursor.
+// ---- fine partition ---------------------------------------------------------------------------------
+// Record v of bucket b (0 <= v < M_b, segments in partition-workgroup order) lives at
+// segst[s] + v - segpre[s]. Each thread visits increasing v, so it walks the segment list with a cursor.
 __device__ __forceinline__ u32 seg_addr(u32 v, u32& s, const u32* segpre, const u32* segst) {
   while (segpre[s + 1] <= v) ++s;
   return segst[s] + (v - segpre[s]);
 }
 
+// bucket b's segment table into LDS; returns M_b
+__device__ __forceinline__ u32 load_segments(const BinGeom& g, u32 G, u32 b, const u32* __restrict__ segoff,
+                                             const u32* __restrict__ seglen, u32* segpre, u32* segst) {
+  const u32 M = block_scan<kFTPB, 4>(
+      G, [&](u32 w) { return seglen[b * G + w]; },
+      [&](u32 w, u32 excl) {
+        segpre[w] = excl;
+        segst[w] = segoff[b * G + w];
+      });
+  if (threadIdx.x == 0) segpre[G] = M;
+  __syncthreads();
+  return M;
+}
+
+// per item: records per slab -> H[slab] (exact counts after dedup)
+__global__ __launch_bounds__(kFTPB) void bin_fcount_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
+                                                           const BinCtl* bc, const u32* __restrict__ segoff,
+                                                           const u32* __restrict__ seglen,
+                                                           const u32* __restrict__ addr_in, u32* __restrict__ H) {
+  __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
+  __shared__ u32 fh[kMaxDigit];
+  const int tid = threadIdx.x;
+  const u32 nit = bc->nfitems;
+  for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
+    const uint2 d = fitems[it];
+    const u32 b = d.x;
+    for (u32 f = tid; f < g.nf; f += kFTPB) fh[f] = 0;
+    const u32 M = load_segments(g, G, b, segoff, seglen, segpre, segst);
+    const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
+    u32 s = 0;
+    for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
+      u32 a[kFPer];
+#pragma unroll
+      for (int q = 0; q < kFPer; ++q) {
+        const u32 v = t0 + q * kFTPB + tid;
+        a[q] = v < v1 ? addr_in[seg_addr(v, s, segpre, segst)] : kEmptySlot;
+      }
+#pragma unroll
+      for (int q = 0; q < kFPer; ++q)
+        if (a[q] != kEmptySlot) atomicAdd(&fh[fine_of(a[q], g)], 1u);
+    }
+    __syncthreads();
+    for (u32 f = tid; f < g.nf; f += kFTPB)
+      if (fh[f]) atomicAdd(&H[b * g.nf + f], fh[f]);
+    __syncthreads();
+  }
+}
+
+// per item: its records moved to their slab ranges. Slab f of bucket b starts at
+// ob(b) + exclusive scan of H[b][*]; an item reserves its share of each slab with one returning
+// atomic (cur2), then moves tiles of kFTile records, staged in LDS so the stores are runs. The
+// bucket's first item also writes the apply items of its slabs.
 template <typename A>
-__global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, const u32* __restrict__ T,
+__global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
+                                                          BinCtl* bc, const u32* __restrict__ T,
+                                                          const u32* __restrict__ H, u32* __restrict__ cur2,
                                                           const u32* __restrict__ segoff,
                                                           const u32* __restrict__ seglen,
                                                           const u32* __restrict__ addr_in,
                                                           const A* __restrict__ val_in, u32* __restrict__ addr_out,
                                                           A* __restrict__ val_out, uint4* __restrict__ cdesc,
-                                                          BinCtl* bc, u64* hint) {
+                                                          u64* hint) {
   __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
-  __shared__ u32 fcnt[kMaxDigit], fcur[kMaxDigit], tcnt[kMaxDigit], tpos[kMaxDigit];
+  __shared__ u32 sst[kMaxDigit], fcur[kMaxDigit], tcnt[kMaxDigit], tpos[kMaxDigit];
   __shared__ u32 st_a[kFTile];
   __shared__ A st_v[kFTile];
   const int tid = threadIdx.x;
-  const u32 b = blockIdx.x;
-  if (b == 0 && tid == 0 && hint)  // for the host's next binned push: how much did dedup keep?
+  if (blockIdx.x == 0 && tid == 0 && hint)  // for the host's next binned push: how much did dedup keep?
     __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  // where this bucket's records go, and its apply item slots
-  u32 ob = 0, ib = 0;
-  for (u32 x = tid; x < b; x += kFTPB) {
-    const u32 t = T[x];
-    ob += t;
-    ib += g.nf + (t + kCItem - 1) / kCItem;
-  }
-  ob = block_sum<kFTPB>(ob);
-  ib = block_sum<kFTPB>(ib);
-  const u32 nslots = g.nf + (T[b] + kCItem - 1) / kCItem;
-  if (b == g.nb - 1 && tid == 0) bc->nslots = ib + nslots;  // bin_apply's item count
-  // the bucket's segments, one per partition workgroup
-  const u32 M = block_scan<kFTPB, 4>(
-      G, [&](u32 w) { return seglen[w * g.nb + b]; },
-      [&](u32 w, u32 excl) {
-        segpre[w] = excl;
-        segst[w] = segoff[w * g.nb + b];
-      });
-  if (tid == 0) segpre[G] = M;
-  for (u32 f = tid; f < g.nf; f += kFTPB) {
-    fcnt[f] = 0;
-    tcnt[f] = 0;
-  }
-  __syncthreads();
-  // pass 1: records per slab
-  {
-    u32 s = 0;
-    for (u32 v0 = 0; v0 < M; v0 += kFTile) {
-      u32 a[kFPer];
-#pragma unroll
-      for (int q = 0; q < kFPer; ++q) {
-        const u32 v = v0 + q * kFTPB + tid;
-        a[q] = v < M ? addr_in[seg_addr(v, s, segpre, segst)] : kEmptySlot;
-      }
-#pragma unroll
-      for (int q = 0; q < kFPer; ++q)
-        if (a[q] != kEmptySlot) atomicAdd(&fcnt[fine_of(a[q], g)], 1u);
+  const u32 nit = bc->nfitems;
+  for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
+    const uint2 d = fitems[it];
+    const u32 b = d.x;
+    // where the bucket's records go (raw capacities: holes only at bucket ends) and its item slots
+    u32 ob = 0, ib = 0;
+    for (u32 x = tid; x < b; x += kFTPB) {
+      const u32 t = T[x];
+      ob += t;
+      ib += g.nf + (t + kCItem - 1) / kCItem;
     }
-  }
-  __syncthreads();
-  // slab starts, then the apply items of the bucket's slabs {slab, first, end, exclusive}
-  block_scan<kFTPB, 4>(g.nf, [&](u32 f) { return fcnt[f]; }, [&](u32 f, u32 excl) { fcur[f] = ob + excl; });
-  const u32 used_slots = block_scan<kFTPB, 4>(
-      g.nf, [&](u32 f) { return (fcnt[f] + kCItem - 1) / kCItem; },
-      [&](u32 f, u32 excl) {
-        const u32 c = fcnt[f], s0 = fcur[f];
-        const u32 m = (c + kCItem - 1) / kCItem;
-        for (u32 q = 0; q < m; ++q)
-          cdesc[ib + excl + q] = make_uint4(b * g.nf + f, s0 + q * kCItem, s0 + min(c, (q + 1) * kCItem), m == 1u ? 1u : 0u);
-      });
-  for (u32 x = used_slots + tid; x < nslots; x += kFTPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
-  // pass 2: tiles of kFTile records moved to their slab ranges, staged in LDS so stores are runs
-  {
+    ob = block_sum<kFTPB>(ob);
+    ib = block_sum<kFTPB>(ib);
+    for (u32 f = tid; f < g.nf; f += kFTPB) tcnt[f] = 0;
+    block_scan<kFTPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
+    if (d.y == 0) {  // the bucket's apply items {slab, first, end, exclusive}, then unused slots
+      const u32 nslots = g.nf + (T[b] + kCItem - 1) / kCItem;
+      if (b == g.nb - 1 && tid == 0) bc->nslots = ib + nslots;  // bin_apply's item count
+      const u32 used_slots = block_scan<kFTPB, 4>(
+          g.nf, [&](u32 f) { return (H[b * g.nf + f] + kCItem - 1) / kCItem; },
+          [&](u32 f, u32 excl) {
+            const u32 c = H[b * g.nf + f], s0 = sst[f];
+            const u32 m = (c + kCItem - 1) / kCItem;
+            for (u32 q = 0; q < m; ++q)
+              cdesc[ib + excl + q] =
+                  make_uint4(b * g.nf + f, s0 + q * kCItem, s0 + min(c, (q + 1) * kCItem), m == 1u ? 1u : 0u);
+          });
+      for (u32 x = used_slots + tid; x < nslots; x += kFTPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
+    }
+    const u32 M = load_segments(g, G, b, segoff, seglen, segpre, segst);
+    const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
+    // pass 1: this item's records per slab; reserve the item's share of each slab
+    {
+      u32 s = 0;
+      for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
+        u32 a[kFPer];
+#pragma unroll
+        for (int q = 0; q < kFPer; ++q) {
+          const u32 v = t0 + q * kFTPB + tid;
+          a[q] = v < v1 ? addr_in[seg_addr(v, s, segpre, segst)] : kEmptySlot;
+        }
+#pragma unroll
+        for (int q = 0; q < kFPer; ++q)
+          if (a[q] != kEmptySlot) atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
+      }
+    }
+    __syncthreads();
+    for (u32 f = tid; f < g.nf; f += kFTPB) {
+      const u32 c = tcnt[f];
+      fcur[f] = c ? sst[f] + atomicAdd(&cur2[b * g.nf + f], c) : 0u;
+      tcnt[f] = 0;
+    }
+    __syncthreads();
+    // pass 2: tiles moved to their slab ranges
     u32 s = 0;
-    for (u32 v0 = 0; v0 < M; v0 += kFTile) {
+    for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
       u32 a[kFPer], rank[kFPer];
       A val[kFPer];
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
-        const u32 v = v0 + q * kFTPB + tid;
+        const u32 v = t0 + q * kFTPB + tid;
         a[q] = kEmptySlot;
-        if (v < M) {
+        if (v < v1) {
           const u32 r = seg_addr(v, s, segpre, segst);
           a[q] = addr_in[r];
           val[q] = val_in[r];
@@ -542,7 +617,26 @@ constexpr int kCRB = 4;  // records per thread per batch: loads issue together, 
 
 // One work item = up to kCItem records of one slab: summed in LDS (A, a byte flag per touched
 // element), then one coalesced read-modify-write of the touched pairs (exclusive items) or device
-// atomics (items of a slab that was cut into several).
+// atomics (items of a slab that was cut into several). Software-pipelined: the next item's
+// descriptor and first record batch are loaded before this item's read-modify-write, so their
+// latencies overlap.
+template <typename A>
+__device__ __forceinline__ void apply_fetch(const uint4& d, const u32* __restrict__ addr, const A* __restrict__ val,
+                                            u32 (&ad)[kCRB], A (&v)[kCRB]) {
+#pragma unroll
+  for (int q = 0; q < kCRB; ++q) {  // clamped, branch-free loads
+    const u32 j = d.y + q * kCTPB + threadIdx.x;
+    const u32 jj = j < d.z ? j : d.z - 1;
+    ad[q] = kEmptySlot;
+    v[q] = A(0);
+    if (d.w != kItemEmpty && d.z > d.y) {
+      ad[q] = addr[jj];
+      v[q] = val[jj];
+      if (j >= d.z) ad[q] = kEmptySlot;
+    }
+  }
+}
+
 template <typename V>
 __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict__ addr,
                                                           const typename LdsAcc<V>::T* __restrict__ val,
@@ -554,10 +648,27 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
   __shared__ uint8_t touched[kSlab];  // plain byte stores: no atomic serialisation on hot elements
   constexpr int kPairsPerThread = kSlab / 2 / kCTPB;
   const int tid = threadIdx.x;
+  const uint4 kEmpty4 = make_uint4(0u, 0u, 0u, kItemEmpty);
   const u32 nslots = bc->nslots;  // written by bin_fpart: slots past it hold an older push's items
-  for (u32 it = blockIdx.x; it < nslots; it += gridDim.x) {
-    const uint4 d4 = cdesc[it];
-    if (d4.w == kItemEmpty) continue;  // block-uniform
+  u32 it = blockIdx.x;
+  uint4 nd = it < nslots ? cdesc[it] : kEmpty4;
+  u32 pa[kCRB];
+  A pv[kCRB];
+  apply_fetch<A>(nd, addr, val, pa, pv);
+  for (; it < nslots; it += gridDim.x) {
+    const uint4 d4 = nd;
+    u32 ca[kCRB];
+    A cv[kCRB];
+#pragma unroll
+    for (int q = 0; q < kCRB; ++q) {
+      ca[q] = pa[q];
+      cv[q] = pv[q];
+    }
+    nd = it + gridDim.x < nslots ? cdesc[it + gridDim.x] : kEmpty4;
+    if (d4.w == kItemEmpty) {  // block-uniform
+      apply_fetch<A>(nd, addr, val, pa, pv);
+      continue;
+    }
     const u32 slab = d4.x;
     const bool exclusive = d4.w == 1u;
     const u32 r_lo = d4.y, r_hi = d4.z;
@@ -576,27 +687,21 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
     for (int e = tid; e < kSlab; e += kCTPB) acc[e] = A(0);
     for (int w = tid; w < kSlab / 16; w += kCTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    for (u32 j0 = r_lo; j0 < r_hi; j0 += (u32)kCTPB * kCRB) {
-      u32 ad[kCRB];
-      A v[kCRB];
-#pragma unroll
-      for (int q = 0; q < kCRB; ++q) {  // clamped, branch-free loads
-        const u32 j = j0 + q * kCTPB + tid;
-        const u32 jj = j < r_hi ? j : r_hi - 1;
-        ad[q] = addr[jj];
-        v[q] = val[jj];
-        if (j >= r_hi) ad[q] = kEmptySlot;
-      }
+    for (u32 j0 = r_lo;;) {  // the first batch came with the prefetch
 #pragma unroll
       for (int q = 0; q < kCRB; ++q) {
-        if (ad[q] == kEmptySlot) continue;
-        const u32 e = ad[q] & (kSlab - 1);
-        lds_add(&acc[e], v[q]);
+        if (ca[q] == kEmptySlot) continue;
+        const u32 e = ca[q] & (kSlab - 1);
+        lds_add(&acc[e], cv[q]);
         touched[e] = 1;
       }
+      j0 += (u32)kCTPB * kCRB;
+      if (j0 >= r_hi) break;
+      apply_fetch<A>(make_uint4(0u, j0, r_hi, 0u), addr, val, ca, cv);
     }
     asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
     __syncthreads();
+    apply_fetch<A>(nd, addr, val, pa, pv);  // the next item's first batch: in flight during the RMW
     if (exclusive) {
       // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair instead
       // (one cached line), so all loads issue back to back without a branch
@@ -645,9 +750,9 @@ BinGeom bin_geometry(i64 elems) {
   const i64 slabs = (elems + kSlab - 1) / kSlab;
   u32 sb = 0;
   while (((i64)1 << sb) < slabs) ++sb;
-  // up to 1024 coarse buckets (one fine-partition workgroup each: enough to fill the chip), the rest
-  // of the slab bits fine (<= 10: slabs < 2^20 for u32 addresses)
-  const u32 cb = std::min<u32>(sb, 10u);
+  // up to 256 coarse buckets (few enough that a partition chunk's records form runs per bucket), more
+  // only when the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses)
+  const u32 cb = std::min<u32>(sb, std::max<u32>(8u, sb > 10u ? sb - 10u : 0u));
   BinGeom g;
   g.fb = sb - cb;
   g.nb = 1u << cb;
@@ -682,23 +787,29 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? 1 : 2)));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
-  // [BinCtl | T] zeroed per push; then R, segoff, seglen, item slots, the two record buffers
+  const i64 max_fitems = (i64)g.nb + n / kFItem + 1;
+  // [BinCtl | T | H | cur2] zeroed per push; then R, segoff, seglen, item maps, the record buffers
   const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
-  const size_t b_cd = pad256((size_t)nslots * 16);
+  const size_t b_H = pad256((size_t)g.nslab * 4);
+  const size_t b_cd = pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8);
   const size_t cap_a = (size_t)nchunks_max * kAChunk;  // the partition's capacity (every chunk full)
   const size_t b_a = pad256(cap_a * 4), b_v = pad256(cap_a * sizeof(A));
-  const size_t need = b_ctl + b_T + 3 * b_seg + b_cd + 2 * (b_a + b_v);
+  const size_t b_zero = b_ctl + b_T + 2 * b_H;
+  const size_t need = b_zero + 3 * b_seg + b_cd + 2 * (b_a + b_v);
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   char* p = (char*)s->d_bin;
   BinCtl* bc = (BinCtl*)p;
   u32* T = (u32*)(p + b_ctl);
-  p += b_ctl + b_T;
+  u32* H = (u32*)(p + b_ctl + b_T);
+  u32* cur2 = (u32*)(p + b_ctl + b_T + b_H);
+  p += b_zero;
   u32* R = (u32*)p;
   u32* segoff = (u32*)(p + b_seg);
   u32* seglen = (u32*)(p + 2 * b_seg);
   p += 3 * b_seg;
   uint4* cdesc = (uint4*)p;
+  uint2* fitems = (uint2*)(p + pad256((size_t)nslots * 16));
   p += b_cd;
   u32* addr_a = (u32*)p;
   A* val_a = (A*)(p + b_a);
@@ -706,20 +817,23 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   A* val_b = (A*)(p + 2 * b_a + b_v);
 
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
-  HIPCHK(hipMemsetAsync(s->d_bin, 0, b_ctl + b_T, st));
+  HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
   bin_count_kernel<MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
   HIPCHK(hipGetLastError());
   if (dedup) {
     bin_part_dedup_kernel<V, MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R,
-                                                       segoff, seglen, addr_a, val_a, a.err, bc);
+                                                       segoff, seglen, addr_a, val_a, a.err, bc, T, fitems);
   } else {
     bin_part_kernel<V, MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff,
-                                                 seglen, addr_a, val_a, a.err, bc);
+                                                 seglen, addr_a, val_a, a.err, bc, T, fitems);
   }
   HIPCHK(hipGetLastError());
-  bin_fpart_kernel<A><<<g.nb, kFTPB, 0, st>>>(g, G, T, segoff, seglen, addr_a, val_a, addr_b, val_b, cdesc, bc,
-                                              s->d_hint ? s->d_hint + 1 : nullptr);
+  const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * 4);
+  bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H);
+  HIPCHK(hipGetLastError());
+  bin_fpart_kernel<A><<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
+                                            val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr);
   HIPCHK(hipGetLastError());
   static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
     const char* e = getenv("GLINT_BIN_APPLY_BPC");
