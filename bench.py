@@ -247,7 +247,7 @@ def main():
         kg = torch.Generator(device=dev)
         kg.manual_seed(1042 + rank)
         keys = torch.randint(0, partitioner.size, (nrec,), dtype=torch.int64, device=dev, generator=kg)
-        vals = vals[:nrec].contiguous()
+        vals = torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
         # distinct elements a rank receives per push (uniform, ~nrec records into n keys): expected value
         uniq = int(n * (1.0 - np.exp(-nrec / n)))
         tag = f"exchange_2p{args.log2_keys}"

@@ -100,7 +100,7 @@ def build_loopback(force: bool = False, verbose: bool = False) -> Path:
     LOOPBACK_BIN.parent.mkdir(parents=True, exist_ok=True)
     tmp = LOOPBACK_BIN.with_suffix(".tmp")
     cc = shutil.which("gcc") or "cc"
-    cmd = [cc, "-O2", "-std=c11", "-Wall", "-pthread", "-o", str(tmp), str(LOOPBACK_SRC), "-ldl"]
+    cmd = [cc, "-O2", "-std=c11", "-Wall", "-pthread", "-o", str(tmp), str(LOOPBACK_SRC), "-ldl", "-lm"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=str(ROOT))
@@ -108,10 +108,36 @@ def build_loopback(force: bool = False, verbose: bool = False) -> Path:
     return LOOPBACK_BIN
 
 
+JNI_SHIM = ROOT / "integration" / "jni" / "glint_jni.c"
+JNI_DRIVER_SRC = ROOT / "tests" / "c" / "fake_jvm.c"
+JNI_DRIVER = ROOT / "tests" / "c" / "build" / "fake_jvm"
+
+
+def build_jni_driver(force: bool = False, verbose: bool = False) -> Path:
+    """The JNI shim (integration/jni/glint_jni.c) compiled against tests/c/jni.h -- a minimal JNI
+    environment -- and linked with a driver that calls its native methods as the actors do. This is
+    the shim's compile check (there is no JDK in the image) and, on a GPU, its end-to-end test."""
+    deps = [JNI_SHIM, JNI_DRIVER_SRC, ROOT / "tests" / "c" / "jni.h", ROOT / "include" / "glint_gpu.h", LIB]
+    if not force and not _stale(JNI_DRIVER, deps):
+        return JNI_DRIVER
+    JNI_DRIVER.parent.mkdir(parents=True, exist_ok=True)
+    tmp = JNI_DRIVER.with_suffix(".tmp")
+    cc = shutil.which("gcc") or "cc"
+    cmd = [cc, "-O2", "-Wall", "-Werror", "-std=c11", "-I", str(ROOT / "tests" / "c"), "-I", str(ROOT / "include"),
+           str(JNI_DRIVER_SRC), str(JNI_SHIM), "-L", str(LIB_DIR), "-lglint_gpu", f"-Wl,-rpath,{LIB_DIR}",
+           "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=str(ROOT))
+    os.replace(tmp, JNI_DRIVER)
+    return JNI_DRIVER
+
+
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_gpu_lib(force=force, verbose=verbose)
     build_oracle(force=force, verbose=verbose)
     build_loopback(force=force, verbose=verbose)
+    build_jni_driver(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":

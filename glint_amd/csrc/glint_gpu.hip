@@ -722,6 +722,12 @@ void free_shard(glint_shard* s) {
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->order_ev) (void)hipEventDestroy(s->order_ev);
+    for (auto& r : s->ring) {
+      if (r.h) (void)hipHostFree(r.h);
+      if (r.d) (void)hipFree(r.d);
+      if (r.herr) (void)hipHostFree(r.herr);
+      if (r.done) (void)hipEventDestroy(r.done);
+    }
     (void)hipGetLastError();
   }
   delete s;
@@ -1015,6 +1021,134 @@ int finish(glint_shard* s) {
   return GLINT_EOUTOFRANGE;
 }
 
+// ---- pinned ring (pipelined ingest) -------------------------------------------------------------
+constexpr i64 kRingMaxRecords = (i64)1 << 20;
+
+struct StageLayout {
+  size_t kb, cb, vb, total;  // keys | cols (matrix) | values, each section 256-aligned
+};
+StageLayout stage_layout(const glint_shard* s, i64 n) {
+  StageLayout L;
+  L.kb = pad256((size_t)n * 8);
+  L.cb = s->part.cols != 0 ? pad256((size_t)n * 4) : 0;
+  L.vb = pad256((size_t)n * s->vsize);
+  L.total = L.kb + L.cb + L.vb;
+  return L;
+}
+
+// wait for a slot's push; remember the first error it saw that was not reported yet
+int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
+  if (!r.inflight) return GLINT_OK;
+  HIPCHK(hipEventSynchronize(r.done));
+  r.inflight = false;
+  const u64 enc = r.herr->min_bad_enc;  // cumulative until cleared: skip what was reported already
+  if (enc != 0 && enc != s->reported_enc && s->ring_bad < 0) {
+    s->ring_bad = (i64)~enc;
+    s->ring_bad_enc = enc;
+  }
+  return GLINT_OK;
+}
+
+int ring_acquire_locked(glint_shard* s, i64 n, int* slot) {
+  if (n < 0 || n > kRingMaxRecords) return GLINT_EINVAL;
+  const StageLayout L = stage_layout(s, n);
+  for (int tries = 0; tries < GLINT_RING_SLOTS; ++tries) {
+    const int idx = s->ring_next;
+    s->ring_next = (idx + 1) % GLINT_RING_SLOTS;
+    glint_shard::RingSlot& r = s->ring[idx];
+    if (r.acquired) continue;  // handed out and not pushed yet
+    int rc = ring_retire(s, r);
+    if (rc) return rc;
+    if (r.hcap < L.total) {
+      if (r.h) (void)hipHostFree(r.h);
+      r.h = r.hd = nullptr;
+      r.hcap = 0;
+      size_t cap = (size_t)1 << 16;
+      while (cap < L.total) cap <<= 1;
+      if (hipHostMalloc((void**)&r.h, cap, hipHostMallocMapped) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&r.hd, r.h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        if (r.h) (void)hipHostFree(r.h);
+        r.h = r.hd = nullptr;
+        return GLINT_ENOMEM;
+      }
+      r.hcap = cap;
+    }
+    if (!r.done && hipEventCreateWithFlags(&r.done, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      r.done = nullptr;
+      return GLINT_EDEVICE;
+    }
+    if (!r.herr && hipHostMalloc((void**)&r.herr, sizeof(ErrState), hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      r.herr = nullptr;
+      return GLINT_ENOMEM;
+    }
+    r.acquired = true;
+    r.n = n;
+    *slot = idx;
+    return GLINT_OK;
+  }
+  return GLINT_ENOMEM;  // every slot handed out and not pushed
+}
+
+// Enqueues the push staged in slot idx. Small pushes are read by the kernel from the mapped pinned
+// slot itself (no copy command in the stream); larger ones are copied with one DMA first.
+int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
+  if (idx < 0 || idx >= GLINT_RING_SLOTS) return GLINT_EINVAL;
+  glint_shard::RingSlot& r = s->ring[idx];
+  if (!r.acquired || n < 0 || n > r.n) return GLINT_EINVAL;
+  int rc = order_after_dev(s);
+  if (rc) return rc;
+  const StageLayout L = stage_layout(s, r.n);  // the sections as handed out
+  const bool mat = s->part.cols != 0;
+  const char* base = r.hd;
+  if (n > GLINT_ZERO_COPY_MAX) {
+    rc = grow((void**)&r.d, &r.dcap, L.total);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(r.d, r.h, L.total, hipMemcpyHostToDevice, s->stream));
+    base = r.d;
+  }
+  const i64* keys = (const i64*)base;
+  const int32_t* cols = mat ? (const int32_t*)(base + L.kb) : nullptr;
+  const void* vals = base + L.kb + L.cb;
+  const int hflags = flags | kPushHostSequential;  // the actor's update: message order by default
+  if (n > 0) {
+    if (mat) {
+      rc = [&]() -> int { GLINT_DISPATCH(s->dtype, push_mat_t, s, keys, cols, vals, n, hflags, s->stream); }();
+    } else {
+      rc = [&]() -> int { GLINT_DISPATCH(s->dtype, push_vec_t, s, keys, nullptr, vals, n, hflags, s->stream); }();
+    }
+    if (rc) {
+      (void)hipStreamSynchronize(s->stream);
+      r.acquired = false;
+      return rc;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipEventRecord(r.done, s->stream));
+  r.ticket = ++s->ticket_next;
+  r.inflight = true;
+  r.acquired = false;
+  if (ticket) *ticket = r.ticket;
+  return GLINT_OK;
+}
+
+int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
+  for (auto& r : s->ring)
+    if (r.inflight && r.ticket <= ticket) {
+      int rc = ring_retire(s, r);
+      if (rc) return rc;
+    }
+  if (s->ring_bad < 0) return GLINT_OK;
+  s->last_bad = s->ring_bad;
+  if (first_bad) *first_bad = s->ring_bad;
+  s->ring_bad = -1;
+  s->reported_enc = s->ring_bad_enc;
+  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
+  return GLINT_EOUTOFRANGE;
+}
+
 int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols, const void* vals, int64_t n,
               int flags) {
   if (n < 0 || (n > 0 && (!keys || !vals || (mat && !cols)))) return GLINT_EINVAL;
@@ -1024,6 +1158,20 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
   DeviceGuard g(s->device);
   int rc = order_after_dev(s);
   if (rc) return rc;
+  if (n <= GLINT_ZERO_COPY_MAX) {  // Akka-sized: one pinned slot, read in place by the kernel, then wait
+    int slot = -1;
+    rc = ring_acquire_locked(s, n, &slot);
+    if (rc) return rc;
+    glint_shard::RingSlot& r = s->ring[slot];
+    const StageLayout L = stage_layout(s, n);
+    std::memcpy(r.h, keys, (size_t)n * 8);
+    if (mat) std::memcpy(r.h + L.kb, cols, (size_t)n * 4);
+    std::memcpy(r.h + L.kb + L.cb, vals, (size_t)n * s->vsize);
+    u64 ticket = 0;
+    rc = ring_push_locked(s, slot, n, flags, &ticket);
+    if (rc) return rc;
+    return ring_wait_locked(s, ticket, nullptr);
+  }
   Staged st;
   const void* src[3] = {keys, mat ? (const void*)cols : vals, vals};
   size_t bytes[3] = {(size_t)n * 8, mat ? (size_t)n * 4 : (size_t)n * s->vsize, (size_t)n * s->vsize};
@@ -1056,6 +1204,38 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   DeviceGuard g(s->device);
   int rc = order_after_dev(s);
   if (rc) return rc;
+  if (kind != 2 && n <= GLINT_ZERO_COPY_MAX) {
+    // Akka-sized: the kernel reads the keys from a mapped pinned ring slot and writes the answer
+    // into it, so the call is one launch and one event wait, with no copy command either way
+    int slot = -1;
+    rc = ring_acquire_locked(s, n, &slot);
+    if (rc) return rc;
+    glint_shard::RingSlot& r = s->ring[slot];
+    const StageLayout L = stage_layout(s, n);
+    std::memcpy(r.h, keys, (size_t)n * 8);
+    if (kind == 1) std::memcpy(r.h + L.kb, cols, (size_t)n * 4);
+    char* out_d = r.hd + L.kb + L.cb;
+    r.acquired = false;
+    if (kind == 0) {
+      rc = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)r.hd, out_d, n, s->stream); }();
+    } else {
+      rc = [&]() -> int {
+        GLINT_DISPATCH(s->dtype, launch_mat_pull, s, (const i64*)r.hd, (const int32_t*)(r.hd + L.kb), out_d, n,
+                       s->stream);
+      }();
+    }
+    if (rc) {
+      (void)hipStreamSynchronize(s->stream);
+      return rc;
+    }
+    HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipEventRecord(r.done, s->stream));
+    r.ticket = ++s->ticket_next;
+    r.inflight = true;
+    rc = ring_wait_locked(s, r.ticket, nullptr);  // also reports errors of pushes enqueued before it
+    if (rc == GLINT_OK) std::memcpy(out, r.h + L.kb + L.cb, (size_t)n * s->vsize);
+    return rc;
+  }
   const size_t out_bytes = (size_t)n * s->vsize * (kind == 2 ? (size_t)s->part.cols : 1);
   Staged st;
   const void* src[2] = {keys, cols};
@@ -1138,6 +1318,60 @@ int glint_push_wire(glint_shard_t s, const uint8_t* payload, size_t len, int32_t
   const uint8_t* cols = keys + (size_t)n * 8;
   const uint8_t* vals = cols + (mat ? (size_t)n * 4 : 0);
   return host_push(s, mat, (const int64_t*)keys, (const int32_t*)cols, vals, n, flags);
+}
+
+int glint_stage_acquire(glint_shard_t s, int64_t n, void** keys, void** cols, void** vals, int* slot) {
+  if (!s || !keys || !vals || !slot) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  int rc = ring_acquire_locked(s, n, slot);
+  if (rc) return rc;
+  glint_shard::RingSlot& r = s->ring[*slot];
+  const StageLayout L = stage_layout(s, n);
+  *keys = r.h;
+  if (cols) *cols = s->part.cols != 0 ? r.h + L.kb : nullptr;
+  *vals = r.h + L.kb + L.cb;
+  return GLINT_OK;
+}
+
+int glint_push_staged(glint_shard_t s, int slot, int64_t n, int flags, uint64_t* ticket) {
+  if (!s) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  return ring_push_locked(s, slot, n, flags, (u64*)ticket);
+}
+
+int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, int32_t* id, int flags,
+                          uint64_t* ticket) {
+  if (!s || !payload || len < 9) return GLINT_EINVAL;
+  bool mat = false;
+  const int dt = wire_dtype_of_push(payload[0], &mat);
+  if (dt < 0 || dt != s->dtype || mat != (s->part.cols != 0)) return GLINT_EINVAL;
+  int32_t n = 0, mid = 0;
+  std::memcpy(&n, payload + 1, 4);
+  std::memcpy(&mid, payload + 5, 4);
+  if (n < 0) return GLINT_EINVAL;
+  if (len != 9 + (size_t)n * (8 + (mat ? 4 : 0) + s->vsize)) return GLINT_EINVAL;
+  if (id) *id = mid;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  int slot = -1;
+  int rc = ring_acquire_locked(s, n, &slot);
+  if (rc) return rc;
+  glint_shard::RingSlot& r = s->ring[slot];
+  const StageLayout L = stage_layout(s, n);
+  const uint8_t* kp = payload + 9;  // unaligned sections, copied as they lie
+  std::memcpy(r.h, kp, (size_t)n * 8);
+  if (mat) std::memcpy(r.h + L.kb, kp + (size_t)n * 8, (size_t)n * 4);
+  std::memcpy(r.h + L.kb + L.cb, kp + (size_t)n * (8 + (mat ? 4 : 0)), (size_t)n * s->vsize);
+  return ring_push_locked(s, slot, n, flags, (u64*)ticket);
+}
+
+int glint_shard_wait(glint_shard_t s, uint64_t ticket, int64_t* first_bad) {
+  if (!s) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  return ring_wait_locked(s, (u64)ticket, (i64*)first_bad);
 }
 
 // RequestSerializer.fromBinary for the pull messages + ResponseSerializer.toBinary of the answer

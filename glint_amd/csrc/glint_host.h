@@ -43,6 +43,25 @@ struct glint_shard {
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
   ErrState* h_err = nullptr;  // pinned: the device error state lands here with the push's last copy
+  // pipelined ingest (glint_stage_acquire / glint_push_staged / glint_push_wire_async / glint_shard_wait):
+  // a ring of pinned, device-mapped host slots; each in-flight push owns one until its event completes
+  struct RingSlot {
+    char* h = nullptr;       // pinned host memory, mapped (small pushes are read in place by the kernel)
+    char* hd = nullptr;      // its device-side address
+    size_t hcap = 0;
+    char* d = nullptr;       // device copy target for larger pushes
+    size_t dcap = 0;
+    hipEvent_t done = nullptr;
+    ErrState* herr = nullptr;  // pinned: the shard's error state right after this push
+    uint64_t ticket = 0;
+    int64_t n = 0;
+    bool inflight = false, acquired = false;
+  } ring[GLINT_RING_SLOTS];
+  int ring_next = 0;
+  uint64_t ticket_next = 0;
+  int64_t ring_bad = -1;       // first bad record of a retired push, not reported yet
+  uint64_t ring_bad_enc = 0;
+  uint64_t reported_enc = 0;   // error state last reported (cumulative until cleared)
   u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
   u64* d_hint = nullptr;
   i64 last_bad = -1;

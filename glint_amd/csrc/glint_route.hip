@@ -193,7 +193,7 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   if (n > 0 && !keys) return GLINT_EINVAL;
   if (n >= ((i64)1 << 32)) return GLINT_EINVAL;  // 32-bit offsets
   if (out.vals && out.vsize != 4 && out.vsize != 8) return GLINT_EINVAL;
-  if ((out.vals && !out.in_vals) || (out.cols && !out.in_cols)) return GLINT_EINVAL;
+  if (n > 0 && ((out.vals && !out.in_vals) || (out.cols && !out.in_cols))) return GLINT_EINVAL;
   int dev = 0;
   if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();

@@ -129,6 +129,50 @@ class _Shard:
         check(self.lib.glint_shard_data(self.handle, C.byref(p)), self.handle)
         return p.value or 0
 
+    # pipelined host ingest (include/glint_gpu.h): enqueue now, wait for the ticket before acknowledging
+    def push_async(self, *arrays, deterministic: bool = False, unordered: bool = False) -> int:
+        """Stage (keys, values) -- or (rows, cols, values) for a matrix -- in a pinned ring slot and
+        enqueue the push; returns its ticket (glint_stage_acquire + glint_push_staged)."""
+        mat = self.cols != 0
+        if len(arrays) != (3 if mat else 2):
+            raise ValueError("push_async(keys, values) for vectors, (rows, cols, values) for matrices")
+        keys = _host(arrays[0], np.int64).reshape(-1)
+        cols = _host(arrays[1], np.int32).reshape(-1) if mat else None
+        vals = _host(arrays[-1], self.np_dtype).reshape(-1)
+        if keys.size != vals.size or (mat and cols.size != keys.size):
+            raise ValueError("argument lengths differ")
+        n = keys.size
+        kp, cp, vp, slot = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int(-1)
+        check(self.lib.glint_stage_acquire(self.handle, n, C.byref(kp), C.byref(cp), C.byref(vp), C.byref(slot)),
+              self.handle)
+        if n:
+            C.memmove(kp.value, keys.ctypes.data, keys.nbytes)
+            if mat:
+                C.memmove(cp.value, cols.ctypes.data, cols.nbytes)
+            C.memmove(vp.value, vals.ctypes.data, vals.nbytes)
+        ticket = C.c_uint64()
+        check(self.lib.glint_push_staged(self.handle, slot.value, n, _flags(deterministic, unordered),
+                                         C.byref(ticket)), self.handle)
+        return ticket.value
+
+    def push_wire_async(self, payload: bytes, deterministic: bool = False):
+        """Enqueue a RequestSerializer push image; returns (message id, ticket)."""
+        buf = (C.c_uint8 * len(payload)).from_buffer_copy(payload)
+        mid, ticket = C.c_int32(), C.c_uint64()
+        flags = N.GLINT_PUSH_DETERMINISTIC if deterministic else N.GLINT_PUSH_DEFAULT
+        check(self.lib.glint_push_wire_async(self.handle, buf, len(payload), C.byref(mid), flags, C.byref(ticket)),
+              self.handle)
+        return mid.value, ticket.value
+
+    def wait(self, ticket: int) -> None:
+        """Until the push with this ticket (and every earlier one) is applied; raises if one of them
+        rejected a record (ArrayIndexOutOfBoundsException, as the actor's update would)."""
+        bad = C.c_int64(-1)
+        rc = self.lib.glint_shard_wait(self.handle, ticket, C.byref(bad))
+        if rc == N.GLINT_EOUTOFRANGE:
+            raise ArrayIndexOutOfBoundsException(f"record {bad.value} is outside the partition", bad.value)
+        check(rc, self.handle)
+
     def sync(self, stream: Optional[int] = None) -> None:
         """Wait for device-resident calls and raise if any of them rejected a record."""
         bad = C.c_int64(-1)

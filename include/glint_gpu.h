@@ -152,6 +152,33 @@ int glint_push_wire(glint_shard_t shard, const uint8_t* payload, size_t len, int
 int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uint8_t* response,
                     size_t cap, size_t* out_len);
 
+/* ---- pipelined host ingest ----------------------------------------------------------------------- *
+ * For servers whose messages arrive faster than one at a time (GranularBigVector/AsyncBigVector send
+ * a batch's messages without waiting for one another, GranularBigVector.scala:39-50): a push is put
+ * in one of the shard's GLINT_RING_SLOTS pinned host slots and enqueued on the shard's stream without
+ * waiting. Pushes of up to GLINT_ZERO_COPY_MAX records are read by the kernel straight from the
+ * pinned slot (no copy command); larger ones cross PCIe in one DMA. Tickets number the enqueued
+ * pushes of a shard; glint_shard_wait(ticket) returns once that push and every push enqueued before
+ * it are applied -- what the actor needs before it answers AcknowledgeReceipt
+ * (PushLogic.scala:40-66) -- with GLINT_EOUTOFRANGE (first bad record via glint_shard_last_error) if
+ * one of them rejected a record. Every other call on the shard is ordered after the enqueued pushes.
+ * Flags as for glint_vec_push (message order kept for Float/Double unless GLINT_PUSH_UNORDERED). */
+#define GLINT_RING_SLOTS 8
+#define GLINT_ZERO_COPY_MAX 4096
+
+/* A free slot for a push of n records, with the section pointers the caller fills: keys (i64 x n),
+ * cols (i32 x n, matrix shards only, else NULL) and vals (n values of the shard's type). Waits for
+ * the slot's previous push if it is still in flight. The JNI shim copies the JVM arrays straight in
+ * (Get<T>ArrayRegion): no critical region, no second copy. n <= 2^20. */
+int glint_stage_acquire(glint_shard_t shard, int64_t n, void** keys, void** cols, void** vals, int* slot);
+/* Enqueues the push of the n records staged in `slot`; *ticket receives its ticket. */
+int glint_push_staged(glint_shard_t shard, int slot, int64_t n, int flags, uint64_t* ticket);
+/* glint_push_wire, enqueued: the payload is copied into a slot before the call returns. */
+int glint_push_wire_async(glint_shard_t shard, const uint8_t* payload, size_t len, int32_t* id, int flags,
+                          uint64_t* ticket);
+/* Waits for the push with this ticket and every earlier one; reports their errors. */
+int glint_shard_wait(glint_shard_t shard, uint64_t ticket, int64_t* first_bad);
+
 /* ---- client routing (device) -------------------------------------------------------------- *
  * Replaces the client-side grouping in AsyncBigVector/AsyncBigMatrix.mapPartitions
  * (src/main/scala/glint/models/client/async/AsyncBigVector.scala:96-98, AsyncBigMatrix.scala:

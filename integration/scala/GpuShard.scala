@@ -1,8 +1,11 @@
 package glint.models.server.gpu
 
-import akka.actor.ActorLogging
-import glint.messages.server.request.{PullMatrix, PullMatrixRows, PullVector, PushMatrixDouble, PushVectorDouble}
-import glint.messages.server.response.{ResponseDouble, ResponseRowsDouble}
+import scala.collection.mutable
+
+import akka.actor.{ActorLogging, ActorRef}
+import glint.messages.server.logic.AcknowledgeReceipt
+import glint.messages.server.request._
+import glint.messages.server.response.{ResponseDouble, ResponseFloat, ResponseInt, ResponseLong}
 import glint.models.server.{PartialMatrix, PartialVector}
 import glint.partitioning.Partition
 import glint.partitioning.cyclic.CyclicPartition
@@ -10,21 +13,46 @@ import glint.partitioning.range.RangePartition
 import spire.implicits._
 
 /**
-  * JNI bindings of libglint_gpu.so (include/glint_gpu.h) -- see integration/jni/glint_jni.c.
+  * JNI bindings of libglint_gpu.so (include/glint_gpu.h) -- integration/jni/glint_jni.c. One typed
+  * entry point per value type of the reference's partial models. Pushes return a ticket: the push
+  * is applied in order on the shard's GPU stream, and `await(ticket)` returns once it (and every
+  * earlier push of the shard) is applied; pulls are ordered after every enqueued push.
   */
 object GpuShard {
   System.loadLibrary("glint_jni")
 
+  final val I32 = 0
+  final val I64 = 1
+  final val F32 = 2
   final val F64 = 3
+
   @native def createRange(device: Int, dtype: Int, start: Long, end: Long, cols: Int): Long
   @native def createCyclic(device: Int, dtype: Int, index: Int, parts: Int, keys: Long, cols: Int): Long
   @native def destroy(handle: Long): Unit
   @native def zero(handle: Long): Unit
-  @native def vecPush(handle: Long, keys: Array[Long], values: AnyRef, deterministic: Int): Unit
-  @native def vecPull(handle: Long, keys: Array[Long], out: AnyRef): Unit
-  @native def matPush(handle: Long, rows: Array[Long], cols: Array[Int], values: AnyRef, deterministic: Int): Unit
-  @native def matPull(handle: Long, rows: Array[Long], cols: Array[Int], out: AnyRef): Unit
-  @native def matPullRows(handle: Long, rows: Array[Long], out: AnyRef): Unit
+  @native def await(handle: Long, ticket: Long): Unit
+
+  @native def vecPushD(handle: Long, keys: Array[Long], values: Array[Double], flags: Int): Long
+  @native def vecPushF(handle: Long, keys: Array[Long], values: Array[Float], flags: Int): Long
+  @native def vecPushL(handle: Long, keys: Array[Long], values: Array[Long], flags: Int): Long
+  @native def vecPushI(handle: Long, keys: Array[Long], values: Array[Int], flags: Int): Long
+  @native def matPushD(handle: Long, rows: Array[Long], cols: Array[Int], values: Array[Double], flags: Int): Long
+  @native def matPushF(handle: Long, rows: Array[Long], cols: Array[Int], values: Array[Float], flags: Int): Long
+  @native def matPushL(handle: Long, rows: Array[Long], cols: Array[Int], values: Array[Long], flags: Int): Long
+  @native def matPushI(handle: Long, rows: Array[Long], cols: Array[Int], values: Array[Int], flags: Int): Long
+
+  @native def vecPullD(handle: Long, keys: Array[Long], out: Array[Double]): Unit
+  @native def vecPullF(handle: Long, keys: Array[Long], out: Array[Float]): Unit
+  @native def vecPullL(handle: Long, keys: Array[Long], out: Array[Long]): Unit
+  @native def vecPullI(handle: Long, keys: Array[Long], out: Array[Int]): Unit
+  @native def matPullD(handle: Long, rows: Array[Long], cols: Array[Int], out: Array[Double]): Unit
+  @native def matPullF(handle: Long, rows: Array[Long], cols: Array[Int], out: Array[Float]): Unit
+  @native def matPullL(handle: Long, rows: Array[Long], cols: Array[Int], out: Array[Long]): Unit
+  @native def matPullI(handle: Long, rows: Array[Long], cols: Array[Int], out: Array[Int]): Unit
+  @native def matPullRowsD(handle: Long, rows: Array[Long], out: Array[Double]): Unit
+  @native def matPullRowsF(handle: Long, rows: Array[Long], out: Array[Float]): Unit
+  @native def matPullRowsL(handle: Long, rows: Array[Long], out: Array[Long]): Unit
+  @native def matPullRowsI(handle: Long, rows: Array[Long], out: Array[Int]): Unit
 
   /** The shard of `partition` on GPU `device` (range or cyclic layout, as the partitioner chose). */
   def create(partition: Partition, dtype: Int, cols: Int, device: Int): Long = partition match {
@@ -39,75 +67,183 @@ object GpuShard {
 }
 
 /**
-  * PartialVectorDouble with its data in HBM. `receive` and PushLogic are exactly those of
-  * PartialVectorDouble (src/main/scala/glint/models/server/PartialVectorDouble.scala:17-23); only
-  * update/get run on the GPU. An out-of-partition key throws ArrayIndexOutOfBoundsException from
-  * update/get as on the JVM, so Akka restarts the actor, whose constructor allocates a new, zeroed
-  * shard (the reference's restart re-creates `new Array[Double](size)`).
+  * The GPU half of a partial model actor. `receive` and PushLogic are those of the reference's
+  * PartialVector*/PartialMatrix* actors (e.g. PartialVectorDouble.scala:17-23) with one change in
+  * timing: a push is enqueued (its update runs on the GPU in message order) and `updateFinished(id)`
+  * -- which makes the id acknowledgeable -- runs when the AcknowledgeReceipt for it arrives, after
+  * `await(ticket)`. The client's PushFSM (PushFSM.scala:88-120) sends that acknowledgement request
+  * right after the push, so the actor answers it exactly as before, once the push is applied, and
+  * meanwhile takes the next messages. An out-of-partition key surfaces from that await as
+  * ArrayIndexOutOfBoundsException, Akka restarts the actor, and its constructor allocates a new,
+  * zeroed shard (the reference's restart re-creates `new Array[V](size)`).
   */
-class GpuPartialVectorDouble(partition: Partition) extends PartialVector[Double](partition) with ActorLogging {
+trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
+  protected def shard: Long
+  private val pending = mutable.HashMap.empty[Int, Long]  // push id -> ticket
 
-  override val data: Array[Double] = Array.emptyDoubleArray  // lives in HBM
-  private val shard: Long = GpuShard.create(partition, GpuShard.F64, 0, GpuShard.deviceFor(partition))
+  protected def enqueued(id: Int, ticket: Long): Unit = pending.put(id, ticket)
 
-  override def update(keys: Array[Long], values: Array[Double]): Boolean = {
-    GpuShard.vecPush(shard, keys, values, 0)
-    true
-  }
-
-  override def get(keys: Array[Long]): Array[Double] = {
-    val out = new Array[Double](keys.length)
-    GpuShard.vecPull(shard, keys, out)
-    out
+  /** AcknowledgeReceipt(id) of an enqueued push: wait for it, then mark it received (PushLogic). */
+  protected def settle(message: Any, finished: Int => Unit): Unit = message match {
+    case AcknowledgeReceipt(id) =>
+      pending.remove(id).foreach { ticket =>
+        GpuShard.await(shard, ticket)
+        finished(id)
+      }
+    case _ =>
   }
 
   override def postStop(): Unit = GpuShard.destroy(shard)
+}
 
+// ---- vectors: PartialVector{Double,Float,Long,Int}.scala --------------------------------------------
+class GpuPartialVectorDouble(partition: Partition) extends PartialVector[Double](partition) with GpuShardActor {
+  override val data: Array[Double] = Array.emptyDoubleArray  // lives in HBM
+  protected val shard: Long = GpuShard.create(partition, GpuShard.F64, 0, GpuShard.deviceFor(partition))
+  override def update(keys: Array[Long], values: Array[Double]): Boolean = {
+    GpuShard.await(shard, GpuShard.vecPushD(shard, keys, values, 0)); true
+  }
+  override def get(keys: Array[Long]): Array[Double] = {
+    val out = new Array[Double](keys.length); GpuShard.vecPullD(shard, keys, out); out
+  }
   override def receive: Receive = {
     case pull: PullVector => sender ! ResponseDouble(get(pull.keys))
-    case push: PushVectorDouble =>
-      update(push.keys, push.values)
-      updateFinished(push.id)
-    case x => handleLogic(x, sender)
+    case push: PushVectorDouble => enqueued(push.id, GpuShard.vecPushD(shard, push.keys, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
   }
 }
 
-/**
-  * PartialMatrixDouble with its rows in HBM (row-major, PartialMatrixDouble.scala:19-28).
-  */
+class GpuPartialVectorFloat(partition: Partition) extends PartialVector[Float](partition) with GpuShardActor {
+  override val data: Array[Float] = Array.emptyFloatArray
+  protected val shard: Long = GpuShard.create(partition, GpuShard.F32, 0, GpuShard.deviceFor(partition))
+  override def update(keys: Array[Long], values: Array[Float]): Boolean = {
+    GpuShard.await(shard, GpuShard.vecPushF(shard, keys, values, 0)); true
+  }
+  override def get(keys: Array[Long]): Array[Float] = {
+    val out = new Array[Float](keys.length); GpuShard.vecPullF(shard, keys, out); out
+  }
+  override def receive: Receive = {
+    case pull: PullVector => sender ! ResponseFloat(get(pull.keys))
+    case push: PushVectorFloat => enqueued(push.id, GpuShard.vecPushF(shard, push.keys, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
+  }
+}
+
+class GpuPartialVectorLong(partition: Partition) extends PartialVector[Long](partition) with GpuShardActor {
+  override val data: Array[Long] = Array.emptyLongArray
+  protected val shard: Long = GpuShard.create(partition, GpuShard.I64, 0, GpuShard.deviceFor(partition))
+  override def update(keys: Array[Long], values: Array[Long]): Boolean = {
+    GpuShard.await(shard, GpuShard.vecPushL(shard, keys, values, 0)); true
+  }
+  override def get(keys: Array[Long]): Array[Long] = {
+    val out = new Array[Long](keys.length); GpuShard.vecPullL(shard, keys, out); out
+  }
+  override def receive: Receive = {
+    case pull: PullVector => sender ! ResponseLong(get(pull.keys))
+    case push: PushVectorLong => enqueued(push.id, GpuShard.vecPushL(shard, push.keys, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
+  }
+}
+
+class GpuPartialVectorInt(partition: Partition) extends PartialVector[Int](partition) with GpuShardActor {
+  override val data: Array[Int] = Array.emptyIntArray
+  protected val shard: Long = GpuShard.create(partition, GpuShard.I32, 0, GpuShard.deviceFor(partition))
+  override def update(keys: Array[Long], values: Array[Int]): Boolean = {
+    GpuShard.await(shard, GpuShard.vecPushI(shard, keys, values, 0)); true
+  }
+  override def get(keys: Array[Long]): Array[Int] = {
+    val out = new Array[Int](keys.length); GpuShard.vecPullI(shard, keys, out); out
+  }
+  override def receive: Receive = {
+    case pull: PullVector => sender ! ResponseInt(get(pull.keys))
+    case push: PushVectorInt => enqueued(push.id, GpuShard.vecPushI(shard, push.keys, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
+  }
+}
+
+// ---- matrices: PartialMatrix{Double,Float,Long,Int}.scala (rows live row-major in HBM) ---------------
+// Row pulls answer with the flattened rows x cols array: what ResponseSerializer sends for
+// ResponseRows* (ResponseSerializer.scala:52-61) and what the client's AsyncBigMatrix* decodes.
 class GpuPartialMatrixDouble(partition: Partition, cols: Int) extends PartialMatrix[Double](partition, cols)
-  with ActorLogging {
-
-  override val data: Array[Array[Double]] = Array.empty[Array[Double]]  // lives in HBM
-  private val shard: Long = GpuShard.create(partition, GpuShard.F64, cols, GpuShard.deviceFor(partition))
-
-  override def update(rows: Array[Long], cols: Array[Int], values: Array[Double]): Boolean = {
-    GpuShard.matPush(shard, rows, cols, values, 0)
-    true
+  with GpuShardActor {
+  override val data: Array[Array[Double]] = Array.empty[Array[Double]]
+  protected val shard: Long = GpuShard.create(partition, GpuShard.F64, cols, GpuShard.deviceFor(partition))
+  override def update(rows: Array[Long], cs: Array[Int], values: Array[Double]): Boolean = {
+    GpuShard.await(shard, GpuShard.matPushD(shard, rows, cs, values, 0)); true
   }
-
-  override def get(rows: Array[Long], cols: Array[Int]): Array[Double] = {
-    val out = new Array[Double](rows.length)
-    GpuShard.matPull(shard, rows, cols, out)
-    out
+  override def get(rows: Array[Long], cs: Array[Int]): Array[Double] = {
+    val out = new Array[Double](rows.length); GpuShard.matPullD(shard, rows, cs, out); out
   }
-
-  /** Rows as one flattened array: reply with ResponseDouble directly (what the serializer makes of
-    * ResponseRowsDouble anyway, ResponseSerializer.scala:52-61, and what AsyncBigMatrixDouble expects). */
   def getRowsFlat(rows: Array[Long]): Array[Double] = {
-    val out = new Array[Double](rows.length * this.cols)
-    GpuShard.matPullRows(shard, rows, out)
-    out
+    val out = new Array[Double](rows.length * cols); GpuShard.matPullRowsD(shard, rows, out); out
   }
-
-  override def postStop(): Unit = GpuShard.destroy(shard)
-
   override def receive: Receive = {
     case pull: PullMatrix => sender ! ResponseDouble(get(pull.rows, pull.cols))
     case pull: PullMatrixRows => sender ! ResponseDouble(getRowsFlat(pull.rows))
-    case push: PushMatrixDouble =>
-      update(push.rows, push.cols, push.values)
-      updateFinished(push.id)
-    case x => handleLogic(x, sender)
+    case push: PushMatrixDouble => enqueued(push.id, GpuShard.matPushD(shard, push.rows, push.cols, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
+  }
+}
+
+class GpuPartialMatrixFloat(partition: Partition, cols: Int) extends PartialMatrix[Float](partition, cols)
+  with GpuShardActor {
+  override val data: Array[Array[Float]] = Array.empty[Array[Float]]
+  protected val shard: Long = GpuShard.create(partition, GpuShard.F32, cols, GpuShard.deviceFor(partition))
+  override def update(rows: Array[Long], cs: Array[Int], values: Array[Float]): Boolean = {
+    GpuShard.await(shard, GpuShard.matPushF(shard, rows, cs, values, 0)); true
+  }
+  override def get(rows: Array[Long], cs: Array[Int]): Array[Float] = {
+    val out = new Array[Float](rows.length); GpuShard.matPullF(shard, rows, cs, out); out
+  }
+  def getRowsFlat(rows: Array[Long]): Array[Float] = {
+    val out = new Array[Float](rows.length * cols); GpuShard.matPullRowsF(shard, rows, out); out
+  }
+  override def receive: Receive = {
+    case pull: PullMatrix => sender ! ResponseFloat(get(pull.rows, pull.cols))
+    case pull: PullMatrixRows => sender ! ResponseFloat(getRowsFlat(pull.rows))
+    case push: PushMatrixFloat => enqueued(push.id, GpuShard.matPushF(shard, push.rows, push.cols, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
+  }
+}
+
+class GpuPartialMatrixLong(partition: Partition, cols: Int) extends PartialMatrix[Long](partition, cols)
+  with GpuShardActor {
+  override val data: Array[Array[Long]] = Array.empty[Array[Long]]
+  protected val shard: Long = GpuShard.create(partition, GpuShard.I64, cols, GpuShard.deviceFor(partition))
+  override def update(rows: Array[Long], cs: Array[Int], values: Array[Long]): Boolean = {
+    GpuShard.await(shard, GpuShard.matPushL(shard, rows, cs, values, 0)); true
+  }
+  override def get(rows: Array[Long], cs: Array[Int]): Array[Long] = {
+    val out = new Array[Long](rows.length); GpuShard.matPullL(shard, rows, cs, out); out
+  }
+  def getRowsFlat(rows: Array[Long]): Array[Long] = {
+    val out = new Array[Long](rows.length * cols); GpuShard.matPullRowsL(shard, rows, out); out
+  }
+  override def receive: Receive = {
+    case pull: PullMatrix => sender ! ResponseLong(get(pull.rows, pull.cols))
+    case pull: PullMatrixRows => sender ! ResponseLong(getRowsFlat(pull.rows))
+    case push: PushMatrixLong => enqueued(push.id, GpuShard.matPushL(shard, push.rows, push.cols, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
+  }
+}
+
+class GpuPartialMatrixInt(partition: Partition, cols: Int) extends PartialMatrix[Int](partition, cols)
+  with GpuShardActor {
+  override val data: Array[Array[Int]] = Array.empty[Array[Int]]
+  protected val shard: Long = GpuShard.create(partition, GpuShard.I32, cols, GpuShard.deviceFor(partition))
+  override def update(rows: Array[Long], cs: Array[Int], values: Array[Int]): Boolean = {
+    GpuShard.await(shard, GpuShard.matPushI(shard, rows, cs, values, 0)); true
+  }
+  override def get(rows: Array[Long], cs: Array[Int]): Array[Int] = {
+    val out = new Array[Int](rows.length); GpuShard.matPullI(shard, rows, cs, out); out
+  }
+  def getRowsFlat(rows: Array[Long]): Array[Int] = {
+    val out = new Array[Int](rows.length * cols); GpuShard.matPullRowsI(shard, rows, out); out
+  }
+  override def receive: Receive = {
+    case pull: PullMatrix => sender ! ResponseInt(get(pull.rows, pull.cols))
+    case pull: PullMatrixRows => sender ! ResponseInt(getRowsFlat(pull.rows))
+    case push: PushMatrixInt => enqueued(push.id, GpuShard.matPushI(shard, push.rows, push.cols, push.values, 0))
+    case x => settle(x, updateFinished); handleLogic(x, sender)
   }
 }

@@ -1,0 +1,166 @@
+/* The JNIEnv of tests/c/jni.h over plain C arrays, plus a driver that calls the shim's native
+ * methods in the order the GPU actors (integration/scala/GpuShard.scala) call them:
+ * create -> push (ticket) -> await -> pull; an order-sensitive Double push; an out-of-partition
+ * push -> await throws ArrayIndexOutOfBoundsException -> zero (the Akka restart) -> push again;
+ * argument errors (value type, short arrays); a matrix shard's element and row pulls; destroy.
+ * Exit status 0 and "ok" on stdout when every check passes. */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "jni.h"
+
+typedef struct {
+  jsize len;
+  size_t esize;
+  char* data;
+} Arr;
+
+static char pending[256];  /* the exception the shim raised: "Class: message" */
+
+static jclass FindClass(JNIEnv* e, const char* n) { (void)e; return (jclass)n; }
+static jint ThrowNew(JNIEnv* e, jclass c, const char* m) {
+  (void)e;
+  snprintf(pending, sizeof pending, "%s: %s", (const char*)c, m);
+  return 0;
+}
+static jsize GetArrayLength(JNIEnv* e, jarray a) { (void)e; return ((Arr*)a)->len; }
+static void get_region(jarray a, jsize s, jsize n, void* buf) {
+  Arr* x = (Arr*)a;
+  if (s < 0 || n < 0 || s + n > x->len) { fprintf(stderr, "region out of bounds\n"); exit(3); }
+  memcpy(buf, x->data + (size_t)s * x->esize, (size_t)n * x->esize);
+}
+static void set_region(jarray a, jsize s, jsize n, const void* buf) {
+  Arr* x = (Arr*)a;
+  if (s < 0 || n < 0 || s + n > x->len) { fprintf(stderr, "region out of bounds\n"); exit(3); }
+  memcpy(x->data + (size_t)s * x->esize, buf, (size_t)n * x->esize);
+}
+static void GL(JNIEnv* e, jlongArray a, jsize s, jsize n, jlong* b) { (void)e; get_region(a, s, n, b); }
+static void GI(JNIEnv* e, jintArray a, jsize s, jsize n, jint* b) { (void)e; get_region(a, s, n, b); }
+static void GF(JNIEnv* e, jfloatArray a, jsize s, jsize n, jfloat* b) { (void)e; get_region(a, s, n, b); }
+static void GD(JNIEnv* e, jdoubleArray a, jsize s, jsize n, jdouble* b) { (void)e; get_region(a, s, n, b); }
+static void SL(JNIEnv* e, jlongArray a, jsize s, jsize n, const jlong* b) { (void)e; set_region(a, s, n, b); }
+static void SI(JNIEnv* e, jintArray a, jsize s, jsize n, const jint* b) { (void)e; set_region(a, s, n, b); }
+static void SF(JNIEnv* e, jfloatArray a, jsize s, jsize n, const jfloat* b) { (void)e; set_region(a, s, n, b); }
+static void SD(JNIEnv* e, jdoubleArray a, jsize s, jsize n, const jdouble* b) { (void)e; set_region(a, s, n, b); }
+
+static const struct JNINativeInterface_ table = {FindClass, ThrowNew, GetArrayLength, GL, GI, GF, GD, SL, SI, SF, SD};
+static JNIEnv env_ptr = &table;
+static JNIEnv* env = &env_ptr;
+
+static Arr* arr(jsize n, size_t es) {
+  Arr* a = (Arr*)calloc(1, sizeof(Arr));
+  a->len = n;
+  a->esize = es;
+  a->data = (char*)calloc((size_t)(n > 0 ? n : 1), es);
+  return a;
+}
+
+/* the shim's native methods (integration/jni/glint_jni.c) */
+#define NAT(name) Java_glint_models_server_gpu_GpuShard_##name
+jlong NAT(createRange)(JNIEnv*, jclass, jint, jint, jlong, jlong, jint);
+void NAT(destroy)(JNIEnv*, jclass, jlong);
+void NAT(zero)(JNIEnv*, jclass, jlong);
+void NAT(await)(JNIEnv*, jclass, jlong, jlong);
+jlong NAT(vecPushD)(JNIEnv*, jclass, jlong, jlongArray, jdoubleArray, jint);
+jlong NAT(vecPushF)(JNIEnv*, jclass, jlong, jlongArray, jfloatArray, jint);
+void NAT(vecPullD)(JNIEnv*, jclass, jlong, jlongArray, jdoubleArray);
+jlong NAT(matPushI)(JNIEnv*, jclass, jlong, jlongArray, jintArray, jintArray, jint);
+void NAT(matPullI)(JNIEnv*, jclass, jlong, jlongArray, jintArray, jintArray);
+void NAT(matPullRowsI)(JNIEnv*, jclass, jlong, jlongArray, jintArray);
+
+static int failures = 0;
+#define CHECK(cond, what)                                            \
+  do {                                                               \
+    if (!(cond)) { fprintf(stderr, "FAILED: %s\n", what); ++failures; } \
+  } while (0)
+static int took(const char* cls) {
+  const int hit = strncmp(pending, cls, strlen(cls)) == 0;
+  pending[0] = 0;
+  return hit;
+}
+
+int main(int argc, char** argv) {
+  const int dev = argc > 1 ? atoi(argv[1]) : 0;
+  /* a PartialVectorDouble of RangePartition(0, 1000, 2000) */
+  jlong h = NAT(createRange)(env, NULL, dev, 3, 1000, 2000, 0);
+  CHECK(h != 0 && !pending[0], "createRange");
+  Arr* k = arr(1000, 8);
+  Arr* v = arr(1000, 8);
+  for (int i = 0; i < 1000; ++i) {
+    ((jlong*)k->data)[i] = 1000 + i;
+    ((jdouble*)v->data)[i] = 0.5 * i;
+  }
+  jlong t = NAT(vecPushD)(env, NULL, h, k, v, 0);
+  CHECK(t > 0 && !pending[0], "vecPushD ticket");
+  NAT(await)(env, NULL, h, t);
+  CHECK(!pending[0], "await");
+  Arr* out = arr(1000, 8);
+  NAT(vecPullD)(env, NULL, h, k, out);
+  int same = 1;
+  for (int i = 0; i < 1000; ++i) same &= ((jdouble*)out->data)[i] == 0.5 * i;
+  CHECK(same && !pending[0], "pull after push");
+  /* one message, one key three times: the JVM's ((d + 1e16) + 1) + 1, not d + (1e16 + 2) */
+  Arr* k3 = arr(3, 8);
+  Arr* v3 = arr(3, 8);
+  for (int i = 0; i < 3; ++i) ((jlong*)k3->data)[i] = 1000;
+  ((jdouble*)v3->data)[0] = 1e16;
+  ((jdouble*)v3->data)[1] = 1.0;
+  ((jdouble*)v3->data)[2] = 1.0;
+  NAT(await)(env, NULL, h, NAT(vecPushD)(env, NULL, h, k3, v3, 0));
+  Arr* o1 = arr(1, 8);
+  NAT(vecPullD)(env, NULL, h, k3, o1);
+  volatile double seq = 0.0;
+  seq = seq + 1e16;
+  seq = seq + 1.0;
+  seq = seq + 1.0;
+  CHECK(((jdouble*)o1->data)[0] == seq, "sequential Double order");
+  /* an out-of-partition key: the await throws ArrayIndexOutOfBoundsException; restart = zero */
+  Arr* kb = arr(2, 8);
+  Arr* vb = arr(2, 8);
+  ((jlong*)kb->data)[0] = 1001;
+  ((jlong*)kb->data)[1] = 2000;
+  t = NAT(vecPushD)(env, NULL, h, kb, vb, 0);
+  NAT(await)(env, NULL, h, t);
+  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "out-of-partition key raises");
+  NAT(zero)(env, NULL, h);
+  NAT(await)(env, NULL, h, NAT(vecPushD)(env, NULL, h, k3, v3, 0));
+  NAT(vecPullD)(env, NULL, h, k3, o1);
+  CHECK(((jdouble*)o1->data)[0] == seq && !pending[0], "push after restart");
+  /* argument errors */
+  Arr* vf = arr(1000, 4);
+  NAT(vecPushF)(env, NULL, h, k, vf, 0);
+  CHECK(took("java/lang/IllegalArgumentException"), "value type mismatch");
+  Arr* vs = arr(999, 8);
+  NAT(vecPushD)(env, NULL, h, k, vs, 0);
+  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "short values");
+  NAT(destroy)(env, NULL, h);
+
+  /* a PartialMatrixInt of 10 rows x 7 cols */
+  jlong m = NAT(createRange)(env, NULL, dev, 0, 0, 10, 7);
+  Arr* r = arr(70, 8);
+  Arr* c = arr(70, 4);
+  Arr* mv = arr(70, 4);
+  for (int i = 0; i < 70; ++i) {
+    ((jlong*)r->data)[i] = i / 7;
+    ((jint*)c->data)[i] = i % 7;
+    ((jint*)mv->data)[i] = 3 * i - 100;
+  }
+  NAT(await)(env, NULL, m, NAT(matPushI)(env, NULL, m, r, c, mv, 0));
+  Arr* mo = arr(70, 4);
+  NAT(matPullI)(env, NULL, m, r, c, mo);
+  CHECK(!memcmp(mo->data, mv->data, 280), "matrix element pull");
+  Arr* rows = arr(10, 8);
+  for (int i = 0; i < 10; ++i) ((jlong*)rows->data)[i] = i;
+  Arr* ro = arr(70, 4);
+  NAT(matPullRowsI)(env, NULL, m, rows, ro);
+  CHECK(!memcmp(ro->data, mv->data, 280) && !pending[0], "matrix row pull (flattened)");
+  Arr* cs = arr(69, 4);
+  NAT(matPushI)(env, NULL, m, r, cs, mv, 0);
+  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "short cols");
+  NAT(destroy)(env, NULL, m);
+  if (failures) return 1;
+  printf("ok\n");
+  return 0;
+}

@@ -1,0 +1,117 @@
+"""Pipelined host ingest (pinned ring slots, enqueue without waiting, ticketed waits): results equal
+the sequential oracle over the pushes in enqueue order -- PartialVector.update per message, messages
+applied one at a time as an actor does (PartialVectorDouble.scala:17-23) -- and a wait reports the
+rejected records of the pushes it covers (PushLogic.scala:40-66 acknowledges only applied pushes)."""
+import zlib
+
+import numpy as np
+import pytest
+
+from glint_amd import ArrayIndexOutOfBoundsException, PartialMatrix, PartialVector, RangePartition
+from glint_amd import _native as N
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DT = ["double", "float", "long", "int"]
+
+
+def _vals(rng, dtype, n):
+    npd = {"double": np.float64, "float": np.float32, "long": np.int64, "int": np.int32}[dtype]
+    if np.issubdtype(npd, np.floating):
+        return (rng.uniform(-1, 1, n) * 10.0 ** rng.integers(-6, 6, n)).astype(npd)
+    return rng.integers(-1000, 1000, n).astype(npd)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("sizes", [[1000] * 37, [1, 4096, 4097, 79_999, 12, 3000]])
+def test_async_pushes_equal_sequential_oracle(gpu, dtype, sizes):
+    """More pushes in flight than ring slots (8); small ones read in place, large ones copied."""
+    rng = np.random.default_rng(zlib.crc32(f"ring/{dtype}/{len(sizes)}".encode()))
+    start, size = 1 << 34, 60_000
+    ref = O.OracleVector(O.part_range(start, start + size), O.CODE[dtype])
+    with PartialVector(RangePartition(0, start, start + size), dtype, gpu) as sh:
+        tickets = []
+        for n in sizes:
+            keys = (np.minimum(rng.zipf(1.3, n) - 1, size - 1) + start).astype(np.int64)
+            vals = _vals(rng, dtype, n)
+            tickets.append(sh.push_async(keys, vals))
+            assert ref.update(keys, vals) == -1
+        assert tickets == sorted(tickets) and len(set(tickets)) == len(tickets)
+        sh.wait(tickets[-1])
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+def test_wire_async_and_pull_ordering(gpu):
+    """Wire images enqueued without waiting; a pull issued before any wait sees every push."""
+    rng = np.random.default_rng(5)
+    size = 20_000
+    ref = O.OracleVector(O.part_range(0, size), O.O_F64)
+    with PartialVector(RangePartition(0, 0, size), "double", gpu) as sh:
+        last = 0
+        for mid in range(50):
+            keys = rng.integers(0, size, 1000).astype(np.int64)
+            vals = rng.uniform(-1, 1, 1000)
+            got_id, last = sh.push_wire_async(O.encode_push_vector(O.O_F64, mid + 100, keys, vals))
+            assert got_id == mid + 100
+            ref.update(keys, vals)
+        q = np.arange(size, dtype=np.int64)
+        np.testing.assert_array_equal(sh.get(q), ref.data)  # ordered after the enqueued pushes
+        sh.wait(last)
+
+
+@pytest.mark.parametrize("dtype", ["double", "int"])
+def test_async_matrix_pushes(gpu, dtype):
+    rng = np.random.default_rng(9)
+    rows_n, cols_n = 500, 129
+    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE[dtype])
+    with PartialMatrix(RangePartition(0, 0, rows_n), cols_n, dtype, gpu) as sh:
+        t = 0
+        for n in (1000, 3000, 5000, 10):
+            r = rng.integers(0, rows_n, n).astype(np.int64)
+            c = rng.integers(0, cols_n, n).astype(np.int32)
+            v = _vals(rng, dtype, n)
+            t = sh.push_async(r, c, v)
+            ref.update(r, c, v)
+        sh.wait(t)
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+def test_async_error_reported_once(gpu):
+    size = 1000
+    with PartialVector(RangePartition(0, 0, size), "long", gpu) as sh:
+        t1 = sh.push_async(np.array([1, 2], np.int64), np.array([1, 1], np.int64))
+        t2 = sh.push_async(np.array([3, size + 9, 4], np.int64), np.array([1, 1, 1], np.int64))
+        t3 = sh.push_async(np.array([5], np.int64), np.array([1], np.int64))
+        sh.wait(t1)  # covers only the first push: clean
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.wait(t3)
+        assert ei.value.record == 1
+        t4 = sh.push_async(np.array([6], np.int64), np.array([1], np.int64))
+        sh.wait(t4)  # the error is not reported twice
+        got = sh.get(np.arange(8, dtype=np.int64))
+        assert got.tolist() == [0, 1, 1, 1, 1, 1, 1, 0]
+        assert t2 < t3
+
+
+def test_stage_acquire_rejects_bad_arguments(gpu):
+    import ctypes as C
+    lib = N.load()
+    with PartialVector(RangePartition(0, 0, 10), "double", gpu) as sh:
+        kp, cp, vp, slot = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int()
+        assert lib.glint_stage_acquire(sh.handle, (1 << 20) + 1, C.byref(kp), C.byref(cp), C.byref(vp),
+                                       C.byref(slot)) == N.GLINT_EINVAL
+        assert lib.glint_push_staged(sh.handle, 99, 1, 0, None) == N.GLINT_EINVAL
+        assert lib.glint_stage_acquire(sh.handle, 5, C.byref(kp), C.byref(cp), C.byref(vp), C.byref(slot)) == 0
+        assert cp.value is None  # no cols section for a vector shard
+        assert lib.glint_push_staged(sh.handle, slot.value, 6, 0, None) == N.GLINT_EINVAL  # more than staged
+        assert lib.glint_push_staged(sh.handle, slot.value, 0, 0, None) == 0
+
+
+def test_jni_shim_end_to_end(gpu):
+    """The shim's native methods, called in the actors' order through a minimal JNI environment
+    (tests/c/fake_jvm.c): push -> await -> pull, sequential Double order, restart after an
+    out-of-partition key, argument errors, matrix element and row pulls."""
+    import subprocess
+    from glint_amd.build import build_jni_driver
+    r = subprocess.run([str(build_jni_driver()), str(gpu)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr

@@ -125,3 +125,41 @@ def test_loopback_harness_cpu_backend():
         assert d["push_messages"] >= -(-keys // msg)
         first = O.JavaRandom(42).nextDoubles(3)
         assert d["first_values"][:min(3, keys)] == list(first[:min(3, keys)])
+
+
+def test_jni_shim_compiles_and_links():
+    """integration/jni/glint_jni.c builds (-Wall -Werror) against the minimal JNI environment of
+    tests/c/jni.h and links with libglint_gpu.so: every native method of GpuShard.scala exists."""
+    import subprocess
+    from glint_amd.build import JNI_DRIVER, build_jni_driver
+    build_jni_driver()
+    syms = subprocess.run(["nm", "-D", "--defined-only", str(JNI_DRIVER)], capture_output=True, text=True).stdout
+    syms += subprocess.run(["nm", "--defined-only", str(JNI_DRIVER)], capture_output=True, text=True).stdout
+    scala = (Path(__file__).resolve().parent.parent / "integration" / "scala" / "GpuShard.scala").read_text()
+    import re
+    natives = re.findall(r"@native def (\w+)", scala)
+    assert len(natives) == 25  # lifetime 5, typed pushes 8, typed pulls 12
+    for name in natives:
+        assert f"Java_glint_models_server_gpu_GpuShard_{name}" in syms, name
+
+
+@pytest.mark.parametrize("args", [
+    ["--clients", "16", "--servers", "4", "--keys", "200003", "--msg", "777"],             # 4a: owned ranges
+    ["--clients", "8", "--servers", "3", "--keys", "50000", "--pattern", "uniform", "--records", "20000",
+     "--dtype", "long"],                                                                        # 4b: Long exact
+    ["--clients", "8", "--servers", "3", "--keys", "50000", "--pattern", "uniform", "--records", "20000"],
+    ["--clients", "2", "--servers", "2", "--keys", "30000", "--window", "1"],                  # one in flight
+])
+def test_loopback_concurrent_clients_cpu_backend(args):
+    """configs[3]'s shape over loopback TCP with the oracle's server loop: many clients, each with up
+    to W messages in flight per server (GranularBigVector issues every chunk at once), messages of
+    different clients interleaving at the servers."""
+    import json
+    import subprocess
+    from glint_amd.build import LOOPBACK_BIN, ORACLE_LIB, build_loopback
+    build_loopback()
+    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "oracle", "--lib", str(ORACLE_LIB)] + args,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["check"] is True and d["resends"] == 0

@@ -1,5 +1,6 @@
 """Per-call latency of the host-pointer entry points (what the JNI shim calls once per Akka message):
-glint_vec_push / glint_vec_pull / glint_push_wire with pageable numpy arrays, by message size. The
+glint_vec_push / glint_vec_pull / glint_push_wire with pageable numpy arrays, by message size, and
+the pipelined glint_push_wire_async (messages enqueued back to back, one wait at the end). The
 small sizes are the reference's own message shapes: 1000 records per push in
 GranularBigVectorSpec.scala:21, and the 79 999-record frame cap of the granular client.
 One JSON line per (op, n) on stdout.
@@ -61,8 +62,25 @@ for n in (1, 1000, 10_000, 79_999, 1 << 18, 1 << 20, 1 << 24):
         rc = lib.glint_push_wire(h, wbuf, len(wire), C.byref(mid), 0)
         assert rc == 0, rc
 
-    for op, fn, bpr in (("vec_push", push, 16), ("vec_pull", pull, 16), ("push_wire", push_wire, 16)):
-        dt = per_call(fn, reps)
+    ticket = C.c_uint64()
+
+    def push_wire_async():
+        rc = lib.glint_push_wire_async(h, wbuf, len(wire), C.byref(mid), 0, C.byref(ticket))
+        assert rc == 0, rc
+
+    def pipelined(fn, reps):  # enqueue `reps` messages, one wait at the end: per-message throughput cost
+        for _ in range(5):
+            fn()
+        lib.glint_shard_wait(h, ticket.value, None)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        assert lib.glint_shard_wait(h, ticket.value, None) == 0
+        return (time.perf_counter() - t0) / reps
+
+    for op, fn, bpr in (("vec_push", push, 16), ("vec_pull", pull, 16), ("push_wire", push_wire, 16),
+                        ("push_wire_async", push_wire_async, 16)):
+        dt = pipelined(fn, reps) if op == "push_wire_async" else per_call(fn, reps)
         print(json.dumps({"op": op, "records": n, "pinned_stage_max": os.environ.get("GLINT_PINNED_STAGE_MAX", "default"), "us_per_call": round(dt * 1e6, 2),
                           "Mrecords_per_s": round(n / dt / 1e6, 2), "host_GBps": round(n * bpr / dt / 1e9, 2),
                           "reps": reps}), flush=True)

@@ -1,31 +1,41 @@
 /*
- * glint_loopback.c -- BASELINE.json configs[0] over loopback TCP: 1 client + S parameter servers,
- * a Double vector of N keys range-partitioned over the servers, a dense push of keys 0..N-1 with
- * java.util.Random(42).nextDouble() values in messages of <= M records, then a pull of every key
- * and an exact check. It restates the message flow of the reference's Akka path:
+ * glint_loopback.c -- Glint's push/pull message flow over loopback TCP, C clients x S parameter
+ * servers, with the server's shard as a pluggable backend. It restates the reference's Akka path:
  *
- *   client  GranularBigVector.push (src/main/scala/glint/models/client/granular/GranularBigVector.scala:72-81)
- *           slices the keys into <= M-record chunks; AsyncBigVector.push (.../async/AsyncBigVector.scala:96-121)
- *           groups each chunk by partition (RangePartitioner.partition, RangePartitioner.scala:27-43);
- *           PushFSM (.../async/PushFSM.scala:55-141) runs the exactly-once protocol per message:
- *             GetUniqueID -> UniqueID(id); PushVectorDouble(id, keys, values);
- *             AcknowledgeReceipt(id) -> AcknowledgeReceipt(id) | NotAcknowledgeReceipt(id) (resend);
- *             Forget(id) -> Forget(id)
- *   server  PartialVectorDouble.receive (src/main/scala/glint/models/server/PartialVectorDouble.scala:17-23):
- *           push -> update(keys, values); updateFinished(id); pull -> ResponseDouble(get(keys));
- *           PushLogic.handleLogic (src/main/scala/glint/models/server/PushLogic.scala:40-66)
+ *   client  GranularBigVector.push/pull (src/main/scala/glint/models/client/granular/
+ *           GranularBigVector.scala:26-50) slices the caller's keys into <= M-record chunks and issues
+ *           every chunk at once (one future each); AsyncBigVector.push/pull (.../async/
+ *           AsyncBigVector.scala:49-121) groups each chunk by partition (RangePartitioner.partition,
+ *           RangePartitioner.scala:27-43) and sends one message per partition. Each push runs the
+ *           exactly-once PushFSM (.../async/PushFSM.scala:55-141):
+ *             GetUniqueID -> UniqueID(id); PushVector*(id, keys, values); AcknowledgeReceipt(id) ->
+ *             AcknowledgeReceipt(id) | NotAcknowledgeReceipt(id) (resend); Forget(id) -> Forget(id)
+ *           Here every (client, server) connection keeps up to W messages in flight (-window).
+ *   server  PartialVector{Double,Long}.receive (src/main/scala/glint/models/server/
+ *           PartialVectorDouble.scala:17-23) -- one message at a time per server, whatever connection
+ *           it came from -- with PushLogic (PushLogic.scala:40-66) for the ids and receipts.
  *
  * Push and pull payloads are the exact RequestSerializer / ResponseSerializer byte images
  * (RequestSerializer.scala:150-173, ResponseSerializer.scala:45-61); the logic messages, which Akka
  * serialises with Java serialisation, are 5-byte frames here. Every frame is [u32 length][payload].
- * Each client connection runs its protocol synchronously (one message in flight per server).
  *
- * The server's shard is a backend loaded at run time:
- *   --backend oracle --lib oracle/build/libglint_oracle.so  the CPU restatement of the server loop
- *            (deserialise into arrays as FastPrimitiveDeserializer does, then the scalar update):
- *            the CPU baseline, run only from bench.py's cpu_baseline leg;
- *   --backend gpu --lib glint_amd/lib/libglint_gpu.so       an HBM shard fed the raw wire image
- *            through glint_push_wire / glint_pull_wire (include/glint_gpu.h): the drop-in, end to end.
+ * Backends (loaded at run time):
+ *   --backend oracle --lib oracle/build/libglint_oracle.so   the CPU restatement of the server loop:
+ *            deserialise into arrays as FastPrimitiveDeserializer does, then the scalar update
+ *            (the CPU baseline, run only from bench.py's cpu_baseline leg and the tests);
+ *   --backend gpu --lib glint_amd/lib/libglint_gpu.so        an HBM shard per server fed the raw wire
+ *            images: pushes are enqueued (glint_push_wire_async) and the server waits for them
+ *            (glint_shard_wait) only when it has drained the messages that have arrived and owes an
+ *            AcknowledgeReceipt -- what PushLogic needs, one wait per burst; pulls are
+ *            glint_pull_wire, ordered after the enqueued pushes.
+ *
+ * Workloads (--pattern): dense -- client c pushes then pulls its own contiguous key range
+ * (BASELINE configs[0] at C = 1: GranularBigVectorSpec's 1M keys with java.util.Random(42)
+ * values; configs[3] 4a at C = 64: each client owns N / C keys); uniform -- every client pushes R
+ * uniform keys over the whole space and pulls them back (configs[3] 4b). Checks: dense, every pulled
+ * value equals the pushed one bit for bit; uniform, the pulled sums equal the sequential sum over all
+ * clients' records (Long: bit-exact; Double: within 1e-9 of the sum of magnitudes, since concurrent
+ * clients' messages reach a server in no fixed order, as with Akka).
  *
  * Output: one JSON line.
  */
@@ -33,19 +43,23 @@
 #include <arpa/inet.h>
 #include <dlfcn.h>
 #include <errno.h>
+#include <math.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/ioctl.h>
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
 
 enum {
-  W_PULL_VECTOR = 0x02, W_PUSH_VEC_D = 0x07, W_RESP_D = 0x10, /* SerializationConstants.scala:24-38 */
+  W_PULL_VECTOR = 0x02, W_PUSH_VEC_D = 0x07, W_PUSH_VEC_L = 0x0A, /* SerializationConstants.scala:24-38 */
+  W_RESP_D = 0x10, W_RESP_L = 0x13,
   L_GET_UID = 0x20, L_UID = 0x21, L_ACK = 0x22, L_NACK = 0x23, L_FORGET = 0x24, L_STOP = 0x7F
 };
 
@@ -81,10 +95,6 @@ static int read_all(int fd, void* p, size_t n) {
   }
   return 1;
 }
-static void send_frame(int fd, const uint8_t* payload, uint32_t len) {
-  write_all(fd, &len, 4);
-  write_all(fd, payload, len);
-}
 /* returns payload length (0 on EOF); *buf grows as needed */
 static uint32_t recv_frame(int fd, uint8_t** buf, size_t* cap) {
   uint32_t len;
@@ -97,33 +107,58 @@ static uint32_t recv_frame(int fd, uint8_t** buf, size_t* cap) {
   if (!read_all(fd, *buf, len)) return 0;
   return len;
 }
-static void send_logic(int fd, uint8_t type, int32_t id) {
+
+/* an output buffer of frames, sent with one write */
+typedef struct { uint8_t* p; size_t len, cap; } obuf;
+static void ob_put(obuf* o, const void* d, size_t n) {
+  if (o->len + n > o->cap) {
+    o->cap = (o->len + n) * 2 + 4096;
+    o->p = (uint8_t*)realloc(o->p, o->cap);
+    if (!o->p) die("realloc");
+  }
+  memcpy(o->p + o->len, d, n);
+  o->len += n;
+}
+static void ob_frame(obuf* o, const void* payload, uint32_t len) { ob_put(o, &len, 4); ob_put(o, payload, len); }
+static void ob_logic(obuf* o, uint8_t type, int32_t id) {
   uint8_t m[5];
   m[0] = type;
   memcpy(m + 1, &id, 4);
-  send_frame(fd, m, 5);
+  ob_frame(o, m, 5);
+}
+static void ob_flush(obuf* o, int fd) {
+  if (o->len) write_all(fd, o->p, o->len);
+  o->len = 0;
+}
+
+static void tune_socket(int fd) {
+  int one = 1, big = 8 << 20;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof(big));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof(big));
 }
 
 /* ---- backends ----------------------------------------------------------------------------------- */
+static void* dl;
+static int use_gpu;
+static int gpu_device;
+static int dtype_long; /* 0: Double values, 1: Long values */
+
 typedef struct {
-  int gpu;
   /* oracle (CPU restatement) */
   struct { int32_t kind; int32_t pad; int64_t start, end; int32_t cidx, cparts; int64_t ckeys; } opart;
   int64_t (*o_update)(const void*, int, void*, int32_t, const int64_t*, const void*, int64_t);
   int64_t (*o_get)(const void*, int, const void*, int32_t, const int64_t*, void*, int64_t);
-  double* data;
+  void* data;
   int32_t size;
   /* gpu */
   void* shard;
   int (*g_create)(int, int, int64_t, int64_t, int32_t, void**);
-  int (*g_push_wire)(void*, const uint8_t*, size_t, int32_t*, int);
+  int (*g_push_async)(void*, const uint8_t*, size_t, int32_t*, int, uint64_t*);
+  int (*g_wait)(void*, uint64_t, int64_t*);
   int (*g_pull_wire)(void*, const uint8_t*, size_t, uint8_t*, size_t, size_t*);
   int (*g_destroy)(void*);
 } backend;
-
-static void* dl;
-static int use_gpu;
-static int gpu_device;
 
 static void backend_open(const char* kind, const char* path) {
   dl = dlopen(path, RTLD_NOW | RTLD_LOCAL);
@@ -131,30 +166,33 @@ static void backend_open(const char* kind, const char* path) {
   use_gpu = strcmp(kind, "gpu") == 0;
 }
 
+static int value_code(void) { return dtype_long ? 1 /* GLINT_I64 / O_I64 */ : 3 /* F64 */; }
+
 static void backend_init(backend* b, int64_t start, int64_t end) {
   memset(b, 0, sizeof(*b));
-  b->gpu = use_gpu;
-  if (b->gpu) {
+  if (use_gpu) {
     *(void**)&b->g_create = dlsym(dl, "glint_shard_create");
-    *(void**)&b->g_push_wire = dlsym(dl, "glint_push_wire");
+    *(void**)&b->g_push_async = dlsym(dl, "glint_push_wire_async");
+    *(void**)&b->g_wait = dlsym(dl, "glint_shard_wait");
     *(void**)&b->g_pull_wire = dlsym(dl, "glint_pull_wire");
     *(void**)&b->g_destroy = dlsym(dl, "glint_shard_destroy");
-    if (!b->g_create || !b->g_push_wire || !b->g_pull_wire || !b->g_destroy) die("dlsym glint_*");
-    int rc = b->g_create(gpu_device, 3 /* GLINT_F64 */, start, end, 0, &b->shard);
+    if (!b->g_create || !b->g_push_async || !b->g_wait || !b->g_pull_wire || !b->g_destroy) die("dlsym glint_*");
+    int rc = b->g_create(gpu_device, value_code(), start, end, 0, &b->shard);
     if (rc) { fprintf(stderr, "glint_loopback: glint_shard_create failed (%d)\n", rc); exit(3); }
-    /* actor start-up (preStart): one push of +0.0 and one pull, so the first timed message does not
-     * pay the HIP runtime's lazy code-object load; x + 0.0 leaves every (zeroed) element unchanged */
+    /* actor start-up (preStart): one push of +0 and one pull, so the first timed message does not pay
+     * the HIP runtime's lazy code-object load; x + 0 leaves every (zeroed) element unchanged */
     if (end > start) {
-      uint8_t w[25] = {W_PUSH_VEC_D, 1, 0, 0, 0, 0, 0, 0, 0};
-      const double zero = 0.0;
+      uint8_t w[25] = {dtype_long ? W_PUSH_VEC_L : W_PUSH_VEC_D, 1, 0, 0, 0, 0, 0, 0, 0};
       memcpy(w + 9, &start, 8);
-      memcpy(w + 17, &zero, 8);
+      memset(w + 17, 0, 8);
       int32_t id;
+      uint64_t t;
       uint8_t q[13] = {W_PULL_VECTOR, 1, 0, 0, 0};
       memcpy(q + 5, &start, 8);
       uint8_t r[13];
       size_t rl;
-      if (b->g_push_wire(b->shard, w, sizeof(w), &id, 0) || b->g_pull_wire(b->shard, q, sizeof(q), r, sizeof(r), &rl))
+      if (b->g_push_async(b->shard, w, sizeof(w), &id, 0, &t) || b->g_wait(b->shard, t, NULL) ||
+          b->g_pull_wire(b->shard, q, sizeof(q), r, sizeof(r), &rl))
         die("warm-up");
     }
   } else {
@@ -165,126 +203,209 @@ static void backend_init(backend* b, int64_t start, int64_t end) {
     b->opart.start = start;
     b->opart.end = end;
     b->size = (int32_t)(end - start); /* RangePartition.size, RangePartition.scala:24 */
-    b->data = (double*)calloc((size_t)(b->size > 0 ? b->size : 1), 8); /* new Array[Double](size) */
+    b->data = calloc((size_t)(b->size > 0 ? b->size : 1), 8); /* new Array[V](size) */
   }
 }
 
-/* a PushVectorDouble image: [0x07][n:i32][id:i32][keys i64 x n][values f64 x n] */
-static int backend_push(backend* b, const uint8_t* msg, uint32_t len, int32_t* id) {
-  if (b->gpu) return b->g_push_wire(b->shard, msg, len, id, 0);
-  int32_t n;
-  memcpy(&n, msg + 1, 4);
-  memcpy(id, msg + 5, 4);
-  /* FastPrimitiveDeserializer.readArrayLong/readArrayDouble: copy out of the frame into arrays */
-  int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
-  double* vals = (double*)malloc((size_t)n * 8 + 8);
-  memcpy(keys, msg + 9, (size_t)n * 8);
-  memcpy(vals, msg + 9 + (size_t)n * 8, (size_t)n * 8);
-  const int64_t bad = b->o_update(&b->opart, 3, b->data, b->size, keys, vals, n);
-  free(keys);
-  free(vals);
-  return bad >= 0 ? 1 : 0;
-}
-
-/* a PullVector image [0x02][n][keys] -> a ResponseDouble image [0x10][n][values] */
-static int backend_pull(backend* b, const uint8_t* msg, uint32_t len, uint8_t* out, size_t cap, size_t* out_len) {
-  if (b->gpu) return b->g_pull_wire(b->shard, msg, len, out, cap, out_len);
-  int32_t n;
-  memcpy(&n, msg + 1, 4);
-  int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
-  memcpy(keys, msg + 5, (size_t)n * 8);
-  const int64_t bad = b->o_get(&b->opart, 3, b->data, b->size, keys, out + 5, n);
-  free(keys);
-  out[0] = W_RESP_D;
-  memcpy(out + 1, &n, 4);
-  *out_len = 5 + (size_t)n * 8;
-  return bad >= 0 ? 1 : 0;
-}
-
 static void backend_close(backend* b) {
-  if (b->gpu) b->g_destroy(b->shard);
+  if (use_gpu) b->g_destroy(b->shard);
   else free(b->data);
 }
 
-/* ---- server: PartialVectorDouble.receive + PushLogic ------------------------------------------- */
+/* ---- server: PartialVector*.receive + PushLogic, one thread per client connection ---------------- */
 typedef struct {
   int64_t start, end;
-  int listen_fd;
-  int port;
-  int64_t records_applied;
-  int errors;
-} server_arg;
-
-static pthread_barrier_t servers_ready;
-
-static void* server_main(void* p) {
-  server_arg* a = (server_arg*)p;
+  int listen_fd, port;
   backend b;
-  backend_init(&b, a->start, a->end);
-  pthread_barrier_wait(&servers_ready); /* the client's clock starts once every shard exists */
-  int fd = accept(a->listen_fd, NULL, NULL);
-  if (fd < 0) die("accept");
-  int one = 1;
-  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  int32_t uid = 0;                       /* PushLogic.uid */
-  size_t rcap = 1 << 16;                 /* PushLogic.receipt, indexed by id */
-  uint8_t* receipt = (uint8_t*)calloc(rcap, 1);
+  pthread_mutex_t mu; /* one message at a time per server (the actor) + PushLogic's state */
+  int32_t uid;        /* PushLogic.uid */
+  uint8_t* receipt;   /* PushLogic.receipt, indexed by id */
+  size_t rcap;
+  int errors;
+} server;
+
+static void receipt_set(server* s, int32_t id, uint8_t v) {
+  if ((size_t)id >= s->rcap) {
+    size_t nc = s->rcap ? s->rcap : 1024;
+    while ((size_t)id >= nc) nc *= 2;
+    s->receipt = (uint8_t*)realloc(s->receipt, nc);
+    memset(s->receipt + s->rcap, 0, nc - s->rcap);
+    s->rcap = nc;
+  }
+  s->receipt[id] = v;
+}
+static int receipt_has(server* s, int32_t id) { return (size_t)id < s->rcap && s->receipt[id]; }
+
+typedef struct {
+  server* s;
+  int fd;
+} conn_arg;
+
+/* Replies leave a connection in request order. A reply is either ready (its frame is in `out`) or an
+ * AcknowledgeReceipt of a push still on the GPU, answered after one wait per drained burst. */
+typedef struct { size_t end; int32_t ack_id; } hold;  /* out[prev end .. end) is ready, then ack_id */
+
+static int readable_now(int fd) {
+  int avail = 0;
+  if (ioctl(fd, FIONREAD, &avail) < 0) return 0;
+  return avail > 0;
+}
+
+static void* conn_main(void* p) {
+  conn_arg* a = (conn_arg*)p;
+  server* s = a->s;
+  const int fd = a->fd;
   uint8_t* buf = NULL;
   size_t cap = 0;
-  size_t ocap = 1 << 20;
-  uint8_t* out = (uint8_t*)malloc(ocap);
+  obuf out = {0};
+  uint8_t* resp = NULL;
+  size_t rcap = 0;
+  int32_t* pending = NULL; /* ids of this connection's pushes enqueued on the GPU since the last wait */
+  size_t npend = 0, pcap = 0;
+  uint64_t last_ticket = 0;
+  hold* holds = NULL;      /* held acks, in reply order */
+  size_t nhold = 0, hcap = 0;
   for (;;) {
     const uint32_t len = recv_frame(fd, &buf, &cap);
     if (len == 0) break;
     const uint8_t t = buf[0];
     int32_t id = 0;
     if (len >= 5 && t >= L_GET_UID && t <= L_FORGET) memcpy(&id, buf + 1, 4);
-    if (t == W_PUSH_VEC_D) {
+    if (t == W_PUSH_VEC_D || t == W_PUSH_VEC_L) {
       int32_t mid = 0;
-      if (backend_push(&b, buf, len, &mid) != 0) a->errors++;
-      int32_t n;
-      memcpy(&n, buf + 1, 4);
-      a->records_applied += n;
-      if ((size_t)mid >= rcap) {                         /* updateFinished(id) */
-        size_t nc = rcap;
-        while ((size_t)mid >= nc) nc *= 2;
-        receipt = (uint8_t*)realloc(receipt, nc);
-        memset(receipt + rcap, 0, nc - rcap);
-        rcap = nc;
+      if (use_gpu) { /* enqueued: update runs on the GPU in arrival order; no reply */
+        uint64_t ticket = 0;
+        if (s->b.g_push_async(s->b.shard, buf, len, &mid, 0, &ticket) != 0) s->errors++;
+        if (npend == pcap) { pcap = pcap ? 2 * pcap : 64; pending = (int32_t*)realloc(pending, pcap * 4); }
+        pending[npend++] = mid;
+        last_ticket = ticket;
+      } else {
+        int32_t n;
+        memcpy(&n, buf + 1, 4);
+        memcpy(&mid, buf + 5, 4);
+        /* FastPrimitiveDeserializer.readArrayLong/readArray*: copy out of the frame into arrays */
+        int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
+        void* vals = malloc((size_t)n * 8 + 8);
+        memcpy(keys, buf + 9, (size_t)n * 8);
+        memcpy(vals, buf + 9 + (size_t)n * 8, (size_t)n * 8);
+        pthread_mutex_lock(&s->mu);
+        if (s->b.o_update(&s->b.opart, value_code(), s->b.data, s->b.size, keys, vals, n) >= 0) s->errors++;
+        receipt_set(s, mid, 1); /* updateFinished(id) */
+        pthread_mutex_unlock(&s->mu);
+        free(keys);
+        free(vals);
       }
-      receipt[mid] = 1;
     } else if (t == W_PULL_VECTOR) {
       int32_t n;
       memcpy(&n, buf + 1, 4);
       const size_t need = 5 + (size_t)n * 8;
-      if (need > ocap) { ocap = need; out = (uint8_t*)realloc(out, ocap); }
+      if (need > rcap) { rcap = need; resp = (uint8_t*)realloc(resp, rcap); }
       size_t olen = 0;
-      if (backend_pull(&b, buf, len, out, ocap, &olen) != 0) a->errors++;
-      send_frame(fd, out, (uint32_t)olen);
+      if (use_gpu) { /* ordered after every push enqueued on the shard */
+        if (s->b.g_pull_wire(s->b.shard, buf, len, resp, rcap, &olen) != 0) s->errors++;
+      } else {
+        int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
+        memcpy(keys, buf + 5, (size_t)n * 8);
+        pthread_mutex_lock(&s->mu);
+        if (s->b.o_get(&s->b.opart, value_code(), s->b.data, s->b.size, keys, resp + 5, n) >= 0) s->errors++;
+        pthread_mutex_unlock(&s->mu);
+        free(keys);
+        resp[0] = dtype_long ? W_RESP_L : W_RESP_D;
+        memcpy(resp + 1, &n, 4);
+        olen = need;
+      }
+      ob_frame(&out, resp, (uint32_t)olen);
     } else if (t == L_GET_UID) {
-      send_logic(fd, L_UID, ++uid);                      /* sender ! UniqueID(nextId()) */
+      pthread_mutex_lock(&s->mu);
+      const int32_t u = ++s->uid; /* sender ! UniqueID(nextId()) */
+      pthread_mutex_unlock(&s->mu);
+      ob_logic(&out, L_UID, u);
     } else if (t == L_ACK) {
-      const int got = (size_t)id < rcap && receipt[id];
-      send_logic(fd, got ? L_ACK : L_NACK, id);
+      int mine = 0;
+      for (size_t i = 0; i < npend && !mine; ++i) mine = pending[i] == id;
+      if (mine) { /* its push is still on the GPU: answered after the burst's wait */
+        if (nhold == hcap) { hcap = hcap ? 2 * hcap : 64; holds = (hold*)realloc(holds, hcap * sizeof(hold)); }
+        holds[nhold].end = out.len;
+        holds[nhold].ack_id = id;
+        ++nhold;
+      } else {
+        pthread_mutex_lock(&s->mu);
+        ob_logic(&out, receipt_has(s, id) ? L_ACK : L_NACK, id);
+        pthread_mutex_unlock(&s->mu);
+      }
     } else if (t == L_FORGET) {
-      if ((size_t)id < rcap) receipt[id] = 0;
-      send_logic(fd, L_FORGET, id);
+      pthread_mutex_lock(&s->mu);
+      if (receipt_has(s, id)) receipt_set(s, id, 0);
+      pthread_mutex_unlock(&s->mu);
+      ob_logic(&out, L_FORGET, id);
     } else if (t == L_STOP) {
       break;
     } else {
-      a->errors++;
+      s->errors++;
+    }
+    if (!readable_now(fd)) { /* the burst is drained: one wait for the enqueued pushes, then reply */
+      if (npend) {
+        const int rc = s->b.g_wait(s->b.shard, last_ticket, NULL);
+        pthread_mutex_lock(&s->mu);
+        for (size_t i = 0; i < npend; ++i)
+          if (rc == 0) receipt_set(s, pending[i], 1); /* updateFinished(id) */
+        pthread_mutex_unlock(&s->mu);
+        if (rc != 0) s->errors++;
+        npend = 0;
+      }
+      if (nhold) { /* splice the held acks into the reply stream at their places */
+        obuf merged = {0};
+        size_t from = 0;
+        pthread_mutex_lock(&s->mu);
+        for (size_t i = 0; i < nhold; ++i) {
+          ob_put(&merged, out.p + from, holds[i].end - from);
+          from = holds[i].end;
+          ob_logic(&merged, receipt_has(s, holds[i].ack_id) ? L_ACK : L_NACK, holds[i].ack_id);
+        }
+        pthread_mutex_unlock(&s->mu);
+        ob_put(&merged, out.p + from, out.len - from);
+        free(out.p);
+        out = merged;
+        nhold = 0;
+      }
+      ob_flush(&out, fd);
     }
   }
+  ob_flush(&out, fd);
   close(fd);
   free(buf);
-  free(out);
-  free(receipt);
-  backend_close(&b);
+  free(resp);
+  free(out.p);
+  free(pending);
+  free(holds);
+  free(a);
   return NULL;
 }
 
-/* ---- client ------------------------------------------------------------------------------------ */
-/* java.util.Random(42).nextDouble() -- the values of GranularBigVectorSpec.scala:14-35 */
+typedef struct {
+  server* s;
+  int nconn;
+} acceptor_arg;
+
+static void* acceptor_main(void* p) {
+  acceptor_arg* a = (acceptor_arg*)p;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)a->nconn);
+  for (int i = 0; i < a->nconn; ++i) {
+    int fd = accept(a->s->listen_fd, NULL, NULL);
+    if (fd < 0) die("accept");
+    tune_socket(fd);
+    conn_arg* c = (conn_arg*)malloc(sizeof(conn_arg));
+    c->s = a->s;
+    c->fd = fd;
+    pthread_create(&th[i], NULL, conn_main, c);
+  }
+  for (int i = 0; i < a->nconn; ++i) pthread_join(th[i], NULL);
+  free(th);
+  return NULL;
+}
+
+/* ---- clients ------------------------------------------------------------------------------------ */
+/* java.util.Random -- the values of GranularBigVectorSpec.scala:14-35 (seed 42) */
 typedef struct { uint64_t seed; } jrandom;
 static void jr_init(jrandom* r, int64_t s) { r->seed = ((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
 static int32_t jr_next(jrandom* r, int bits) {
@@ -294,202 +415,326 @@ static int32_t jr_next(jrandom* r, int bits) {
 static double jr_double(jrandom* r) {
   return (double)(((int64_t)jr_next(r, 26) << 27) + jr_next(r, 27)) * (1.0 / (double)(1LL << 53));
 }
+static uint64_t splitmix(uint64_t* x) {
+  uint64_t z = (*x += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static int S, C, M, W;
+static int64_t N;
+static int32_t n_small, q_small;
+static int64_t small_keys;
+static int32_t owner_of(int64_t k) {
+  return k < small_keys ? (int32_t)(k / q_small) : (int32_t)(n_small + (k - small_keys) / ((int64_t)q_small + 1));
+}
 
 typedef struct {
+  int c;               /* client index */
+  int part;            /* server / partition */
   int fd;
-  int part;
-  const int64_t* keys;
-  const double* vals;
-  const int32_t* owner;
-  int64_t nkeys;
-  int msg;
+  const int64_t* keys; /* the client's records */
+  const void* vals;
+  int64_t n;
+  void* pulled;        /* values pulled back, at the records' positions */
+  int mode;            /* 0 push, 1 pull */
   int64_t messages, resends;
-  double* pulled;
-  int mode; /* 0 push, 1 pull */
-} client_arg;
+} link_arg;
 
-static void* client_main(void* p) {
-  client_arg* c = (client_arg*)p;
+/* one message of this link: the records of slice i (GranularBigVector) owned by `part` */
+static int32_t gather(const link_arg* l, int64_t i0, int64_t* idx) {
+  const int64_t i1 = i0 + M < l->n ? i0 + M : l->n;
+  int32_t m = 0;
+  for (int64_t j = i0; j < i1; ++j)
+    if (owner_of(l->keys[j]) == l->part) idx[m++] = j;
+  return m;
+}
+
+typedef struct {
+  int32_t id;
+  int32_t n;
+  int64_t* idx; /* record positions of the message */
+} fsm;
+
+static void* link_main(void* p) {
+  link_arg* l = (link_arg*)p;
   uint8_t* buf = NULL;
   size_t cap = 0;
-  uint8_t* m = (uint8_t*)malloc(9 + (size_t)c->msg * 16);
-  int64_t* idx = (int64_t*)malloc((size_t)c->msg * 8);
-  /* GranularBigVector: <= msg-record slices of the caller's keys; AsyncBigVector groups each slice
-   * by partition, one message per partition -- this thread sends partition `part`'s messages */
-  for (int64_t i = 0; i < c->nkeys; i += c->msg) {
-    const int64_t end = i + c->msg < c->nkeys ? i + c->msg : c->nkeys;
-    int32_t n = 0;
-    for (int64_t j = i; j < end; ++j)
-      if (c->owner[j] == c->part) idx[n++] = j;
-    if (n == 0) continue;
-    if (c->mode == 0) {
-      send_logic(c->fd, L_GET_UID, 0);                       /* prepare(): GetUniqueID */
-      uint32_t len = recv_frame(c->fd, &buf, &cap);
-      int32_t id;
-      if (len != 5 || buf[0] != L_UID) die("protocol: UniqueID");
-      memcpy(&id, buf + 1, 4);
-      m[0] = W_PUSH_VEC_D;                                   /* RequestSerializer.scala:165-173 */
-      memcpy(m + 1, &n, 4);
-      memcpy(m + 5, &id, 4);
-      for (int32_t q = 0; q < n; ++q) {
-        memcpy(m + 9 + (size_t)q * 8, &c->keys[idx[q]], 8);
-        memcpy(m + 9 + (size_t)n * 8 + (size_t)q * 8, &c->vals[idx[q]], 8);
-      }
-      for (;;) {
-        send_frame(c->fd, m, 9 + (uint32_t)n * 16);          /* execute(): actorRef ! message(id) */
-        c->messages++;
-        send_logic(c->fd, L_ACK, id);                        /* acknowledge() */
-        len = recv_frame(c->fd, &buf, &cap);
-        if (len != 5) die("protocol: ack");
-        if (buf[0] == L_ACK) break;
-        c->resends++;                                        /* NotAcknowledgeReceipt: execute() again */
-      }
-      send_logic(c->fd, L_FORGET, id);                       /* forget() */
-      len = recv_frame(c->fd, &buf, &cap);
-      if (len != 5 || buf[0] != L_FORGET) die("protocol: forget");
-    } else {
-      m[0] = W_PULL_VECTOR;                                  /* RequestSerializer.scala:150-155 */
-      memcpy(m + 1, &n, 4);
-      for (int32_t q = 0; q < n; ++q) memcpy(m + 5 + (size_t)q * 8, &c->keys[idx[q]], 8);
-      send_frame(c->fd, m, 5 + (uint32_t)n * 8);
-      c->messages++;
-      const uint32_t len = recv_frame(c->fd, &buf, &cap);
-      int32_t rn;
-      if (len < 5 || buf[0] != W_RESP_D) die("protocol: response");
-      memcpy(&rn, buf + 1, 4);
-      if (rn != n || len != 5 + (uint32_t)n * 8) die("protocol: response size");
-      for (int32_t q = 0; q < n; ++q) memcpy(&c->pulled[idx[q]], buf + 5 + (size_t)q * 8, 8);
-    }
+  obuf out = {0};
+  const int64_t nslices = (l->n + M - 1) / M;
+  /* the messages of this link, in slice order (empty slices send nothing) */
+  fsm* msgs = (fsm*)calloc((size_t)(nslices > 0 ? nslices : 1), sizeof(fsm));
+  int64_t nmsg = 0;
+  int64_t* scratch = (int64_t*)malloc((size_t)M * 8);
+  for (int64_t s = 0; s < nslices; ++s) {
+    const int32_t m = gather(l, s * M, scratch);
+    if (!m) continue;
+    msgs[nmsg].n = m;
+    msgs[nmsg].idx = (int64_t*)malloc((size_t)m * 8);
+    memcpy(msgs[nmsg].idx, scratch, (size_t)m * 8);
+    ++nmsg;
   }
+  free(scratch);
+  uint8_t* m = (uint8_t*)malloc(9 + (size_t)M * 16);
+  /* replies come back in request order on a connection: a FIFO of (kind, message) */
+  int64_t* fifo_msg = (int64_t*)malloc(sizeof(int64_t) * (size_t)(4 * W + 8));
+  uint8_t* fifo_kind = (uint8_t*)malloc((size_t)(4 * W + 8));
+  size_t fh = 0, ft = 0;
+  const size_t fcap = (size_t)(4 * W + 8);
+#define FPUSH(kind, mi) do { fifo_kind[ft % fcap] = (kind); fifo_msg[ft % fcap] = (mi); ++ft; } while (0)
+  int64_t started = 0, done = 0;
+  const uint8_t ptype = dtype_long ? W_PUSH_VEC_L : W_PUSH_VEC_D;
+  while (done < nmsg) {
+    while (started < nmsg && started - done < W) { /* issue: GetUniqueID (push) or the pull itself */
+      if (l->mode == 0) {
+        ob_logic(&out, L_GET_UID, 0);
+        FPUSH(L_UID, started);
+      } else {
+        fsm* f = &msgs[started];
+        m[0] = W_PULL_VECTOR; /* RequestSerializer.scala:150-155 */
+        memcpy(m + 1, &f->n, 4);
+        for (int32_t q = 0; q < f->n; ++q) memcpy(m + 5 + (size_t)q * 8, &l->keys[f->idx[q]], 8);
+        ob_frame(&out, m, 5 + (uint32_t)f->n * 8);
+        l->messages++;
+        FPUSH(W_PULL_VECTOR, started);
+      }
+      ++started;
+    }
+    ob_flush(&out, l->fd);
+    const uint32_t len = recv_frame(l->fd, &buf, &cap);
+    if (len == 0) die("protocol: connection closed");
+    if (fh == ft) die("protocol: unexpected reply");
+    const uint8_t kind = fifo_kind[fh % fcap];
+    const int64_t mi = fifo_msg[fh % fcap];
+    ++fh;
+    fsm* f = &msgs[mi];
+    if (kind == L_UID) {
+      if (len != 5 || buf[0] != L_UID) die("protocol: UniqueID");
+      memcpy(&f->id, buf + 1, 4);
+      goto execute;
+    } else if (kind == L_ACK) {
+      if (len != 5) die("protocol: ack");
+      if (buf[0] == L_ACK) {
+        ob_logic(&out, L_FORGET, f->id); /* forget() */
+        FPUSH(L_FORGET, mi);
+      } else {
+        l->resends++; /* NotAcknowledgeReceipt: execute() again */
+        goto execute;
+      }
+    } else if (kind == L_FORGET) {
+      if (len != 5 || buf[0] != L_FORGET) die("protocol: forget");
+      ++done;
+    } else { /* a pull response */
+      int32_t rn;
+      if (len < 5 || buf[0] != (dtype_long ? W_RESP_L : W_RESP_D)) die("protocol: response");
+      memcpy(&rn, buf + 1, 4);
+      if (rn != f->n || len != 5 + (uint32_t)f->n * 8) die("protocol: response size");
+      for (int32_t q = 0; q < f->n; ++q) memcpy((char*)l->pulled + (size_t)f->idx[q] * 8, buf + 5 + (size_t)q * 8, 8);
+      ++done;
+    }
+    continue;
+  execute:
+    m[0] = ptype; /* RequestSerializer.scala:157-173 */
+    memcpy(m + 1, &f->n, 4);
+    memcpy(m + 5, &f->id, 4);
+    for (int32_t q = 0; q < f->n; ++q) {
+      memcpy(m + 9 + (size_t)q * 8, &l->keys[f->idx[q]], 8);
+      memcpy(m + 9 + (size_t)f->n * 8 + (size_t)q * 8, (const char*)l->vals + (size_t)f->idx[q] * 8, 8);
+    }
+    ob_frame(&out, m, 9 + (uint32_t)f->n * 16); /* execute(): actorRef ! message(id) */
+    l->messages++;
+    ob_logic(&out, L_ACK, f->id); /* acknowledge() */
+    FPUSH(L_ACK, mi);
+  }
+  ob_flush(&out, l->fd);
+  for (int64_t i = 0; i < nmsg; ++i) free(msgs[i].idx);
+  free(msgs);
   free(m);
-  free(idx);
+  free(fifo_msg);
+  free(fifo_kind);
   free(buf);
+  free(out.p);
   return NULL;
 }
 
 int main(int argc, char** argv) {
   const char* kind = "oracle";
   const char* lib = NULL;
-  int S = 2, msg = 1000;
-  int64_t N = 1000000;
+  const char* pattern = "dense";
+  S = 2;
+  C = 1;
+  M = 1000;
+  W = 64;
+  N = 1000000;
+  int64_t R = 0;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--backend") && i + 1 < argc) kind = argv[++i];
     else if (!strcmp(argv[i], "--lib") && i + 1 < argc) lib = argv[++i];
     else if (!strcmp(argv[i], "--servers") && i + 1 < argc) S = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--clients") && i + 1 < argc) C = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--keys") && i + 1 < argc) N = atoll(argv[++i]);
-    else if (!strcmp(argv[i], "--msg") && i + 1 < argc) msg = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--records") && i + 1 < argc) R = atoll(argv[++i]);
+    else if (!strcmp(argv[i], "--msg") && i + 1 < argc) M = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--window") && i + 1 < argc) W = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--pattern") && i + 1 < argc) pattern = argv[++i];
+    else if (!strcmp(argv[i], "--dtype") && i + 1 < argc) dtype_long = !strcmp(argv[++i], "long");
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) gpu_device = atoi(argv[++i]);
-    else { fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--keys N] [--msg M] [--device D]\n", argv[0]); return 2; }
+    else {
+      fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--clients C] [--keys N] "
+                      "[--pattern dense|uniform] [--records R] [--msg M] [--window W] [--dtype double|long] "
+                      "[--device D]\n", argv[0]);
+      return 2;
+    }
   }
-  if (!lib || S <= 0 || N <= 0 || msg <= 0) { fprintf(stderr, "glint_loopback: bad arguments\n"); return 2; }
+  const int uniform = !strcmp(pattern, "uniform");
+  if (!lib || S <= 0 || C <= 0 || N <= 0 || M <= 0 || W <= 0) { fprintf(stderr, "glint_loopback: bad arguments\n"); return 2; }
+  if (uniform && R <= 0) R = N / C;
   backend_open(kind, lib);
 
   /* RangePartitioner.apply(S, N) (RangePartitioner.scala:62-84) and partition() (:27-43) */
-  const int32_t n_large = (int32_t)(N % S), n_small = S - n_large;
-  const int32_t q = (int32_t)((N - N % S) / S);
-  int64_t* starts = (int64_t*)malloc(sizeof(int64_t) * S);
-  int64_t* ends = (int64_t*)malloc(sizeof(int64_t) * S);
+  const int32_t n_large = (int32_t)(N % S);
+  n_small = S - n_large;
+  q_small = (int32_t)((N - N % S) / S);
+  small_keys = (int64_t)n_small * q_small;
+  server* sv = (server*)calloc((size_t)S, sizeof(server));
   {
-    int64_t start = 0, end = q;
+    int64_t start = 0;
     for (int i = 0; i < S; ++i) {
-      if (i < n_small) { starts[i] = start; ends[i] = end; start += q; end += q; }
-      else { end += 1; starts[i] = start; ends[i] = end; start += q + 1; end += q; }
+      const int64_t size = i < n_small ? q_small : (int64_t)q_small + 1;
+      sv[i].start = start;
+      sv[i].end = start + size;
+      start += size;
     }
   }
-  const int64_t small_keys = (int64_t)n_small * q;
-  int64_t* keys = (int64_t*)malloc((size_t)N * 8);
-  double* vals = (double*)malloc((size_t)N * 8);
-  double* pulled = (double*)calloc((size_t)N, 8);
-  int32_t* owner = (int32_t*)malloc((size_t)N * 4);
-  jrandom jr;
-  jr_init(&jr, 42);
-  for (int64_t k = 0; k < N; ++k) {
-    keys[k] = k;
-    vals[k] = jr_double(&jr);
-    owner[k] = k < small_keys ? (int32_t)(k / q) : (int32_t)(n_small + (k - small_keys) / ((int64_t)q + 1));
+  /* the clients' records */
+  int64_t* cn = (int64_t*)calloc((size_t)C, 8);
+  int64_t** ck = (int64_t**)calloc((size_t)C, sizeof(int64_t*));
+  void** cv = (void**)calloc((size_t)C, sizeof(void*));
+  void** cp = (void**)calloc((size_t)C, sizeof(void*));
+  for (int c = 0; c < C; ++c) {
+    int64_t lo = 0, n;
+    if (uniform) n = R;
+    else { lo = N * c / C; n = N * (c + 1) / C - lo; }
+    cn[c] = n;
+    ck[c] = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+    cv[c] = malloc((size_t)(n > 0 ? n : 1) * 8);
+    cp[c] = calloc((size_t)(n > 0 ? n : 1), 8);
+    jrandom jr;
+    jr_init(&jr, 42 + c); /* client 0: GranularBigVectorSpec's java.util.Random(42) */
+    uint64_t sm = 0x5EED0000ULL + (uint64_t)c;
+    for (int64_t j = 0; j < n; ++j) {
+      ck[c][j] = uniform ? (int64_t)(splitmix(&sm) % (uint64_t)N) : lo + j;
+      if (dtype_long) ((int64_t*)cv[c])[j] = (int64_t)(splitmix(&sm) % 2001) - 1000;
+      else ((double*)cv[c])[j] = jr_double(&jr);
+    }
   }
 
-  server_arg* sa = (server_arg*)calloc((size_t)S, sizeof(server_arg));
-  pthread_t* st = (pthread_t*)malloc(sizeof(pthread_t) * S);
-  pthread_barrier_init(&servers_ready, NULL, (unsigned)S + 1);
+  /* servers: one acceptor per server, one thread per client connection */
+  pthread_t* at = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)S);
+  acceptor_arg* aa = (acceptor_arg*)calloc((size_t)S, sizeof(acceptor_arg));
   for (int i = 0; i < S; ++i) {
-    sa[i].start = starts[i];
-    sa[i].end = ends[i];
-    sa[i].listen_fd = socket(AF_INET, SOCK_STREAM, 0);
-    if (sa[i].listen_fd < 0) die("socket");
+    backend_init(&sv[i].b, sv[i].start, sv[i].end);
+    pthread_mutex_init(&sv[i].mu, NULL);
+    sv[i].listen_fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (sv[i].listen_fd < 0) die("socket");
     struct sockaddr_in ad;
     memset(&ad, 0, sizeof(ad));
     ad.sin_family = AF_INET;
     ad.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    ad.sin_port = 0;
-    if (bind(sa[i].listen_fd, (struct sockaddr*)&ad, sizeof(ad)) < 0) die("bind");
-    if (listen(sa[i].listen_fd, 1) < 0) die("listen");
+    if (bind(sv[i].listen_fd, (struct sockaddr*)&ad, sizeof(ad)) < 0) die("bind");
+    if (listen(sv[i].listen_fd, C + 8) < 0) die("listen");
     socklen_t sl = sizeof(ad);
-    getsockname(sa[i].listen_fd, (struct sockaddr*)&ad, &sl);
-    sa[i].port = ntohs(ad.sin_port);
-    pthread_create(&st[i], NULL, server_main, &sa[i]);
+    getsockname(sv[i].listen_fd, (struct sockaddr*)&ad, &sl);
+    sv[i].port = ntohs(ad.sin_port);
+    aa[i].s = &sv[i];
+    aa[i].nconn = C;
+    pthread_create(&at[i], NULL, acceptor_main, &aa[i]);
   }
-  pthread_barrier_wait(&servers_ready);
-  client_arg* ca = (client_arg*)calloc((size_t)S, sizeof(client_arg));
-  for (int i = 0; i < S; ++i) {
-    ca[i].fd = socket(AF_INET, SOCK_STREAM, 0);
-    struct sockaddr_in ad;
-    memset(&ad, 0, sizeof(ad));
-    ad.sin_family = AF_INET;
-    ad.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    ad.sin_port = htons((uint16_t)sa[i].port);
-    if (connect(ca[i].fd, (struct sockaddr*)&ad, sizeof(ad)) < 0) die("connect");
-    int one = 1;
-    setsockopt(ca[i].fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-    ca[i].part = i;
-    ca[i].keys = keys;
-    ca[i].vals = vals;
-    ca[i].owner = owner;
-    ca[i].nkeys = N;
-    ca[i].msg = msg;
-    ca[i].pulled = pulled;
-  }
-  pthread_t* ct = (pthread_t*)malloc(sizeof(pthread_t) * S);
+  const int L = C * S;
+  link_arg* la = (link_arg*)calloc((size_t)L, sizeof(link_arg));
+  for (int c = 0; c < C; ++c)
+    for (int i = 0; i < S; ++i) {
+      link_arg* l = &la[c * S + i];
+      l->fd = socket(AF_INET, SOCK_STREAM, 0);
+      struct sockaddr_in ad;
+      memset(&ad, 0, sizeof(ad));
+      ad.sin_family = AF_INET;
+      ad.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+      ad.sin_port = htons((uint16_t)sv[i].port);
+      if (connect(l->fd, (struct sockaddr*)&ad, sizeof(ad)) < 0) die("connect");
+      tune_socket(l->fd);
+      l->c = c;
+      l->part = i;
+      l->keys = ck[c];
+      l->vals = cv[c];
+      l->n = cn[c];
+      l->pulled = cp[c];
+    }
+  pthread_t* lt = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)L);
   double t[3];
-  int64_t msgs[2] = {0, 0};
+  int64_t msgs[2] = {0, 0}, resends = 0;
   for (int mode = 0; mode < 2; ++mode) {
     t[mode] = now_s();
-    for (int i = 0; i < S; ++i) {
-      ca[i].mode = mode;
-      ca[i].messages = 0;
-      pthread_create(&ct[i], NULL, client_main, &ca[i]);
+    for (int x = 0; x < L; ++x) {
+      la[x].mode = mode;
+      la[x].messages = 0;
+      pthread_create(&lt[x], NULL, link_main, &la[x]);
     }
-    for (int i = 0; i < S; ++i) {
-      pthread_join(ct[i], NULL);
-      msgs[mode] += ca[i].messages;
+    for (int x = 0; x < L; ++x) {
+      pthread_join(lt[x], NULL);
+      msgs[mode] += la[x].messages;
+      resends += la[x].resends;
     }
   }
   t[2] = now_s();
-  for (int i = 0; i < S; ++i) {
-    uint8_t stop[5] = {L_STOP, 0, 0, 0, 0};
-    send_frame(ca[i].fd, stop, 5);
+  for (int x = 0; x < L; ++x) {
+    uint8_t stop[9] = {5, 0, 0, 0, L_STOP, 0, 0, 0, 0};
+    write_all(la[x].fd, stop, 9);
   }
   int errors = 0;
-  int64_t resends = 0;
   for (int i = 0; i < S; ++i) {
-    pthread_join(st[i], NULL);
-    errors += sa[i].errors;
-    resends += ca[i].resends;
-    close(ca[i].fd);
-    close(sa[i].listen_fd);
+    pthread_join(at[i], NULL);
+    errors += sv[i].errors;
+    close(sv[i].listen_fd);
   }
-  /* GranularBigVectorSpec: the pulled values equal the pushed ones exactly (one add onto 0.0) */
+  for (int x = 0; x < L; ++x) close(la[x].fd);
+
+  /* checks */
   int ok = errors == 0;
-  for (int64_t k = 0; k < N && ok; ++k) ok = memcmp(&pulled[k], &vals[k], 8) == 0;
+  int64_t total = 0;
+  for (int c = 0; c < C; ++c) total += cn[c];
+  if (!uniform) { /* each key pushed once: pulled == pushed, bit for bit */
+    for (int c = 0; c < C && ok; ++c) ok = memcmp(cp[c], cv[c], (size_t)cn[c] * 8) == 0;
+  } else { /* the sequential sum over every client's records, then compared per pulled record */
+    void* sum = calloc((size_t)N, 8);
+    double* mag = dtype_long ? NULL : (double*)calloc((size_t)N, 8);
+    for (int c = 0; c < C; ++c)
+      for (int64_t j = 0; j < cn[c]; ++j) {
+        const int64_t k = ck[c][j];
+        if (dtype_long) ((int64_t*)sum)[k] = (int64_t)((uint64_t)((int64_t*)sum)[k] + (uint64_t)((int64_t*)cv[c])[j]);
+        else { ((double*)sum)[k] += ((double*)cv[c])[j]; mag[k] += fabs(((double*)cv[c])[j]); }
+      }
+    for (int c = 0; c < C && ok; ++c)
+      for (int64_t j = 0; j < cn[c] && ok; ++j) {
+        const int64_t k = ck[c][j];
+        if (dtype_long) ok = ((int64_t*)cp[c])[j] == ((int64_t*)sum)[k];
+        else ok = fabs(((double*)cp[c])[j] - ((double*)sum)[k]) <= 1e-9 * mag[k] + 1e-300;
+      }
+    free(sum);
+    free(mag);
+  }
+  for (int i = 0; i < S; ++i) backend_close(&sv[i].b);
   const double tp = t[1] - t[0], tl = t[2] - t[1];
-  printf("{\"backend\": \"%s\", \"servers\": %d, \"keys\": %lld, \"max_records_per_message\": %d, "
+  printf("{\"backend\": \"%s\", \"pattern\": \"%s\", \"dtype\": \"%s\", \"servers\": %d, \"clients\": %d, "
+         "\"keys\": %lld, \"records\": %lld, \"max_records_per_message\": %d, \"window\": %d, "
          "\"push_messages\": %lld, \"pull_messages\": %lld, \"resends\": %lld, \"push_s\": %.6f, \"pull_s\": %.6f, "
          "\"push_records_per_s\": %.1f, \"pull_records_per_s\": %.1f, \"push_payload_MBps\": %.2f, "
          "\"pull_payload_MBps\": %.2f, \"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
-         kind, S, (long long)N, msg, (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl,
-         (double)N / tp, (double)N / tl, 16.0 * (double)N / tp / 1e6, 16.0 * (double)N / tl / 1e6,
-         vals[0], N > 1 ? vals[1] : 0.0, N > 2 ? vals[2] : 0.0, ok ? "true" : "false");
-  free(keys); free(vals); free(pulled); free(owner); free(sa); free(st); free(ca); free(ct);
-  free(starts); free(ends);
+         kind, pattern, dtype_long ? "long" : "double", S, C, (long long)N, (long long)total, M, W,
+         (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl, (double)total / tp, (double)total / tl,
+         16.0 * (double)total / tp / 1e6, 16.0 * (double)total / tl / 1e6,
+         dtype_long ? 0.0 : ((double*)cv[0])[0], (!dtype_long && cn[0] > 1) ? ((double*)cv[0])[1] : 0.0,
+         (!dtype_long && cn[0] > 2) ? ((double*)cv[0])[2] : 0.0, ok ? "true" : "false");
   return ok ? 0 : 1;
 }
