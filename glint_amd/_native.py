@@ -20,7 +20,7 @@ GLINT_K_PUSH_CHECK = 5
 GLINT_K_PUSH_BINNED = 6
 GLINT_K_PUSH_ORDERED = 7
 GLINT_ROUTE_RANGE, GLINT_ROUTE_CYCLIC = 0, 1
-GLINT_RING_SLOTS, GLINT_ZERO_COPY_MAX = 8, 4096
+GLINT_RING_SLOTS, GLINT_ZERO_COPY_MAX = 16, 4096
 
 # every symbol include/glint_gpu.h declares, with its C signature
 _P = C.c_void_p
@@ -53,6 +53,8 @@ SIGNATURES = {
     "glint_push_staged": (_I, [_P, _I, _I64, _I, C.POINTER(C.c_uint64)]),
     "glint_push_wire_async": (_I, [_P, _P, _SZ, C.POINTER(_I32), _I, C.POINTER(C.c_uint64)]),
     "glint_shard_wait": (_I, [_P, C.c_uint64, C.POINTER(_I64)]),
+    "glint_pull_async": (_I, [_P, _I, _P, _P, _P, _I64, C.POINTER(C.c_uint64)]),
+    "glint_pull_wire_async": (_I, [_P, _P, _SZ, _P, _SZ, C.POINTER(_SZ), C.POINTER(C.c_uint64)]),
     "glint_pull_wire": (_I, [_P, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     "glint_route_dev": (_I, [_P, _I64, _I, _I32, _I64, _P, _P, C.POINTER(_I64), _P]),
     "glint_route_gather_dev": (_I, [_P, _P, _P, _I, _I64, _I, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -49,6 +49,25 @@ __device__ __forceinline__ void record_error(ErrState* e, i64 idx) {
   atomicAdd(&e->count, 1ull);
 }
 
+// End of a single-workgroup ring launch (MsgSig). Every wave first waits for its own stores
+// (answers written into mapped host memory, error atomics) to reach L2; then one lane publishes the
+// error state and, behind a system-scope release (the L2 writes back what those stores left in it,
+// and the lane waits for the write-backs -- plain stores to mapped host memory can sit in L2 until
+// then), the ticket. Once the host sees the ticket, everything before it is in host memory. Called
+// by every thread (workgroup-uniform `done`).
+__device__ __forceinline__ void msg_signal(const MsgSig& g, const ErrState* err) {
+  if (!g.done) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u64 enc = __hip_atomic_load(&err->min_bad_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 cnt = __hip_atomic_load(&err->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&g.herr->min_bad_enc, enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&g.herr->count, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(g.done, g.ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // address of a record; false when the JVM would throw ArrayIndexOutOfBoundsException
 template <bool MAT, int KIND = -1>
 __device__ __forceinline__ bool rec_addr(const PartDesc& p, i64 key, int32_t col, i64& addr) {

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
 // PartialVector.get (PartialVector.scala:51-60): out[i] = data(globalToLocal(keys(i)))
 template <typename V, bool PAIRS>
 __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, const V* data, PartDesc part,
-                                                        V* out, ErrState* err) {
+                                                        V* out, ErrState* err, MsgSig sig) {
   typedef typename Vec2<V>::T V2;
   const i64 stride = (i64)gridDim.x * kTPB;
   if (PAIRS) {
@@ -418,25 +418,27 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
       out[i] = o ? data[l] : V(0);
     }
   }
+  msg_signal(sig, err);
 }
 
 // PartialMatrix.get (PartialMatrix.scala:55-65)
 template <typename V>
 __global__ __launch_bounds__(kTPB) void mat_pull_kernel(const i64* rows, const int32_t* cols, i64 n, const V* data,
-                                                        PartDesc part, V* out, ErrState* err) {
+                                                        PartDesc part, V* out, ErrState* err, MsgSig sig) {
   for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += (i64)gridDim.x * kTPB) {
     i64 ad;
     const bool o = rec_addr<true>(part, rows[i], cols[i], ad);
     if (!o) record_error(err, i);
     out[i] = o ? data[ad] : V(0);
   }
+  msg_signal(sig, err);
 }
 
 // PartialMatrix.getRows (PartialMatrix.scala:37-46) + the row flattening of ResponseSerializer
 // (ResponseSerializer.scala:52-61): one wave per requested row, 16 B per lane when rows allow.
 template <typename V, bool VEC16>
 __global__ __launch_bounds__(kTPB) void mat_pull_rows_kernel(const i64* rows, i64 n, const V* data, PartDesc part,
-                                                             V* out, ErrState* err) {
+                                                             V* out, ErrState* err, MsgSig sig) {
   const int lane = threadIdx.x & 63;
   const i64 w0 = (i64)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const i64 nw = (i64)gridDim.x * (kTPB / 64);
@@ -458,6 +460,7 @@ __global__ __launch_bounds__(kTPB) void mat_pull_rows_kernel(const i64* rows, i6
       for (i64 c = lane; c < cols; c += 64) dst[c] = ok ? src[c] : V(0);
     }
   }
+  msg_signal(sig, err);
 }
 
 }  // namespace glint
@@ -514,6 +517,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.err = s->d_err;
   a.elems = s->elems;
   a.hint = s->d_hint;
+  a.sig = s->sig;
   a.sweep_blocks = 0;
   const i64 ntiles = (n + kTile - 1) / kTile;
   if (ntiles >= (i64)0xFFFFFFF0ll) return GLINT_EINVAL;
@@ -526,7 +530,9 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   // deterministic one, and host-pointer / wire pushes unless the caller said UNORDERED -- are one
   // launch of the order-preserving fold (glint_ordered.hip). Int/Long sums are exact in any order.
   const bool seq = det || (fp && (flags & kPushHostSequential) && !unordered);
-  if (seq && n <= kOrderedMax && s->elems < ((i64)1 << 32)) return push_ordered<V, MAT>(s, a, st);
+  // a ring launch (one workgroup that signals its own completion) is always the ordered fold: for
+  // Int/Long it is one more exact summation order
+  if (a.sig.done || (seq && n <= kOrderedMax && s->elems < ((i64)1 << 32))) return push_ordered<V, MAT>(s, a, st);
   // control region: [LaunchCtl slot 0 | slot 1 | pad to 256][tile descriptors i64 x ntiles]. An
   // ordered push uses one slot while its push_check zeroes the other for the next push, so no
   // memset runs per push (pushes on one shard are stream-ordered, as the actor's messages are).
@@ -582,20 +588,22 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
 }
 
 // ---- pulls ------------------------------------------------------------------------------------
+// A ring launch (s->sig.done set) is one workgroup that signals its own completion.
 template <typename V>
 int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream_t st) {
   if (n <= 0) return GLINT_OK;
   if (!keys || !out) return GLINT_EINVAL;
+  const MsgSig sig = s->sig;
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
   if (pairs) {
     // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5)
-    const unsigned g = grid_for((n + 1) / 2, kTPB, (i64)s->cus * 4);
+    const unsigned g = sig.done ? 1u : grid_for((n + 1) / 2, kTPB, (i64)s->cus * 4);
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, true>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
-                    (V*)out, s->d_err));
+                    (V*)out, s->d_err, sig));
   } else {
-    const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);
+    const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, false>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
-                    (V*)out, s->d_err));
+                    (V*)out, s->d_err, sig));
   }
   return GLINT_OK;
 }
@@ -604,9 +612,10 @@ template <typename V>
 int launch_mat_pull(glint_shard* s, const i64* rows, const int32_t* cols, void* out, i64 n, hipStream_t st) {
   if (n <= 0) return GLINT_OK;
   if (!rows || !cols || !out) return GLINT_EINVAL;
-  const unsigned g = grid_for(n, kTPB, (i64)s->cus * 8);
+  const MsgSig sig = s->sig;
+  const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
   HIPCHK(launch_k(s, GLINT_K_MAT_PULL, mat_pull_kernel<V>, g, kTPB, st, rows, cols, n, (const V*)s->data, s->part,
-                  (V*)out, s->d_err));
+                  (V*)out, s->d_err, sig));
   return GLINT_OK;
 }
 
@@ -614,10 +623,11 @@ template <typename V>
 int launch_mat_pull_rows(glint_shard* s, const i64* rows, void* out, i64 n, hipStream_t st) {
   if (n <= 0) return GLINT_OK;
   if (!rows || !out) return GLINT_EINVAL;
+  const MsgSig sig = s->sig;
   const bool v16 = ((i64)s->part.cols * (i64)sizeof(V)) % 16 == 0 && aligned(out, 16);
-  const unsigned g = grid_for(n, kTPB / 64, (i64)s->cus * 8);
+  const unsigned g = sig.done ? 1u : grid_for(n, kTPB / 64, (i64)s->cus * 8);
   HIPCHK(launch_k(s, GLINT_K_MAT_PULL_ROWS, v16 ? mat_pull_rows_kernel<V, true> : mat_pull_rows_kernel<V, false>, g,
-                  kTPB, st, rows, n, (const V*)s->data, s->part, (V*)out, s->d_err));
+                  kTPB, st, rows, n, (const V*)s->data, s->part, (V*)out, s->d_err, sig));
   return GLINT_OK;
 }
 
@@ -648,6 +658,8 @@ int collect_errors(glint_shard* s, hipStream_t st, int64_t* first_bad) {
   if (h.min_bad_enc != 0) {
     HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), st));
     HIPCHK(hipStreamSynchronize(st));
+    s->reported_enc = h.min_bad_enc;  // ring entries still unretired may carry it: do not report twice
+    s->clear_ticket = s->ticket_next;
     s->last_bad = (i64)~h.min_bad_enc;
     if (first_bad) *first_bad = s->last_bad;
     return GLINT_EOUTOFRANGE;
@@ -725,9 +737,10 @@ void free_shard(glint_shard* s) {
     for (auto& r : s->ring) {
       if (r.h) (void)hipHostFree(r.h);
       if (r.d) (void)hipFree(r.d);
-      if (r.herr) (void)hipHostFree(r.herr);
+        if (r.herr) (void)hipHostFree(r.herr);
       if (r.done) (void)hipEventDestroy(r.done);
     }
+    if (s->h_done) (void)hipHostFree(s->h_done);
     (void)hipGetLastError();
   }
   delete s;
@@ -1016,6 +1029,8 @@ int finish(glint_shard* s) {
   HIPCHK(hipStreamSynchronize(s->stream));
   if (s->h_err->min_bad_enc == 0) return GLINT_OK;
   s->last_bad = (i64)~s->h_err->min_bad_enc;
+  s->reported_enc = s->h_err->min_bad_enc;  // ring entries still unretired may carry it
+  s->clear_ticket = s->ticket_next;
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
   return GLINT_EOUTOFRANGE;
@@ -1036,22 +1051,60 @@ StageLayout stage_layout(const glint_shard* s, i64 n) {
   return L;
 }
 
-// wait for a slot's push; remember the first error it saw that was not reported yet
+// Waits until the launch that carries `ticket` has written it to h_done (tickets complete in stream
+// order, so a later ticket there covers this one). Spins briefly -- a message-sized launch is a few
+// microseconds -- then lets HIP block on the stream, which also surfaces a device error.
+int wait_done(glint_shard* s, u64 ticket) {
+  for (int i = 0; i < (1 << 16); ++i) {
+    if (__atomic_load_n(s->h_done, __ATOMIC_ACQUIRE) >= ticket) return GLINT_OK;
+    __builtin_ia32_pause();
+  }
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return __atomic_load_n(s->h_done, __ATOMIC_ACQUIRE) >= ticket ? GLINT_OK : GLINT_EDEVICE;
+}
+
+// Retires a slot: waits for its entry, remembers the first error it saw that was not reported yet,
+// and hands an async pull its answer.
 int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   if (!r.inflight) return GLINT_OK;
-  HIPCHK(hipEventSynchronize(r.done));
+  if (r.sig) {
+    const int rc = wait_done(s, r.ticket);
+    if (rc) return rc;
+  } else {
+    HIPCHK(hipEventSynchronize(r.done));
+  }
   r.inflight = false;
-  const u64 enc = r.herr->min_bad_enc;  // cumulative until cleared: skip what was reported already
-  if (enc != 0 && enc != s->reported_enc && s->ring_bad < 0) {
+  // cumulative until cleared: an entry enqueued before the last clear may still carry the error
+  // reported then; later entries carry only new ones
+  const u64 enc = __atomic_load_n(&r.herr->min_bad_enc, __ATOMIC_ACQUIRE);
+  const bool stale = r.ticket <= s->clear_ticket && enc == s->reported_enc;
+  if (enc != 0 && !stale && s->ring_bad < 0) {
     s->ring_bad = (i64)~enc;
     s->ring_bad_enc = enc;
+  }
+  if (r.out) {
+    std::memcpy(r.out, r.h + r.out_off, r.out_bytes);
+    r.out = nullptr;
   }
   return GLINT_OK;
 }
 
-int ring_acquire_locked(glint_shard* s, i64 n, int* slot) {
+// Hands out a free slot sized for n records (and, for a pull, an answer of out_bytes behind the
+// key sections). Retires the slot's previous entry first.
+int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) {
   if (n < 0 || n > kRingMaxRecords) return GLINT_EINVAL;
   const StageLayout L = stage_layout(s, n);
+  const size_t need = std::max(L.total, L.kb + L.cb + pad256(out_bytes));
+  if (!s->h_done) {
+    if (hipHostMalloc((void**)&s->h_done, 256, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->d_done, s->h_done, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      if (s->h_done) (void)hipHostFree(s->h_done);
+      s->h_done = s->d_done = nullptr;
+      return GLINT_ENOMEM;
+    }
+    __atomic_store_n(s->h_done, (u64)0, __ATOMIC_RELEASE);
+  }
   for (int tries = 0; tries < GLINT_RING_SLOTS; ++tries) {
     const int idx = s->ring_next;
     s->ring_next = (idx + 1) % GLINT_RING_SLOTS;
@@ -1059,12 +1112,12 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot) {
     if (r.acquired) continue;  // handed out and not pushed yet
     int rc = ring_retire(s, r);
     if (rc) return rc;
-    if (r.hcap < L.total) {
+    if (r.hcap < need) {
       if (r.h) (void)hipHostFree(r.h);
       r.h = r.hd = nullptr;
       r.hcap = 0;
       size_t cap = (size_t)1 << 16;
-      while (cap < L.total) cap <<= 1;
+      while (cap < need) cap <<= 1;
       if (hipHostMalloc((void**)&r.h, cap, hipHostMallocMapped) != hipSuccess ||
           hipHostGetDevicePointer((void**)&r.hd, r.h, 0) != hipSuccess) {
         (void)hipGetLastError();
@@ -1079,21 +1132,56 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot) {
       r.done = nullptr;
       return GLINT_EDEVICE;
     }
-    if (!r.herr && hipHostMalloc((void**)&r.herr, sizeof(ErrState), hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      r.herr = nullptr;
-      return GLINT_ENOMEM;
+    if (!r.herr) {
+      if (hipHostMalloc((void**)&r.herr, sizeof(ErrState), hipHostMallocMapped) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&r.herr_d, r.herr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        if (r.herr) (void)hipHostFree(r.herr);
+        r.herr = r.herr_d = nullptr;
+        return GLINT_ENOMEM;
+      }
     }
     r.acquired = true;
     r.n = n;
+    r.cap_need = need;
+    r.out = nullptr;
     *slot = idx;
     return GLINT_OK;
   }
   return GLINT_ENOMEM;  // every slot handed out and not pushed
 }
 
-// Enqueues the push staged in slot idx. Small pushes are read by the kernel from the mapped pinned
-// slot itself (no copy command in the stream); larger ones are copied with one DMA first.
+// whether an entry of n records is one signalling launch reading (and answering) in the mapped slot
+inline bool ring_direct(const glint_shard* s, i64 n) { return n <= GLINT_ZERO_COPY_MAX && s->elems < ((i64)1 << 32); }
+
+// Runs `launch` (the entry's kernels on s->stream) for slot r: a direct entry is one workgroup that
+// signals its ticket itself; any other entry ends with an error-state copy and an event.
+template <typename F>
+int ring_dispatch(glint_shard* s, glint_shard::RingSlot& r, bool direct, F launch) {
+  const u64 ticket = s->ticket_next + 1;
+  if (direct) s->sig = MsgSig{s->d_done, ticket, r.herr_d};
+  const int rc = launch();
+  s->sig = MsgSig{nullptr, 0, nullptr};
+  if (rc) {
+    (void)hipStreamSynchronize(s->stream);
+    r.acquired = false;
+    r.out = nullptr;
+    return rc;
+  }
+  if (!direct) {
+    HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipEventRecord(r.done, s->stream));
+  }
+  s->ticket_next = ticket;
+  r.ticket = ticket;
+  r.sig = direct;
+  r.inflight = true;
+  r.acquired = false;
+  return GLINT_OK;
+}
+
+// Enqueues the push staged in slot idx. Message-sized pushes are read by the kernel from the mapped
+// pinned slot itself (no copy command in the stream); larger ones are copied with one DMA first.
 int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
   if (idx < 0 || idx >= GLINT_RING_SLOTS) return GLINT_EINVAL;
   glint_shard::RingSlot& r = s->ring[idx];
@@ -1102,8 +1190,9 @@ int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
   if (rc) return rc;
   const StageLayout L = stage_layout(s, r.n);  // the sections as handed out
   const bool mat = s->part.cols != 0;
+  const bool direct = ring_direct(s, n);
   const char* base = r.hd;
-  if (n > GLINT_ZERO_COPY_MAX) {
+  if (!direct) {
     rc = grow((void**)&r.d, &r.dcap, L.total);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(r.d, r.h, L.total, hipMemcpyHostToDevice, s->stream));
@@ -1113,23 +1202,62 @@ int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
   const int32_t* cols = mat ? (const int32_t*)(base + L.kb) : nullptr;
   const void* vals = base + L.kb + L.cb;
   const int hflags = flags | kPushHostSequential;  // the actor's update: message order by default
-  if (n > 0) {
+  rc = ring_dispatch(s, r, direct && n > 0, [&]() -> int {
+    if (n == 0) return GLINT_OK;
     if (mat) {
-      rc = [&]() -> int { GLINT_DISPATCH(s->dtype, push_mat_t, s, keys, cols, vals, n, hflags, s->stream); }();
-    } else {
-      rc = [&]() -> int { GLINT_DISPATCH(s->dtype, push_vec_t, s, keys, nullptr, vals, n, hflags, s->stream); }();
+      GLINT_DISPATCH(s->dtype, push_mat_t, s, keys, cols, vals, n, hflags, s->stream);
     }
+    GLINT_DISPATCH(s->dtype, push_vec_t, s, keys, nullptr, vals, n, hflags, s->stream);
+  });
+  if (rc) return rc;
+  if (ticket) *ticket = r.ticket;
+  return GLINT_OK;
+}
+
+// Enqueues a pull whose keys (and cols) are in slot idx; kind 0 vector get, 1 matrix get, 2 rows.
+// The answer is written into the slot behind the key sections and copied to `out` when the slot
+// retires (glint_shard_wait, or the slot's reuse).
+int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t out_bytes, u64* ticket) {
+  glint_shard::RingSlot& r = s->ring[idx];
+  int rc = order_after_dev(s);
+  if (rc) {
+    r.acquired = false;
+    return rc;
+  }
+  const StageLayout L = stage_layout(s, n);
+  const bool direct = n > 0 && ring_direct(s, n) && (kind != 2 || out_bytes <= ((size_t)1 << 20));
+  const char* base = r.hd;
+  char* ans = r.hd + L.kb + L.cb;
+  if (!direct) {  // keys over by DMA, the answer back by DMA into the slot
+    rc = grow((void**)&r.d, &r.dcap, L.kb + L.cb + pad256(out_bytes));
     if (rc) {
-      (void)hipStreamSynchronize(s->stream);
       r.acquired = false;
       return rc;
     }
+    HIPCHK(hipMemcpyAsync(r.d, r.h, L.kb + L.cb, hipMemcpyHostToDevice, s->stream));
+    base = r.d;
+    ans = r.d + L.kb + L.cb;
   }
-  HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
-  HIPCHK(hipEventRecord(r.done, s->stream));
-  r.ticket = ++s->ticket_next;
-  r.inflight = true;
-  r.acquired = false;
+  const i64* keys = (const i64*)base;
+  const int32_t* cols = (const int32_t*)(base + L.kb);
+  r.out = out;
+  r.out_bytes = out_bytes;
+  r.out_off = L.kb + L.cb;
+  rc = ring_dispatch(s, r, direct, [&]() -> int {
+    int e;
+    if (kind == 0) {
+      e = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, keys, ans, n, s->stream); }();
+    } else if (kind == 1) {
+      e = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_mat_pull, s, keys, cols, ans, n, s->stream); }();
+    } else {
+      e = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_mat_pull_rows, s, keys, ans, n, s->stream); }();
+    }
+    if (e || direct) return e;
+    return hipMemcpyAsync(r.h + L.kb + L.cb, ans, out_bytes, hipMemcpyDeviceToHost, s->stream) == hipSuccess
+               ? GLINT_OK
+               : GLINT_EDEVICE;
+  });
+  if (rc) return rc;
   if (ticket) *ticket = r.ticket;
   return GLINT_OK;
 }
@@ -1145,8 +1273,29 @@ int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
   if (first_bad) *first_bad = s->ring_bad;
   s->ring_bad = -1;
   s->reported_enc = s->ring_bad_enc;
+  s->clear_ticket = s->ticket_next;  // entries up to here were enqueued before the clear
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   return GLINT_EOUTOFRANGE;
+}
+
+// pull answer bytes: n values, or n rows of cols values
+inline size_t pull_bytes(const glint_shard* s, int kind, i64 n) {
+  return (size_t)n * s->vsize * (kind == 2 ? (size_t)s->part.cols : 1);
+}
+
+// Copies a pull's keys (and cols) into a fresh slot and enqueues it. The slot's answer reaches `out`
+// when the slot retires.
+int pull_enqueue_locked(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols, void* out, int64_t n,
+                        u64* ticket) {
+  int slot = -1;
+  const size_t ob = pull_bytes(s, kind, n);
+  int rc = ring_acquire_locked(s, n, &slot, ob);
+  if (rc) return rc;
+  glint_shard::RingSlot& r = s->ring[slot];
+  const StageLayout L = stage_layout(s, n);
+  std::memcpy(r.h, keys, (size_t)n * 8);
+  if (kind == 1) std::memcpy(r.h + L.kb, cols, (size_t)n * 4);
+  return ring_pull_locked(s, slot, kind, n, out, ob, ticket);
 }
 
 int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols, const void* vals, int64_t n,
@@ -1204,37 +1353,13 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   DeviceGuard g(s->device);
   int rc = order_after_dev(s);
   if (rc) return rc;
-  if (kind != 2 && n <= GLINT_ZERO_COPY_MAX) {
-    // Akka-sized: the kernel reads the keys from a mapped pinned ring slot and writes the answer
-    // into it, so the call is one launch and one event wait, with no copy command either way
-    int slot = -1;
-    rc = ring_acquire_locked(s, n, &slot);
+  if (n <= GLINT_ZERO_COPY_MAX) {
+    // Akka-sized: one workgroup reads the keys from a mapped pinned ring slot, writes the answer into
+    // it and signals its ticket, so the call is one launch and a wait on host memory
+    u64 ticket = 0;
+    rc = pull_enqueue_locked(s, kind, keys, cols, out, n, &ticket);
     if (rc) return rc;
-    glint_shard::RingSlot& r = s->ring[slot];
-    const StageLayout L = stage_layout(s, n);
-    std::memcpy(r.h, keys, (size_t)n * 8);
-    if (kind == 1) std::memcpy(r.h + L.kb, cols, (size_t)n * 4);
-    char* out_d = r.hd + L.kb + L.cb;
-    r.acquired = false;
-    if (kind == 0) {
-      rc = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)r.hd, out_d, n, s->stream); }();
-    } else {
-      rc = [&]() -> int {
-        GLINT_DISPATCH(s->dtype, launch_mat_pull, s, (const i64*)r.hd, (const int32_t*)(r.hd + L.kb), out_d, n,
-                       s->stream);
-      }();
-    }
-    if (rc) {
-      (void)hipStreamSynchronize(s->stream);
-      return rc;
-    }
-    HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipEventRecord(r.done, s->stream));
-    r.ticket = ++s->ticket_next;
-    r.inflight = true;
-    rc = ring_wait_locked(s, r.ticket, nullptr);  // also reports errors of pushes enqueued before it
-    if (rc == GLINT_OK) std::memcpy(out, r.h + L.kb + L.cb, (size_t)n * s->vsize);
-    return rc;
+    return ring_wait_locked(s, ticket, nullptr);  // also reports errors of pushes enqueued before it
   }
   const size_t out_bytes = (size_t)n * s->vsize * (kind == 2 ? (size_t)s->part.cols : 1);
   Staged st;
@@ -1374,10 +1499,24 @@ int glint_shard_wait(glint_shard_t s, uint64_t ticket, int64_t* first_bad) {
   return ring_wait_locked(s, (u64)ticket, (i64*)first_bad);
 }
 
+int glint_pull_async(glint_shard_t s, int kind, const int64_t* keys, const int32_t* cols, void* out, int64_t n,
+                     uint64_t* ticket) {
+  if (!s || !ticket || kind < 0 || kind > 2) return GLINT_EINVAL;
+  if (n < 0 || (n > 0 && (!keys || !out || (kind == 1 && !cols)))) return GLINT_EINVAL;
+  if ((kind == 0) != (s->part.cols == 0)) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  if (n == 0) {  // nothing to enqueue: the ticket of everything so far
+    *ticket = s->ticket_next;
+    return GLINT_OK;
+  }
+  return pull_enqueue_locked(s, kind, keys, cols, out, n, (u64*)ticket);
+}
+
 // RequestSerializer.fromBinary for the pull messages + ResponseSerializer.toBinary of the answer
 // (ResponseSerializer.scala:43-117; row answers are flattened rows x cols, :52-61).
-int glint_pull_wire(glint_shard_t s, const uint8_t* payload, size_t len, uint8_t* response, size_t cap,
-                    size_t* out_len) {
+static int pull_wire(glint_shard_t s, const uint8_t* payload, size_t len, uint8_t* response, size_t cap,
+                     size_t* out_len, uint64_t* ticket) {
   if (!s || !payload || len < 5 || !out_len) return GLINT_EINVAL;
   const uint8_t t = payload[0];
   int32_t n = 0;
@@ -1401,7 +1540,23 @@ int glint_pull_wire(glint_shard_t s, const uint8_t* payload, size_t len, uint8_t
   std::memcpy(response + 1, &c32, 4);
   const uint8_t* keys = payload + 5;
   const uint8_t* cols = keys + (size_t)n * 8;
+  if (ticket) {
+    *ticket = 0;
+    return glint_pull_async(s, kind, (const int64_t*)keys, kind == 1 ? (const int32_t*)cols : nullptr,
+                            response + 5, n, ticket);
+  }
   return host_pull(s, kind, (const int64_t*)keys, kind == 1 ? (const int32_t*)cols : nullptr, response + 5, n);
+}
+
+int glint_pull_wire(glint_shard_t s, const uint8_t* payload, size_t len, uint8_t* response, size_t cap,
+                    size_t* out_len) {
+  return pull_wire(s, payload, len, response, cap, out_len, nullptr);
+}
+
+int glint_pull_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, uint8_t* response, size_t cap,
+                          size_t* out_len, uint64_t* ticket) {
+  if (!ticket) return GLINT_EINVAL;
+  return pull_wire(s, payload, len, response, cap, out_len, ticket);
 }
 
 }  // extern "C"

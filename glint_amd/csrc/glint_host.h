@@ -43,25 +43,36 @@ struct glint_shard {
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
   ErrState* h_err = nullptr;  // pinned: the device error state lands here with the push's last copy
-  // pipelined ingest (glint_stage_acquire / glint_push_staged / glint_push_wire_async / glint_shard_wait):
-  // a ring of pinned, device-mapped host slots; each in-flight push owns one until its event completes
+  // pipelined ingest (glint_stage_acquire / glint_push_staged / glint_push_wire_async / glint_pull_async /
+  // glint_shard_wait): a ring of pinned, device-mapped host slots; each in-flight entry owns one until it
+  // completes. Message-sized entries are one single-workgroup kernel that reads its input from the
+  // slot (and writes a pull's answer into it) and then writes its ticket to h_done.
   struct RingSlot {
     char* h = nullptr;       // pinned host memory, mapped (small pushes are read in place by the kernel)
     char* hd = nullptr;      // its device-side address
     size_t hcap = 0;
     char* d = nullptr;       // device copy target for larger pushes
     size_t dcap = 0;
-    hipEvent_t done = nullptr;
-    ErrState* herr = nullptr;  // pinned: the shard's error state right after this push
+    hipEvent_t done = nullptr;  // completion of a multi-kernel (DMA) entry
+    ErrState* herr = nullptr;   // pinned, mapped: the shard's error state right after this entry
+    ErrState* herr_d = nullptr;
     uint64_t ticket = 0;
     int64_t n = 0;
+    size_t cap_need = 0;        // bytes this entry's layout uses
+    void* out = nullptr;        // an async pull's destination: filled from the slot when retired
+    size_t out_bytes = 0, out_off = 0;
     bool inflight = false, acquired = false;
+    bool sig = false;           // one-workgroup launch that signals through h_done (no event)
   } ring[GLINT_RING_SLOTS];
+  u64* h_done = nullptr;  // host-mapped: ticket of the last completed signalling launch
+  u64* d_done = nullptr;
+  MsgSig sig{};           // set only while a ring entry dispatches its one launch
   int ring_next = 0;
   uint64_t ticket_next = 0;
   int64_t ring_bad = -1;       // first bad record of a retired push, not reported yet
   uint64_t ring_bad_enc = 0;
   uint64_t reported_enc = 0;   // error state last reported (cumulative until cleared)
+  uint64_t clear_ticket = 0;   // last ticket enqueued before that report's clear
   u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
   u64* d_hint = nullptr;
   i64 last_bad = -1;

@@ -62,6 +62,15 @@ struct ErrState {
   u64 count;        // number of rejected records
 };
 
+// Completion of a single-workgroup launch on the pinned-ring path (message-sized host calls): the
+// kernel itself writes the shard's error state and then its ticket to host-mapped words, so the
+// host waits on memory -- no event marker and no error copy in the stream (glint_gpu.hip, ring_*).
+struct MsgSig {
+  u64* done;       // host-mapped ticket word; nullptr = an ordinary launch
+  u64 ticket;
+  ErrState* herr;  // host-mapped: the error state after this launch
+};
+
 // Partition -> local index, for both partitioner kinds (kind is launch-uniform)
 struct PartDesc {
   int32_t kind;   // 0 range, 1 cyclic
@@ -96,6 +105,7 @@ struct PushArgs {
   ErrState* err;
   u32 sweep_blocks;  // blocks of push_apply that take part in the affine sweep (<= grid)
   u64* hint;  // host-mapped word: the unordered-tail size push_apply saw (binned-path heuristic)
+  MsgSig sig;  // ring launches only (one workgroup)
 };
 
 }  // namespace glint

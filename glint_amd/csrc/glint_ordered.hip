@@ -180,13 +180,15 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
   }
   __syncthreads();
   ordered_flush<V>(skey, sval, s_cnt, a.data);
+  msg_signal(a.sig, a.err);
 }
 
 template <typename V, bool MAT>
 int push_ordered(glint_shard* s, const PushArgs<V>& a, hipStream_t st) {
   if (a.n <= 0) return GLINT_OK;
   if (a.n > kOrderedMax || s->elems >= ((i64)1 << 32)) return GLINT_EINVAL;
-  const unsigned g = grid_for(a.n, 1024, (i64)s->cus);
+  if (a.sig.done && a.n > kOrdCap) return GLINT_EINVAL;  // a ring launch is one workgroup: one list
+  const unsigned g = a.sig.done ? 1u : grid_for(a.n, 1024, (i64)s->cus);
   const int vec = aligned(a.keys, 16) && aligned(a.vals, 2 * sizeof(V)) && (!MAT || aligned(a.cols, 8));
   HIPCHK(launch_k(s, GLINT_K_PUSH_ORDERED, push_ordered_kernel<V, MAT>, g, kOrdTPB, st, a, vec));
   return GLINT_OK;

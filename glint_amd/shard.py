@@ -164,6 +164,24 @@ class _Shard:
               self.handle)
         return mid.value, ticket.value
 
+    def pull_async(self, *arrays, rows: bool = False, out=None):
+        """Enqueue a pull -- get(keys) for vectors, get(rows, cols) or getRows(rows) (rows=True) for
+        matrices -- behind everything enqueued before it (glint_pull_async). Returns (ticket, out):
+        `out` holds the answer once wait(ticket) has returned; keep it alive until then."""
+        mat = self.cols != 0
+        kind = 0 if not mat else (2 if rows else 1)
+        if len(arrays) != (2 if kind == 1 else 1):
+            raise ValueError("pull_async(keys) for vectors and row pulls, (rows, cols) for matrix elements")
+        keys = _host(arrays[0], np.int64).reshape(-1)
+        cols = _host(arrays[1], np.int32).reshape(-1) if kind == 1 else None
+        if kind == 1 and cols.size != keys.size:
+            raise ValueError("argument lengths differ")
+        out = self._host_out(out, (keys.size, self.cols) if kind == 2 else (keys.size,))
+        ticket = C.c_uint64()
+        check(self.lib.glint_pull_async(self.handle, kind, keys.ctypes.data, None if cols is None else cols.ctypes.data,
+                                        out.ctypes.data, keys.size, C.byref(ticket)), self.handle)
+        return ticket.value, out
+
     def wait(self, ticket: int) -> None:
         """Until the push with this ticket (and every earlier one) is applied; raises if one of them
         rejected a record (ArrayIndexOutOfBoundsException, as the actor's update would)."""

@@ -162,8 +162,12 @@ int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uin
  * it are applied -- what the actor needs before it answers AcknowledgeReceipt
  * (PushLogic.scala:40-66) -- with GLINT_EOUTOFRANGE (first bad record via glint_shard_last_error) if
  * one of them rejected a record. Every other call on the shard is ordered after the enqueued pushes.
- * Flags as for glint_vec_push (message order kept for Float/Double unless GLINT_PUSH_UNORDERED). */
-#define GLINT_RING_SLOTS 8
+ * Flags as for glint_vec_push (message order kept for Float/Double unless GLINT_PUSH_UNORDERED).
+ * An entry of up to GLINT_ZERO_COPY_MAX records is ONE single-workgroup kernel that signals its own
+ * completion through a host-mapped word (no event, no copy command): a few microseconds of stream
+ * time per message. Pulls can be enqueued the same way (glint_pull_async), so a server answering a
+ * burst of Pull messages waits once for all of them. Tickets number pushes and pulls together. */
+#define GLINT_RING_SLOTS 16
 #define GLINT_ZERO_COPY_MAX 4096
 
 /* A free slot for a push of n records, with the section pointers the caller fills: keys (i64 x n),
@@ -176,8 +180,18 @@ int glint_push_staged(glint_shard_t shard, int slot, int64_t n, int flags, uint6
 /* glint_push_wire, enqueued: the payload is copied into a slot before the call returns. */
 int glint_push_wire_async(glint_shard_t shard, const uint8_t* payload, size_t len, int32_t* id, int flags,
                           uint64_t* ticket);
-/* Waits for the push with this ticket and every earlier one; reports their errors. */
+/* Waits for the entry with this ticket and every earlier one; reports their errors (a rejected key
+ * of a pull included) and completes their pulls' answers. */
 int glint_shard_wait(glint_shard_t shard, uint64_t ticket, int64_t* first_bad);
+/* glint_vec_pull (kind 0), glint_mat_pull (1) or glint_mat_pull_rows (2), enqueued: the keys (and
+ * cols) are copied before the call returns; `out` receives the answer by the time
+ * glint_shard_wait(*ticket) returns and must stay valid until then. n <= 2^20. */
+int glint_pull_async(glint_shard_t shard, int kind, const int64_t* keys, const int32_t* cols, void* out,
+                     int64_t n, uint64_t* ticket);
+/* glint_pull_wire, enqueued: the response header is written at once, its values by the time
+ * glint_shard_wait(*ticket) returns (the response buffer must stay valid until then). */
+int glint_pull_wire_async(glint_shard_t shard, const uint8_t* payload, size_t len, uint8_t* response,
+                          size_t cap, size_t* out_len, uint64_t* ticket);
 
 /* ---- client routing (device) -------------------------------------------------------------- *
  * Replaces the client-side grouping in AsyncBigVector/AsyncBigMatrix.mapPartitions

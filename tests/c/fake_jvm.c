@@ -109,13 +109,14 @@ int main(int argc, char** argv) {
   ((jdouble*)v3->data)[1] = 1.0;
   ((jdouble*)v3->data)[2] = 1.0;
   NAT(await)(env, NULL, h, NAT(vecPushD)(env, NULL, h, k3, v3, 0));
-  Arr* o1 = arr(1, 8);
+  Arr* o1 = arr(3, 8);
   NAT(vecPullD)(env, NULL, h, k3, o1);
+  CHECK(!pending[0], "pull of a repeated key");
   volatile double seq = 0.0;
   seq = seq + 1e16;
   seq = seq + 1.0;
   seq = seq + 1.0;
-  CHECK(((jdouble*)o1->data)[0] == seq, "sequential Double order");
+  CHECK(((jdouble*)o1->data)[0] == seq && ((jdouble*)o1->data)[2] == seq, "sequential Double order");
   /* an out-of-partition key: the await throws ArrayIndexOutOfBoundsException; restart = zero */
   Arr* kb = arr(2, 8);
   Arr* vb = arr(2, 8);

@@ -25,7 +25,7 @@ def _vals(rng, dtype, n):
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("sizes", [[1000] * 37, [1, 4096, 4097, 79_999, 12, 3000]])
 def test_async_pushes_equal_sequential_oracle(gpu, dtype, sizes):
-    """More pushes in flight than ring slots (8); small ones read in place, large ones copied."""
+    """More pushes in flight than ring slots; small ones read in place, large ones copied."""
     rng = np.random.default_rng(zlib.crc32(f"ring/{dtype}/{len(sizes)}".encode()))
     start, size = 1 << 34, 60_000
     ref = O.OracleVector(O.part_range(start, start + size), O.CODE[dtype])
@@ -115,3 +115,77 @@ def test_jni_shim_end_to_end(gpu):
     from glint_amd.build import build_jni_driver
     r = subprocess.run([str(build_jni_driver()), str(gpu)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_async_pulls_interleaved_with_pushes(gpu, dtype):
+    """Pulls enqueued between pushes see exactly the pushes enqueued before them (the actor's
+    mailbox order); small pulls run in place in the mapped slot, large ones through DMA; more
+    entries in flight than ring slots."""
+    rng = np.random.default_rng(zlib.crc32(f"pull-async/{dtype}".encode()))
+    size = 50_000
+    ref = O.OracleVector(O.part_range(0, size), O.CODE[dtype])
+    with PartialVector(RangePartition(0, 0, size), dtype, gpu) as sh:
+        want, got = [], []
+        t = 0
+        for step, n in enumerate([1000, 1, 4096, 4097, 30_000, 777] * 4):
+            keys = rng.integers(0, size, n).astype(np.int64)
+            if step % 2 == 0:
+                vals = _vals(rng, dtype, n)
+                t = sh.push_async(keys, vals)
+                ref.update(keys, vals)
+            else:
+                t, out = sh.pull_async(keys)
+                got.append(out)
+                want.append(ref.data[keys].copy())
+        sh.wait(t)
+        for w, g in zip(want, got):
+            np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("dtype", ["double", "int"])
+def test_async_matrix_pulls(gpu, dtype):
+    rng = np.random.default_rng(21)
+    rows_n, cols_n = 300, 65
+    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE[dtype])
+    with PartialMatrix(RangePartition(0, 0, rows_n), cols_n, dtype, gpu) as sh:
+        r = rng.integers(0, rows_n, 5000).astype(np.int64)
+        c = rng.integers(0, cols_n, 5000).astype(np.int32)
+        v = _vals(rng, dtype, 5000)
+        sh.push_async(r, c, v)
+        ref.update(r, c, v)
+        qr = rng.integers(0, rows_n, 999).astype(np.int64)
+        qc = rng.integers(0, cols_n, 999).astype(np.int32)
+        t1, elems = sh.pull_async(qr, qc)
+        t2, rows_small = sh.pull_async(qr[:200], rows=True)     # 200 x 65 values: in place
+        t3, rows_big = sh.pull_async(qr, rows=True)            # 999 x 65 values
+        sh.wait(t3)
+        assert t1 < t2 < t3
+        np.testing.assert_array_equal(elems, ref.data.reshape(rows_n, cols_n)[qr, qc])
+        np.testing.assert_array_equal(rows_small, ref.data.reshape(rows_n, cols_n)[qr[:200]])
+        np.testing.assert_array_equal(rows_big, ref.data.reshape(rows_n, cols_n)[qr])
+
+
+def test_async_pull_bad_key_and_wire(gpu):
+    size = 1000
+    with PartialVector(RangePartition(0, 0, size), "double", gpu) as sh:
+        sh.update(np.arange(size, dtype=np.int64), np.arange(size, dtype=np.float64))
+        t, out = sh.pull_async(np.array([5, size + 3, 7], np.int64))
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.wait(t)
+        assert ei.value.record == 1
+        assert out[0] == 5.0 and out[2] == 7.0
+        # the wire form: header at once, values after the wait
+        import ctypes as C
+        keys = np.array([9, 1, 9], np.int64)
+        req = O.encode_pull_vector(keys)
+        buf = (C.c_uint8 * len(req)).from_buffer_copy(req)
+        resp = (C.c_uint8 * 64)()
+        olen, ticket = C.c_size_t(), C.c_uint64()
+        assert sh.lib.glint_pull_wire_async(sh.handle, buf, len(req), resp, 64, C.byref(olen), C.byref(ticket)) == 0
+        assert olen.value == 5 + 24
+        sh.wait(ticket.value)
+        assert np.frombuffer(bytes(resp)[5:29], np.float64).tolist() == [9.0, 1.0, 9.0]
+        t0, empty = sh.pull_async(np.zeros(0, np.int64))
+        sh.wait(t0)
+        assert empty.size == 0

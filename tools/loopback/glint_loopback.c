@@ -26,8 +26,9 @@
  *   --backend gpu --lib glint_amd/lib/libglint_gpu.so        an HBM shard per server fed the raw wire
  *            images: pushes are enqueued (glint_push_wire_async) and the server waits for them
  *            (glint_shard_wait) only when it has drained the messages that have arrived and owes an
- *            AcknowledgeReceipt -- what PushLogic needs, one wait per burst; pulls are
- *            glint_pull_wire, ordered after the enqueued pushes.
+ *            AcknowledgeReceipt or a Response -- what PushLogic needs, one wait per burst; pulls are
+ *            enqueued the same way (glint_pull_wire_async, ordered after the enqueued pushes) and
+ *            their Responses are sent, in request order, after that wait.
  *
  * Workloads (--pattern): dense -- client c pushes then pulls its own contiguous key range
  * (BASELINE configs[0] at C = 1: GranularBigVectorSpec's 1M keys with java.util.Random(42)
@@ -157,6 +158,7 @@ typedef struct {
   int (*g_push_async)(void*, const uint8_t*, size_t, int32_t*, int, uint64_t*);
   int (*g_wait)(void*, uint64_t, int64_t*);
   int (*g_pull_wire)(void*, const uint8_t*, size_t, uint8_t*, size_t, size_t*);
+  int (*g_pull_async)(void*, const uint8_t*, size_t, uint8_t*, size_t, size_t*, uint64_t*);
   int (*g_destroy)(void*);
 } backend;
 
@@ -175,8 +177,10 @@ static void backend_init(backend* b, int64_t start, int64_t end) {
     *(void**)&b->g_push_async = dlsym(dl, "glint_push_wire_async");
     *(void**)&b->g_wait = dlsym(dl, "glint_shard_wait");
     *(void**)&b->g_pull_wire = dlsym(dl, "glint_pull_wire");
+    *(void**)&b->g_pull_async = dlsym(dl, "glint_pull_wire_async");
     *(void**)&b->g_destroy = dlsym(dl, "glint_shard_destroy");
-    if (!b->g_create || !b->g_push_async || !b->g_wait || !b->g_pull_wire || !b->g_destroy) die("dlsym glint_*");
+    if (!b->g_create || !b->g_push_async || !b->g_wait || !b->g_pull_wire || !b->g_pull_async || !b->g_destroy)
+      die("dlsym glint_*");
     int rc = b->g_create(gpu_device, value_code(), start, end, 0, &b->shard);
     if (rc) { fprintf(stderr, "glint_loopback: glint_shard_create failed (%d)\n", rc); exit(3); }
     /* actor start-up (preStart): one push of +0 and one pull, so the first timed message does not pay
@@ -241,9 +245,15 @@ typedef struct {
   int fd;
 } conn_arg;
 
-/* Replies leave a connection in request order. A reply is either ready (its frame is in `out`) or an
- * AcknowledgeReceipt of a push still on the GPU, answered after one wait per drained burst. */
-typedef struct { size_t end; int32_t ack_id; } hold;  /* out[prev end .. end) is ready, then ack_id */
+/* Replies leave a connection in request order. A reply is either ready (its frame is in `out`), an
+ * AcknowledgeReceipt of a push still on the GPU, or the Response of a pull still on the GPU; the
+ * held ones are answered after one wait per drained burst. */
+typedef struct {
+  size_t end;      /* out[prev end .. end) is ready, then this reply */
+  int32_t ack_id;  /* an AcknowledgeReceipt, or */
+  uint8_t* resp;   /* a pull's Response frame (filled by the wait) */
+  size_t resp_len;
+} hold;
 
 static int readable_now(int fd) {
   int avail = 0;
@@ -263,8 +273,9 @@ static void* conn_main(void* p) {
   int32_t* pending = NULL; /* ids of this connection's pushes enqueued on the GPU since the last wait */
   size_t npend = 0, pcap = 0;
   uint64_t last_ticket = 0;
-  hold* holds = NULL;      /* held acks, in reply order */
+  hold* holds = NULL;      /* held replies, in reply order */
   size_t nhold = 0, hcap = 0;
+  int enqueued = 0;        /* GPU work enqueued since the last wait */
   for (;;) {
     const uint32_t len = recv_frame(fd, &buf, &cap);
     if (len == 0) break;
@@ -279,6 +290,7 @@ static void* conn_main(void* p) {
         if (npend == pcap) { pcap = pcap ? 2 * pcap : 64; pending = (int32_t*)realloc(pending, pcap * 4); }
         pending[npend++] = mid;
         last_ticket = ticket;
+        enqueued = 1;
       } else {
         int32_t n;
         memcpy(&n, buf + 1, 4);
@@ -301,8 +313,18 @@ static void* conn_main(void* p) {
       const size_t need = 5 + (size_t)n * 8;
       if (need > rcap) { rcap = need; resp = (uint8_t*)realloc(resp, rcap); }
       size_t olen = 0;
-      if (use_gpu) { /* ordered after every push enqueued on the shard */
-        if (s->b.g_pull_wire(s->b.shard, buf, len, resp, rcap, &olen) != 0) s->errors++;
+      if (use_gpu) { /* enqueued after every push on the shard; its Response is held until the wait */
+        uint8_t* r = (uint8_t*)malloc(need);
+        uint64_t ticket = 0;
+        if (s->b.g_pull_async(s->b.shard, buf, len, r, need, &olen, &ticket) != 0) s->errors++;
+        if (ticket > last_ticket) last_ticket = ticket;
+        enqueued = 1;
+        if (nhold == hcap) { hcap = hcap ? 2 * hcap : 64; holds = (hold*)realloc(holds, hcap * sizeof(hold)); }
+        holds[nhold].end = out.len;
+        holds[nhold].ack_id = 0;
+        holds[nhold].resp = r;
+        holds[nhold].resp_len = olen;
+        ++nhold;
       } else {
         int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
         memcpy(keys, buf + 5, (size_t)n * 8);
@@ -313,8 +335,8 @@ static void* conn_main(void* p) {
         resp[0] = dtype_long ? W_RESP_L : W_RESP_D;
         memcpy(resp + 1, &n, 4);
         olen = need;
+        ob_frame(&out, resp, (uint32_t)olen);
       }
-      ob_frame(&out, resp, (uint32_t)olen);
     } else if (t == L_GET_UID) {
       pthread_mutex_lock(&s->mu);
       const int32_t u = ++s->uid; /* sender ! UniqueID(nextId()) */
@@ -327,6 +349,7 @@ static void* conn_main(void* p) {
         if (nhold == hcap) { hcap = hcap ? 2 * hcap : 64; holds = (hold*)realloc(holds, hcap * sizeof(hold)); }
         holds[nhold].end = out.len;
         holds[nhold].ack_id = id;
+        holds[nhold].resp = NULL;
         ++nhold;
       } else {
         pthread_mutex_lock(&s->mu);
@@ -343,8 +366,8 @@ static void* conn_main(void* p) {
     } else {
       s->errors++;
     }
-    if (!readable_now(fd)) { /* the burst is drained: one wait for the enqueued pushes, then reply */
-      if (npend) {
+    if (!readable_now(fd)) { /* the burst is drained: one wait for the enqueued work, then reply */
+      if (enqueued) {
         const int rc = s->b.g_wait(s->b.shard, last_ticket, NULL);
         pthread_mutex_lock(&s->mu);
         for (size_t i = 0; i < npend; ++i)
@@ -352,6 +375,7 @@ static void* conn_main(void* p) {
         pthread_mutex_unlock(&s->mu);
         if (rc != 0) s->errors++;
         npend = 0;
+        enqueued = 0;
       }
       if (nhold) { /* splice the held acks into the reply stream at their places */
         obuf merged = {0};
@@ -360,7 +384,12 @@ static void* conn_main(void* p) {
         for (size_t i = 0; i < nhold; ++i) {
           ob_put(&merged, out.p + from, holds[i].end - from);
           from = holds[i].end;
-          ob_logic(&merged, receipt_has(s, holds[i].ack_id) ? L_ACK : L_NACK, holds[i].ack_id);
+          if (holds[i].resp) {
+            ob_frame(&merged, holds[i].resp, (uint32_t)holds[i].resp_len);
+            free(holds[i].resp);
+          } else {
+            ob_logic(&merged, receipt_has(s, holds[i].ack_id) ? L_ACK : L_NACK, holds[i].ack_id);
+          }
         }
         pthread_mutex_unlock(&s->mu);
         ob_put(&merged, out.p + from, out.len - from);
