@@ -65,6 +65,83 @@ struct BinCtl {
   u32 nfitems; // fine-partition items (written by bin_part's workgroup 0)
 };
 
+// Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
+// workgroup sums clock64() deltas per phase into g_bin_prof; the product build compiles it away.
+#ifdef GLINT_BIN_PROF
+__device__ unsigned long long g_bin_prof[64];
+struct PhaseClock {  // slots base .. base + 11 of g_bin_prof
+  u64 last, acc[12];
+  int base;
+  __device__ explicit PhaseClock(int b) : last((u64)clock64()), base(b) {
+    for (int i = 0; i < 12; ++i) acc[i] = 0;
+  }
+  __device__ void mark(int slot) {  // scheduling barriers: the clock read stays where it is written
+    __builtin_amdgcn_sched_barrier(0);
+    const u64 t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    if (threadIdx.x == 0) {
+      acc[slot - base] += t - last;
+      last = t;
+    }
+  }
+  __device__ void flush(int n) {
+    if (threadIdx.x != 0) return;
+    for (int i = 0; i < n; ++i) atomicAdd(&g_bin_prof[base + i], acc[i]);
+  }
+};
+#else
+struct PhaseClock {
+  __device__ explicit PhaseClock(int) {}
+  __device__ void mark(int) {}
+  __device__ void flush(int) {}
+};
+#endif
+
+// ---- counted memory operations --------------------------------------------------------------------
+// On gfx9 loads and stores share one counter (vmcnt), and the compiler can keep loads of a later
+// chunk in flight across a wait only if every path issues the same number of memory instructions.
+// So the hot loops have no data-dependent stores: a lane with nothing to store writes through a
+// buffer descriptor at an out-of-range offset, which the buffer unit drops, and rejected records
+// are counted in registers and reported once at the end instead of by an atomic per record.
+typedef u32 v2u32 __attribute__((ext_vector_type(2)));
+struct BufOut {
+  __amdgpu_buffer_rsrc_t r;
+  u32 oob;  // the descriptor's size: a store at this offset is dropped
+};
+// base and bytes must be workgroup-uniform; readfirstlane makes that provable to the compiler, which
+// otherwise wraps every buffer store in a waterfall loop
+__device__ __forceinline__ BufOut buf_out(const void* base, u32 bytes) {
+  const u64 b = (u64)base;
+  const u32 lo = __builtin_amdgcn_readfirstlane((u32)b), hi = __builtin_amdgcn_readfirstlane((u32)(b >> 32));
+  const u32 nb = __builtin_amdgcn_readfirstlane(bytes);
+  void* p = (void*)(((u64)hi << 32) | lo);
+  return BufOut{__builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)nb, 0x00020000), nb};
+}
+template <typename T>
+__device__ __forceinline__ void bput(const BufOut& b, u32 off, bool on, T v) {
+  const int o = (int)(on ? off : b.oob);
+  if constexpr (sizeof(T) == 4) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(u32, v), b.r, o, 0, 0);
+  } else {
+    static_assert(sizeof(T) == 8, "4- or 8-byte stores");
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, v), b.r, o, 0, 0);
+  }
+}
+struct BadRecs {  // this thread's rejected records: the first one and how many
+  i64 first = -1;
+  u32 count = 0;
+  __device__ void add(i64 i) {
+    first = count ? min(first, i) : i;
+    ++count;
+  }
+  __device__ void report(ErrState* err) const {
+    if (count) {
+      atomicMax(&err->min_bad_enc, ~(u64)first);
+      atomicAdd(&err->count, (unsigned long long)count);
+    }
+  }
+};
+
 // ---- block-level helpers ------------------------------------------------------------------------
 // Exclusive scan over N values by one workgroup of TPB threads, in tiles of TPB x PER: each thread
 // loads a run of PER values into registers (all loads in flight together), scans them and calls
@@ -136,17 +213,26 @@ __device__ __forceinline__ u32 chunk_base(u32 w, u32 G, i64 nchunks) {
   return w * q + min(w, r);
 }
 
+// One partition chunk's records, kAPer per thread, in registers. The partition kernels keep two of
+// these in flight (chunks c + G and c + 2G load while chunk c is partitioned): one chunk of loads per
+// workgroup left too little in flight per CU to cover HBM latency.
 template <typename V, bool MAT>
+struct RecRegs {
+  i64 k[kAPer];
+  int32_t cl[kAPer];
+  V v[kAPer];
+};
+
+template <typename V, bool MAT, bool VALS = true>
 __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
-                                          const V* __restrict__ vals, i64 c0, i64 c1, i64 (&k)[kAPer],
-                                          int32_t (&cl)[kAPer], V (&v)[kAPer]) {
+                                          const V* __restrict__ vals, i64 c0, i64 c1, RecRegs<V, MAT>& r) {
 #pragma unroll
   for (int q = 0; q < kAPer; ++q) {  // clamped, branch-free loads
     const i64 i = c0 + q * kATPB + threadIdx.x;
     const i64 ii = i < c1 ? i : c1 - 1;
-    k[q] = keys[ii];
-    cl[q] = MAT ? cols[ii] : 0;
-    if (vals) v[q] = vals[ii];
+    r.k[q] = keys[ii];
+    r.cl[q] = MAT ? cols[ii] : 0;
+    if (VALS) r.v[q] = vals[ii];
   }
 }
 
@@ -164,23 +250,20 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
   __syncthreads();
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
-  i64 k[kAPer];
-  int32_t cl[kAPer];
-  double vdummy[kAPer];  // load_recs reads no values here
-  (void)vdummy;
+  RecRegs<double, MAT> r;  // keys (and cols) only: load_recs reads no values here
   u32 nvalid = 0;
   i64 c = blockIdx.x;
-  if (c < nchunks) load_recs<double, MAT>(keys, cols, nullptr, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), k, cl, vdummy);
+  if (c < nchunks) load_recs<double, MAT, false>(keys, cols, nullptr, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), r);
   for (; c < nchunks; c += gridDim.x) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
     u32 bk[kAPer];
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       i64 ad;
-      bk[q] = (c0 + q * kATPB + tid < c1 && rec_addr<MAT>(part, k[q], cl[q], ad)) ? bucket_of((u32)ad, g) : kEmptySlot;
+      bk[q] = (c0 + q * kATPB + tid < c1 && rec_addr<MAT>(part, r.k[q], r.cl[q], ad)) ? bucket_of((u32)ad, g) : kEmptySlot;
     }
     const i64 cn = c + gridDim.x;  // the next chunk's loads overlap this chunk's histogram
-    if (cn < nchunks) load_recs<double, MAT>(keys, cols, nullptr, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), k, cl, vdummy);
+    if (cn < nchunks) load_recs<double, MAT, false>(keys, cols, nullptr, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       if (bk[q] != kEmptySlot) {
@@ -206,14 +289,15 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
 // ranges: cur[b] = next free slot of bucket b. dcnt and gpos are scratch (dcnt zero on entry/exit).
 template <typename A, int P>
 __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u32 valid, const BinGeom& g,
-                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v,
-                                         u32* __restrict__ addr_out, A* __restrict__ val_out) {
+                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v, const BufOut& oa,
+                                         const BufOut& ov, u32 wbase, PhaseClock& ph, int pb) {
   const int tid = threadIdx.x;
   u32 rank[P];
 #pragma unroll
   for (int j = 0; j < P; ++j)
     if (valid & (1u << j)) rank[j] = atomicAdd(&dcnt[bucket_of(ad[j], g)], 1u);
   __syncthreads();
+  ph.mark(pb);
   const u32 total = block_scan<kATPB, 1>(
       g.nb, [&](u32 d) { return dcnt[d]; },
       [&](u32 d, u32 excl) {
@@ -222,6 +306,7 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
         cur[d] += c;
         dcnt[d] = excl;
       });
+  ph.mark(pb + 1);
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     if (valid & (1u << j)) {
@@ -231,15 +316,28 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
     }
   }
   __syncthreads();
-  for (u32 p = tid; p < total; p += kATPB) {  // consecutive threads: consecutive slots of one run
+  ph.mark(pb + 2);
+  static_assert(P * kATPB == kAChunk, "the store loop covers a whole chunk");
+#pragma unroll
+  for (int j = 0; j < P; ++j) {  // consecutive threads: consecutive slots of one run
+    if ((u32)(j * kATPB) >= total) break;  // workgroup-uniform: no store instructions past the chunk
+    const u32 p = tid + j * kATPB;
+    const bool on = p < total;
     const u32 a = st_a[p];
-    const u32 pos = gpos[bucket_of(a, g)] + p;
-    addr_out[pos] = a;
-    val_out[pos] = st_v[p];
+    const u32 rel = gpos[on ? bucket_of(a, g) : 0u] + p - wbase;  // within this workgroup's range
+#ifdef GLINT_BIN_NOSTORE  // timing experiment only: every partition store dropped
+    bput(oa, rel * 4u, false, a);
+    bput(ov, rel * (u32)sizeof(A), false, st_v[p]);
+#else
+    bput(oa, rel * 4u, on, a);
+    bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
+#endif
   }
   __syncthreads();
+  ph.mark(pb + 3);
   for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
   __syncthreads();
+  ph.mark(pb + 4);
   return total;
 }
 
@@ -293,15 +391,17 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   const u32 w = blockIdx.x;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
+  PhaseClock ph(0);
   if (w == 0) part_items(g, T, fitems, bc);
   part_setup(g, w, nchunks, R, segoff, cur, dcnt);
-  i64 k[kAPer];
-  int32_t cl[kAPer];
-  V v[kAPer];
+  ph.mark(0);
+  const i64 G = gridDim.x;
+  const u32 wbase = chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
+  const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
+  const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
+  BadRecs bad;
   u32 emitted = 0;
-  i64 c = w;
-  if (c < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), k, cl, v);
-  for (; c < nchunks; c += gridDim.x) {
+  auto step = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
     u32 ad[kAPer];
     A va[kAPer];
@@ -311,21 +411,34 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
       const i64 i = c0 + q * kATPB + tid;
       i64 a64;
       ad[q] = 0;
-      va[q] = (A)v[q];
+      va[q] = (A)r.v[q];
       if (i < c1) {
-        if (rec_addr<MAT>(part, k[q], cl[q], a64)) {
+        if (rec_addr<MAT>(part, r.k[q], r.cl[q], a64)) {
           ad[q] = (u32)a64;
           valid |= 1u << q;
         } else {
-          record_error(err, i);
+          bad.add(i);
         }
       }
     }
-    const i64 cn = c + gridDim.x;  // next chunk's loads overlap this chunk's partition
-    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), k, cl, v);
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, addr_out, val_out);
+    ph.mark(1);
+    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 3);
+    // two chunks ahead, into the registers just consumed: in flight across the next chunk's work
+    const i64 cn = c + 2 * G;
+    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
+    ph.mark(2);
+  };
+  RecRegs<V, MAT> ra, rb;
+  i64 c = w;
+  if (c < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), ra);
+  if (c + G < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + (c + G) * kAChunk, min(n, r0 + (c + G + 1) * kAChunk), rb);
+  for (; c < nchunks; c += 2 * G) {
+    step(c, ra);
+    if (c + G < nchunks) step(c + G, rb);
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
+  bad.report(err);
+  ph.flush(8);
 }
 
 // Dedup front end for duplicate-heavy tails: per chunk, equal elements are summed in an LDS hash
@@ -357,16 +470,18 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     hv[sl] = A(0);
   }
   if (tid == 0) nused = 0;
+  PhaseClock ph(8);
   if (w == 0) part_items(g, T, fitems, bc);
   part_setup(g, w, nchunks, R, segoff, cur, dcnt);
+  ph.mark(8);
   const u64 below = (1ull << lane) - 1ull;
-  i64 k[kAPer];
-  int32_t cl[kAPer];
-  V v[kAPer];
+  const i64 G = gridDim.x;
+  const u32 wbase = chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
+  const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
+  const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
+  BadRecs bad;
   u32 emitted = 0;
-  i64 c = w;
-  if (c < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), k, cl, v);
-  for (; c < nchunks; c += gridDim.x) {
+  auto step = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
@@ -375,8 +490,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
       u32 h = 0;
       if (i < c1) {
         i64 a64;
-        if (!rec_addr<MAT>(part, k[q], cl[q], a64)) {
-          record_error(err, i);
+        if (!rec_addr<MAT>(part, r.k[q], r.cl[q], a64)) {
+          bad.add(i);
         } else {
           const u32 a = (u32)a64;
           h = (a * 0x9E3779B1u) >> (32 - 13);
@@ -386,7 +501,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
             if (prev == a) break;
             h = (h + 1) & (kASlots - 1);
           }
-          lds_add(&hv[h], (A)v[q]);
+          lds_add(&hv[h], (A)r.v[q]);
         }
       }
       const u64 b = __ballot(claimed);  // the wave's new slots join the list with one LDS atomic
@@ -397,8 +512,12 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
         if (claimed) used[base + (u32)__popcll(b & below)] = (uint16_t)h;
       }
     }
-    const i64 cn = c + gridDim.x;  // next chunk's loads overlap the append below
-    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), k, cl, v);
+    ph.mark(9);
+    const i64 cn = c + 2 * G;  // two chunks ahead: in flight across this chunk and the next
+#ifndef GLINT_DEDUP_LATE_LOAD
+    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
+#endif
+    ph.mark(10);
     __syncthreads();
     const u32 D = nused;
     u32 ad[kAPer];
@@ -419,7 +538,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     }
     __syncthreads();
     if (tid == 0) nused = 0;
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, addr_out, val_out);
+    ph.mark(11);
+    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 12);
     for (int sl = tid; sl < kStageA; sl += kATPB) hv[sl] = A(0);  // staging overlaid these
 #pragma unroll
     for (int j = 0; j < kAPer; ++j) {  // and the table's own slots of this chunk
@@ -429,9 +549,23 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
         if (sl >= (u32)kStageA) hv[sl] = A(0);
       }
     }
+#ifdef GLINT_DEDUP_LATE_LOAD
+    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
+#endif
     __syncthreads();
+    ph.mark(17);
+  };
+  RecRegs<V, MAT> ra, rb;
+  i64 c = w;
+  if (c < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), ra);
+  if (c + G < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + (c + G) * kAChunk, min(n, r0 + (c + G + 1) * kAChunk), rb);
+  for (; c < nchunks; c += 2 * G) {
+    step(c, ra);
+    if (c + G < nchunks) step(c + G, rb);
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
+  bad.report(err);
+  ph.flush(10);
 }
 
 // ---- fine partition ---------------------------------------------------------------------------------
@@ -440,6 +574,19 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 __device__ __forceinline__ u32 seg_addr(u32 v, u32& s, const u32* segpre, const u32* segst) {
   while (segpre[s + 1] <= v) ++s;
   return segst[s] + (v - segpre[s]);
+}
+
+// the addresses of records [t0, t0 + kFTile) of a bucket (kEmptySlot past v1); s is the thread's
+// segment cursor (its records only move forward)
+// (clamped and branch-free: every lane issues kFPer loads; needs v1 > 0)
+__device__ __forceinline__ void fetch_addr(u32 t0, u32 v1, u32& s, const u32* segpre, const u32* segst,
+                                           const u32* __restrict__ addr_in, u32 (&a)[kFPer]) {
+#pragma unroll
+  for (int q = 0; q < kFPer; ++q) {
+    const u32 v = t0 + q * kFTPB + threadIdx.x;
+    const u32 x = addr_in[seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst)];
+    a[q] = v < v1 ? x : kEmptySlot;
+  }
 }
 
 // bucket b's segment table into LDS; returns M_b
@@ -460,7 +607,8 @@ __device__ __forceinline__ u32 load_segments(const BinGeom& g, u32 G, u32 b, con
 __global__ __launch_bounds__(kFTPB) void bin_fcount_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
                                                            const BinCtl* bc, const u32* __restrict__ segoff,
                                                            const u32* __restrict__ seglen,
-                                                           const u32* __restrict__ addr_in, u32* __restrict__ H) {
+                                                           const u32* __restrict__ addr_in, u32* __restrict__ H,
+                                                           u32* __restrict__ IH) {
   __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
   __shared__ u32 fh[kMaxDigit];
   const int tid = threadIdx.x;
@@ -472,20 +620,23 @@ __global__ __launch_bounds__(kFTPB) void bin_fcount_kernel(BinGeom g, u32 G, con
     const u32 M = load_segments(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
     u32 s = 0;
+    u32 a[kFPer];
+    if (v1 > v0) fetch_addr(v0, v1, s, segpre, segst, addr_in, a);
     for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
-      u32 a[kFPer];
+      u32 cur[kFPer];
 #pragma unroll
-      for (int q = 0; q < kFPer; ++q) {
-        const u32 v = t0 + q * kFTPB + tid;
-        a[q] = v < v1 ? addr_in[seg_addr(v, s, segpre, segst)] : kEmptySlot;
-      }
+      for (int q = 0; q < kFPer; ++q) cur[q] = a[q];
+      fetch_addr(t0 + kFTile, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
 #pragma unroll
       for (int q = 0; q < kFPer; ++q)
-        if (a[q] != kEmptySlot) atomicAdd(&fh[fine_of(a[q], g)], 1u);
+        if (cur[q] != kEmptySlot) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
     }
     __syncthreads();
-    for (u32 f = tid; f < g.nf; f += kFTPB)
-      if (fh[f]) atomicAdd(&H[b * g.nf + f], fh[f]);
+    for (u32 f = tid; f < g.nf; f += kFTPB) {
+      const u32 c = fh[f];
+      IH[(size_t)it * g.nf + f] = c;  // this item's own histogram: bin_fpart reserves from it
+      if (c) atomicAdd(&H[b * g.nf + f], c);
+    }
     __syncthreads();
   }
 }
@@ -503,7 +654,7 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
                                                           const u32* __restrict__ addr_in,
                                                           const A* __restrict__ val_in, u32* __restrict__ addr_out,
                                                           A* __restrict__ val_out, uint4* __restrict__ cdesc,
-                                                          u64* hint) {
+                                                          u64* hint, const u32* __restrict__ IH) {
   __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
   __shared__ u32 sst[kMaxDigit], fcur[kMaxDigit], tcnt[kMaxDigit], tpos[kMaxDigit];
   __shared__ u32 st_a[kFTile];
@@ -512,6 +663,7 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
   if (blockIdx.x == 0 && tid == 0 && hint)  // for the host's next binned push: how much did dedup keep?
     __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const u32 nit = bc->nfitems;
+  PhaseClock ph(20);
   for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
     const uint2 d = fitems[it];
     const u32 b = d.x;
@@ -526,6 +678,7 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
     ib = block_sum<kFTPB>(ib);
     for (u32 f = tid; f < g.nf; f += kFTPB) tcnt[f] = 0;
     block_scan<kFTPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
+    ph.mark(20);
     if (d.y == 0) {  // the bucket's apply items {slab, first, end, exclusive}, then unused slots
       const u32 nslots = g.nf + (T[b] + kCItem - 1) / kCItem;
       if (b == g.nb - 1 && tid == 0) bc->nslots = ib + nslots;  // bin_apply's item count
@@ -540,49 +693,52 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
           });
       for (u32 x = used_slots + tid; x < nslots; x += kFTPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
     }
+    ph.mark(21);
     const u32 M = load_segments(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
-    // pass 1: this item's records per slab; reserve the item's share of each slab
-    {
-      u32 s = 0;
-      for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
-        u32 a[kFPer];
-#pragma unroll
-        for (int q = 0; q < kFPer; ++q) {
-          const u32 v = t0 + q * kFTPB + tid;
-          a[q] = v < v1 ? addr_in[seg_addr(v, s, segpre, segst)] : kEmptySlot;
-        }
-#pragma unroll
-        for (int q = 0; q < kFPer; ++q)
-          if (a[q] != kEmptySlot) atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
-      }
-    }
+    ph.mark(22);
+    // this item's records per slab (counted by bin_fcount); reserve the item's share of each slab
     __syncthreads();
+    ph.mark(23);
     for (u32 f = tid; f < g.nf; f += kFTPB) {
-      const u32 c = tcnt[f];
+      const u32 c = IH[(size_t)it * g.nf + f];
       fcur[f] = c ? sst[f] + atomicAdd(&cur2[b * g.nf + f], c) : 0u;
       tcnt[f] = 0;
     }
     __syncthreads();
+    ph.mark(24);
     // pass 2: tiles moved to their slab ranges
     u32 s = 0;
+    u32 na[kFPer];
+    A nv[kFPer];
+    auto fetch = [&](u32 t0) {  // a tile's addresses and values (clamped, branch-free)
+#pragma unroll
+      for (int q = 0; q < kFPer; ++q) {
+        const u32 v = t0 + q * kFTPB + tid;
+        const u32 r = seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst);
+        const u32 x = addr_in[r];
+        nv[q] = val_in[r];
+        na[q] = v < v1 ? x : kEmptySlot;
+      }
+    };
+    // the bucket's output range as buffer descriptors (counted stores)
+    const BufOut oa = buf_out(addr_out + ob, T[b] * 4u), ov = buf_out(val_out + ob, T[b] * (u32)sizeof(A));
+    if (v1 > v0) fetch(v0);
     for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
       u32 a[kFPer], rank[kFPer];
       A val[kFPer];
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
-        const u32 v = t0 + q * kFTPB + tid;
-        a[q] = kEmptySlot;
-        if (v < v1) {
-          const u32 r = seg_addr(v, s, segpre, segst);
-          a[q] = addr_in[r];
-          val[q] = val_in[r];
-        }
+        a[q] = na[q];
+        val[q] = nv[q];
       }
+      fetch(t0 + kFTile);  // the next tile, in flight during this one's ranking, scan and stores
+      ph.mark(25);
 #pragma unroll
       for (int q = 0; q < kFPer; ++q)
         if (a[q] != kEmptySlot) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
       __syncthreads();
+      ph.mark(26);
       const u32 total = block_scan<kFTPB, 4>(
           g.nf, [&](u32 f) { return tcnt[f]; },
           [&](u32 f, u32 excl) {
@@ -590,6 +746,7 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
             fcur[f] += tcnt[f];
             tcnt[f] = excl;
           });
+      ph.mark(27);
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
         if (a[q] != kEmptySlot) {
@@ -599,17 +756,25 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
         }
       }
       __syncthreads();
-      for (u32 p = tid; p < total; p += kFTPB) {
+      ph.mark(28);
+#pragma unroll
+      for (int j = 0; j < kFPer; ++j) {  // total <= kFTile
+        if ((u32)(j * kFTPB) >= total) break;  // workgroup-uniform: no store instructions past the tile
+        const u32 p = tid + j * kFTPB;
+        const bool on = p < total;
         const u32 x = st_a[p];
-        const u32 pos = tpos[fine_of(x, g)] + p;
-        addr_out[pos] = x;
-        val_out[pos] = st_v[p];
+        const u32 rel = tpos[on ? fine_of(x, g) : 0u] + p - ob;
+        bput(oa, rel * 4u, on, x);
+        bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
       }
       __syncthreads();
+      ph.mark(29);
       for (u32 f = tid; f < g.nf; f += kFTPB) tcnt[f] = 0;
       __syncthreads();
+      ph.mark(30);
     }
   }
+  ph.flush(11);
 }
 
 // ---- slab apply ----------------------------------------------------------------------------------------
@@ -655,6 +820,12 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
   u32 pa[kCRB];
   A pv[kCRB];
   apply_fetch<A>(nd, addr, val, pa, pv);
+  // acc and touched are zero between items: cleared once here, then by each item's write-back as it
+  // reads them (no clearing pass and no barrier for it per item)
+  for (int e = tid; e < kSlab; e += kCTPB) acc[e] = A(0);
+  for (int w = tid; w < kSlab / 16; w += kCTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  PhaseClock ph(40);
   for (; it < nslots; it += gridDim.x) {
     const uint4 d4 = nd;
     u32 ca[kCRB];
@@ -684,9 +855,8 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
       for (int l = tid; l < kLines; l += kCTPB)
         if (sbase_g + (i64)l * kPerLine < elems) warm ^= *reinterpret_cast<const u32*>(sbase + (i64)l * kPerLine);
     }
-    for (int e = tid; e < kSlab; e += kCTPB) acc[e] = A(0);
-    for (int w = tid; w < kSlab / 16; w += kCTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
+    ph.mark(40);
+    ph.mark(41);
     for (u32 j0 = r_lo;;) {  // the first batch came with the prefetch
 #pragma unroll
       for (int q = 0; q < kCRB; ++q) {
@@ -700,7 +870,9 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
       apply_fetch<A>(make_uint4(0u, j0, r_hi, 0u), addr, val, ca, cv);
     }
     asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
+    ph.mark(42);
     __syncthreads();
+    ph.mark(43);
     apply_fetch<A>(nd, addr, val, pa, pv);  // the next item's first batch: in flight during the RMW
     if (exclusive) {
       // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair instead
@@ -713,6 +885,7 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
         t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
         const bool vec = t[q] != 0u && sbase_g + e0 + 1 < elems;
         dd[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
+        if (t[q]) *reinterpret_cast<uint16_t*>(touched + e0) = 0;
       }
 #pragma unroll
       for (int q = 0; q < kPairsPerThread; ++q) {
@@ -726,13 +899,23 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
         } else {  // the shard's last element, odd count
           sbase[e0] = acc_add(sbase[e0], acc[e0]);
         }
+        acc[e0] = A(0);
+        acc[e0 + 1] = A(0);
       }
     } else {
-      for (int e = tid; e < kSlab; e += kCTPB)
-        if (touched[e]) gadd(sbase + e, (V)acc[e]);
+      for (int e = tid; e < kSlab; e += kCTPB) {
+        if (touched[e]) {
+          gadd(sbase + e, (V)acc[e]);
+          acc[e] = A(0);
+          touched[e] = 0;
+        }
+      }
     }
+    ph.mark(44);
     __syncthreads();
+    ph.mark(45);
   }
+  ph.flush(6);
 }
 
 // ---- host side ----------------------------------------------------------------------------------------
@@ -791,7 +974,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // [BinCtl | T | H | cur2] zeroed per push; then R, segoff, seglen, item maps, the record buffers
   const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
   const size_t b_H = pad256((size_t)g.nslab * 4);
-  const size_t b_cd = pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8);
+  const size_t b_cd = pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8) +
+                      pad256((size_t)max_fitems * g.nf * 4);  // + per-item slab histograms
   const size_t cap_a = (size_t)nchunks_max * kAChunk;  // the partition's capacity (every chunk full)
   const size_t b_a = pad256(cap_a * 4), b_v = pad256(cap_a * sizeof(A));
   const size_t b_zero = b_ctl + b_T + 2 * b_H;
@@ -810,6 +994,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   p += 3 * b_seg;
   uint4* cdesc = (uint4*)p;
   uint2* fitems = (uint2*)(p + pad256((size_t)nslots * 16));
+  u32* IH = (u32*)(p + pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8));
   p += b_cd;
   u32* addr_a = (u32*)p;
   A* val_a = (A*)(p + b_a);
@@ -830,10 +1015,10 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   }
   HIPCHK(hipGetLastError());
   const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * 4);
-  bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H);
+  bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
   bin_fpart_kernel<A><<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
-                                            val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr);
+                                            val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
   HIPCHK(hipGetLastError());
   static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
     const char* e = getenv("GLINT_BIN_APPLY_BPC");
@@ -857,3 +1042,15 @@ GLINT_INST(double, true)
 #undef GLINT_INST
 
 }  // namespace glint
+
+#ifdef GLINT_BIN_PROF
+// tuning build only: the summed phase clocks (and reset)
+extern "C" int glint_debug_bin_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(glint::g_bin_prof), sizeof(glint::g_bin_prof)) != hipSuccess) return 1;
+  if (reset) {
+    static unsigned long long z[64] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(glint::g_bin_prof), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

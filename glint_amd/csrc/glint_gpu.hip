@@ -737,10 +737,11 @@ void free_shard(glint_shard* s) {
     for (auto& r : s->ring) {
       if (r.h) (void)hipHostFree(r.h);
       if (r.d) (void)hipFree(r.d);
-        if (r.herr) (void)hipHostFree(r.herr);
+      if (r.herr) (void)hipHostFree(r.herr);
       if (r.done) (void)hipEventDestroy(r.done);
     }
     if (s->h_done) (void)hipHostFree(s->h_done);
+    if (s->host_ev) (void)hipEventDestroy(s->host_ev);
     (void)hipGetLastError();
   }
   delete s;
@@ -775,6 +776,11 @@ uint8_t wire_response_type(int dtype) {
     default: return W_RESP_L;
   }
 }
+
+// defined with the ring below: device-resident calls are ordered after the ring's entries
+int dev_order_after_host(glint_shard* s, hipStream_t st);
+int ring_flush_locked(glint_shard* s);
+int ring_retire_through(glint_shard* s, u64 t);
 
 }  // namespace
 
@@ -851,12 +857,18 @@ int glint_shard_zero(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
-  int rc = order_after_dev(s);
+  int rc = ring_flush_locked(s);  // the restart comes after every message enqueued before it
+  if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(s->data, 0, (size_t)s->elems * s->vsize, s->stream));
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
-  return GLINT_OK;
+  rc = ring_retire_through(s, s->ticket_next);  // all complete: pulls get their answers
+  s->ring_bad = -1;  // a fresh shard: nothing before the restart is reported any more
+  s->reported_enc = 0;
+  s->clear_ticket = s->ticket_next;
+  s->host_pending = false;
+  return rc;
 }
 
 int glint_shard_info(glint_shard_t s, int32_t* size, int32_t* cols, int* dtype, int* device) {
@@ -928,6 +940,7 @@ int glint_vec_push_dev(glint_shard_t s, const int64_t* keys, const void* vals, i
   if (s->part.cols != 0) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)keys, nullptr, vals, n, flags, pick(s, stream));
 }
 
@@ -937,6 +950,7 @@ int glint_mat_push_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
   if (s->part.cols == 0) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
 }
 
@@ -945,6 +959,7 @@ int glint_vec_pull_dev(glint_shard_t s, const int64_t* keys, void* out, int64_t 
   if (s->part.cols != 0) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)keys, out, n, pick(s, stream));
 }
 
@@ -954,6 +969,7 @@ int glint_mat_pull_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
   if (s->part.cols == 0) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, launch_mat_pull, s, (const i64*)rows, cols, out, n, pick(s, stream));
 }
 
@@ -962,6 +978,7 @@ int glint_mat_pull_rows_dev(glint_shard_t s, const int64_t* rows, void* out, int
   if (s->part.cols == 0) return GLINT_EINVAL;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, launch_mat_pull_rows, s, (const i64*)rows, out, n, pick(s, stream));
 }
 
@@ -1063,8 +1080,8 @@ int wait_done(glint_shard* s, u64 ticket) {
   return __atomic_load_n(s->h_done, __ATOMIC_ACQUIRE) >= ticket ? GLINT_OK : GLINT_EDEVICE;
 }
 
-// Retires a slot: waits for its entry, remembers the first error it saw that was not reported yet,
-// and hands an async pull its answer.
+// Retires a slot: waits for its entry, remembers the first error it saw that was not reported yet
+// (and which message it belongs to), and hands an async pull its answer.
 int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   if (!r.inflight) return GLINT_OK;
   if (r.sig) {
@@ -1079,7 +1096,15 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   const u64 enc = __atomic_load_n(&r.herr->min_bad_enc, __ATOMIC_ACQUIRE);
   const bool stale = r.ticket <= s->clear_ticket && enc == s->reported_enc;
   if (enc != 0 && !stale && s->ring_bad < 0) {
-    s->ring_bad = (i64)~enc;
+    const i64 idx = (i64)~enc;  // a record index within this entry (a batch: within the batch)
+    s->ring_bad = idx;
+    s->ring_bad_ticket = r.msgs.empty() ? r.ticket : r.msgs.front().ticket;
+    for (const auto& m : r.msgs)
+      if (idx >= m.off && idx < m.off + m.n) {
+        s->ring_bad = idx - m.off;
+        s->ring_bad_ticket = m.ticket;
+        break;
+      }
     s->ring_bad_enc = enc;
   }
   if (r.out) {
@@ -1089,8 +1114,21 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   return GLINT_OK;
 }
 
+// Retires, oldest first, every in-flight entry that covers a ticket <= t (errors then belong to
+// the earliest message that saw them).
+int ring_retire_through(glint_shard* s, u64 t) {
+  for (;;) {
+    glint_shard::RingSlot* next = nullptr;
+    for (auto& r : s->ring)
+      if (r.inflight && r.ticket_lo <= t && (!next || r.ticket_lo < next->ticket_lo)) next = &r;
+    if (!next) return GLINT_OK;
+    const int rc = ring_retire(s, *next);
+    if (rc) return rc;
+  }
+}
+
 // Hands out a free slot sized for n records (and, for a pull, an answer of out_bytes behind the
-// key sections). Retires the slot's previous entry first.
+// key sections). Retires the slot's previous entry (and every older one) first.
 int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) {
   if (n < 0 || n > kRingMaxRecords) return GLINT_EINVAL;
   const StageLayout L = stage_layout(s, n);
@@ -1109,9 +1147,11 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
     const int idx = s->ring_next;
     s->ring_next = (idx + 1) % GLINT_RING_SLOTS;
     glint_shard::RingSlot& r = s->ring[idx];
-    if (r.acquired) continue;  // handed out and not pushed yet
-    int rc = ring_retire(s, r);
-    if (rc) return rc;
+    if (r.acquired) continue;  // handed out (or an open batch) and not launched yet
+    if (r.inflight) {
+      const int rc = ring_retire_through(s, r.ticket_lo);
+      if (rc) return rc;
+    }
     if (r.hcap < need) {
       if (r.h) (void)hipHostFree(r.h);
       r.h = r.hd = nullptr;
@@ -1136,7 +1176,7 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
       if (hipHostMalloc((void**)&r.herr, sizeof(ErrState), hipHostMallocMapped) != hipSuccess ||
           hipHostGetDevicePointer((void**)&r.herr_d, r.herr, 0) != hipSuccess) {
         (void)hipGetLastError();
-        if (r.herr) (void)hipHostFree(r.herr);
+      if (r.herr) (void)hipHostFree(r.herr);
         r.herr = r.herr_d = nullptr;
         return GLINT_ENOMEM;
       }
@@ -1145,6 +1185,8 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
     r.n = n;
     r.cap_need = need;
     r.out = nullptr;
+    r.fill = 0;
+    r.msgs.clear();
     *slot = idx;
     return GLINT_OK;
   }
@@ -1154,42 +1196,118 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
 // whether an entry of n records is one signalling launch reading (and answering) in the mapped slot
 inline bool ring_direct(const glint_shard* s, i64 n) { return n <= GLINT_ZERO_COPY_MAX && s->elems < ((i64)1 << 32); }
 
-// Runs `launch` (the entry's kernels on s->stream) for slot r: a direct entry is one workgroup that
-// signals its ticket itself; any other entry ends with an error-state copy and an event.
+// Runs `launch` (the entry's kernels on s->stream) for slot r, covering tickets [lo, hi]: a direct
+// entry is one workgroup that signals hi itself; any other entry ends with an error-state copy and
+// an event.
 template <typename F>
-int ring_dispatch(glint_shard* s, glint_shard::RingSlot& r, bool direct, F launch) {
-  const u64 ticket = s->ticket_next + 1;
-  if (direct) s->sig = MsgSig{s->d_done, ticket, r.herr_d};
+int ring_dispatch(glint_shard* s, glint_shard::RingSlot& r, bool direct, u64 lo, u64 hi, F launch) {
+  if (direct) s->sig = MsgSig{s->d_done, hi, r.herr_d};
   const int rc = launch();
   s->sig = MsgSig{nullptr, 0, nullptr};
   if (rc) {
     (void)hipStreamSynchronize(s->stream);
     r.acquired = false;
     r.out = nullptr;
+    r.msgs.clear();
     return rc;
   }
   if (!direct) {
     HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipEventRecord(r.done, s->stream));
   }
-  s->ticket_next = ticket;
-  r.ticket = ticket;
+  r.ticket_lo = lo;
+  r.ticket = hi;
   r.sig = direct;
   r.inflight = true;
   r.acquired = false;
+  s->host_pending = true;
   return GLINT_OK;
 }
 
-// Enqueues the push staged in slot idx. Message-sized pushes are read by the kernel from the mapped
-// pinned slot itself (no copy command in the stream); larger ones are copied with one DMA first.
+// ---- message coalescing -------------------------------------------------------------------------
+// Consecutive message-sized pushes with the same flags are appended to one open ring slot and go to
+// the GPU as ONE single-workgroup ordered push when the slot is full or anything else needs the
+// stream (another entry, a wait, a device call). The fold runs over the concatenation in arrival
+// order -- each message applied after the one before it, the actor's own sequence -- so results
+// are those of one launch per message. Every message keeps its ticket; the launch signals the last.
+constexpr i64 kBatchMax = GLINT_ZERO_COPY_MAX;
+
+int launch_push_entry(glint_shard* s, glint_shard::RingSlot& r, const char* base, const StageLayout& L, i64 n,
+                      int flags, bool direct, u64 lo, u64 hi) {
+  const bool mat = s->part.cols != 0;
+  const i64* keys = (const i64*)base;
+  const int32_t* cols = mat ? (const int32_t*)(base + L.kb) : nullptr;
+  const void* vals = base + L.kb + L.cb;
+  const int hflags = flags | kPushHostSequential;  // the actor's update: message order by default
+  return ring_dispatch(s, r, direct && n > 0, lo, hi, [&]() -> int {
+    if (n == 0) return GLINT_OK;
+    if (mat) {
+      GLINT_DISPATCH(s->dtype, push_mat_t, s, keys, cols, vals, n, hflags, s->stream);
+    }
+    GLINT_DISPATCH(s->dtype, push_vec_t, s, keys, nullptr, vals, n, hflags, s->stream);
+  });
+}
+
+// launches the open batch, if any
+int ring_flush_locked(glint_shard* s) {
+  if (s->open_slot < 0) return GLINT_OK;
+  glint_shard::RingSlot& r = s->ring[s->open_slot];
+  s->open_slot = -1;
+  int rc = order_after_dev(s);
+  if (rc) {
+    r.acquired = false;
+    r.msgs.clear();
+    return rc;
+  }
+  return launch_push_entry(s, r, r.hd, stage_layout(s, kBatchMax), r.fill, s->open_flags, true,
+                           r.msgs.front().ticket, r.msgs.back().ticket);
+}
+
+inline bool batchable(const glint_shard* s, i64 n) { return n > 0 && n <= kBatchMax && s->elems < ((i64)1 << 32); }
+
+// Appends one message-sized push (sections: keys, cols for matrices, values; any alignment) to the
+// open batch, opening one if needed; *ticket = the message's own ticket.
+int ring_append_locked(glint_shard* s, i64 n, int flags, const void* k, const void* c, const void* v, u64* ticket) {
+  int rc;
+  if (s->open_slot >= 0 && (flags != s->open_flags || s->ring[s->open_slot].fill + n > kBatchMax)) {
+    rc = ring_flush_locked(s);
+    if (rc) return rc;
+  }
+  if (s->open_slot < 0) {
+    int slot = -1;
+    rc = ring_acquire_locked(s, kBatchMax, &slot);
+    if (rc) return rc;
+    s->open_slot = slot;
+    s->open_flags = flags;
+  }
+  glint_shard::RingSlot& r = s->ring[s->open_slot];
+  const StageLayout L = stage_layout(s, kBatchMax);
+  std::memcpy(r.h + (size_t)r.fill * 8, k, (size_t)n * 8);
+  if (s->part.cols != 0) std::memcpy(r.h + L.kb + (size_t)r.fill * 4, c, (size_t)n * 4);
+  std::memcpy(r.h + L.kb + L.cb + (size_t)r.fill * s->vsize, v, (size_t)n * s->vsize);
+  const u64 t = ++s->ticket_next;
+  r.msgs.push_back({r.fill, n, t});
+  r.fill += n;
+  if (ticket) *ticket = t;
+  if (r.fill == kBatchMax) return ring_flush_locked(s);
+  return GLINT_OK;
+}
+
+// Enqueues the push staged in slot idx. Message-sized pushes join the open batch (one copy inside
+// pinned memory); larger ones are copied to the device with one DMA and launched at once.
 int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
-  if (idx < 0 || idx >= GLINT_RING_SLOTS) return GLINT_EINVAL;
+  if (idx < 0 || idx >= GLINT_RING_SLOTS || idx == s->open_slot) return GLINT_EINVAL;
   glint_shard::RingSlot& r = s->ring[idx];
   if (!r.acquired || n < 0 || n > r.n) return GLINT_EINVAL;
-  int rc = order_after_dev(s);
-  if (rc) return rc;
   const StageLayout L = stage_layout(s, r.n);  // the sections as handed out
-  const bool mat = s->part.cols != 0;
+  if (batchable(s, n)) {
+    r.acquired = false;  // the records move to the batch; the slot is free again
+    return ring_append_locked(s, n, flags, r.h, r.h + L.kb, r.h + L.kb + L.cb, ticket);
+  }
+  int rc = ring_flush_locked(s);
+  if (rc) return rc;
+  rc = order_after_dev(s);
+  if (rc) return rc;
   const bool direct = ring_direct(s, n);
   const char* base = r.hd;
   if (!direct) {
@@ -1198,19 +1316,11 @@ int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
     HIPCHK(hipMemcpyAsync(r.d, r.h, L.total, hipMemcpyHostToDevice, s->stream));
     base = r.d;
   }
-  const i64* keys = (const i64*)base;
-  const int32_t* cols = mat ? (const int32_t*)(base + L.kb) : nullptr;
-  const void* vals = base + L.kb + L.cb;
-  const int hflags = flags | kPushHostSequential;  // the actor's update: message order by default
-  rc = ring_dispatch(s, r, direct && n > 0, [&]() -> int {
-    if (n == 0) return GLINT_OK;
-    if (mat) {
-      GLINT_DISPATCH(s->dtype, push_mat_t, s, keys, cols, vals, n, hflags, s->stream);
-    }
-    GLINT_DISPATCH(s->dtype, push_vec_t, s, keys, nullptr, vals, n, hflags, s->stream);
-  });
+  const u64 t = ++s->ticket_next;
+  r.msgs.assign(1, glint_shard::RingSlot::Msg{0, n, t});
+  rc = launch_push_entry(s, r, base, L, n, flags, direct, t, t);
   if (rc) return rc;
-  if (ticket) *ticket = r.ticket;
+  if (ticket) *ticket = t;
   return GLINT_OK;
 }
 
@@ -1219,7 +1329,8 @@ int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
 // retires (glint_shard_wait, or the slot's reuse).
 int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t out_bytes, u64* ticket) {
   glint_shard::RingSlot& r = s->ring[idx];
-  int rc = order_after_dev(s);
+  int rc = ring_flush_locked(s);  // the pull sees every push enqueued before it
+  if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) {
     r.acquired = false;
     return rc;
@@ -1243,7 +1354,9 @@ int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t
   r.out = out;
   r.out_bytes = out_bytes;
   r.out_off = L.kb + L.cb;
-  rc = ring_dispatch(s, r, direct, [&]() -> int {
+  const u64 t = ++s->ticket_next;
+  r.msgs.assign(1, glint_shard::RingSlot::Msg{0, n, t});
+  rc = ring_dispatch(s, r, direct, t, t, [&]() -> int {
     int e;
     if (kind == 0) {
       e = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, keys, ans, n, s->stream); }();
@@ -1258,17 +1371,18 @@ int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t
                : GLINT_EDEVICE;
   });
   if (rc) return rc;
-  if (ticket) *ticket = r.ticket;
+  if (ticket) *ticket = t;
   return GLINT_OK;
 }
 
 int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
-  for (auto& r : s->ring)
-    if (r.inflight && r.ticket <= ticket) {
-      int rc = ring_retire(s, r);
-      if (rc) return rc;
-    }
-  if (s->ring_bad < 0) return GLINT_OK;
+  if (s->open_slot >= 0 && s->ring[s->open_slot].msgs.front().ticket <= ticket) {
+    const int rc = ring_flush_locked(s);
+    if (rc) return rc;
+  }
+  int rc = ring_retire_through(s, ticket);
+  if (rc) return rc;
+  if (s->ring_bad < 0 || s->ring_bad_ticket > ticket) return GLINT_OK;  // a later message's error waits
   s->last_bad = s->ring_bad;
   if (first_bad) *first_bad = s->ring_bad;
   s->ring_bad = -1;
@@ -1276,6 +1390,23 @@ int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
   s->clear_ticket = s->ticket_next;  // entries up to here were enqueued before the clear
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   return GLINT_EOUTOFRANGE;
+}
+
+// A device-resident call runs on the caller's stream: it first waits for the ring entries enqueued
+// on the shard's stream (they share the data array and the error state).
+int dev_order_after_host(glint_shard* s, hipStream_t st) {
+  int rc = ring_flush_locked(s);
+  if (rc) return rc;
+  if (!s->host_pending) return GLINT_OK;
+  if (!s->host_ev && hipEventCreateWithFlags(&s->host_ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    s->host_ev = nullptr;
+    return GLINT_EDEVICE;
+  }
+  HIPCHK(hipEventRecord(s->host_ev, s->stream));
+  HIPCHK(hipStreamWaitEvent(st, s->host_ev, 0));
+  s->host_pending = false;
+  return GLINT_OK;
 }
 
 // pull answer bytes: n values, or n rows of cols values
@@ -1307,20 +1438,14 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
   DeviceGuard g(s->device);
   int rc = order_after_dev(s);
   if (rc) return rc;
-  if (n <= GLINT_ZERO_COPY_MAX) {  // Akka-sized: one pinned slot, read in place by the kernel, then wait
-    int slot = -1;
-    rc = ring_acquire_locked(s, n, &slot);
-    if (rc) return rc;
-    glint_shard::RingSlot& r = s->ring[slot];
-    const StageLayout L = stage_layout(s, n);
-    std::memcpy(r.h, keys, (size_t)n * 8);
-    if (mat) std::memcpy(r.h + L.kb, cols, (size_t)n * 4);
-    std::memcpy(r.h + L.kb + L.cb, vals, (size_t)n * s->vsize);
+  if (batchable(s, n)) {  // Akka-sized: into the open batch (read in place by the kernel), then wait
     u64 ticket = 0;
-    rc = ring_push_locked(s, slot, n, flags, &ticket);
+    rc = ring_append_locked(s, n, flags, keys, cols, vals, &ticket);
     if (rc) return rc;
     return ring_wait_locked(s, ticket, nullptr);
   }
+  rc = ring_flush_locked(s);
+  if (rc) return rc;
   Staged st;
   const void* src[3] = {keys, mat ? (const void*)cols : vals, vals};
   size_t bytes[3] = {(size_t)n * 8, mat ? (size_t)n * 4 : (size_t)n * s->vsize, (size_t)n * s->vsize};
@@ -1351,7 +1476,8 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   if (n == 0) return GLINT_OK;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
-  int rc = order_after_dev(s);
+  int rc = ring_flush_locked(s);
+  if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) return rc;
   if (n <= GLINT_ZERO_COPY_MAX) {
     // Akka-sized: one workgroup reads the keys from a mapped pinned ring slot, writes the answer into
@@ -1480,12 +1606,15 @@ int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, i
   if (id) *id = mid;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
+  const uint8_t* kp = payload + 9;  // unaligned sections, copied as they lie
+  if (batchable(s, n))
+    return ring_append_locked(s, n, flags, kp, kp + (size_t)n * 8, kp + (size_t)n * (8 + (mat ? 4 : 0)),
+                              (u64*)ticket);
   int slot = -1;
   int rc = ring_acquire_locked(s, n, &slot);
   if (rc) return rc;
   glint_shard::RingSlot& r = s->ring[slot];
   const StageLayout L = stage_layout(s, n);
-  const uint8_t* kp = payload + 9;  // unaligned sections, copied as they lie
   std::memcpy(r.h, kp, (size_t)n * 8);
   if (mat) std::memcpy(r.h + L.kb, kp + (size_t)n * 8, (size_t)n * 4);
   std::memcpy(r.h + L.kb + L.cb, kp + (size_t)n * (8 + (mat ? 4 : 0)), (size_t)n * s->vsize);

@@ -63,7 +63,19 @@ struct glint_shard {
     size_t out_bytes = 0, out_off = 0;
     bool inflight = false, acquired = false;
     bool sig = false;           // one-workgroup launch that signals through h_done (no event)
+    uint64_t ticket_lo = 0;     // first ticket the entry covers (a coalesced batch covers several)
+    struct Msg {
+      int64_t off, n;
+      uint64_t ticket;
+    };
+    std::vector<Msg> msgs;      // the messages of this entry, for error attribution
+    int64_t fill = 0;           // records appended to an open batch
   } ring[GLINT_RING_SLOTS];
+  int open_slot = -1;     // the batch that message-sized pushes are appended to, not launched yet
+  int open_flags = 0;
+  uint64_t ring_bad_ticket = 0;  // the message the unreported error belongs to
+  bool host_pending = false;     // ring entries enqueued on `stream` since a device call last waited for them
+  hipEvent_t host_ev = nullptr;
   u64* h_done = nullptr;  // host-mapped: ticket of the last completed signalling launch
   u64* d_done = nullptr;
   MsgSig sig{};           // set only while a ring entry dispatches its one launch

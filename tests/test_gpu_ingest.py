@@ -189,3 +189,61 @@ def test_async_pull_bad_key_and_wire(gpu):
         t0, empty = sh.pull_async(np.zeros(0, np.int64))
         sh.wait(t0)
         assert empty.size == 0
+
+
+def test_coalesced_batch_attributes_errors_to_their_message(gpu):
+    """Message-sized pushes are coalesced into one launch; a rejected record is still reported as
+    record i of ITS message, and only by a wait that covers that message."""
+    size = 5000
+    rng = np.random.default_rng(77)
+    ref = O.OracleVector(O.part_range(0, size), O.O_F64)
+    with PartialVector(RangePartition(0, 0, size), "double", gpu) as sh:
+        tickets = []
+        for m in range(6):
+            keys = rng.integers(0, size, 300).astype(np.int64)
+            vals = rng.uniform(-1, 1, 300)
+            if m == 3:
+                keys[7] = size + 1  # out of the partition: record 7 of message 3
+                ok = np.ones(300, bool)
+                ok[7] = False
+                ref.update(keys[ok], vals[ok])
+            else:
+                ref.update(keys, vals)
+            tickets.append(sh.push_async(keys, vals))
+        sh.wait(tickets[2])  # messages 0..2 are clean
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.wait(tickets[5])
+        assert ei.value.record == 7
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+def test_coalescing_keeps_order_across_flags_pulls_and_device_calls(gpu):
+    """Batches break on a flag change, a pull or a device-resident call; every call still sees the
+    pushes enqueued before it, and the Double sums keep the message order bit for bit."""
+    import torch
+    size = 3000
+    rng = np.random.default_rng(78)
+    ref = O.OracleVector(O.part_range(0, size), O.O_F64)
+    dev = torch.device("cuda", gpu)
+    with PartialVector(RangePartition(0, 0, size), "double", gpu) as sh:
+        want, got = [], []
+        for step in range(40):
+            keys = np.minimum(rng.zipf(1.5, 200) - 1, size - 1).astype(np.int64)
+            vals = rng.uniform(-1, 1, 200) * 10.0 ** rng.integers(-8, 8, 200)
+            if step % 10 == 9:  # a device-resident push on the caller's stream, no sync
+                sh.update(torch.from_numpy(keys).to(dev), torch.from_numpy(vals).to(dev), sync=False,
+                          deterministic=True)
+                ref.update(keys, vals)
+            elif step % 7 == 6:
+                t, out = sh.pull_async(keys)
+                got.append(out)
+                want.append(ref.data[keys].copy())
+            else:  # DETERMINISTIC on every 5th: another flags value, so the batch breaks there
+                sh.push_async(keys, vals, deterministic=(step % 5 == 4))
+                ref.update(keys, vals)
+        sh.sync()
+        t, final = sh.pull_async(np.arange(size, dtype=np.int64))
+        sh.wait(t)
+        np.testing.assert_array_equal(final, ref.data)
+        for w, g in zip(want, got):
+            np.testing.assert_array_equal(g, w)

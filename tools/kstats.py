@@ -1,20 +1,21 @@
-"""Print a rocprofv3 kernel summary (name, calls, avg us, total %) from its rocpd SQLite output or
-its *_kernel_stats.csv.   python tools/kstats.py <results.db | kernel_stats.csv> [name-width]"""
+"""Per-kernel average durations from rocprofv3 --stats directories.
+
+    python tools/kstats.py gpurun_out/bin5/zipf_trace [more dirs]
+"""
 import csv
-import sqlite3
+import glob
 import sys
 
-path = sys.argv[1]
-w = int(sys.argv[2]) if len(sys.argv) > 2 else 90
-if path.endswith(".db"):
-    rows = sqlite3.connect(path).execute(
-        "select name, total_calls, average, percentage from top_kernels order by total_duration desc").fetchall()
-    rows = [(r[0], r[1], r[2], r[3]) for r in rows]  # rocpd averages are in us
-else:
-    rows = [(r["Name"], int(r["Calls"]), float(r["AverageNs"]) / 1e3, float(r["Percentage"]))
-            for r in csv.DictReader(open(path))]
-for name, calls, avg_us, pct in rows:
-    short = name.replace("void ", "").split("(")[0] if "rocprim" not in name else \
-        "rocprim::" + ("onesweep_iteration" if "onesweep_iteration" in name else "histogram/offsets" if "onesweep" in name
-                       else "scan" if "scan" in name else "other")
-    print(f"{short[:w]:{w}s} {calls:6d} {avg_us:10.1f} us {pct:6.2f} %")
+for d in sys.argv[1:]:
+    f = glob.glob(f"{d}/**/*kernel_stats.csv", recursive=True)
+    if not f:
+        continue
+    print(d)
+    tot = 0.0
+    for r in csv.DictReader(open(f[0])):
+        name = r["Name"].split("(")[0].replace("void ", "")
+        us = float(r["AverageNs"]) / 1e3
+        if "glint::" in name and int(r["Calls"]) >= 10:
+            tot += us
+        print(f"  {name[-58:]:58s} {r['Calls']:>5s} {us:10.1f} us")
+    print(f"  {'sum of glint kernels called >= 10 times':58s} {'':>5s} {tot:10.1f} us")
