@@ -35,14 +35,25 @@ namespace glint {
 constexpr int kSlabBits = GLINT_SLAB_BITS;  // (a build-time experiment knob; 12 = 32 KiB of Double per slab)
 constexpr int kSlab = 1 << kSlabBits;
 constexpr int kMaxDigit = 1024;        // coarse buckets and fine slabs per bucket, at most
-constexpr int kATPB = 1024;            // partition workgroups: 16 waves
-constexpr int kAChunk = 4096;          // records per partition chunk (and dedup table fill)
-constexpr int kAPer = kAChunk / kATPB;
-constexpr int kASlots = 8192;          // dedup hash slots (load <= 0.5)
+#ifndef GLINT_PART_TPB
+#define GLINT_PART_TPB 1024
+#endif
+constexpr int kATPB = GLINT_PART_TPB;  // partition workgroup size (build-time knob: 1024 or 512)
+constexpr int kAPer = 4;               // records per thread per chunk
+constexpr int kAChunk = kATPB * kAPer; // records per partition chunk (and dedup table fill)
+constexpr int kASlots = 2 * kAChunk;   // dedup hash slots (load <= 0.5)
+constexpr int kASlotBits = kASlots == 8192 ? 13 : kASlots == 4096 ? 12 : 11;
+static_assert((1 << kASlotBits) == kASlots, "dedup table size");
+// partition workgroups per CU: LDS-bound (the dedup table; the plain front end's staging)
+constexpr int kPartWgPerCuDedup = kATPB == 1024 ? 1 : 2;
+constexpr int kPartWgPerCuPlain = kATPB == 1024 ? 2 : 4;
 constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments per bucket)
-constexpr int kFTPB = 256;             // fine partition workgroups
-constexpr int kFTile = 2048;           // records staged per fine-partition step
-constexpr int kFPer = kFTile / kFTPB;
+#ifndef GLINT_FPART_TPB
+#define GLINT_FPART_TPB 256
+#endif
+constexpr int kFTPB = GLINT_FPART_TPB; // fine partition workgroup size (build-time knob)
+constexpr int kFPer = 8;               // records per thread per tile
+constexpr int kFTile = kFTPB * kFPer;  // records staged per fine-partition step
 constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
 constexpr int kCTPB = 256;
 constexpr u32 kCItem = 16384;          // records per apply item at most
@@ -494,7 +505,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
           bad.add(i);
         } else {
           const u32 a = (u32)a64;
-          h = (a * 0x9E3779B1u) >> (32 - 13);
+          h = (a * 0x9E3779B1u) >> (32 - kASlotBits);
           for (;;) {  // the compare-and-swap is the probe: one LDS round trip per slot tried
             const u32 prev = atomicCAS(&hk[h], kEmptySlot, a);
             if (prev == kEmptySlot) { claimed = true; break; }
@@ -967,7 +978,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
-  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? 1 : 2)));
+  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : kPartWgPerCuPlain)));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
   const i64 max_fitems = (i64)g.nb + n / kFItem + 1;

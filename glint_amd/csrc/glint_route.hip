@@ -184,6 +184,30 @@ struct DevGuard {
   }
 };
 
+// One partition and no output: the batch is its own send buffer, so the pass only checks the keys
+// (owner_of: 0 <= key < nkeys for either kind when nparts == 1) -- a streaming read -- and sets
+// counts[0] = n (the exchange sends nothing when a key is bad, so the count matters only when all
+// are good).
+__global__ __launch_bounds__(256) void route_validate(const i64* __restrict__ keys, i64 n, i64 nkeys,
+                                                      i64* counts, u64* bad) {
+  u64 b = 0;
+  const i64 stride = (i64)gridDim.x * 256 * 2;
+  for (i64 i = ((i64)blockIdx.x * 256 + threadIdx.x) * 2; i < n; i += stride) {
+    if (i + 1 < n) {
+      typedef __attribute__((ext_vector_type(2))) long long KP;
+      const KP k = __builtin_nontemporal_load(reinterpret_cast<const KP*>(keys + i));
+      if (k.y < 0 || k.y >= nkeys) b = max(b, ~(u64)(i + 1));
+      if (k.x < 0 || k.x >= nkeys) b = max(b, ~(u64)i);
+    } else {
+      const i64 k = keys[i];
+      if (k < 0 || k >= nkeys) b = max(b, ~(u64)i);
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) b = max(b, (u64)__shfl_xor((unsigned long long)b, d));
+  if ((threadIdx.x & 63) == 0 && b) atomicMax((unsigned long long*)bad, (unsigned long long)b);
+  if (blockIdx.x == 0 && threadIdx.x == 0) counts[0] = n;
+}
+
 // Launches the route (histogram, scan, scatter, counts) on `st`; the first bad record (~index, 0 =
 // none) lands in the device word *bad_dev. No host synchronisation.
 int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of,
@@ -238,6 +262,12 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   u32* offs = (u32*)(b + ((hist_bytes + 255) & ~(size_t)255));
   void* scan_tmp = b + 2 * ((hist_bytes + 255) & ~(size_t)255);
   if (hipMemsetAsync(bad_dev, 0, 8, st) != hipSuccess) return GLINT_EDEVICE;
+  if (nparts == 1 && !out.order && !out.keys && !out.cols && !out.vals && n > 0 &&
+      ((uintptr_t)keys & 15) == 0) {
+    const unsigned g = (unsigned)std::max<i64>(1, std::min<i64>((n / 2 + 255) / 256, 1024));
+    route_validate<<<g, 256, 0, st>>>(keys, n, nkeys, counts, bad_dev);
+    return hipGetLastError() == hipSuccess ? GLINT_OK : GLINT_EDEVICE;
+  }
   if (n == 0) {
     if (hipMemsetAsync(counts, 0, (size_t)nparts * 8, st) != hipSuccess) return GLINT_EDEVICE;
   } else {
@@ -245,7 +275,10 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
     if (rocprim::exclusive_scan(scan_tmp, scan_bytes, hist, offs, 0u, (size_t)nparts * nblocks,
                                 rocprim::plus<u32>(), st) != hipSuccess)
       return GLINT_EDEVICE;
-    route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, offs, nblocks, out);
+    // no output requested (a single partition: the batch is its own send buffer): counts and the
+    // status word only
+    if (out.order || out.keys || out.cols || out.vals)
+      route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, offs, nblocks, out);
     route_counts<<<(unsigned)((nparts + 255) / 256), 256, 0, st>>>(offs, hist, nblocks, nparts, counts);
   }
   if (hipGetLastError() != hipSuccess) return GLINT_EDEVICE;

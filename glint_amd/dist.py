@@ -86,6 +86,14 @@ class Router:
         slot_of, _ = self._device_tables(dev)
         counts = torch.empty(self.nparts, dtype=torch.int64, device=dev)
         bad = torch.empty(1, dtype=torch.int64, device=dev)
+        if self.nparts == 1:
+            # one partition: the batch, in the caller's order, is the send buffer (order = identity,
+            # None); the pass only validates the keys and counts them
+            rc = N.load().glint_route_gather_dev(
+                keys.data_ptr(), None, None, 0, n, self.kind, 1, self.nkeys, None, counts.data_ptr(), None,
+                None, None, None, bad.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+            check(rc)
+            return counts, None, keys, cols, vals, bad
         order = torch.empty(n, dtype=torch.int64, device=dev) if want_order else None
         sk = torch.empty(n, dtype=torch.int64, device=dev)
         sc = torch.empty(n, dtype=torch.int32, device=dev) if cols is not None else None
@@ -103,6 +111,8 @@ class Router:
         group in the caller's order), counts = host int64 array of the group sizes (perm order)."""
         if keys.is_cuda:
             counts, order, _, _, _, bad = self.route(keys, want_order=True)
+            if order is None:  # one partition: the identity
+                order = torch.arange(keys.numel(), dtype=torch.int64, device=keys.device)
             host = torch.cat([counts, bad]).cpu().numpy()
             if host[-1] != 0:
                 i = int(~host[-1])
@@ -304,6 +314,8 @@ class DistributedBigVector(_Distributed):
                     resp.index_copy_(0, idx.to(resp.device), got)
         back = ex.backward(resp).to(keys.device)
         ex.raise_if_bad(keys, self.router.nkeys)  # after the collectives: this rank asked for nothing
+        if order is None:  # one partition: the answer is already in the caller's order
+            return back
         out = torch.empty(keys.numel(), dtype=self.dtype, device=keys.device)
         out.index_copy_(0, order.to(keys.device), back)
         return out
@@ -372,6 +384,8 @@ class DistributedBigMatrix(_Distributed):
                     resp.index_copy_(0, idx.to(resp.device), got)
         back = ex.backward(resp).to(rows.device)
         ex.raise_if_bad(rows, self.router.nkeys)
+        if order is None:  # one partition: the answer is already in the caller's order
+            return back
         out = torch.empty((rows.numel(),) + shape[1:], dtype=self.dtype, device=rows.device)
         out.index_copy_(0, order.to(rows.device), back)
         return out

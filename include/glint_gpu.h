@@ -214,7 +214,8 @@ int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t nparts, in
  * non-NULL output: order (record indices), out_keys, out_cols (from cols), out_vals (vsize = 4 or 8
  * bytes per value, from vals). counts[0..nparts) (device) receives the group sizes. The first bad
  * record is left in the device word *bad_dev as ~index (0 = none); bad records are in no group.
- * Stream-ordered on `stream`; the caller reads counts and *bad_dev when it needs them. */
+ * With every output NULL only counts and *bad_dev are produced (a one-partition batch is its own
+ * send buffer). Stream-ordered on `stream`; the caller reads counts and *bad_dev when it needs them. */
 int glint_route_gather_dev(const int64_t* keys, const int32_t* cols, const void* vals, int vsize, int64_t n,
                            int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of, int64_t* counts,
                            int64_t* order, int64_t* out_keys, int32_t* out_cols, void* out_vals,

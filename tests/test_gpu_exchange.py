@@ -118,3 +118,31 @@ def test_bench_self_launches_ranks(gpu, pattern):
 def test_bench_patterns(gpu, args):
     d = _bench(args + ["--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
     assert d["check"] is True and d["value"] > 0 and d["roofline"]["achieved"] > 0
+
+
+@pytest.mark.parametrize("n", [1, 7, 100_001, 1 << 20])
+def test_route_one_partition_validates_only(gpu, n):
+    """One partition and no outputs: the batch is its own send buffer; the pass checks the keys
+    (the first bad record as ~index) and reports the count."""
+    import torch
+    d = torch.device("cuda", gpu)
+    lib = N.load()
+    nkeys = 1 << 22
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, nkeys, n).astype(np.int64)
+    for bad_at in ([], [n - 1], [n // 3, n // 2] if n > 2 else []):
+        k = keys.copy()
+        for j, b in enumerate(bad_at):
+            k[b] = nkeys + j if j == 0 else -3
+        kt = torch.from_numpy(k).to(d)
+        counts = torch.full((1,), -7, dtype=torch.int64, device=d)
+        bad = torch.full((1,), -7, dtype=torch.int64, device=d)
+        rc = lib.glint_route_gather_dev(kt.data_ptr(), None, None, 0, n, N.GLINT_ROUTE_RANGE, 1, nkeys, None,
+                                        counts.data_ptr(), None, None, None, None, bad.data_ptr(),
+                                        torch.cuda.current_stream(d).cuda_stream)
+        torch.cuda.synchronize(d)
+        assert rc == N.GLINT_OK
+        if bad_at:
+            assert int(bad.item()) != 0 and ~int(bad.item()) == min(bad_at)
+        else:
+            assert int(bad.item()) == 0 and int(counts.item()) == n

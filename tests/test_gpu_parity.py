@@ -434,7 +434,7 @@ def test_route_out_of_range_reports_first_bad(gpu):
 @pytest.mark.parametrize("backend,world,case", [
     ("gloo", 2, "vec_range"), ("gloo", 2, "vec_range_mps3"), ("gloo", 2, "vec_cyclic_mps2"),
     ("gloo", 2, "vec_long_few_keys"), ("gloo", 2, "mat_range_mps2"),
-    ("nccl", 1, "vec_range_mps3"), ("nccl", 1, "mat_range")])
+    ("nccl", 1, "vec_range_mps3"), ("nccl", 1, "vec_range"), ("nccl", 1, "mat_range")])
 def test_dist_exchange_on_gpu(gpu, backend, world, case):
     import socket
     import torch.multiprocessing as mp
