@@ -117,7 +117,8 @@ struct PhaseClock {
 typedef u32 v2u32 __attribute__((ext_vector_type(2)));
 struct BufOut {
   __amdgpu_buffer_rsrc_t r;
-  u32 oob;  // the descriptor's size: a store at this offset is dropped
+  u32 oob;     // the descriptor's size: a store at this offset is dropped
+  void* base;  // the same range as a plain pointer
 };
 // base and bytes must be workgroup-uniform; readfirstlane makes that provable to the compiler, which
 // otherwise wraps every buffer store in a waterfall loop
@@ -126,7 +127,7 @@ __device__ __forceinline__ BufOut buf_out(const void* base, u32 bytes) {
   const u32 lo = __builtin_amdgcn_readfirstlane((u32)b), hi = __builtin_amdgcn_readfirstlane((u32)(b >> 32));
   const u32 nb = __builtin_amdgcn_readfirstlane(bytes);
   void* p = (void*)(((u64)hi << 32) | lo);
-  return BufOut{__builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)nb, 0x00020000), nb};
+  return BufOut{__builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)nb, 0x00020000), nb, p};
 }
 template <typename T>
 __device__ __forceinline__ void bput(const BufOut& b, u32 off, bool on, T v) {
@@ -339,6 +340,11 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
 #ifdef GLINT_BIN_NOSTORE  // timing experiment only: every partition store dropped
     bput(oa, rel * 4u, false, a);
     bput(ov, rel * (u32)sizeof(A), false, st_v[p]);
+#elif defined(GLINT_PART_GLOBAL_STORES)  // experiment: plain global stores
+    if (on) {
+      reinterpret_cast<u32*>(oa.base)[rel] = a;
+      reinterpret_cast<A*>(ov.base)[rel] = st_v[p];
+    }
 #else
     bput(oa, rel * 4u, on, a);
     bput(ov, rel * (u32)sizeof(A), on, st_v[p]);

@@ -18,6 +18,7 @@
 #include <utility>
 #include <new>
 #include <cstring>
+#include <sched.h>
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
@@ -1623,6 +1624,23 @@ int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, i
 
 int glint_shard_wait(glint_shard_t s, uint64_t ticket, int64_t* first_bad) {
   if (!s) return GLINT_EINVAL;
+  {  // launch the open batch if it holds this ticket, then wait WITHOUT the shard lock, so other
+     // threads of the server keep enqueueing meanwhile (one connection per client in the actor model)
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceGuard g(s->device);
+    if (s->open_slot >= 0 && s->ring[s->open_slot].msgs.front().ticket <= ticket) {
+      const int rc = ring_flush_locked(s);
+      if (rc) return rc;
+    }
+  }
+  const u64* done = s->h_done;  // written once, before the first ticket exists
+  if (done) {
+    // bounded: an entry that completes by event (a DMA'd push) never moves the word
+    for (int i = 0; i < (1 << 14) && __atomic_load_n(done, __ATOMIC_ACQUIRE) < ticket; ++i) {
+      if ((i & 255) == 255) sched_yield();
+      else __builtin_ia32_pause();
+    }
+  }
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
   return ring_wait_locked(s, (u64)ticket, (i64*)first_bad);

@@ -7,7 +7,11 @@ Reads the FETCH_SIZE and WRITE_SIZE counter CSVs of two separate `rocprofv3 --pm
   * WRITE_SIZE is in KiB and exact for 16-B-per-lane streaming stores -> bytes = 1024 * WRITE_SIZE.
 Writes profiles/<round>/pmc_<tag>.json with the per-kernel and per-push averages.
 
-    python tools/pmc_traffic.py <fetch.csv> <write.csv> <out.json> <records_per_push>
+    python tools/pmc_traffic.py <fetch.csv> <write.csv> <out.json> <records_per_push> [algorithmic_bytes_per_push]
+
+Every glint push kernel (push_*, bin_*) that runs on (nearly) every push of the profiled command is
+summed; one-off dispatches (the first push of a shard, taken before the adaptive switch has a
+history) are listed but not counted.
 """
 import csv
 import json
@@ -28,18 +32,21 @@ def per_kernel(path, counter):
 
 def main():
     fetch_csv, write_csv, out, records = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    algorithmic = float(sys.argv[5]) if len(sys.argv) > 5 else 32.0 * records
     fetch, nf = per_kernel(fetch_csv, "FETCH_SIZE")
     write, nw = per_kernel(write_csv, "WRITE_SIZE")
     kernels = {}
     total = 0.0
+    most = max(list(nf.values()) + [1])
     for name in sorted(set(fetch) | set(write)):
         rd = 2.0 * 1024.0 * fetch.get(name, 0.0)
         wr = 1024.0 * write.get(name, 0.0)
         kernels[name] = {"read_bytes": rd, "write_bytes": wr, "dispatches": [nf.get(name, 0), nw.get(name, 0)],
                          "FETCH_SIZE_KiB": fetch.get(name, 0.0), "WRITE_SIZE_KiB": write.get(name, 0.0)}
-        if "push_" in name:
+        counted = ("push_" in name or "bin_" in name) and nf.get(name, 0) * 2 >= most
+        kernels[name]["counted"] = counted
+        if counted:
             total += rd + wr
-    algorithmic = 32.0 * records
     res = {"records_per_push": records, "algorithmic_bytes_per_push": algorithmic,
            "hbm_bytes_per_launch": total, "traffic_over_algorithmic": total / algorithmic,
            "correction": "read = 2*1024*FETCH_SIZE (gfx950 half-count of 16 B/lane streaming reads); "
