@@ -1112,6 +1112,11 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
     std::memcpy(r.out, r.h + r.out_off, r.out_bytes);
     r.out = nullptr;
   }
+  if (r.pull_batch) {
+    for (const auto& m : r.msgs)
+      std::memcpy(m.out, r.h + r.out_off + (size_t)m.off * s->vsize, (size_t)m.n * s->vsize);
+    r.pull_batch = false;
+  }
   return GLINT_OK;
 }
 
@@ -1188,6 +1193,7 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
     r.out = nullptr;
     r.fill = 0;
     r.msgs.clear();
+    r.pull_batch = false;
     *slot = idx;
     return GLINT_OK;
   }
@@ -1249,6 +1255,8 @@ int launch_push_entry(glint_shard* s, glint_shard::RingSlot& r, const char* base
   });
 }
 
+int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind);
+
 // launches the open batch, if any
 int ring_flush_locked(glint_shard* s) {
   if (s->open_slot < 0) return GLINT_OK;
@@ -1260,6 +1268,7 @@ int ring_flush_locked(glint_shard* s) {
     r.msgs.clear();
     return rc;
   }
+  if (s->open_kind >= 0) return launch_pull_batch(s, r, s->open_kind);
   return launch_push_entry(s, r, r.hd, stage_layout(s, kBatchMax), r.fill, s->open_flags, true,
                            r.msgs.front().ticket, r.msgs.back().ticket);
 }
@@ -1270,7 +1279,8 @@ inline bool batchable(const glint_shard* s, i64 n) { return n > 0 && n <= kBatch
 // open batch, opening one if needed; *ticket = the message's own ticket.
 int ring_append_locked(glint_shard* s, i64 n, int flags, const void* k, const void* c, const void* v, u64* ticket) {
   int rc;
-  if (s->open_slot >= 0 && (flags != s->open_flags || s->ring[s->open_slot].fill + n > kBatchMax)) {
+  if (s->open_slot >= 0 &&
+      (s->open_kind >= 0 || flags != s->open_flags || s->ring[s->open_slot].fill + n > kBatchMax)) {
     rc = ring_flush_locked(s);
     if (rc) return rc;
   }
@@ -1280,6 +1290,7 @@ int ring_append_locked(glint_shard* s, i64 n, int flags, const void* k, const vo
     if (rc) return rc;
     s->open_slot = slot;
     s->open_flags = flags;
+    s->open_kind = -1;
   }
   glint_shard::RingSlot& r = s->ring[s->open_slot];
   const StageLayout L = stage_layout(s, kBatchMax);
@@ -1376,6 +1387,55 @@ int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t
   return GLINT_OK;
 }
 
+// A coalesced pull batch: consecutive message-sized element pulls of one kind share one launch;
+// each answer is copied to its own destination when the batch retires.
+int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind) {
+  const StageLayout L = stage_layout(s, kBatchMax);
+  const i64* keys = (const i64*)r.hd;
+  const int32_t* cols = (const int32_t*)(r.hd + L.kb);
+  char* ans = r.hd + L.kb + L.cb;
+  const i64 n = r.fill;
+  r.out = nullptr;
+  r.out_off = L.kb + L.cb;
+  const int rc = ring_dispatch(s, r, true, r.msgs.front().ticket, r.msgs.back().ticket, [&]() -> int {
+    if (kind == 0) {
+      GLINT_DISPATCH(s->dtype, launch_vec_pull, s, keys, ans, n, s->stream);
+    }
+    GLINT_DISPATCH(s->dtype, launch_mat_pull, s, keys, cols, ans, n, s->stream);
+  });
+  if (rc == GLINT_OK) r.pull_batch = true;
+  return rc;
+}
+
+int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys, const int32_t* cols, void* out,
+                            u64* ticket) {
+  int rc;
+  if (s->open_slot >= 0 && (s->open_kind != kind || s->ring[s->open_slot].fill + n > kBatchMax)) {
+    rc = ring_flush_locked(s);
+    if (rc) return rc;
+  }
+  if (s->open_slot < 0) {
+    int slot = -1;
+    rc = ring_acquire_locked(s, kBatchMax, &slot, (size_t)kBatchMax * s->vsize);
+    if (rc) return rc;
+    s->open_slot = slot;
+    s->open_kind = kind;
+    s->open_flags = 0;
+  }
+  glint_shard::RingSlot& r = s->ring[s->open_slot];
+  const StageLayout L = stage_layout(s, kBatchMax);
+  std::memcpy(r.h + (size_t)r.fill * 8, keys, (size_t)n * 8);
+  if (kind == 1) std::memcpy(r.h + L.kb + (size_t)r.fill * 4, cols, (size_t)n * 4);
+  const u64 t = ++s->ticket_next;
+  glint_shard::RingSlot::Msg m{r.fill, n, t};
+  m.out = out;
+  r.msgs.push_back(m);
+  r.fill += n;
+  if (ticket) *ticket = t;
+  if (r.fill == kBatchMax) return ring_flush_locked(s);
+  return GLINT_OK;
+}
+
 int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
   if (s->open_slot >= 0 && s->ring[s->open_slot].msgs.front().ticket <= ticket) {
     const int rc = ring_flush_locked(s);
@@ -1419,6 +1479,7 @@ inline size_t pull_bytes(const glint_shard* s, int kind, i64 n) {
 // when the slot retires.
 int pull_enqueue_locked(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols, void* out, int64_t n,
                         u64* ticket) {
+  if (kind != 2 && batchable(s, n)) return ring_append_pull_locked(s, kind, n, keys, cols, out, ticket);
   int slot = -1;
   const size_t ob = pull_bytes(s, kind, n);
   int rc = ring_acquire_locked(s, n, &slot, ob);

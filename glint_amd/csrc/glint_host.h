@@ -67,12 +67,15 @@ struct glint_shard {
     struct Msg {
       int64_t off, n;
       uint64_t ticket;
+      void* out = nullptr;  // a coalesced pull's destination (its answer sits at off in the slot)
     };
     std::vector<Msg> msgs;      // the messages of this entry, for error attribution
     int64_t fill = 0;           // records appended to an open batch
+    bool pull_batch = false;    // a coalesced pull batch: answers go to msgs[i].out when retired
   } ring[GLINT_RING_SLOTS];
-  int open_slot = -1;     // the batch that message-sized pushes are appended to, not launched yet
+  int open_slot = -1;     // the batch that message-sized pushes (or pulls) are appended to, not launched yet
   int open_flags = 0;
+  int open_kind = -1;     // -1: a push batch; 0 / 1: a vector / matrix element pull batch
   uint64_t ring_bad_ticket = 0;  // the message the unreported error belongs to
   bool host_pending = false;     // ring entries enqueued on `stream` since a device call last waited for them
   hipEvent_t host_ev = nullptr;

@@ -166,7 +166,10 @@ int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uin
  * An entry of up to GLINT_ZERO_COPY_MAX records is ONE single-workgroup kernel that signals its own
  * completion through a host-mapped word (no event, no copy command): a few microseconds of stream
  * time per message. Pulls can be enqueued the same way (glint_pull_async), so a server answering a
- * burst of Pull messages waits once for all of them. Tickets number pushes and pulls together. */
+ * burst of Pull messages waits once for all of them. Consecutive message-sized pushes with the same
+ * flags, and consecutive message-sized element pulls, are coalesced into one launch per batch (the
+ * batch goes to the GPU when it is full or anything else needs the stream); every message keeps its
+ * own ticket and its own errors. Tickets number pushes and pulls together. */
 #define GLINT_RING_SLOTS 16
 #define GLINT_ZERO_COPY_MAX 4096
 

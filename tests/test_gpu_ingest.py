@@ -247,3 +247,34 @@ def test_coalescing_keeps_order_across_flags_pulls_and_device_calls(gpu):
         np.testing.assert_array_equal(final, ref.data)
         for w, g in zip(want, got):
             np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("dtype", ["double", "int"])
+def test_coalesced_pulls_answer_each_message(gpu, dtype):
+    """Consecutive message-sized pulls share one launch; every message gets its own answer, and a
+    bad key is reported as record i of its own message."""
+    size = 20_000
+    rng = np.random.default_rng(91)
+    with PartialVector(RangePartition(0, 0, size), dtype, gpu) as sh:
+        base = _vals(rng, dtype, size)
+        sh.update(np.arange(size, dtype=np.int64), base)
+        outs, want, tickets = [], [], []
+        for m in range(40):
+            n = int(rng.integers(1, 300))
+            q = rng.integers(0, size, n).astype(np.int64)
+            t, out = sh.pull_async(q)
+            outs.append(out)
+            want.append(base[q])
+            tickets.append(t)
+        sh.wait(tickets[-1])
+        for w, g in zip(want, outs):
+            np.testing.assert_array_equal(g, w)
+        q1 = np.array([1, 2, 3], np.int64)
+        q2 = np.array([4, size + 2, 6, 7], np.int64)
+        t1, o1 = sh.pull_async(q1)
+        t2, o2 = sh.pull_async(q2)
+        sh.wait(t1)  # the first message is clean
+        np.testing.assert_array_equal(o1, base[q1])
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.wait(t2)
+        assert ei.value.record == 1
