@@ -117,8 +117,7 @@ struct PhaseClock {
 typedef u32 v2u32 __attribute__((ext_vector_type(2)));
 struct BufOut {
   __amdgpu_buffer_rsrc_t r;
-  u32 oob;     // the descriptor's size: a store at this offset is dropped
-  void* base;  // the same range as a plain pointer
+  u32 oob;  // the descriptor's size: a store at this offset is dropped
 };
 // base and bytes must be workgroup-uniform; readfirstlane makes that provable to the compiler, which
 // otherwise wraps every buffer store in a waterfall loop
@@ -127,7 +126,7 @@ __device__ __forceinline__ BufOut buf_out(const void* base, u32 bytes) {
   const u32 lo = __builtin_amdgcn_readfirstlane((u32)b), hi = __builtin_amdgcn_readfirstlane((u32)(b >> 32));
   const u32 nb = __builtin_amdgcn_readfirstlane(bytes);
   void* p = (void*)(((u64)hi << 32) | lo);
-  return BufOut{__builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)nb, 0x00020000), nb, p};
+  return BufOut{__builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)nb, 0x00020000), nb};
 }
 template <typename T>
 __device__ __forceinline__ void bput(const BufOut& b, u32 off, bool on, T v) {
@@ -340,11 +339,6 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
 #ifdef GLINT_BIN_NOSTORE  // timing experiment only: every partition store dropped
     bput(oa, rel * 4u, false, a);
     bput(ov, rel * (u32)sizeof(A), false, st_v[p]);
-#elif defined(GLINT_PART_GLOBAL_STORES)  // experiment: plain global stores
-    if (on) {
-      reinterpret_cast<u32*>(oa.base)[rel] = a;
-      reinterpret_cast<A*>(ov.base)[rel] = st_v[p];
-    }
 #else
     bput(oa, rel * 4u, on, a);
     bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
@@ -531,9 +525,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     }
     ph.mark(9);
     const i64 cn = c + 2 * G;  // two chunks ahead: in flight across this chunk and the next
-#ifndef GLINT_DEDUP_LATE_LOAD
     if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
-#endif
     ph.mark(10);
     __syncthreads();
     const u32 D = nused;
@@ -566,9 +558,6 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
         if (sl >= (u32)kStageA) hv[sl] = A(0);
       }
     }
-#ifdef GLINT_DEDUP_LATE_LOAD
-    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
-#endif
     __syncthreads();
     ph.mark(17);
   };
