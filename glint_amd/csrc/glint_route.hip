@@ -45,11 +45,13 @@ struct RangeDesc {
 __device__ __forceinline__ int32_t owner_of(const RangeDesc& d, i64 key) {
   if (key < 0 || key >= d.nkeys) return -1;
   if (d.cyclic) return (int32_t)(key % d.nparts);
-  // .toInt of the index; a partitioner whose Int sizes overflowed yields an index outside the
-  // partition array (ArrayIndexOutOfBoundsException in the reference) -> rejected like a bad key
-  const int32_t o = key < d.small_keys ? (int32_t)(key / d.q)
-                                       : (int32_t)((i64)d.n_small + (key - d.small_keys) / ((i64)d.q + 1));
-  return o < d.nparts ? o : -1;
+  // largePartitionSize is an Int (smallPartitionSize + 1, :18): it wraps to Int.MinValue when
+  // small partitions hold 2^31-1 keys, as on the JVM. .toInt of the index; a partitioner whose Int
+  // sizes overflowed yields an index outside the partition array (ArrayIndexOutOfBoundsException
+  // in the reference) -> rejected like a bad key
+  const i64 large = (int32_t)((uint32_t)d.q + 1u);
+  const int32_t o = (int32_t)(uint32_t)(u64)(key < d.small_keys ? key / d.q : (i64)d.n_small + (key - d.small_keys) / large);
+  return o >= 0 && o < d.nparts ? o : -1;
 }
 
 // Lanes of the wave whose owner equals this lane's: one ballot per owner bit (owners < 2^nbits,

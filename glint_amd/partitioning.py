@@ -17,6 +17,12 @@ def _to_int(x: int) -> int:
     return x - (1 << 32) if x >= (1 << 31) else x
 
 
+def _jdiv(a: int, b: int) -> int:
+    """Java/Scala Long division: truncates toward zero."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
 class Partition:
     """glint.partitioning.Partition (Partition.scala:8-35)."""
 
@@ -67,7 +73,7 @@ class RangePartitioner:
         self.smallPartitionSize = int(smallPartitionSize)
         self.size = int(size)
         self.numberOfSmallKeys = self.numberOfSmallPartitions * self.smallPartitionSize  # :17
-        self.largePartitionSize = self.smallPartitionSize + 1  # :18
+        self.largePartitionSize = _to_int(self.smallPartitionSize + 1)  # :18 (an Int: wraps)
 
     @classmethod
     def apply(cls, numberOfPartitions: int, numberOfKeys: int) -> "RangePartitioner":
@@ -88,7 +94,7 @@ class RangePartitioner:
             else:
                 end += 1
                 parts.append(RangePartition(i, start, end))
-                start += q + 1
+                start += _to_int(q + 1)  # :78 Int + 1 wraps before widening
                 end += q
         return cls(parts, n_small, q, N)
 
@@ -98,10 +104,13 @@ class RangePartitioner:
         if key < 0 or key >= self.size:
             raise IndexOutOfBoundsException(f"key {key} outside [0, {self.size})")
         if key < self.numberOfSmallKeys:
-            idx = key // self.smallPartitionSize
+            idx = _jdiv(key, self.smallPartitionSize)
         else:
-            idx = self.numberOfSmallPartitions + (key - self.numberOfSmallKeys) // self.largePartitionSize
-        return self.partitions[_to_int(idx)]
+            idx = self.numberOfSmallPartitions + _jdiv(key - self.numberOfSmallKeys, self.largePartitionSize)
+        idx = _to_int(idx)
+        if not 0 <= idx < len(self.partitions):  # partitions(idx): ArrayIndexOutOfBoundsException
+            raise IndexOutOfBoundsException(f"key {key} maps to partition index {idx} of {len(self.partitions)}")
+        return self.partitions[idx]
 
     def partition_indices(self, keys: np.ndarray) -> np.ndarray:
         """Vectorised `partition(k).index` over an int64 array; raises like `partition` for the first
@@ -114,8 +123,15 @@ class RangePartitioner:
         out = np.empty(keys.shape, dtype=np.int64)
         small = keys < self.numberOfSmallKeys
         if self.smallPartitionSize > 0:
-            out[small] = keys[small] // self.smallPartitionSize
-        out[~small] = self.numberOfSmallPartitions + (keys[~small] - self.numberOfSmallKeys) // self.largePartitionSize
+            out[small] = keys[small] // self.smallPartitionSize  # both operands >= 0: floor == trunc
+        rest = keys[~small] - self.numberOfSmallKeys
+        L = self.largePartitionSize
+        out[~small] = self.numberOfSmallPartitions + (rest // L if L > 0 else -(rest // -L))  # Java truncation
+        out = ((out & 0xFFFFFFFF) ^ 0x80000000) - 0x80000000  # .toInt
+        oob = (out < 0) | (out >= len(self.partitions))
+        if oob.any():
+            i = int(np.argmax(oob))
+            raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) maps to partition index {int(out[i])}")
         return out
 
     def all(self):

@@ -44,7 +44,7 @@ void oracle_range_partitioner(int32_t P, int64_t N, int64_t* starts, int64_t* en
     } else {
       end += 1;                                          /* :76 */
       starts[i] = start; ends[i] = end;                  /* :77 */
-      start += (int64_t)q + 1;                           /* :78 */
+      start += (int32_t)((uint32_t)q + 1u);              /* :78 (Int + 1 wraps, then widens) */
       end += q;                                          /* :79 */
     }
   }
@@ -53,13 +53,18 @@ void oracle_range_partitioner(int32_t P, int64_t N, int64_t* starts, int64_t* en
 }
 
 /* RangePartitioner.partition -- RangePartitioner.scala:27-43. Returns -1 where the reference
- * throws IndexOutOfBoundsException (:30-32). */
+ * throws IndexOutOfBoundsException (:30-32) or indexes the partition array below 0. All Int
+ * arithmetic wraps as on the JVM: largePartitionSize = smallPartitionSize + 1 is an Int (:18), so a
+ * partitioner with 2^31-1 keys per small partition divides by Int.MinValue, exactly like the
+ * reference. */
 int32_t oracle_range_partition(int64_t key, int32_t n_small, int32_t small_size, int64_t N) {
   if (key < 0 || key >= N) return -1;                                   /* :30-32 */
   int64_t n_small_keys = (int64_t)n_small * (int64_t)small_size;        /* RangePartitioner.scala:17 */
-  int64_t large = (int64_t)small_size + 1;                              /* :18 (Int + 1) */
-  if (key < n_small_keys) return (int32_t)(key / small_size);           /* :37 */
-  return (int32_t)((int64_t)n_small + (key - n_small_keys) / large);   /* :39 */
+  int64_t large = (int32_t)((uint32_t)small_size + 1u);                /* :18 (Int + 1, wraps) */
+  int64_t idx = key < n_small_keys ? key / small_size                   /* :37 */
+                                   : (int64_t)n_small + (key - n_small_keys) / large; /* :39 */
+  int32_t o = (int32_t)(uint32_t)(uint64_t)idx;                         /* .toInt */
+  return o >= 0 ? o : -1;  /* an index >= P: the caller rejects it (partitions(idx) throws) */
 }
 
 /* RangePartition -- src/main/scala/glint/partitioning/range/RangePartition.scala:17,24,33 */
@@ -203,7 +208,7 @@ int64_t oracle_bucket_range(const int64_t* keys, int64_t n, int32_t P, int32_t n
   for (int32_t p = 0; p < P; ++p) counts[p] = 0;
   for (int64_t i = 0; i < n; ++i) {
     int32_t o = oracle_range_partition(keys[i], n_small, small_size, N);
-    if (o < 0) { free(owner); return i; }
+    if (o < 0 || o >= P) { free(owner); return i; }
     owner[i] = o;
     counts[o]++;
   }

@@ -88,7 +88,9 @@ def range_partitioner(P: int, N: int):
 
 
 def range_partition_of(key: int, n_small: int, small_size: int, N: int) -> int:
-    """RangePartitioner.partition (RangePartitioner.scala:27-43); -1 where the reference throws."""
+    """RangePartitioner.partition (RangePartitioner.scala:27-43) as the .toInt index; -1 where the
+    reference throws for the key or a negative index. An Int-overflowed partitioner can also give an
+    index >= P (the reference's partitions(idx) throws there too)."""
     return lib().oracle_range_partition(key, n_small, small_size, N)
 
 

@@ -91,6 +91,21 @@ def test_route_gather_bad_key_word(gpu):
     assert counts.sum() == keys.size - 2  # bad records are in no group
 
 
+def test_route_int_edge_partitioner(gpu):
+    """largePartitionSize wraps to Int.MinValue at q = 2^31 - 1 (RangePartitioner.scala:18): the
+    route kernel picks the JVM's partition (the hand-worked KATs of test_oracle_kat) and rejects the
+    keys whose wrapped index falls outside the partition array."""
+    from test_oracle_kat import INT_EDGE_CASES
+    for P, N_, cases in INT_EDGE_CASES:
+        keys = np.array([k for k, _ in cases], np.int64)
+        rc, counts, order, ok, *_, bad = route_gather(keys, P, N_, dev=gpu)
+        assert rc == N.GLINT_OK
+        first_bad = next((i for i, (_, w) in enumerate(cases) if w < 0), None)
+        assert (bad == 0) if first_bad is None else (~bad == first_bad)
+        want = np.bincount([w for _, w in cases if w >= 0], minlength=P)
+        np.testing.assert_array_equal(counts, want)
+
+
 def _bench(args, **env):
     e = dict(os.environ, **env)
     e.pop("WORLD_SIZE", None)

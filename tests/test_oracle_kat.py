@@ -213,6 +213,45 @@ def test_range_partitioner_sizes():
     assert q == 1 << 28 and ends[-1] == 1 << 31
 
 
+# RangePartitioner at the Int edge: q = smallPartitionSize = 2^31 - 1, so largePartitionSize
+# (an Int, RangePartitioner.scala:18) wraps to Int.MinValue and apply's `start += q + 1` (:78) wraps
+# too. Expected values worked by hand from the JVM's rules (Int + wraps; Long / truncates).
+INT_EDGE_Q = (1 << 31) - 1
+INT_EDGE_CASES = [
+    # (P, N, [(key, expected index or -1 for a throw)])
+    (3, 3 * INT_EDGE_Q + 2, [(0, 0), (INT_EDGE_Q - 1, 0), (INT_EDGE_Q, 1), (INT_EDGE_Q + (1 << 31) - 1, 1),
+                            (INT_EDGE_Q + (1 << 31), 0), (3 * INT_EDGE_Q + 1, 0)]),
+    (5, 5 * INT_EDGE_Q + 4, [(INT_EDGE_Q + (1 << 32) - 1, 0), (INT_EDGE_Q + (1 << 32), -1),
+                            (5 * INT_EDGE_Q + 3, -1), (5 * INT_EDGE_Q + 4, -1)]),
+]
+
+
+def test_range_partitioner_int_edge():
+    from glint_amd.errors import IndexOutOfBoundsException
+    from glint_amd.partitioning import RangePartitioner
+    for P, N, cases in INT_EDGE_CASES:
+        starts, ends, ns, q = O.range_partitioner(P, N)
+        assert q == INT_EDGE_Q and ns == 1
+        # start after the first large partition: q + (Int)(q + 1) = q - 2^31 = -1 (ends stay Long)
+        assert starts[2] == -1 and ends[1] == 2 * q + 1 and ends[2] == 3 * q + 2
+        rp = RangePartitioner.apply(P, N)
+        assert rp.largePartitionSize == -(1 << 31)
+        assert [p.start for p in rp.partitions] == list(starts) and [p.end for p in rp.partitions] == list(ends)
+        keys = np.array([k for k, _ in cases if k < N], np.int64)
+        for key, want in cases:
+            assert O.range_partition_of(key, ns, q, N) == want, (P, key)
+            if want < 0:
+                with pytest.raises(IndexOutOfBoundsException):
+                    rp.partition(key)
+            else:
+                assert rp.partition(key).index == want
+        good = np.array([k for k, w in cases if w >= 0], np.int64)
+        np.testing.assert_array_equal(rp.partition_indices(good), [w for _, w in cases if w >= 0])
+        if len(good) < len(keys):
+            with pytest.raises(IndexOutOfBoundsException):
+                rp.partition_indices(keys)
+
+
 def test_client_partition_counts(kat):
     for c in kat["client"]:
         assert min(c["keys"], c["modelsPerServer"] * c["servers"]) == c["partitions"], c["spec"]

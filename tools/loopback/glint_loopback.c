@@ -456,7 +456,8 @@ static int64_t N;
 static int32_t n_small, q_small;
 static int64_t small_keys;
 static int32_t owner_of(int64_t k) {
-  return k < small_keys ? (int32_t)(k / q_small) : (int32_t)(n_small + (k - small_keys) / ((int64_t)q_small + 1));
+  const int64_t large = (int32_t)((uint32_t)q_small + 1u); /* an Int, wraps (RangePartitioner.scala:18) */
+  return (int32_t)(uint32_t)(uint64_t)(k < small_keys ? k / q_small : n_small + (k - small_keys) / large);
 }
 
 typedef struct {
@@ -628,12 +629,13 @@ int main(int argc, char** argv) {
   small_keys = (int64_t)n_small * q_small;
   server* sv = (server*)calloc((size_t)S, sizeof(server));
   {
-    int64_t start = 0;
+    int64_t start = 0, end = q_small;                                         /* :68-69 */
     for (int i = 0; i < S; ++i) {
-      const int64_t size = i < n_small ? q_small : (int64_t)q_small + 1;
+      if (i >= n_small) end += 1;                                              /* :76 */
       sv[i].start = start;
-      sv[i].end = start + size;
-      start += size;
+      sv[i].end = end;
+      start += i < n_small ? q_small : (int32_t)((uint32_t)q_small + 1u);     /* :73,:78 (Int + 1 wraps) */
+      end += q_small;                                                          /* :74,:79 */
     }
   }
   /* the clients' records */
