@@ -46,7 +46,8 @@ constexpr int kASlotBits = kASlots == 8192 ? 13 : kASlots == 4096 ? 12 : 11;
 static_assert((1 << kASlotBits) == kASlots, "dedup table size");
 // partition workgroups per CU: LDS-bound (the dedup table; the plain front end's staging)
 constexpr int kPartWgPerCuDedup = kATPB == 1024 ? 1 : 2;
-constexpr int kPartWgPerCuPlain = kATPB == 1024 ? 2 : 4;
+constexpr int kPartWgPerCuPlain = kATPB == 1024 ? 1 : 2;  // what fits (VGPRs): a second round of
+                                                           // workgroups measured 3-9 % slower
 constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments per bucket)
 #ifndef GLINT_FPART_TPB
 #define GLINT_FPART_TPB 256
@@ -74,6 +75,7 @@ struct BinCtl {
   u32 tail;    // valid records in the tail
   u32 nslots;  // apply item slots written by bin_fpart (the last bucket's first item knows the total)
   u32 nfitems; // fine-partition items (written by bin_part's workgroup 0)
+  u32 fnext;   // bin_fpart's item queue: the next item to take
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -670,7 +672,14 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
     __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const u32 nit = bc->nfitems;
   PhaseClock ph(20);
-  for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
+  // items are taken from a queue (one returning atomic per item, fetched one item ahead): the grid
+  // is the resident block count, and items differ in size (a bucket's last item, skewed buckets)
+  __shared__ u32 s_next;
+  if (tid == 0) s_next = atomicAdd(&bc->fnext, 1u);
+  __syncthreads();
+  for (u32 it = s_next; it < nit; it = s_next) {
+    __syncthreads();  // every thread has read s_next
+    if (tid == 0) s_next = atomicAdd(&bc->fnext, 1u);  // the next item, in flight meanwhile
     const uint2 d = fitems[it];
     const u32 b = d.x;
     // where the bucket's records go (raw capacities: holes only at bucket ends) and its item slots
@@ -779,12 +788,14 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
       __syncthreads();
       ph.mark(30);
     }
+    __syncthreads();  // s_next is written
   }
   ph.flush(11);
 }
 
 // ---- slab apply ----------------------------------------------------------------------------------------
 constexpr int kCRB = 4;  // records per thread per batch: loads issue together, then the LDS adds
+constexpr u32 kSparseCap = 2040;  // sparse apply items hold at most this many records (touched list; 4 workgroups per CU fit in LDS)
 
 // One work item = up to kCItem records of one slab: summed in LDS (A, a byte flag per touched
 // element), then one coalesced read-modify-write of the touched pairs (exclusive items) or device
@@ -812,13 +823,19 @@ template <typename V>
 __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict__ addr,
                                                           const typename LdsAcc<V>::T* __restrict__ val,
                                                           const uint4* __restrict__ cdesc, const BinCtl* bc, i64 elems,
-                                                          V* __restrict__ data, u32 pre_min) {
+                                                          V* __restrict__ data, u32 pre_min, u32 sparse_max) {
   typedef typename Vec2<V>::T V2;
   typedef typename LdsAcc<V>::T A;
   __shared__ A acc[kSlab];
   __shared__ uint8_t touched[kSlab];  // plain byte stores: no atomic serialisation on hot elements
+  // sparse items (<= sparse_max records): the elements they touch, listed once each (first touch)
+  __shared__ uint16_t tlist[kSparseCap];
+  __shared__ u32 ntl[2];  // list lengths, alternating per item (the other one is reset meanwhile)
   constexpr int kPairsPerThread = kSlab / 2 / kCTPB;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const u64 below = (1ull << lane) - 1ull;
+  u32 par = 0;
+  if (tid < 2) ntl[tid] = 0;
   const uint4 kEmpty4 = make_uint4(0u, 0u, 0u, kItemEmpty);
   const u32 nslots = bc->nslots;  // written by bin_fpart: slots past it hold an older push's items
   u32 it = blockIdx.x;
@@ -863,13 +880,37 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
     }
     ph.mark(40);
     ph.mark(41);
+    // block-uniform: a sparse item lists its elements at first touch (a returning LDS OR on the
+    // byte's word), so the write-back visits those alone instead of sweeping the slab's 4096 flags
+    const bool sparse = exclusive && r_hi - r_lo <= sparse_max;
     for (u32 j0 = r_lo;;) {  // the first batch came with the prefetch
+      if (sparse) {
 #pragma unroll
-      for (int q = 0; q < kCRB; ++q) {
-        if (ca[q] == kEmptySlot) continue;
-        const u32 e = ca[q] & (kSlab - 1);
-        lds_add(&acc[e], cv[q]);
-        touched[e] = 1;
+        for (int q = 0; q < kCRB; ++q) {
+          bool first = false;
+          u32 e = 0;
+          if (ca[q] != kEmptySlot) {
+            e = ca[q] & (kSlab - 1);
+            lds_add(&acc[e], cv[q]);
+            const u32 sh = 8u * (e & 3u);
+            first = ((atomicOr(reinterpret_cast<u32*>(touched) + (e >> 2), 1u << sh) >> sh) & 0xFFu) == 0u;
+          }
+          const u64 b = __ballot(first);
+          if (b) {
+            u32 base = 0;
+            if (lane == 0) base = atomicAdd(&ntl[par], (u32)__popcll(b));
+            base = __shfl(base, 0);
+            if (first) tlist[base + (u32)__popcll(b & below)] = (uint16_t)e;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kCRB; ++q) {
+          if (ca[q] == kEmptySlot) continue;
+          const u32 e = ca[q] & (kSlab - 1);
+          lds_add(&acc[e], cv[q]);
+          touched[e] = 1;
+        }
       }
       j0 += (u32)kCTPB * kCRB;
       if (j0 >= r_hi) break;
@@ -880,7 +921,19 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
     __syncthreads();
     ph.mark(43);
     apply_fetch<A>(nd, addr, val, pa, pv);  // the next item's first batch: in flight during the RMW
-    if (exclusive) {
+    if (sparse) {
+      // the other parity's list was read by the previous item, before the barrier that ended it,
+      // and is appended to only after the barrier that ends this one
+      if (tid == 0) ntl[par ^ 1u] = 0;
+      const u32 L = ntl[par];
+      for (u32 i = tid; i < L; i += kCTPB) {
+        const u32 e = tlist[i];
+        if (sbase_g + e < elems) sbase[e] = acc_add(sbase[e], acc[e]);
+        acc[e] = A(0);
+        touched[e] = 0;
+      }
+      par ^= 1u;
+    } else if (exclusive) {
       // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair instead
       // (one cached line), so all loads issue back to back without a branch
       V2 dd[kPairsPerThread];
@@ -935,6 +988,29 @@ u32 bin_prefetch_min() {
   return v;
 }
 
+// records per exclusive slab item up to which bin_apply lists the touched elements instead of
+// sweeping the slab (GLINT_BIN_SPARSE_MAX; 0 disables; at most kSparseCap)
+u32 bin_sparse_max() {
+  static const u32 v = [] {
+    const char* e = getenv("GLINT_BIN_SPARSE_MAX");
+    return std::min<u32>(kSparseCap, e ? (u32)strtoul(e, nullptr, 10) : 1024u);
+  }();
+  return v;
+}
+
+// resident blocks per CU of a kernel at its block size (occupancy query); `knob` overrides (tuning)
+template <typename K>
+int resident_per_cu(K kernel, int tpb, const char* knob) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, tpb, 0) != hipSuccess || b < 1) {
+    (void)hipGetLastError();
+    b = 1;
+  }
+  const char* env = getenv(knob);
+  if (env && atoi(env) > 0) b = atoi(env);
+  return b;
+}
+
 BinGeom bin_geometry(i64 elems) {
   const i64 slabs = (elems + kSlab - 1) / kSlab;
   u32 sb = 0;
@@ -973,7 +1049,11 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
-  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : kPartWgPerCuPlain)));
+  static const int plain_wpc = [] {  // GLINT_PART_WPC: plain partition workgroups per CU (tuning knob)
+    const char* e = getenv("GLINT_PART_WPC");
+    return (e && atoi(e) > 0) ? atoi(e) : kPartWgPerCuPlain;
+  }();
+  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : plain_wpc)));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
   const i64 max_fitems = (i64)g.nb + n / kFItem + 1;
@@ -1023,7 +1103,9 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * 4);
   bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
-  bin_fpart_kernel<A><<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
+  static const int fpart_rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC");
+  const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fpart_rpc);
+  bin_fpart_kernel<A><<<gp, kFTPB, 0, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
                                             val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
   HIPCHK(hipGetLastError());
   static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
@@ -1031,7 +1113,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     return (e && atoi(e) > 0) ? atoi(e) : 64;
   }();
   bin_apply_kernel<V><<<(unsigned)std::min<i64>(nslots, (i64)s->cus * apply_bpc), kCTPB, 0, st>>>(
-      addr_b, val_b, cdesc, bc, s->elems, a.data, bin_prefetch_min());
+      addr_b, val_b, cdesc, bc, s->elems, a.data, bin_prefetch_min(), bin_sparse_max());
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }
