@@ -250,7 +250,8 @@ __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const in
 }
 
 // ---- bin_count ----------------------------------------------------------------------------------------
-template <bool MAT>
+// KIND: the partition layout (0 range, -1 read at run time), as push_check is specialised
+template <bool MAT, int KIND>
 __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                           i64 n, PartDesc part, const LaunchCtl* lctl, u32 ntiles,
                                                           int from_break, BinGeom g, u32* __restrict__ T,
@@ -263,26 +264,56 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
   __syncthreads();
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
-  RecRegs<double, MAT> r;  // keys (and cols) only: load_recs reads no values here
+  const i64 G = gridDim.x;
   u32 nvalid = 0;
-  i64 c = blockIdx.x;
-  if (c < nchunks) load_recs<double, MAT, false>(keys, cols, nullptr, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), r);
-  for (; c < nchunks; c += gridDim.x) {
-    const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
+  // keys (and cols) only: load_recs reads no values here. Two chunks in flight per workgroup (the
+  // partition grid is one 1024-thread workgroup per CU). Every step issues its loads unconditionally
+  // (chunk index clamped; a step past the end counts nothing), so the compiler can wait for one
+  // chunk's loads while the next chunk's stay in flight: with conditional loads it waited vmcnt(0).
+  auto load = [&](i64 c, RecRegs<double, MAT>& r) {
+    const i64 cc = min(c, nchunks - 1);
+    if constexpr (KIND == 0) {
+      // the range layout reads only the key's low word ((key - start).toInt): loading the whole key
+      // left its high half dead, the compiler reused that register while the load was in flight and
+      // had to wait for it (vmcnt(0)), so only one chunk was ever in flight
+      const i64 c0 = r0 + cc * kAChunk, c1 = min(n, c0 + kAChunk);
+#pragma unroll
+      for (int q = 0; q < kAPer; ++q) {
+        const i64 i = c0 + q * kATPB + threadIdx.x;
+        const i64 ii = i < c1 ? i : c1 - 1;
+        r.k[q] = (i64)(u64)reinterpret_cast<const u32*>(keys)[2 * ii];
+        r.cl[q] = MAT ? cols[ii] : 0;
+      }
+    } else {
+      load_recs<double, MAT, false>(keys, cols, nullptr, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+    }
+  };
+  auto step = [&](i64 c, RecRegs<double, MAT>& r) {
+    const i64 c0 = r0 + c * kAChunk, c1 = c < nchunks ? min(n, c0 + kAChunk) : c0;
     u32 bk[kAPer];
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       i64 ad;
-      bk[q] = (c0 + q * kATPB + tid < c1 && rec_addr<MAT>(part, r.k[q], r.cl[q], ad)) ? bucket_of((u32)ad, g) : kEmptySlot;
+      bk[q] = (c0 + q * kATPB + tid < c1 && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad)) ? bucket_of((u32)ad, g)
+                                                                                             : kEmptySlot;
     }
-    const i64 cn = c + gridDim.x;  // the next chunk's loads overlap this chunk's histogram
-    if (cn < nchunks) load_recs<double, MAT, false>(keys, cols, nullptr, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
+    load(c + 2 * G, r);  // two chunks ahead, into the registers just consumed
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       if (bk[q] != kEmptySlot) {
         atomicAdd(&h[hc + bk[q]], 1u);
         ++nvalid;
       }
+    }
+  };
+  if ((i64)blockIdx.x < nchunks) {
+    RecRegs<double, MAT> ra, rb;
+    i64 c = blockIdx.x;
+    load(c, ra);
+    load(c + G, rb);
+    for (; c < nchunks; c += 2 * G) {
+      step(c, ra);
+      step(c + G, rb);
     }
   }
   __syncthreads();
@@ -1090,7 +1121,10 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
-  bin_count_kernel<MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
+  if (a.part.kind == 0)
+    bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
+  else
+    bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
   HIPCHK(hipGetLastError());
   if (dedup) {
     bin_part_dedup_kernel<V, MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R,
@@ -1100,7 +1134,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
                                                  seglen, addr_a, val_a, a.err, bc, T, fitems);
   }
   HIPCHK(hipGetLastError());
-  const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * 4);
+  static const int fcount_rpc = resident_per_cu(bin_fcount_kernel, kFTPB, "GLINT_FCOUNT_BPC");
+  const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
   bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
   static const int fpart_rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC");
