@@ -49,6 +49,9 @@ constexpr int kPartWgPerCuDedup = kATPB == 1024 ? 1 : 2;
 constexpr int kPartWgPerCuPlain = kATPB == 1024 ? 1 : 2;  // what fits (VGPRs): a second round of
                                                            // workgroups measured 3-9 % slower
 constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments per bucket)
+#ifndef GLINT_FPART_WAVES
+#define GLINT_FPART_WAVES 4  // bin_fpart's register budget: waves per SIMD (build-time knob)
+#endif
 #ifndef GLINT_FPART_TPB
 #define GLINT_FPART_TPB 256
 #endif
@@ -684,8 +687,12 @@ __global__ __launch_bounds__(kFTPB) void bin_fcount_kernel(BinGeom g, u32 G, con
 // ob(b) + exclusive scan of H[b][*]; an item reserves its share of each slab with one returning
 // atomic (cur2), then moves tiles of kFTile records, staged in LDS so the stores are runs. The
 // bucket's first item also writes the apply items of its slabs.
+// LDS: the tile staging is static; the segment table (2G + 1 words) and the four per-slab arrays
+// (4 nf words) are sized at launch (fpart_dyn_bytes), so that small geometries fit more blocks per CU
+__host__ __device__ constexpr size_t fpart_dyn_bytes(u32 G, u32 nf) { return ((size_t)2 * G + 1 + (size_t)4 * nf) * 4; }
+
 template <typename A>
-__global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
+__global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART_WAVES))) void bin_fpart_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
                                                           BinCtl* bc, const u32* __restrict__ T,
                                                           const u32* __restrict__ H, u32* __restrict__ cur2,
                                                           const u32* __restrict__ segoff,
@@ -694,8 +701,13 @@ __global__ __launch_bounds__(kFTPB) void bin_fpart_kernel(BinGeom g, u32 G, cons
                                                           const A* __restrict__ val_in, u32* __restrict__ addr_out,
                                                           A* __restrict__ val_out, uint4* __restrict__ cdesc,
                                                           u64* hint, const u32* __restrict__ IH) {
-  __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
-  __shared__ u32 sst[kMaxDigit], fcur[kMaxDigit], tcnt[kMaxDigit], tpos[kMaxDigit];
+  extern __shared__ u32 fdyn[];
+  u32* const segst = fdyn;
+  u32* const segpre = fdyn + G;
+  u32* const sst = fdyn + 2 * G + 1;
+  u32* const fcur = sst + g.nf;
+  u32* const tcnt = fcur + g.nf;
+  u32* const tpos = tcnt + g.nf;
   __shared__ u32 st_a[kFTile];
   __shared__ A st_v[kFTile];
   const int tid = threadIdx.x;
@@ -1031,9 +1043,9 @@ u32 bin_sparse_max() {
 
 // resident blocks per CU of a kernel at its block size (occupancy query); `knob` overrides (tuning)
 template <typename K>
-int resident_per_cu(K kernel, int tpb, const char* knob) {
+int resident_per_cu(K kernel, int tpb, const char* knob, size_t dyn_lds = 0) {
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, tpb, 0) != hipSuccess || b < 1) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, tpb, dyn_lds) != hipSuccess || b < 1) {
     (void)hipGetLastError();
     b = 1;
   }
@@ -1138,9 +1150,12 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
   bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
-  static const int fpart_rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC");
-  const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fpart_rpc);
-  bin_fpart_kernel<A><<<gp, kFTPB, 0, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
+  const size_t fdyn = fpart_dyn_bytes(G, g.nf);
+  static int fpart_rpc[kMaxSegs + 1][11] = {};  // resident blocks per CU by (G, log2 nf)
+  int& rpc = fpart_rpc[G][g.fb];
+  if (!rpc) rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC", fdyn);
+  const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * rpc);
+  bin_fpart_kernel<A><<<gp, kFTPB, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
                                             val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
   HIPCHK(hipGetLastError());
   static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
