@@ -29,6 +29,9 @@ constexpr int kOrdChunk = kOrdTPB * kOrdR;     // records streamed per step (409
 constexpr int kOrdCap = 4096;                  // LDS list capacity (records)
 constexpr int kOrdPosBits = 12;                // list position bits in a sort key
 constexpr u64 kOrdPad = ~0ull;                 // sort padding (above every real key: keys < 2^44)
+constexpr int kOrdHashBits = 13;               // distinctness table: 8192 slots (load <= 0.5)
+constexpr int kOrdHash = 1 << kOrdHashBits;
+constexpr u32 kOrdEmpty = 0xFFFFFFFFu;         // no address: shards hold < 2^32 - 1 elements
 
 __device__ __forceinline__ u32 ordered_owner(u64 addr, u32 nwg) {
   const u64 h = addr * 0x9E3779B97F4A7C15ull;
@@ -50,10 +53,51 @@ __device__ __forceinline__ int ld_shard(const int* p) {
   return (int)__hip_atomic_load((const u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// distinctness-table slot of an address: murmur3's fmix32, low bits. It must not correlate with
+// ordered_owner: a multiplicative hash with a golden-ratio constant did (both took top bits of nearly
+// the same product), so a workgroup's addresses crowded 1/nwg of the table into long probe chains
+__device__ __forceinline__ u32 ord_hash(u32 x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x & (kOrdHash - 1);
+}
+
 // Sorts list[0, cnt) and folds each element's run in message order. Block-uniform cnt.
+// Fast path first: when no element occurs twice in the list (the usual message: distinct keys),
+// every run is one record, so each record is added to the shard directly -- no sort. Distinctness
+// is decided exactly by inserting every address into an LDS hash table (htab, all empty on entry and
+// on return); a repeated address sends the whole list down the sorted path.
 template <typename V>
-__device__ void ordered_flush(u64* skey, const V* sval, u32 cnt, V* data) {
+__device__ void ordered_flush(u64* skey, const V* sval, u32 cnt, V* data, u32* htab, u32* s_dup) {
   const u32 tid = threadIdx.x;
+  if (tid == 0) *s_dup = 0;
+  __syncthreads();
+  bool dup = false;
+  for (u32 i = tid; i < cnt; i += kOrdTPB) {
+    const u32 ad = (u32)(skey[i] >> kOrdPosBits);
+    u32 h = ord_hash(ad);
+    for (;;) {
+      const u32 prev = atomicCAS(&htab[h], kOrdEmpty, ad);
+      if (prev == kOrdEmpty) break;
+      if (prev == ad) { dup = true; break; }
+      h = (h + 1) & (kOrdHash - 1);
+    }
+  }
+  if (dup) *s_dup = 1;
+  __syncthreads();
+  const bool fast = *s_dup == 0;  // block-uniform
+  for (u32 h = tid; h < (u32)kOrdHash; h += kOrdTPB) htab[h] = kOrdEmpty;
+  if (fast) {
+    for (u32 i = tid; i < cnt; i += kOrdTPB) {  // list position i holds record position i
+      const u32 ad = (u32)(skey[i] >> kOrdPosBits);
+      data[ad] = vadd(ld_shard(data + ad), sval[i]);
+    }
+    __syncthreads();
+    return;
+  }
   u32 P = 64;
   while (P < cnt) P <<= 1;
   for (u32 i = cnt + tid; i < P; i += kOrdTPB) skey[i] = kOrdPad;
@@ -93,11 +137,13 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
   __shared__ u64 skey[kOrdCap];
   __shared__ V sval[kOrdCap];
   __shared__ u32 wsum[kOrdTPB / 64];
-  __shared__ u32 s_cnt;
+  __shared__ u32 s_cnt, s_dup;
+  __shared__ u32 htab[kOrdHash];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 nwg = gridDim.x, me = blockIdx.x;
   const i64 n = a.n;
   if (tid == 0) s_cnt = 0;
+  for (u32 h = tid; h < (u32)kOrdHash; h += kOrdTPB) htab[h] = kOrdEmpty;
   for (i64 base = 0; base < n; base += kOrdChunk) {
     const i64 r0 = base + (i64)tid * kOrdR;
     i64 k[kOrdR];
@@ -163,7 +209,7 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
     }
     u32 cur = s_cnt;
     if (cur + total > (u32)kOrdCap) {  // block-uniform
-      ordered_flush<V>(skey, sval, cur, a.data);
+      ordered_flush<V>(skey, sval, cur, a.data, htab, &s_dup);
       cur = 0;
     }
     u32 p = cur + woff + incl - cnt_t;
@@ -179,7 +225,7 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
     if (tid == 0) s_cnt = cur + total;
   }
   __syncthreads();
-  ordered_flush<V>(skey, sval, s_cnt, a.data);
+  ordered_flush<V>(skey, sval, s_cnt, a.data, htab, &s_dup);
   msg_signal(a.sig, a.err);
 }
 
