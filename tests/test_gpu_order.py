@@ -117,6 +117,45 @@ def test_order_vectors_matrix_on_gpu(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["double", "float"])
+@pytest.mark.parametrize("n", [1000, 4096, 8192, 79_999])
+@pytest.mark.parametrize("path", ["host", "dev_det"])
+def test_distinct_fast_path_beside_repeats(gpu, dtype, n, path):
+    """The fold's flushes add the records of an all-distinct list directly and sort only a list with
+    a repeated address. One push mixes both: distinct keys everywhere, plus the order-distinguishing
+    vectors on a few keys (their owners' lists take the sorted path). Bit-exact with the oracle."""
+    rng = np.random.default_rng(zlib.crc32(f"fast/{dtype}/{n}/{path}".encode()))
+    npd = np.float64 if dtype == "double" else np.float32
+    vecs = ORDER_VECTORS_F64 if dtype == "double" else ORDER_VECTORS_F32
+    size = 1 << 20
+    ks = rng.permutation(size)[:n + len(vecs)].astype(np.int64)
+    hot, keys = ks[:len(vecs)], list(ks[len(vecs):n])
+    vals = list(rng.uniform(-1, 1, len(keys)).astype(npd))
+    for (_, v), k in zip(vecs, hot):  # each vector's records at random positions, in its order
+        pos = np.sort(rng.choice(len(keys) + len(v), len(v), replace=False))
+        for p, x in zip(pos, v):
+            keys.insert(int(p), int(k))
+            vals.insert(int(p), npd(x))
+    keys, vals = np.array(keys, np.int64), np.array(vals, npd)
+    init = rng.uniform(-1, 1, size).astype(npd)
+    init[hot] = [d for d, _ in vecs]
+    ref = O.OracleVector(O.part_range(0, size), O.CODE[dtype])
+    ref.data[:] = init
+    assert ref.update(keys, vals) == -1
+    with PartialVector(RangePartition(0, 0, size), dtype, gpu) as sh:
+        _seeded_shard(sh, init)
+        if path == "host":
+            sh.update(keys, vals)
+        else:
+            import torch
+            dev = torch.device("cuda", gpu)
+            sh.update(torch.from_numpy(keys).to(dev), torch.from_numpy(vals).to(dev), deterministic=True)
+        got = sh.to_numpy()
+    np.testing.assert_array_equal(got[hot], [sequential(d, v, npd) for d, v in vecs])
+    np.testing.assert_array_equal(got, ref.data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["double", "float"])
 @pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 79_999, 131_072])
 def test_message_sized_pushes_are_sequential(gpu, dtype, n):
     """Akka-sized messages with heavy duplication, replayed onto one shard: the host-pointer path is
