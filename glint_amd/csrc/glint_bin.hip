@@ -252,6 +252,10 @@ __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const in
   }
 }
 
+#ifndef GLINT_COUNT_AHEAD
+#define GLINT_COUNT_AHEAD 2
+#endif
+constexpr int kCountAhead = GLINT_COUNT_AHEAD;  // bin_count: chunks in flight per workgroup
 // ---- bin_count ----------------------------------------------------------------------------------------
 // KIND: the partition layout (0 range, -1 read at run time), as push_check is specialised
 template <bool MAT, int KIND>
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
       bk[q] = (c0 + q * kATPB + tid < c1 && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad)) ? bucket_of((u32)ad, g)
                                                                                              : kEmptySlot;
     }
-    load(c + 2 * G, r);  // two chunks ahead, into the registers just consumed
+    load(c + kCountAhead * G, r);  // kCountAhead chunks ahead, into the registers just consumed
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       if (bk[q] != kEmptySlot) {
@@ -310,13 +314,13 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
     }
   };
   if ((i64)blockIdx.x < nchunks) {
-    RecRegs<double, MAT> ra, rb;
+    RecRegs<double, MAT> r[kCountAhead];
     i64 c = blockIdx.x;
-    load(c, ra);
-    load(c + G, rb);
-    for (; c < nchunks; c += 2 * G) {
-      step(c, ra);
-      step(c + G, rb);
+#pragma unroll
+    for (int j = 0; j < kCountAhead; ++j) load(c + j * G, r[j]);
+    for (; c < nchunks; c += kCountAhead * G) {
+#pragma unroll
+      for (int j = 0; j < kCountAhead; ++j) step(c + j * G, r[j]);
     }
   }
   __syncthreads();
@@ -448,6 +452,12 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
   BadRecs bad;
   u32 emitted = 0;
+  // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
+  // compiler can wait for one chunk's loads while the next chunk's stay in flight
+  auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
+    const i64 cc = min(c, nchunks - 1);
+    load_recs<V, MAT>(keys, cols, vals, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+  };
   auto step = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
     u32 ad[kAPer];
@@ -471,17 +481,18 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
     ph.mark(1);
     emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 3);
     // two chunks ahead, into the registers just consumed: in flight across the next chunk's work
-    const i64 cn = c + 2 * G;
-    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
+    load_chunk(c + 2 * G, r);
     ph.mark(2);
   };
   RecRegs<V, MAT> ra, rb;
   i64 c = w;
-  if (c < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), ra);
-  if (c + G < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + (c + G) * kAChunk, min(n, r0 + (c + G + 1) * kAChunk), rb);
-  for (; c < nchunks; c += 2 * G) {
-    step(c, ra);
-    if (c + G < nchunks) step(c + G, rb);
+  if (c < nchunks) {
+    load_chunk(c, ra);
+    load_chunk(c + G, rb);
+    for (; c < nchunks; c += 2 * G) {
+      step(c, ra);
+      step(c + G, rb);  // past the end: no valid record, nothing stored
+    }
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
   bad.report(err);
@@ -528,6 +539,12 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
   BadRecs bad;
   u32 emitted = 0;
+  // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
+  // compiler can wait for one chunk's loads while the next chunk's stay in flight
+  auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
+    const i64 cc = min(c, nchunks - 1);
+    load_recs<V, MAT>(keys, cols, vals, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+  };
   auto step = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
 #pragma unroll
@@ -560,8 +577,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
       }
     }
     ph.mark(9);
-    const i64 cn = c + 2 * G;  // two chunks ahead: in flight across this chunk and the next
-    if (cn < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + cn * kAChunk, min(n, r0 + (cn + 1) * kAChunk), r);
+    load_chunk(c + 2 * G, r);  // two chunks ahead: in flight across this chunk and the next
     ph.mark(10);
     __syncthreads();
     const u32 D = nused;
@@ -599,11 +615,13 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   };
   RecRegs<V, MAT> ra, rb;
   i64 c = w;
-  if (c < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + c * kAChunk, min(n, r0 + (c + 1) * kAChunk), ra);
-  if (c + G < nchunks) load_recs<V, MAT>(keys, cols, vals, r0 + (c + G) * kAChunk, min(n, r0 + (c + G + 1) * kAChunk), rb);
-  for (; c < nchunks; c += 2 * G) {
-    step(c, ra);
-    if (c + G < nchunks) step(c + G, rb);
+  if (c < nchunks) {
+    load_chunk(c, ra);
+    load_chunk(c + G, rb);
+    for (; c < nchunks; c += 2 * G) {
+      step(c, ra);
+      step(c + G, rb);  // past the end: no valid record, nothing stored
+    }
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
   bad.report(err);
