@@ -27,6 +27,7 @@ constexpr int kOrdTPB = 1024;                  // 16 waves: one workgroup per CU
 constexpr int kOrdR = 4;                       // consecutive records per thread per chunk
 constexpr int kOrdChunk = kOrdTPB * kOrdR;     // records streamed per step (4096)
 constexpr int kOrdCap = 4096;                  // LDS list capacity (records)
+static_assert(kOrdCap % kOrdTPB == 0, "a flush holds at most kOrdCap / kOrdTPB records per thread");
 constexpr int kOrdPosBits = 12;                // list position bits in a sort key
 constexpr u64 kOrdPad = ~0ull;                 // sort padding (above every real key: keys < 2^44)
 constexpr int kOrdHashBits = 13;               // distinctness table: 8192 slots (load <= 0.5)
@@ -66,36 +67,59 @@ __device__ __forceinline__ u32 ord_hash(u32 x) {
 }
 
 // Sorts list[0, cnt) and folds each element's run in message order. Block-uniform cnt.
-// Fast path first: when no element occurs twice in the list (the usual message: distinct keys),
-// every run is one record, so each record is added to the shard directly -- no sort. Distinctness
-// is decided exactly by inserting every address into an LDS hash table (htab, all empty on entry and
-// on return); a repeated address sends the whole list down the sorted path.
+// Only elements that occur more than once in the list need the sort: every address is inserted into
+// an LDS hash table (htab, all empty on entry and on return), a repeated address marks its slot in
+// dupbits, and records whose slot is unmarked -- runs of one record, the usual message is all of
+// them -- are added to the shard directly. The marked records (the repeated elements' whole runs)
+// are compacted to the list's front and bitonic-sorted by (address, position) as before.
 template <typename V>
-__device__ void ordered_flush(u64* skey, const V* sval, u32 cnt, V* data, u32* htab, u32* s_dup) {
+__device__ void ordered_flush(u64* skey, const V* sval, u32 cnt, V* data, u32* htab, u32* dupbits, u32* s_dcnt) {
   const u32 tid = threadIdx.x;
-  if (tid == 0) *s_dup = 0;
-  __syncthreads();
-  bool dup = false;
+  constexpr int kPer = kOrdCap / kOrdTPB;
   for (u32 i = tid; i < cnt; i += kOrdTPB) {
     const u32 ad = (u32)(skey[i] >> kOrdPosBits);
     u32 h = ord_hash(ad);
     for (;;) {
       const u32 prev = atomicCAS(&htab[h], kOrdEmpty, ad);
       if (prev == kOrdEmpty) break;
-      if (prev == ad) { dup = true; break; }
+      if (prev == ad) {
+        atomicOr(&dupbits[h >> 5], 1u << (h & 31));
+        break;
+      }
       h = (h + 1) & (kOrdHash - 1);
     }
   }
-  if (dup) *s_dup = 1;
   __syncthreads();
-  const bool fast = *s_dup == 0;  // block-uniform
-  for (u32 h = tid; h < (u32)kOrdHash; h += kOrdTPB) htab[h] = kOrdEmpty;
-  if (fast) {
-    for (u32 i = tid; i < cnt; i += kOrdTPB) {  // list position i holds record position i
-      const u32 ad = (u32)(skey[i] >> kOrdPosBits);
-      data[ad] = vadd(ld_shard(data + ad), sval[i]);
+  u64 dk[kPer];
+  u32 dmask = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {  // list position i holds record position i
+    const u32 i = tid + (u32)r * kOrdTPB;
+    dk[r] = 0;
+    if (i < cnt) {
+      const u64 key = skey[i];
+      const u32 ad = (u32)(key >> kOrdPosBits);
+      u32 h = ord_hash(ad);
+      while (htab[h] != ad) h = (h + 1) & (kOrdHash - 1);
+      if (dupbits[h >> 5] & (1u << (h & 31))) {
+        dk[r] = key;
+        dmask |= 1u << r;
+      } else {
+        data[ad] = vadd(ld_shard(data + ad), sval[i]);
+      }
     }
-    __syncthreads();
+  }
+  if (tid == 0) *s_dcnt = 0;
+  __syncthreads();  // every record is read (skey is free) and the table's lookups are done
+  for (u32 h = tid; h < (u32)kOrdHash; h += kOrdTPB) htab[h] = kOrdEmpty;
+  for (u32 w = tid; w < (u32)kOrdHash / 32; w += kOrdTPB) dupbits[w] = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r)
+    if (dmask & (1u << r)) skey[atomicAdd(s_dcnt, 1u)] = dk[r];
+  __syncthreads();
+  cnt = *s_dcnt;  // the repeated elements' records, in no particular order: the sort orders them
+  if (cnt == 0) {
+    __syncthreads();  // every thread has read the count before the caller refills the list
     return;
   }
   u32 P = 64;
@@ -137,13 +161,15 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
   __shared__ u64 skey[kOrdCap];
   __shared__ V sval[kOrdCap];
   __shared__ u32 wsum[kOrdTPB / 64];
-  __shared__ u32 s_cnt, s_dup;
+  __shared__ u32 s_cnt, s_dcnt;
   __shared__ u32 htab[kOrdHash];
+  __shared__ u32 dupbits[kOrdHash / 32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 nwg = gridDim.x, me = blockIdx.x;
   const i64 n = a.n;
   if (tid == 0) s_cnt = 0;
   for (u32 h = tid; h < (u32)kOrdHash; h += kOrdTPB) htab[h] = kOrdEmpty;
+  for (u32 w = tid; w < (u32)kOrdHash / 32; w += kOrdTPB) dupbits[w] = 0;
   for (i64 base = 0; base < n; base += kOrdChunk) {
     const i64 r0 = base + (i64)tid * kOrdR;
     i64 k[kOrdR];
@@ -209,7 +235,7 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
     }
     u32 cur = s_cnt;
     if (cur + total > (u32)kOrdCap) {  // block-uniform
-      ordered_flush<V>(skey, sval, cur, a.data, htab, &s_dup);
+      ordered_flush<V>(skey, sval, cur, a.data, htab, dupbits, &s_dcnt);
       cur = 0;
     }
     u32 p = cur + woff + incl - cnt_t;
@@ -225,7 +251,7 @@ __global__ __launch_bounds__(kOrdTPB) void push_ordered_kernel(PushArgs<V> a, in
     if (tid == 0) s_cnt = cur + total;
   }
   __syncthreads();
-  ordered_flush<V>(skey, sval, s_cnt, a.data, htab, &s_dup);
+  ordered_flush<V>(skey, sval, s_cnt, a.data, htab, dupbits, &s_dcnt);
   msg_signal(a.sig, a.err);
 }
 
