@@ -422,6 +422,42 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
   msg_signal(sig, err);
 }
 
+// A ring pull (one signalling workgroup, <= kRingPullMax records, keys read from the mapped slot
+// over PCIe): 1024 threads, four records each, every key load issued before any gather and every
+// gather before any store -- one PCIe round trip and one HBM round trip. The grid-stride kernels
+// above ran 8 dependent iterations per thread at 256 threads (their stores may alias the keys, so
+// the next iteration's loads could not move above them).
+constexpr int kRingPullTPB = 1024;
+constexpr int kRingPullPer = 4;
+constexpr i64 kRingPullMax = (i64)kRingPullTPB * kRingPullPer;
+template <typename V, bool MAT>
+__global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __restrict__ keys,
+                                                                const int32_t* __restrict__ cols, i64 n,
+                                                                const V* __restrict__ data, PartDesc part,
+                                                                V* __restrict__ out, ErrState* err, MsgSig sig) {
+  const i64 r0 = (i64)threadIdx.x * kRingPullPer;
+  i64 k[kRingPullPer];
+  int32_t c[kRingPullPer];
+#pragma unroll
+  for (int j = 0; j < kRingPullPer; ++j) {  // clamped, branch-free: all loads in flight together
+    const i64 r = r0 + j < n ? r0 + j : n - 1;
+    k[j] = keys[r];
+    c[j] = MAT ? cols[r] : 0;
+  }
+  V v[kRingPullPer];
+#pragma unroll
+  for (int j = 0; j < kRingPullPer; ++j) {
+    i64 l;
+    const bool ok = rec_addr<MAT>(part, k[j], c[j], l);
+    v[j] = ok ? data[l] : V(0);
+    if (!ok && r0 + j < n) record_error(err, r0 + j);
+  }
+#pragma unroll
+  for (int j = 0; j < kRingPullPer; ++j)
+    if (r0 + j < n) out[r0 + j] = v[j];
+  msg_signal(sig, err);
+}
+
 // PartialMatrix.get (PartialMatrix.scala:55-65)
 template <typename V>
 __global__ __launch_bounds__(kTPB) void mat_pull_kernel(const i64* rows, const int32_t* cols, i64 n, const V* data,
@@ -595,6 +631,11 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   if (n <= 0) return GLINT_OK;
   if (!keys || !out) return GLINT_EINVAL;
   const MsgSig sig = s->sig;
+  if (sig.done && n <= kRingPullMax) {
+    HIPCHK(launch_k(s, GLINT_K_VEC_PULL, ring_pull_kernel<V, false>, 1u, kRingPullTPB, st, keys, (const int32_t*)nullptr,
+                    n, (const V*)s->data, s->part, (V*)out, s->d_err, sig));
+    return GLINT_OK;
+  }
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
   if (pairs) {
     // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5)
@@ -614,6 +655,11 @@ int launch_mat_pull(glint_shard* s, const i64* rows, const int32_t* cols, void* 
   if (n <= 0) return GLINT_OK;
   if (!rows || !cols || !out) return GLINT_EINVAL;
   const MsgSig sig = s->sig;
+  if (sig.done && n <= kRingPullMax) {
+    HIPCHK(launch_k(s, GLINT_K_MAT_PULL, ring_pull_kernel<V, true>, 1u, kRingPullTPB, st, rows, cols, n,
+                    (const V*)s->data, s->part, (V*)out, s->d_err, sig));
+    return GLINT_OK;
+  }
   const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
   HIPCHK(launch_k(s, GLINT_K_MAT_PULL, mat_pull_kernel<V>, g, kTPB, st, rows, cols, n, (const V*)s->data, s->part,
                   (V*)out, s->d_err, sig));
