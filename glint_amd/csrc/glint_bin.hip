@@ -53,7 +53,7 @@ constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments
 #define GLINT_FPART_WAVES 4  // bin_fpart's register budget: waves per SIMD (build-time knob)
 #endif
 #ifndef GLINT_FPART_TPB
-#define GLINT_FPART_TPB 256
+#define GLINT_FPART_TPB 512
 #endif
 constexpr int kFTPB = GLINT_FPART_TPB; // fine partition workgroup size (build-time knob)
 constexpr int kFPer = 8;               // records per thread per tile
