@@ -59,7 +59,10 @@ constexpr int kFTPB = GLINT_FPART_TPB; // fine partition workgroup size (build-t
 constexpr int kFPer = 8;               // records per thread per tile
 constexpr int kFTile = kFTPB * kFPer;  // records staged per fine-partition step
 constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
-constexpr int kCTPB = 256;
+#ifndef GLINT_APPLY_TPB
+#define GLINT_APPLY_TPB 256
+#endif
+constexpr int kCTPB = GLINT_APPLY_TPB;  // slab-apply workgroup size (build-time knob)
 constexpr u32 kCItem = 16384;          // records per apply item at most
 constexpr u32 kEmptySlot = 0xFFFFFFFFu;
 constexpr u32 kItemEmpty = 2u;         // apply item slot left unused
