@@ -58,6 +58,7 @@ constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments
 constexpr int kFTPB = GLINT_FPART_TPB; // fine partition workgroup size (build-time knob)
 constexpr int kFPer = 8;               // records per thread per tile
 constexpr int kFTile = kFTPB * kFPer;  // records staged per fine-partition step
+constexpr int kFCTPB = 256;            // bin_fcount's workgroup size (512 measured slower there)
 constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
 #ifndef GLINT_APPLY_TPB
 #define GLINT_APPLY_TPB 256
@@ -639,23 +640,25 @@ __device__ __forceinline__ u32 seg_addr(u32 v, u32& s, const u32* segpre, const 
   return segst[s] + (v - segpre[s]);
 }
 
-// the addresses of records [t0, t0 + kFTile) of a bucket (kEmptySlot past v1); s is the thread's
+// the addresses of records [t0, t0 + TPB * kFPer) of a bucket (kEmptySlot past v1); s is the thread's
 // segment cursor (its records only move forward)
 // (clamped and branch-free: every lane issues kFPer loads; needs v1 > 0)
+template <int TPB>
 __device__ __forceinline__ void fetch_addr(u32 t0, u32 v1, u32& s, const u32* segpre, const u32* segst,
                                            const u32* __restrict__ addr_in, u32 (&a)[kFPer]) {
 #pragma unroll
   for (int q = 0; q < kFPer; ++q) {
-    const u32 v = t0 + q * kFTPB + threadIdx.x;
+    const u32 v = t0 + q * TPB + threadIdx.x;
     const u32 x = addr_in[seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst)];
     a[q] = v < v1 ? x : kEmptySlot;
   }
 }
 
 // bucket b's segment table into LDS; returns M_b
+template <int TPB>
 __device__ __forceinline__ u32 load_segments(const BinGeom& g, u32 G, u32 b, const u32* __restrict__ segoff,
                                              const u32* __restrict__ seglen, u32* segpre, u32* segst) {
-  const u32 M = block_scan<kFTPB, 4>(
+  const u32 M = block_scan<TPB, 4>(
       G, [&](u32 w) { return seglen[b * G + w]; },
       [&](u32 w, u32 excl) {
         segpre[w] = excl;
@@ -667,7 +670,7 @@ __device__ __forceinline__ u32 load_segments(const BinGeom& g, u32 G, u32 b, con
 }
 
 // per item: records per slab -> H[slab] (exact counts after dedup)
-__global__ __launch_bounds__(kFTPB) void bin_fcount_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
+__global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
                                                            const BinCtl* bc, const u32* __restrict__ segoff,
                                                            const u32* __restrict__ seglen,
                                                            const u32* __restrict__ addr_in, u32* __restrict__ H,
@@ -679,23 +682,23 @@ __global__ __launch_bounds__(kFTPB) void bin_fcount_kernel(BinGeom g, u32 G, con
   for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
     const uint2 d = fitems[it];
     const u32 b = d.x;
-    for (u32 f = tid; f < g.nf; f += kFTPB) fh[f] = 0;
-    const u32 M = load_segments(g, G, b, segoff, seglen, segpre, segst);
+    for (u32 f = tid; f < g.nf; f += kFCTPB) fh[f] = 0;
+    const u32 M = load_segments<kFCTPB>(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
     u32 s = 0;
     u32 a[kFPer];
-    if (v1 > v0) fetch_addr(v0, v1, s, segpre, segst, addr_in, a);
-    for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
+    if (v1 > v0) fetch_addr<kFCTPB>(v0, v1, s, segpre, segst, addr_in, a);
+    for (u32 t0 = v0; t0 < v1; t0 += kFCTPB * kFPer) {
       u32 cur[kFPer];
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) cur[q] = a[q];
-      fetch_addr(t0 + kFTile, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
+      fetch_addr<kFCTPB>(t0 + kFCTPB * kFPer, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
 #pragma unroll
       for (int q = 0; q < kFPer; ++q)
         if (cur[q] != kEmptySlot) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
     }
     __syncthreads();
-    for (u32 f = tid; f < g.nf; f += kFTPB) {
+    for (u32 f = tid; f < g.nf; f += kFCTPB) {
       const u32 c = fh[f];
       IH[(size_t)it * g.nf + f] = c;  // this item's own histogram: bin_fpart reserves from it
       if (c) atomicAdd(&H[b * g.nf + f], c);
@@ -773,7 +776,7 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
       for (u32 x = used_slots + tid; x < nslots; x += kFTPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
     }
     ph.mark(21);
-    const u32 M = load_segments(g, G, b, segoff, seglen, segpre, segst);
+    const u32 M = load_segments<kFTPB>(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
     ph.mark(22);
     // this item's records per slab (counted by bin_fcount); reserve the item's share of each slab
@@ -1167,9 +1170,9 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
                                                  seglen, addr_a, val_a, a.err, bc, T, fitems);
   }
   HIPCHK(hipGetLastError());
-  static const int fcount_rpc = resident_per_cu(bin_fcount_kernel, kFTPB, "GLINT_FCOUNT_BPC");
+  static const int fcount_rpc = resident_per_cu(bin_fcount_kernel, kFCTPB, "GLINT_FCOUNT_BPC");
   const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
-  bin_fcount_kernel<<<gf, kFTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
+  bin_fcount_kernel<<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
   const size_t fdyn = fpart_dyn_bytes(G, g.nf);
   static int fpart_rpc[kMaxSegs + 1][11] = {};  // resident blocks per CU by (G, log2 nf)
