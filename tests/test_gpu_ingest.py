@@ -166,6 +166,32 @@ def test_async_matrix_pulls(gpu, dtype):
         np.testing.assert_array_equal(rows_big, ref.data.reshape(rows_n, cols_n)[qr])
 
 
+@pytest.mark.parametrize("n", [4095, 4096, 4097])
+def test_async_matrix_element_pulls_at_the_ring_bound(gpu, n):
+    """Element pulls of up to 4096 records run as one 1024-thread signalling kernel reading the
+    mapped slot; 4097 goes through DMA. Both answer like the oracle, and a bad column is reported
+    as its record index."""
+    rng = np.random.default_rng(n)
+    rows_n, cols_n = 700, 33
+    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE["double"])
+    with PartialMatrix(RangePartition(0, 0, rows_n), cols_n, "double", gpu) as sh:
+        r = rng.integers(0, rows_n, 20_000).astype(np.int64)
+        c = rng.integers(0, cols_n, 20_000).astype(np.int32)
+        v = _vals(rng, "double", 20_000)
+        sh.push_async(r, c, v)
+        ref.update(r, c, v)
+        qr = rng.integers(0, rows_n, n).astype(np.int64)
+        qc = rng.integers(0, cols_n, n).astype(np.int32)
+        t, elems = sh.pull_async(qr, qc)
+        sh.wait(t)
+        np.testing.assert_array_equal(elems, ref.data.reshape(rows_n, cols_n)[qr, qc])
+        qc[n - 2] = cols_n  # out of range: the JVM throws at record n - 2
+        t, _ = sh.pull_async(qr, qc)
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.wait(t)
+        assert ei.value.record == n - 2
+
+
 def test_async_pull_bad_key_and_wire(gpu):
     size = 1000
     with PartialVector(RangePartition(0, 0, size), "double", gpu) as sh:
