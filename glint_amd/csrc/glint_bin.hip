@@ -25,6 +25,7 @@
 #include "glint_device.h"
 #include "glint_host.h"
 
+#include <atomic>
 #include <cstring>
 
 namespace glint {
@@ -1175,9 +1176,13 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   bin_fcount_kernel<<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
   const size_t fdyn = fpart_dyn_bytes(G, g.nf);
-  static int fpart_rpc[kMaxSegs + 1][11] = {};  // resident blocks per CU by (G, log2 nf)
-  int& rpc = fpart_rpc[G][g.fb];
-  if (!rpc) rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC", fdyn);
+  // resident blocks per CU by (G, log2 nf); shards on several host threads may fill it at once
+  static std::atomic<int> fpart_rpc[kMaxSegs + 1][11] = {};
+  int rpc = fpart_rpc[G][g.fb].load(std::memory_order_relaxed);
+  if (!rpc) {
+    rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC", fdyn);
+    fpart_rpc[G][g.fb].store(rpc, std::memory_order_relaxed);
+  }
   const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * rpc);
   bin_fpart_kernel<A><<<gp, kFTPB, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
                                             val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
