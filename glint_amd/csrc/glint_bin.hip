@@ -53,12 +53,8 @@ constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments
 #ifndef GLINT_FPART_WAVES
 #define GLINT_FPART_WAVES 4  // bin_fpart's register budget: waves per SIMD (build-time knob)
 #endif
-#ifndef GLINT_FPART_TPB
-#define GLINT_FPART_TPB 512
-#endif
-constexpr int kFTPB = GLINT_FPART_TPB; // fine partition workgroup size (build-time knob)
-constexpr int kFPer = 8;               // records per thread per tile
-constexpr int kFTile = kFTPB * kFPer;  // records staged per fine-partition step
+constexpr int kFPer = 8;               // records per thread per fine-partition tile (tile = TPB * kFPer;
+                                       // bin_fpart runs at 256 or 512 threads, chosen per push)
 constexpr int kFCTPB = 256;            // bin_fcount's workgroup size (512 measured slower there)
 constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
 #ifndef GLINT_APPLY_TPB
@@ -710,14 +706,14 @@ __global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, co
 
 // per item: its records moved to their slab ranges. Slab f of bucket b starts at
 // ob(b) + exclusive scan of H[b][*]; an item reserves its share of each slab with one returning
-// atomic (cur2), then moves tiles of kFTile records, staged in LDS so the stores are runs. The
+// atomic (cur2), then moves tiles of TPB * kFPer records, staged in LDS so the stores are runs. The
 // bucket's first item also writes the apply items of its slabs.
 // LDS: the tile staging is static; the segment table (2G + 1 words) and the four per-slab arrays
 // (4 nf words) are sized at launch (fpart_dyn_bytes), so that small geometries fit more blocks per CU
 __host__ __device__ constexpr size_t fpart_dyn_bytes(u32 G, u32 nf) { return ((size_t)2 * G + 1 + (size_t)4 * nf) * 4; }
 
-template <typename A>
-__global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART_WAVES))) void bin_fpart_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
+template <typename A, int TPB>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART_WAVES))) void bin_fpart_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
                                                           BinCtl* bc, const u32* __restrict__ T,
                                                           const u32* __restrict__ H, u32* __restrict__ cur2,
                                                           const u32* __restrict__ segoff,
@@ -733,8 +729,8 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
   u32* const fcur = sst + g.nf;
   u32* const tcnt = fcur + g.nf;
   u32* const tpos = tcnt + g.nf;
-  __shared__ u32 st_a[kFTile];
-  __shared__ A st_v[kFTile];
+  __shared__ u32 st_a[(TPB * kFPer)];
+  __shared__ A st_v[(TPB * kFPer)];
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0 && hint)  // for the host's next binned push: how much did dedup keep?
     __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -752,20 +748,20 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
     const u32 b = d.x;
     // where the bucket's records go (raw capacities: holes only at bucket ends) and its item slots
     u32 ob = 0, ib = 0;
-    for (u32 x = tid; x < b; x += kFTPB) {
+    for (u32 x = tid; x < b; x += TPB) {
       const u32 t = T[x];
       ob += t;
       ib += g.nf + (t + kCItem - 1) / kCItem;
     }
-    ob = block_sum<kFTPB>(ob);
-    ib = block_sum<kFTPB>(ib);
-    for (u32 f = tid; f < g.nf; f += kFTPB) tcnt[f] = 0;
-    block_scan<kFTPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
+    ob = block_sum<TPB>(ob);
+    ib = block_sum<TPB>(ib);
+    for (u32 f = tid; f < g.nf; f += TPB) tcnt[f] = 0;
+    block_scan<TPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
     ph.mark(20);
     if (d.y == 0) {  // the bucket's apply items {slab, first, end, exclusive}, then unused slots
       const u32 nslots = g.nf + (T[b] + kCItem - 1) / kCItem;
       if (b == g.nb - 1 && tid == 0) bc->nslots = ib + nslots;  // bin_apply's item count
-      const u32 used_slots = block_scan<kFTPB, 4>(
+      const u32 used_slots = block_scan<TPB, 4>(
           g.nf, [&](u32 f) { return (H[b * g.nf + f] + kCItem - 1) / kCItem; },
           [&](u32 f, u32 excl) {
             const u32 c = H[b * g.nf + f], s0 = sst[f];
@@ -774,16 +770,16 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
               cdesc[ib + excl + q] =
                   make_uint4(b * g.nf + f, s0 + q * kCItem, s0 + min(c, (q + 1) * kCItem), m == 1u ? 1u : 0u);
           });
-      for (u32 x = used_slots + tid; x < nslots; x += kFTPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
+      for (u32 x = used_slots + tid; x < nslots; x += TPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
     }
     ph.mark(21);
-    const u32 M = load_segments<kFTPB>(g, G, b, segoff, seglen, segpre, segst);
+    const u32 M = load_segments<TPB>(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
     ph.mark(22);
     // this item's records per slab (counted by bin_fcount); reserve the item's share of each slab
     __syncthreads();
     ph.mark(23);
-    for (u32 f = tid; f < g.nf; f += kFTPB) {
+    for (u32 f = tid; f < g.nf; f += TPB) {
       const u32 c = IH[(size_t)it * g.nf + f];
       fcur[f] = c ? sst[f] + atomicAdd(&cur2[b * g.nf + f], c) : 0u;
       tcnt[f] = 0;
@@ -797,7 +793,7 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
     auto fetch = [&](u32 t0) {  // a tile's addresses and values (clamped, branch-free)
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
-        const u32 v = t0 + q * kFTPB + tid;
+        const u32 v = t0 + q * TPB + tid;
         const u32 r = seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst);
         const u32 x = addr_in[r];
         nv[q] = val_in[r];
@@ -807,7 +803,7 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
     // the bucket's output range as buffer descriptors (counted stores)
     const BufOut oa = buf_out(addr_out + ob, T[b] * 4u), ov = buf_out(val_out + ob, T[b] * (u32)sizeof(A));
     if (v1 > v0) fetch(v0);
-    for (u32 t0 = v0; t0 < v1; t0 += kFTile) {
+    for (u32 t0 = v0; t0 < v1; t0 += (TPB * kFPer)) {
       u32 a[kFPer], rank[kFPer];
       A val[kFPer];
 #pragma unroll
@@ -815,14 +811,14 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
         a[q] = na[q];
         val[q] = nv[q];
       }
-      fetch(t0 + kFTile);  // the next tile, in flight during this one's ranking, scan and stores
+      fetch(t0 + (TPB * kFPer));  // the next tile, in flight during this one's ranking, scan and stores
       ph.mark(25);
 #pragma unroll
       for (int q = 0; q < kFPer; ++q)
         if (a[q] != kEmptySlot) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
       __syncthreads();
       ph.mark(26);
-      const u32 total = block_scan<kFTPB, 4>(
+      const u32 total = block_scan<TPB, 4>(
           g.nf, [&](u32 f) { return tcnt[f]; },
           [&](u32 f, u32 excl) {
             tpos[f] = fcur[f] - excl;  // output slot of staging position p (slab f) = tpos[f] + p
@@ -841,9 +837,9 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
       __syncthreads();
       ph.mark(28);
 #pragma unroll
-      for (int j = 0; j < kFPer; ++j) {  // total <= kFTile
-        if ((u32)(j * kFTPB) >= total) break;  // workgroup-uniform: no store instructions past the tile
-        const u32 p = tid + j * kFTPB;
+      for (int j = 0; j < kFPer; ++j) {  // total <= (TPB * kFPer)
+        if ((u32)(j * TPB) >= total) break;  // workgroup-uniform: no store instructions past the tile
+        const u32 p = tid + j * TPB;
         const bool on = p < total;
         const u32 x = st_a[p];
         const u32 rel = tpos[on ? fine_of(x, g) : 0u] + p - ob;
@@ -852,7 +848,7 @@ __global__ __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPA
       }
       __syncthreads();
       ph.mark(29);
-      for (u32 f = tid; f < g.nf; f += kFTPB) tcnt[f] = 0;
+      for (u32 f = tid; f < g.nf; f += TPB) tcnt[f] = 0;
       __syncthreads();
       ph.mark(30);
     }
@@ -1176,16 +1172,28 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   bin_fcount_kernel<<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
   const size_t fdyn = fpart_dyn_bytes(G, g.nf);
-  // resident blocks per CU by (G, log2 nf); shards on several host threads may fill it at once
-  static std::atomic<int> fpart_rpc[kMaxSegs + 1][11] = {};
-  int rpc = fpart_rpc[G][g.fb].load(std::memory_order_relaxed);
-  if (!rpc) {
-    rpc = resident_per_cu(bin_fpart_kernel<A>, kFTPB, "GLINT_FPART_BPC", fdyn);
-    fpart_rpc[G][g.fb].store(rpc, std::memory_order_relaxed);
-  }
-  const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * rpc);
-  bin_fpart_kernel<A><<<gp, kFTPB, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
+  // workgroup size: 512 threads (4096-record tiles, whole-line runs) unless the push has no more
+  // items than 256-thread blocks fit at once (small pushes: parallelism beats tile size)
+  static std::atomic<int> fpart_rpc[2][kMaxSegs + 1][11] = {};  // resident blocks per CU by (TPB, G, log2 nf)
+  auto rpc_of = [&](int w, auto kernel, int tpb) {
+    int r = fpart_rpc[w][G][g.fb].load(std::memory_order_relaxed);
+    if (!r) {
+      r = resident_per_cu(kernel, tpb, "GLINT_FPART_BPC", fdyn);
+      fpart_rpc[w][G][g.fb].store(r, std::memory_order_relaxed);
+    }
+    return r;
+  };
+  const int r256 = rpc_of(0, bin_fpart_kernel<A, 256>, 256);
+  if (max_fitems <= (i64)s->cus * r256) {
+    const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * r256);
+    bin_fpart_kernel<A, 256><<<gp, 256, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
                                             val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
+  } else {
+    const int r512 = rpc_of(1, bin_fpart_kernel<A, 512>, 512);
+    const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * r512);
+    bin_fpart_kernel<A, 512><<<gp, 512, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
+                                            val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
+  }
   HIPCHK(hipGetLastError());
   static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
     const char* e = getenv("GLINT_BIN_APPLY_BPC");
