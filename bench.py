@@ -9,11 +9,12 @@ Workload (default): BASELINE.json configs[1] -- 1 GPU, 2^28-key Double vector, d
 push (keys[i] = start + i, values U[-1,1) from seed 42). With N GPUs (torchrun), the key space is
 RangePartitioner(N, N * 2^28) and every rank pushes its own dense range (cfg4a: clients own
 contiguous key ranges, no exchange step) -- weak scaling, no collective in the timed region.
+The default 1-GPU run also measures the north-star size (2^30 keys, `north_star_2p30`).
 
 Algorithmic bytes per record: 8 (key) + 8 (value) + 8 + 8 (shard read + write)
 = 32 B; value = all ranks' algorithmic bytes / max-over-ranks wall time of the K timed steps.
-The roofline figure uses the push kernel's own device time from HIP events recorded around each
-launch on its stream (glint_prof_*); PMC HBM traffic comes from profiles/ when present.
+The roofline figure uses the push kernels' own device time from HIP events carried on each launch
+on its stream (glint_prof_*); PMC HBM traffic comes from profiles/ when present.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--log2-keys 28]
                     [--pattern dense|zipf|matrix|exchange|pull|rowpull] [--scaling weak|strong]
@@ -25,6 +26,11 @@ under torchrun (WORLD_SIZE set) every process is one rank.
 shard of RangePartitioner(N, N * 2^17) rows (8 x 2^17 = the 2^20-row matrix at N = 8), pushed
 2^23 triplets (2^26 / 8) with rows Zipf(1.0) and cols uniform: PartialMatrix.update
 (PartialMatrix.scala:74-83) through glint_mat_push_dev. Algorithmic bytes n(8+4+8) + 16U.
+
+--pattern exchange is cfg4b: every rank pushes 2^26 uniform keys of the whole key space through
+DistributedBigVector.push (route + all-to-all + local push, AsyncBigVector.scala:96-121); the
+post-run check regenerates every rank's batches and compares the rank's shard with a torch fp64
+segment sum, and U (distinct elements a shard receives) is counted, not estimated.
 """
 from __future__ import annotations
 
@@ -58,6 +64,7 @@ def parse():
                     help="weak: 2^k keys per GPU (cfg4a); strong: one 2^k-key vector split over the GPUs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true", help="skip the 2^30 leg of the default 1-GPU run")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run shard check")
     return ap.parse_args()
 
@@ -95,13 +102,15 @@ def cpu_baseline(log2_keys: int, seconds: float):
         if el >= seconds:
             break
     gbs = 32.0 * n * passes / el / 1e9
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     out = {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+           "host_cores": os.cpu_count(), "cores_available_to_process": avail,
            "sample": f"{passes} x PartialVector[Double].update of 2^{min(log2_keys, 26)} dense records "
                      f"(oracle/glint_oracle.c scalar loop, 1 thread = 1 actor), {el:.1f} s"}
     # the same sample as P = 8 range shards (cfg4's partition count), one actor thread per shard on
     # min(P, host cores) threads
     P = 8
-    threads = max(1, min(P, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    threads = max(1, min(P, avail))
     q = n // P
     starts, ends = [i * q for i in range(P)], [(i + 1) * q for i in range(P)]
     datas = [data[i * q:(i + 1) * q] for i in range(P)]
@@ -150,88 +159,70 @@ def spawn_ranks(n: int) -> int:
     return max(codes, key=abs)
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
+def zipf_rows(rng, n: int, count: int):
+    """Zipf(1.0) ranks over [0, n) (word frequency; inverse CDF of the 1/k law)."""
+    import numpy as np
+    return np.minimum(np.floor(np.power(float(n), rng.random(count))).astype(np.int64) - 1, n - 1)
+
+
+def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: int, check: bool) -> dict:
+    """Builds the workload of one bench line, times `steps` pushes (or pulls) after `warmup`, checks
+    the shard afterwards and returns the line's fields (without the CPU baseline)."""
     import numpy as np
     import torch
     import torch.distributed as dist
-    import glint_amd  # noqa: F401  (loads libglint_gpu.so; fails loudly without it)
     from glint_amd import PartialMatrix, PartialVector, RangePartitioner
     from glint_amd import _native as N
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    # rehearsal hooks (not used by the driver): GLINT_BENCH_DEVICE pins every rank to one GPU and
-    # GLINT_BENCH_BACKEND=gloo replaces RCCL, so the N > 1 path can run on a one-GPU box
-    local = int(os.environ.get("GLINT_BENCH_DEVICE", local))
-    backend = os.environ.get("GLINT_BENCH_BACKEND", "nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    pat = args.pattern
+    lib, dev, world, rank, backend = ctx["lib"], ctx["dev"], ctx["world"], ctx["rank"], ctx["backend"]
+    local = dev.index
     exch = pat == "exchange"
-    if world > 1 or exch:
-        if world == 1:  # the exchange path needs a process group even alone (RCCL world 1)
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29561")
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
-    lib = N.load()
     mat = pat in ("matrix", "rowpull")
-    strong = args.scaling == "strong"
+    strong = scaling == "strong"
     cols_n = 512
     if mat:
         partitioner = RangePartitioner.apply(world, world * (1 << 17))
     elif strong:  # total work fixed: one 2^k-key vector range-sharded over the ranks
-        partitioner = RangePartitioner.apply(world, 1 << args.log2_keys)
+        partitioner = RangePartitioner.apply(world, 1 << log2_keys)
     else:
-        partitioner = RangePartitioner.apply(world, world * (1 << args.log2_keys))
+        partitioner = RangePartitioner.apply(world, world * (1 << log2_keys))
     part = partitioner.all()[rank]
     shard = PartialMatrix(part, cols_n, "double", device=local) if mat else PartialVector(part, "double", device=local)
     n = part.size
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
-    vals = torch.rand(n if not mat else 1 << 23, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
     cols = out = None
     push = pat in ("dense", "zipf", "matrix", "exchange")
     scope = "per GPU" if not strong else f"1/{world} of the vector per GPU"
+    fill_v = None
+    u_note = ""
     if pat == "matrix":
-        # cfg5: rows Zipf(1.0) (word frequency; inverse CDF of the 1/k law) through a seeded
-        # permutation of the shard's rows, cols uniform [0, 512), seed 42 + rank
+        # cfg5: rows Zipf(1.0) through a seeded permutation of the shard's rows, cols uniform [0, 512)
         rng = np.random.default_rng(42 + rank)
         nrec = 1 << 23
-        ranks = np.minimum(np.floor(np.power(float(n), rng.random(nrec))).astype(np.int64) - 1, n - 1)
-        r = rng.permutation(n)[ranks].astype(np.int64)
+        r = rng.permutation(n)[zipf_rows(rng, n, nrec)].astype(np.int64)
         c = rng.integers(0, cols_n, nrec).astype(np.int32)
         uniq = int(np.unique(r * cols_n + c).size)
         keys = torch.from_numpy(r + part.start).to(dev)
         cols = torch.from_numpy(c).to(dev)
+        vals = torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
         tag = "matrix_2p17x512"
         bytes_per_step = 20.0 * nrec + 16.0 * uniq  # SURVEY.md section 8d: n(8+4+8) + U(8+8)
         workload = (f"cfg5 per GPU: {nrec} Zipf(1.0)-row x uniform-col triplets into a 2^17 x 512 Double "
                     f"matrix shard of RangePartitioner({world}, {world}x2^17) rows")
     elif pat == "rowpull":
         # cfg5 row pull: r = 2^16 Zipf(1.0) rows (PartialMatrix.getRows, PartialMatrix.scala:37-46)
-        # from a 2^17 x 512 Double shard filled by a dense row-major push beforehand
+        # from a 2^17 x 512 Double shard filled by one dense row-major push beforehand
         rng = np.random.default_rng(42 + rank)
         nrec = 1 << 16
-        ranks = np.minimum(np.floor(np.power(float(n), rng.random(nrec))).astype(np.int64) - 1, n - 1)
-        keys = torch.from_numpy(rng.permutation(n)[ranks].astype(np.int64) + part.start).to(dev)
+        keys = torch.from_numpy(rng.permutation(n)[zipf_rows(rng, n, nrec)].astype(np.int64) + part.start).to(dev)
         fill_r = torch.arange(part.start, part.end, dtype=torch.int64, device=dev).repeat_interleave(cols_n)
         fill_c = torch.arange(cols_n, dtype=torch.int32, device=dev).repeat(n)
         fill_v = torch.rand(n * cols_n, dtype=torch.float64, device=dev, generator=gen)
         shard.update(fill_r, fill_c, fill_v)
         del fill_r, fill_c
         out = torch.empty((nrec, cols_n), dtype=torch.float64, device=dev)
+        vals = None
         uniq = nrec
         tag = "rowpull_2p17x512"
         bytes_per_step = (8.0 + 2.0 * cols_n * 8) * nrec  # 8 200 B per row
@@ -240,39 +231,48 @@ def main():
     elif exch:
         # cfg4b: every rank's batch holds keys of every rank's range (uniform over the whole key
         # space), so each push is route + gather (glint_route_gather_dev) + all_to_all_single + the
-        # local push
+        # local push. Keys and values come from per-rank generators that every rank can replay.
         from glint_amd.dist import DistributedBigVector
         dv = DistributedBigVector(partitioner, [shard], partitioner.size, np.float64, None, dev)
         nrec = 1 << 26
-        kg = torch.Generator(device=dev)
-        kg.manual_seed(1042 + rank)
-        keys = torch.randint(0, partitioner.size, (nrec,), dtype=torch.int64, device=dev, generator=kg)
-        vals = torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
-        # distinct elements a rank receives per push (uniform, ~nrec records into n keys): expected value
+
+        def batch(src):
+            kg = torch.Generator(device=dev)
+            kg.manual_seed(1042 + src)
+            vg = torch.Generator(device=dev)
+            vg.manual_seed(2042 + src)
+            k = torch.randint(0, partitioner.size, (nrec,), dtype=torch.int64, device=dev, generator=kg)
+            return k, torch.rand(nrec, dtype=torch.float64, device=dev, generator=vg) * 2 - 1
+
+        keys, vals = batch(rank)
+        # distinct elements a rank receives per push: counted over all ranks' batches by the check,
+        # the expected value until then
         uniq = int(n * (1.0 - np.exp(-nrec / n)))
-        tag = f"exchange_2p{args.log2_keys}"
+        u_note = " (U estimated)"
+        tag = f"exchange_2p{log2_keys}"
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
         workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({world}, "
-                    f"{partitioner.size}); route + gather + RCCL all-to-all + local push (U estimated)")
+                    f"{partitioner.size}); route + gather + RCCL all-to-all + local push")
     elif pat in ("dense", "pull"):
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
+        vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
         nrec, uniq = n, n
         if pat == "pull":  # PartialVector.get (PartialVector.scala:51-60) of every key of the shard
             shard.update(keys, vals)
             out = torch.empty(n, dtype=torch.float64, device=dev)
-            tag = f"pull_2p{args.log2_keys}"
+            tag = f"pull_2p{log2_keys}"
             bytes_per_step = 24.0 * nrec  # key 8 + element 8 + out 8
             workload = f"dense pull (get) of every key, 2^{n.bit_length() - 1}-key Double shard {scope}"
         else:
-            tag = f"dense_2p{args.log2_keys}"
+            tag = f"dense_2p{log2_keys}"
             bytes_per_step = 32.0 * nrec  # key 8 + value 8 + element read 8 + write 8
             if strong:
-                workload = (f"strong scaling: one 2^{args.log2_keys}-key Double vector, RangePartitioner({world}, "
-                            f"2^{args.log2_keys}); each rank pushes its own dense range")
+                workload = (f"strong scaling: one 2^{log2_keys}-key Double vector, RangePartitioner({world}, "
+                            f"2^{log2_keys}); each rank pushes its own dense range")
             elif world == 1:
-                workload = f"cfg2: dense contiguous-range push, 2^{args.log2_keys}-key Double vector per GPU"
+                workload = f"cfg2: dense contiguous-range push, 2^{log2_keys}-key Double vector per GPU"
             else:
-                workload = (f"cfg4a: {world} GPUs, RangePartitioner({world}, {world}x2^{args.log2_keys}), "
+                workload = (f"cfg4a: {world} GPUs, RangePartitioner({world}, {world}x2^{log2_keys}), "
                             f"each rank pushes its own dense range")
     else:
         # cfg3: Zipf(1.1) ranks mapped through a seeded permutation of the shard, n = N/4 records
@@ -285,10 +285,10 @@ def main():
         k = perm[ranks].astype(np.int64) + part.start
         uniq = int(np.unique(k).size)
         keys = torch.from_numpy(k).to(dev)
-        vals = vals[:nrec].contiguous()
-        tag = f"zipf_2p{args.log2_keys}"
+        vals = torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+        tag = f"zipf_2p{log2_keys}"
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
-        workload = f"cfg3: Zipf(1.1) push of {nrec} records into a 2^{args.log2_keys}-key Double shard"
+        workload = f"cfg3: Zipf(1.1) push of {nrec} records into a 2^{log2_keys}-key Double shard"
     stream = torch.cuda.current_stream(dev).cuda_stream
     h = shard.handle
 
@@ -307,11 +307,12 @@ def main():
         if rc:
             raise RuntimeError(N.strerror(rc))
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-        # one push at a time: the adaptive tail switch reads the previous push's hint (written by
-        # its push_apply) at launch, so its one-time scratch allocation lands in the warm-up
-        torch.cuda.synchronize(dev)
+        # one push at a time, each ended by the shard's sync point: the adaptive tail switch decides
+        # from the previous push's tail as published at its sync, so the timed pushes take the path
+        # the warm-up settled on (and its one-time scratch allocation lands in the warm-up)
+        shard.sync(stream)
     shard.sync(stream)
     lib.glint_prof_reset(h)
     lib.glint_prof_enable(h, 1)
@@ -319,7 +320,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -338,43 +339,66 @@ def main():
         return (ms.value / cnt.value if cnt.value else 0.0), cnt.value
 
     # post-run check. Dense push: the shard holds (W+K) additions of each record, bit-exact (each
-    # key once per push, the ordered path). Zipf / matrix: repeated keys sum in an unordered way, so
-    # the check is a torch fp64 segment sum of one push times (W+K), within the north star's 1e-6
-    # relative. Pulls: the pulled values equal the shard's contents bit for bit.
+    # key once per push, the ordered path). Zipf / matrix / exchange: repeated keys sum in an
+    # unordered way, so the check is a torch fp64 segment sum of one push (of every rank's batch,
+    # for the exchange) times (W+K), within the north star's 1e-6 relative. Pulls: the pulled values
+    # equal what was pushed, bit for bit (a row pull: the dense fill's rows).
     ok = None
-    if not args.no_check and not exch:  # the exchange layer's parity lives in tests/ (dist_workers)
-        reps = args.warmup + args.steps
+    reps = warmup + steps
+    recv = nrec  # records this rank's shard takes per push
+    if check:
         if pat == "dense":
             acc = torch.zeros_like(vals)
             for _ in range(reps):
                 acc += vals
-            got = shard.get(keys)
-            ok = bool(torch.equal(got, acc))
+            ok = bool(torch.equal(shard.get(keys), acc))
             del acc
         elif pat == "pull":
             ok = bool(torch.equal(out, vals))
         elif pat == "rowpull":
-            ok = bool(torch.equal(out, shard.getRows(keys)))
+            ok = bool(torch.equal(out, fill_v.view(n, cols_n)[keys - part.start]))
         else:
-            if mat:
+            if exch:
+                # every rank's batch, replayed: the records of this rank's range, in local addresses
+                addr_l, val_l = [], []
+                for src in range(world):
+                    k_s, v_s = (keys, vals) if src == rank else batch(src)
+                    m = (k_s >= part.start) & (k_s < part.end)
+                    addr_l.append(k_s[m] - part.start)
+                    val_l.append(v_s[m])
+                    del k_s, v_s, m
+                addr, v_all = torch.cat(addr_l), torch.cat(val_l)
+                del addr_l, val_l
+                recv = int(addr.numel())
+                got = shard.get(torch.arange(part.start, part.end, dtype=torch.int64, device=dev))
+            elif mat:
                 addr = (keys - part.start) * cols_n + cols.to(torch.int64)
+                v_all = vals
                 got = shard.getRows(torch.arange(part.start, part.end, dtype=torch.int64, device=dev)).reshape(-1)
             else:
                 addr = keys - part.start
+                v_all = vals
                 got = shard.get(torch.arange(part.start, part.end, dtype=torch.int64, device=dev))
             # segment sums over the sorted addresses (an atomic index_add_ serialises on Zipf's hot key)
             a, order = torch.sort(addr)
             uq, counts = torch.unique_consecutive(a, return_counts=True)
-            sums = torch.segment_reduce(vals[order], "sum", lengths=counts) * reps
+            sums = torch.segment_reduce(v_all[order], "sum", lengths=counts) * reps
             ok = bool(torch.allclose(got[uq], sums, rtol=1e-6, atol=1e-9 * reps))
             got[uq] = 0
             ok = ok and not bool(got.any())  # nothing outside the pushed addresses
-            del a, order, uq, counts, sums, addr
-            del got
+            if exch:
+                uniq, u_note = int(uq.numel()), ""
+                bytes_per_step = 16.0 * recv + 16.0 * uniq
+            del a, order, uq, counts, sums, addr, v_all, got
         if not ok:
-            raise SystemExit("post-run shard check FAILED")
+            raise SystemExit(f"post-run shard check FAILED ({pat}, 2^{log2_keys})")
 
-    value = world * bytes_per_step * args.steps / dt / 1e9
+    total_bytes = bytes_per_step
+    if world > 1:  # every rank's algorithmic bytes (exchange: its own recv and U)
+        t = torch.tensor([bytes_per_step], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        total_bytes = float(t.item())
+    value = total_bytes * steps / dt / 1e9
     if push:
         # The push is push_check (reads the keys) + push_apply (values and shard for the ordered
         # prefix) + the unordered tail (push_scatter, or the binned pipeline for large tails).
@@ -385,7 +409,7 @@ def main():
         scat_ms, _ = kernel_avg(N.GLINT_K_PUSH_SCATTER)
         bin_ms, bin_n = kernel_avg(N.GLINT_K_PUSH_BINNED)
         if apply_n:
-            bin_ms = bin_ms * bin_n / apply_n  # per push (the binned pipeline may skip the warm-up pushes)
+            bin_ms = bin_ms * bin_n / apply_n  # per push (the binned pipeline may skip pushes)
         kern = "push_check+push_apply+push_scatter+push_binned"
         kern_ms = check_ms + apply_ms + scat_ms + bin_ms
         launches = apply_n
@@ -398,22 +422,23 @@ def main():
         kern_ms, launches = kernel_avg(kid)
         shares = {kern: round(kern_ms, 4)}
         metric = "device-resident pull gather GB/s (and % HBM peak)"
-    achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
+    achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(tag)
-    out_line = {
+    line = {
         "metric": metric,
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (keys per BASELINE.md config, values U[-1,1) seed 42+rank), resident in HBM",
-        "config": {"workload": workload, "keys_per_gpu": n * (cols_n if mat else 1), "records_per_step_per_gpu": nrec,
+        "config": {"workload": workload + u_note, "keys_per_gpu": n * (cols_n if mat else 1),
+                   "records_per_step_per_gpu": nrec, "records_received_per_step_per_gpu": recv,
                    "distinct_keys_per_step_per_gpu": uniq, "key_dtype": "i64", "value_dtype": "f64",
                    "parallelism": f"range-sharded x{world}, " + ("route + all-to-all exchange" if exch else "no exchange")},
         "pct_hbm_peak_per_gpu": round(100.0 * value / world / HBM_PEAK_GBS, 2),
@@ -424,11 +449,56 @@ def main():
                      "launches_timed": launches, "kernels_ms": shares},
         "check": ok,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out_line["cpu_baseline"] = cpu_baseline(args.log2_keys, args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(out_line), flush=True)
     shard.destroy()
+    return line
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    import torch
+    import torch.distributed as dist
+    import glint_amd  # noqa: F401  (loads libglint_gpu.so; fails loudly without it)
+    from glint_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # rehearsal hooks (not used by the driver): GLINT_BENCH_DEVICE pins every rank to one GPU and
+    # GLINT_BENCH_BACKEND=gloo replaces RCCL, so the N > 1 path can run on a one-GPU box
+    local = int(os.environ.get("GLINT_BENCH_DEVICE", local))
+    backend = os.environ.get("GLINT_BENCH_BACKEND", "nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    exch = args.pattern == "exchange"
+    if world > 1 or exch:
+        if world == 1:  # the exchange path needs a process group even alone (RCCL world 1)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29561")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    ctx = {"lib": N.load(), "dev": dev, "world": world, "rank": rank, "backend": backend}
+    line = run_line(ctx, args.pattern, args.log2_keys, args.scaling, args.steps, args.warmup, not args.no_check)
+    # the north star's own size (BASELINE.json north_star: >= 70 % of HBM roofline at 1 GPU over a
+    # 2^30-key Double vector) beside the driver's cfg2 line, with its own roofline and check
+    if (world == 1 and args.pattern == "dense" and args.scaling == "weak" and args.log2_keys == 28
+            and not args.no_north_star):
+        torch.cuda.empty_cache()
+        ns = run_line(ctx, "dense", 30, "weak", 10, 2, not args.no_check)
+        line["north_star_2p30"] = {k: ns[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
+                                                      "pct_hbm_peak_per_gpu", "roofline", "check")}
+        line["north_star_2p30"]["workload"] = ns["config"]["workload"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.log2_keys, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if world > 1 or exch:
         dist.destroy_process_group()
 

@@ -1097,12 +1097,13 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   if (n >= ((i64)1 << 32) - 2 * kAChunk || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
   const BinGeom g = bin_geometry(s->elems);
   // front end: dedup when the last probe kept < 60 % of the records (the device reports m and the
-  // tail size of each push through a host-mapped word; read without a sync, so it may be one push
-  // old); re-probe every 16 pushes. GLINT_BIN_FRONT = dedup | prep forces one (tests, tuning).
-  if (s->h_hint) {
-    const u64 w = __atomic_load_n(s->h_hint + 1, __ATOMIC_RELAXED);
+  // tail size of each push through a host-mapped word, taken at the shard's last sync point, so the
+  // choice does not depend on timing); re-probe every 16 pushes. GLINT_BIN_FRONT = dedup | prep
+  // forces one (tests, tuning).
+  {
+    const u64 w = s->hint_bin;
     const u32 m = (u32)(w >> 32), tail = (u32)w;
-    if (tail > 0 && s->bin_last_dedup) s->bin_dedup_ratio = (double)m / (double)tail;
+    if (tail > 0 && s->hint_bin_dedup) s->bin_dedup_ratio = (double)m / (double)tail;
   }
   bool dedup = s->bin_dedup_ratio < 0.6 || (++s->bin_pushes & 15) == 0;
   if (const char* e = getenv("GLINT_BIN_FRONT")) {

@@ -551,7 +551,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   a.n = n;
   a.data = (V*)s->data;
   a.part = s->part;
-  a.err = s->d_err;
+  a.err = err_of(s);
   a.elems = s->elems;
   a.hint = s->d_hint;
   a.sig = s->sig;
@@ -586,7 +586,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   i64* desc = (i64*)((char*)s->d_ctl + 256);
 
   const int bmode = binned_mode();
-  const i64 last_tail = s->h_hint ? (i64)__atomic_load_n(s->h_hint, __ATOMIC_RELAXED) : 0;
+  const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
   if (binned && unordered) return push_binned<V, MAT>(s, a, false, st);
@@ -633,7 +633,7 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   const MsgSig sig = s->sig;
   if (sig.done && n <= kRingPullMax) {
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, ring_pull_kernel<V, false>, 1u, kRingPullTPB, st, keys, (const int32_t*)nullptr,
-                    n, (const V*)s->data, s->part, (V*)out, s->d_err, sig));
+                    n, (const V*)s->data, s->part, (V*)out, err_of(s), sig));
     return GLINT_OK;
   }
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
@@ -641,11 +641,11 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
     // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5)
     const unsigned g = sig.done ? 1u : grid_for((n + 1) / 2, kTPB, (i64)s->cus * 4);
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, true>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
-                    (V*)out, s->d_err, sig));
+                    (V*)out, err_of(s), sig));
   } else {
     const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, false>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
-                    (V*)out, s->d_err, sig));
+                    (V*)out, err_of(s), sig));
   }
   return GLINT_OK;
 }
@@ -657,12 +657,12 @@ int launch_mat_pull(glint_shard* s, const i64* rows, const int32_t* cols, void* 
   const MsgSig sig = s->sig;
   if (sig.done && n <= kRingPullMax) {
     HIPCHK(launch_k(s, GLINT_K_MAT_PULL, ring_pull_kernel<V, true>, 1u, kRingPullTPB, st, rows, cols, n,
-                    (const V*)s->data, s->part, (V*)out, s->d_err, sig));
+                    (const V*)s->data, s->part, (V*)out, err_of(s), sig));
     return GLINT_OK;
   }
   const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
   HIPCHK(launch_k(s, GLINT_K_MAT_PULL, mat_pull_kernel<V>, g, kTPB, st, rows, cols, n, (const V*)s->data, s->part,
-                  (V*)out, s->d_err, sig));
+                  (V*)out, err_of(s), sig));
   return GLINT_OK;
 }
 
@@ -674,7 +674,7 @@ int launch_mat_pull_rows(glint_shard* s, const i64* rows, void* out, i64 n, hipS
   const bool v16 = ((i64)s->part.cols * (i64)sizeof(V)) % 16 == 0 && aligned(out, 16);
   const unsigned g = sig.done ? 1u : grid_for(n, kTPB / 64, (i64)s->cus * 8);
   HIPCHK(launch_k(s, GLINT_K_MAT_PULL_ROWS, v16 ? mat_pull_rows_kernel<V, true> : mat_pull_rows_kernel<V, false>, g,
-                  kTPB, st, rows, n, (const V*)s->data, s->part, (V*)out, s->d_err, sig));
+                  kTPB, st, rows, n, (const V*)s->data, s->part, (V*)out, err_of(s), sig));
   return GLINT_OK;
 }
 
@@ -697,7 +697,7 @@ int push_mat_t(glint_shard* s, const i64* k, const int32_t* c, const void* v, i6
   return launch_push<V, true>(s, k, c, v, n, f, st);
 }
 
-// read and clear the device error state (caller has synchronised the stream)
+// read and clear the device-resident calls' error state (caller has synchronised the stream)
 int collect_errors(glint_shard* s, hipStream_t st, int64_t* first_bad) {
   ErrState h{};
   HIPCHK(hipMemcpyAsync(&h, s->d_err, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -705,8 +705,6 @@ int collect_errors(glint_shard* s, hipStream_t st, int64_t* first_bad) {
   if (h.min_bad_enc != 0) {
     HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), st));
     HIPCHK(hipStreamSynchronize(st));
-    s->reported_enc = h.min_bad_enc;  // ring entries still unretired may carry it: do not report twice
-    s->clear_ticket = s->ticket_next;
     s->last_bad = (i64)~h.min_bad_enc;
     if (first_bad) *first_bad = s->last_bad;
     return GLINT_EOUTOFRANGE;
@@ -741,7 +739,8 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
     (void)hipGetLastError();
     return GLINT_ENOMEM;
   }
-  if (hipMalloc((void**)&s->d_err, sizeof(ErrState)) != hipSuccess) {
+  if (hipMalloc((void**)&s->d_err, sizeof(ErrState)) != hipSuccess ||
+      hipMalloc((void**)&s->d_err_host, sizeof(ErrState)) != hipSuccess) {
     (void)hipGetLastError();
     return GLINT_ENOMEM;
   }
@@ -760,6 +759,7 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   }
   HIPCHK(hipMemsetAsync(s->data, 0, bytes, s->stream));  // new Array[V](size) is zeroed
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
+  HIPCHK(hipMemsetAsync(s->d_err_host, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
   return GLINT_OK;
 }
@@ -772,6 +772,7 @@ void free_shard(glint_shard* s) {
     prof_drain(s);
     if (s->data) (void)hipFree(s->data);
     if (s->d_err) (void)hipFree(s->d_err);
+    if (s->d_err_host) (void)hipFree(s->d_err_host);
     if (s->d_ctl) (void)hipFree(s->d_ctl);
     if (s->d_scratch) (void)hipFree(s->d_scratch);
     if (s->d_det) (void)hipFree(s->d_det);
@@ -909,11 +910,10 @@ int glint_shard_zero(glint_shard_t s) {
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(s->data, 0, (size_t)s->elems * s->vsize, s->stream));
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
+  HIPCHK(hipMemsetAsync(s->d_err_host, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
   rc = ring_retire_through(s, s->ticket_next);  // all complete: pulls get their answers
-  s->ring_bad = -1;  // a fresh shard: nothing before the restart is reported any more
-  s->reported_enc = 0;
-  s->clear_ticket = s->ticket_next;
+  s->failed.clear();  // a fresh shard: nothing before the restart is reported any more
   s->host_pending = false;
   return rc;
 }
@@ -977,7 +977,10 @@ int glint_shard_sync(glint_shard_t s, void* stream, int64_t* first_bad) {
   DeviceGuard g(s->device);
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(st));
-  if (st == s->last_dev_stream) s->dev_dirty = false;  // everything enqueued there has completed
+  if (st == s->last_dev_stream) {
+    s->dev_dirty = false;  // everything enqueued there has completed
+    latch_hints(s);        // a sync point: later pushes decide from the pushes up to here
+  }
   return collect_errors(s, st, first_bad);
 }
 
@@ -1085,23 +1088,60 @@ int stage(glint_shard* s, const void* const* src, const size_t* bytes, int count
 // Ends a host call: the device error state rides back with the call's last copy (pinned, async),
 // so a clean call costs one stream synchronisation.
 int finish(glint_shard* s) {
-  if (!s->h_err) {
-    HIPCHK(hipStreamSynchronize(s->stream));
-    return collect_errors(s, s->stream, nullptr);
+  ErrState local{};
+  ErrState* h = s->h_err ? s->h_err : &local;
+  HIPCHK(hipMemcpyAsync(h, s->d_err_host, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (!s->dev_dirty) latch_hints(s);  // a sync point (the shard's pushes all ran on this stream)
+  if (h->min_bad_enc == 0) return GLINT_OK;
+  s->last_bad = (i64)~h->min_bad_enc;
+  HIPCHK(hipMemsetAsync(s->d_err_host, 0, sizeof(ErrState), s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return GLINT_EOUTOFRANGE;
+}
+
+// ---- host-side validation of ring messages ------------------------------------------------------
+// The first record of a message the reference would reject -- RangePartition.globalToLocal /
+// CyclicPartition.globalToLocal (`.toInt` included) outside [0, size), or a column outside [0, cols)
+// (PartialVector.scala:37-41, PartialMatrix.scala:77-81 throw ArrayIndexOutOfBoundsException there)
+// -- or -1. The arrays are host memory the call copies anyway (any alignment: wire sections start at
+// odd offsets). A ring message is checked here, before it is enqueued, so its error belongs to the
+// call that enqueues it -- the Push or Pull message itself, as in the reference -- and a rejected
+// message is not applied at all.
+i64 host_first_bad(const glint_shard* s, const void* keys, const void* cols, i64 n) {
+  const PartDesc& p = s->part;
+  const char* kb = (const char*)keys;
+  const char* cb = (const char*)cols;
+  for (i64 i = 0; i < n; ++i) {
+    int64_t k;
+    std::memcpy(&k, kb + 8 * i, 8);
+    const int32_t l = p.kind == 0 ? (int32_t)(k - p.start) : (int32_t)((k - (i64)p.cidx) / (i64)p.cparts);
+    bool ok = l >= 0 && l < p.size;
+    if (cb) {
+      int32_t c;
+      std::memcpy(&c, cb + 4 * i, 4);
+      ok = ok && c >= 0 && c < p.cols;
+    }
+    if (!ok) return i;
   }
-  HIPCHK(hipMemcpyAsync(s->h_err, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
-  if (s->h_err->min_bad_enc == 0) return GLINT_OK;
-  s->last_bad = (i64)~s->h_err->min_bad_enc;
-  s->reported_enc = s->h_err->min_bad_enc;  // ring entries still unretired may carry it
-  s->clear_ticket = s->ticket_next;
-  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
+  return -1;
+}
+
+// GLINT_EOUTOFRANGE with the record index for glint_shard_last_error when a message has a bad record
+inline int reject_if_bad(glint_shard* s, const void* keys, const void* cols, i64 n) {
+  const i64 bad = host_first_bad(s, keys, cols, n);
+  if (bad < 0) return GLINT_OK;
+  s->last_bad = bad;
   return GLINT_EOUTOFRANGE;
 }
 
 // ---- pinned ring (pipelined ingest) -------------------------------------------------------------
 constexpr i64 kRingMaxRecords = (i64)1 << 20;
+// an async pull whose answer is larger than this is answered synchronously (staged copies) instead of
+// through a ring slot, and a slot grown above kSlotKeepBytes is released when its entry retires: the
+// ring's pinned memory stays bounded by what message-sized traffic needs
+constexpr size_t kRingAnswerMax = (size_t)16 << 20;
+constexpr size_t kSlotKeepBytes = (size_t)4 << 20;
 
 struct StageLayout {
   size_t kb, cb, vb, total;  // keys | cols (matrix) | values, each section 256-aligned
@@ -1127,8 +1167,9 @@ int wait_done(glint_shard* s, u64 ticket) {
   return __atomic_load_n(s->h_done, __ATOMIC_ACQUIRE) >= ticket ? GLINT_OK : GLINT_EDEVICE;
 }
 
-// Retires a slot: waits for its entry, remembers the first error it saw that was not reported yet
-// (and which message it belongs to), and hands an async pull its answer.
+// Retires a slot: waits for its entry and hands an async pull its answer. Ring messages were
+// validated on the host before they were enqueued, so their kernels reject nothing: a rejected
+// record here means the device and the host check disagree, a device fault.
 int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   if (!r.inflight) return GLINT_OK;
   if (r.sig) {
@@ -1138,22 +1179,7 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
     HIPCHK(hipEventSynchronize(r.done));
   }
   r.inflight = false;
-  // cumulative until cleared: an entry enqueued before the last clear may still carry the error
-  // reported then; later entries carry only new ones
-  const u64 enc = __atomic_load_n(&r.herr->min_bad_enc, __ATOMIC_ACQUIRE);
-  const bool stale = r.ticket <= s->clear_ticket && enc == s->reported_enc;
-  if (enc != 0 && !stale && s->ring_bad < 0) {
-    const i64 idx = (i64)~enc;  // a record index within this entry (a batch: within the batch)
-    s->ring_bad = idx;
-    s->ring_bad_ticket = r.msgs.empty() ? r.ticket : r.msgs.front().ticket;
-    for (const auto& m : r.msgs)
-      if (idx >= m.off && idx < m.off + m.n) {
-        s->ring_bad = idx - m.off;
-        s->ring_bad_ticket = m.ticket;
-        break;
-      }
-    s->ring_bad_enc = enc;
-  }
+  const int err = __atomic_load_n(&r.herr->min_bad_enc, __ATOMIC_ACQUIRE) != 0 ? GLINT_EDEVICE : GLINT_OK;
   if (r.out) {
     std::memcpy(r.out, r.h + r.out_off, r.out_bytes);
     r.out = nullptr;
@@ -1163,7 +1189,17 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
       std::memcpy(m.out, r.h + r.out_off + (size_t)m.off * s->vsize, (size_t)m.n * s->vsize);
     r.pull_batch = false;
   }
-  return GLINT_OK;
+  if (r.hcap > kSlotKeepBytes) {  // a large entry's slot: give the pinned memory back
+    (void)hipHostFree(r.h);
+    r.h = r.hd = nullptr;
+    r.hcap = 0;
+  }
+  if (r.dcap > kSlotKeepBytes) {
+    (void)hipFree(r.d);
+    r.d = nullptr;
+    r.dcap = 0;
+  }
+  return err;
 }
 
 // Retires, oldest first, every in-flight entry that covers a ticket <= t (errors then belong to
@@ -1252,21 +1288,35 @@ inline bool ring_direct(const glint_shard* s, i64 n) { return n <= GLINT_ZERO_CO
 // Runs `launch` (the entry's kernels on s->stream) for slot r, covering tickets [lo, hi]: a direct
 // entry is one workgroup that signals hi itself; any other entry ends with an error-state copy and
 // an event.
+// A launch that fails after the entry's tickets were handed out drops the entry: its tickets are
+// remembered as failed, so the wait that covers them reports the failure.
+void drop_entry(glint_shard* s, glint_shard::RingSlot& r, u64 lo, u64 hi, int rc) {
+  r.acquired = false;
+  r.out = nullptr;
+  r.pull_batch = false;
+  r.msgs.clear();
+  if (hi >= lo && lo > 0) s->failed.push_back({lo, hi, rc});
+}
+
 template <typename F>
 int ring_dispatch(glint_shard* s, glint_shard::RingSlot& r, bool direct, u64 lo, u64 hi, F launch) {
   if (direct) s->sig = MsgSig{s->d_done, hi, r.herr_d};
-  const int rc = launch();
+  int rc;
+  {
+    HostCall hc(s);  // ring messages are host-pointer calls: their kernels use the host error state
+    rc = launch();
+  }
   s->sig = MsgSig{nullptr, 0, nullptr};
+  if (rc == GLINT_OK && !direct &&
+      (hipMemcpyAsync(r.herr, s->d_err_host, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+       hipEventRecord(r.done, s->stream) != hipSuccess)) {
+    (void)hipGetLastError();
+    rc = GLINT_EDEVICE;
+  }
   if (rc) {
     (void)hipStreamSynchronize(s->stream);
-    r.acquired = false;
-    r.out = nullptr;
-    r.msgs.clear();
+    drop_entry(s, r, lo, hi, rc);
     return rc;
-  }
-  if (!direct) {
-    HIPCHK(hipMemcpyAsync(r.herr, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipEventRecord(r.done, s->stream));
   }
   r.ticket_lo = lo;
   r.ticket = hi;
@@ -1310,8 +1360,7 @@ int ring_flush_locked(glint_shard* s) {
   s->open_slot = -1;
   int rc = order_after_dev(s);
   if (rc) {
-    r.acquired = false;
-    r.msgs.clear();
+    drop_entry(s, r, r.msgs.front().ticket, r.msgs.back().ticket, rc);
     return rc;
   }
   if (s->open_kind >= 0) return launch_pull_batch(s, r, s->open_kind);
@@ -1324,7 +1373,8 @@ inline bool batchable(const glint_shard* s, i64 n) { return n > 0 && n <= kBatch
 // Appends one message-sized push (sections: keys, cols for matrices, values; any alignment) to the
 // open batch, opening one if needed; *ticket = the message's own ticket.
 int ring_append_locked(glint_shard* s, i64 n, int flags, const void* k, const void* c, const void* v, u64* ticket) {
-  int rc;
+  int rc = reject_if_bad(s, k, s->part.cols != 0 ? c : nullptr, n);
+  if (rc) return rc;
   if (s->open_slot >= 0 &&
       (s->open_kind >= 0 || flags != s->open_flags || s->ring[s->open_slot].fill + n > kBatchMax)) {
     rc = ring_flush_locked(s);
@@ -1359,20 +1409,28 @@ int ring_push_locked(glint_shard* s, int idx, i64 n, int flags, u64* ticket) {
   if (!r.acquired || n < 0 || n > r.n) return GLINT_EINVAL;
   const StageLayout L = stage_layout(s, r.n);  // the sections as handed out
   if (batchable(s, n)) {
-    r.acquired = false;  // the records move to the batch; the slot is free again
-    return ring_append_locked(s, n, flags, r.h, r.h + L.kb, r.h + L.kb + L.cb, ticket);
+    // the records move to the batch; the slot stays acquired until they are copied (the batch's
+    // slot search then cannot pick it), and is free again after
+    const int rc = ring_append_locked(s, n, flags, r.h, r.h + L.kb, r.h + L.kb + L.cb, ticket);
+    r.acquired = false;
+    return rc;
   }
-  int rc = ring_flush_locked(s);
-  if (rc) return rc;
-  rc = order_after_dev(s);
-  if (rc) return rc;
+  int rc = reject_if_bad(s, r.h, s->part.cols != 0 ? r.h + L.kb : nullptr, n);
+  if (rc == GLINT_OK) rc = ring_flush_locked(s);
+  if (rc == GLINT_OK) rc = order_after_dev(s);
   const bool direct = ring_direct(s, n);
   const char* base = r.hd;
-  if (!direct) {
+  if (rc == GLINT_OK && !direct) {
     rc = grow((void**)&r.d, &r.dcap, L.total);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(r.d, r.h, L.total, hipMemcpyHostToDevice, s->stream));
+    if (rc == GLINT_OK && hipMemcpyAsync(r.d, r.h, L.total, hipMemcpyHostToDevice, s->stream) != hipSuccess) {
+      (void)hipGetLastError();
+      rc = GLINT_EDEVICE;
+    }
     base = r.d;
+  }
+  if (rc) {
+    r.acquired = false;  // nothing enqueued: the slot is free again
+    return rc;
   }
   const u64 t = ++s->ticket_next;
   r.msgs.assign(1, glint_shard::RingSlot::Msg{0, n, t});
@@ -1403,7 +1461,11 @@ int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t
       r.acquired = false;
       return rc;
     }
-    HIPCHK(hipMemcpyAsync(r.d, r.h, L.kb + L.cb, hipMemcpyHostToDevice, s->stream));
+    if (hipMemcpyAsync(r.d, r.h, L.kb + L.cb, hipMemcpyHostToDevice, s->stream) != hipSuccess) {
+      (void)hipGetLastError();
+      r.acquired = false;
+      return GLINT_EDEVICE;
+    }
     base = r.d;
     ans = r.d + L.kb + L.cb;
   }
@@ -1455,7 +1517,8 @@ int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind) {
 
 int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys, const int32_t* cols, void* out,
                             u64* ticket) {
-  int rc;
+  int rc = reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
+  if (rc) return rc;
   if (s->open_slot >= 0 && (s->open_kind != kind || s->ring[s->open_slot].fill + n > kBatchMax)) {
     rc = ring_flush_locked(s);
     if (rc) return rc;
@@ -1489,14 +1552,17 @@ int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
   }
   int rc = ring_retire_through(s, ticket);
   if (rc) return rc;
-  if (s->ring_bad < 0 || s->ring_bad_ticket > ticket) return GLINT_OK;  // a later message's error waits
-  s->last_bad = s->ring_bad;
-  if (first_bad) *first_bad = s->ring_bad;
-  s->ring_bad = -1;
-  s->reported_enc = s->ring_bad_enc;
-  s->clear_ticket = s->ticket_next;  // entries up to here were enqueued before the clear
-  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
-  return GLINT_EOUTOFRANGE;
+  // entries whose launch failed after their tickets were handed out: reported once, by the first
+  // wait that covers them (rejected records never reach the ring: their calls returned the error)
+  for (size_t i = 0; i < s->failed.size(); ++i) {
+    if (s->failed[i].lo <= ticket) {
+      rc = s->failed[i].rc;
+      s->failed.erase(s->failed.begin() + (long)i);
+      return rc;
+    }
+  }
+  if (first_bad) *first_bad = -1;
+  return GLINT_OK;
 }
 
 // A device-resident call runs on the caller's stream: it first waits for the ring entries enqueued
@@ -1526,9 +1592,11 @@ inline size_t pull_bytes(const glint_shard* s, int kind, i64 n) {
 int pull_enqueue_locked(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols, void* out, int64_t n,
                         u64* ticket) {
   if (kind != 2 && batchable(s, n)) return ring_append_pull_locked(s, kind, n, keys, cols, out, ticket);
+  int rc = reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
+  if (rc) return rc;
   int slot = -1;
   const size_t ob = pull_bytes(s, kind, n);
-  int rc = ring_acquire_locked(s, n, &slot, ob);
+  rc = ring_acquire_locked(s, n, &slot, ob);
   if (rc) return rc;
   glint_shard::RingSlot& r = s->ring[slot];
   const StageLayout L = stage_layout(s, n);
@@ -1560,6 +1628,7 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
   rc = stage(s, src, bytes, mat ? 3 : 2, st, 0, nullptr);
   if (rc) return rc;
   const int hflags = flags | kPushHostSequential;  // the actor's update: message order by default
+  HostCall hc(s);  // this call's rejected records are its own (d_err_host, read by finish)
   if (mat) {
     rc = [&]() -> int {
       GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)st.p[0], (const int32_t*)st.p[1], st.p[2], n, hflags,
@@ -1587,13 +1656,14 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   int rc = ring_flush_locked(s);
   if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) return rc;
-  if (n <= GLINT_ZERO_COPY_MAX) {
+  if (n <= GLINT_ZERO_COPY_MAX && pull_bytes(s, kind, n) <= kRingAnswerMax) {
     // Akka-sized: one workgroup reads the keys from a mapped pinned ring slot, writes the answer into
-    // it and signals its ticket, so the call is one launch and a wait on host memory
+    // it and signals its ticket, so the call is one launch and a wait on host memory. The keys are
+    // checked first: a rejected pull enqueues nothing and throws, as get() does in the reference.
     u64 ticket = 0;
     rc = pull_enqueue_locked(s, kind, keys, cols, out, n, &ticket);
     if (rc) return rc;
-    return ring_wait_locked(s, ticket, nullptr);  // also reports errors of pushes enqueued before it
+    return ring_wait_locked(s, ticket, nullptr);
   }
   const size_t out_bytes = (size_t)n * s->vsize * (kind == 2 ? (size_t)s->part.cols : 1);
   Staged st;
@@ -1602,6 +1672,7 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   char* d_out = nullptr;
   rc = stage(s, src, bytes, kind == 1 ? 2 : 1, st, out_bytes, &d_out);
   if (rc) return rc;
+  HostCall hc(s);  // this call's rejected records are its own (d_err_host, read by finish)
   if (kind == 0) {
     rc = [&]() -> int { GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)st.p[0], d_out, n, s->stream); }();
   } else if (kind == 1) {
@@ -1758,6 +1829,14 @@ int glint_pull_async(glint_shard_t s, int kind, const int64_t* keys, const int32
   if (!s || !ticket || kind < 0 || kind > 2) return GLINT_EINVAL;
   if (n < 0 || (n > 0 && (!keys || !out || (kind == 1 && !cols)))) return GLINT_EINVAL;
   if ((kind == 0) != (s->part.cols == 0)) return GLINT_EINVAL;
+  if (n > 0 && pull_bytes(s, kind, n) > kRingAnswerMax) {
+    // an answer too large for a ring slot (row pulls of wide matrices): answered now, through the
+    // staged copies; the ticket is that of everything enqueued so far (complete on return)
+    const int rc = host_pull(s, kind, keys, cols, out, n);
+    std::lock_guard<std::mutex> lk(s->mu);
+    *ticket = s->ticket_next;
+    return rc;
+  }
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
   if (n == 0) {  // nothing to enqueue: the ticket of everything so far

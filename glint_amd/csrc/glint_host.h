@@ -27,7 +27,9 @@ struct glint_shard {
   void* d_ctl = nullptr;
   size_t ctl_bytes = 0;
   int ctl_par = 0;  // which of the two LaunchCtl slots the next ordered push uses
-  ErrState* d_err = nullptr;
+  ErrState* d_err = nullptr;       // device-resident calls' error state: reported by glint_shard_sync
+  ErrState* d_err_host = nullptr;  // host-pointer calls' own (read and cleared by the call itself)
+  bool host_call = false;          // set while a host-pointer call launches: its kernels use d_err_host
   // grow-only device scratch for host-pointer calls and the deterministic path
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -76,7 +78,6 @@ struct glint_shard {
   int open_slot = -1;     // the batch that message-sized pushes (or pulls) are appended to, not launched yet
   int open_flags = 0;
   int open_kind = -1;     // -1: a push batch; 0 / 1: a vector / matrix element pull batch
-  uint64_t ring_bad_ticket = 0;  // the message the unreported error belongs to
   bool host_pending = false;     // ring entries enqueued on `stream` since a device call last waited for them
   hipEvent_t host_ev = nullptr;
   u64* h_done = nullptr;  // host-mapped: ticket of the last completed signalling launch
@@ -84,12 +85,21 @@ struct glint_shard {
   MsgSig sig{};           // set only while a ring entry dispatches its one launch
   int ring_next = 0;
   uint64_t ticket_next = 0;
-  int64_t ring_bad = -1;       // first bad record of a retired push, not reported yet
-  uint64_t ring_bad_enc = 0;
-  uint64_t reported_enc = 0;   // error state last reported (cumulative until cleared)
-  uint64_t clear_ticket = 0;   // last ticket enqueued before that report's clear
+  // tickets of ring entries whose launch failed after their tickets were handed out: a wait that
+  // covers one returns the failure (once)
+  struct Failed {
+    uint64_t lo, hi;
+    int rc;
+  };
+  std::vector<Failed> failed;
   u64* h_hint = nullptr;  // host-mapped: unordered-tail size of the last push (written by push_apply)
   u64* d_hint = nullptr;
+  // the hints as of the shard's last sync point (glint_shard_sync, the end of a host call): what the
+  // adaptive tail switch and the binned front end decide from, so a given sequence of calls and
+  // syncs takes the same path every run
+  u64 hint_tail = 0;  // h_hint[0]
+  u64 hint_bin = 0;   // h_hint[1]
+  bool hint_bin_dedup = false;  // whether the binned push that wrote hint_bin ran the dedup front end
   i64 last_bad = -1;
   // ordering of host-pointer calls (private stream) after device-resident calls (caller's stream):
   // the last stream a *_dev call used; a host call records an event there and waits on it
@@ -243,6 +253,26 @@ inline void prof_drain(glint_shard* s) {
   }
   (void)hipGetLastError();
 }
+
+// At a sync point (the stream that carried the shard's pushes has drained): the hint words the last
+// push wrote become the ones the next pushes decide from.
+inline void latch_hints(glint_shard* s) {
+  if (!s->h_hint) return;
+  s->hint_tail = __atomic_load_n(s->h_hint, __ATOMIC_ACQUIRE);
+  s->hint_bin = __atomic_load_n(s->h_hint + 1, __ATOMIC_ACQUIRE);
+  s->hint_bin_dedup = s->bin_last_dedup;  // the stream has drained: the hint is the last binned push's
+}
+
+// The error state a launch of this call records into: a host-pointer call's own, or the one
+// glint_shard_sync reports for device-resident calls.
+inline ErrState* err_of(const glint_shard* s) { return s->host_call ? s->d_err_host : s->d_err; }
+
+// Marks the launches of a host-pointer call (their rejected records are the call's own errors).
+struct HostCall {
+  glint_shard* s;
+  explicit HostCall(glint_shard* s_) : s(s_) { s->host_call = true; }
+  ~HostCall() { s->host_call = false; }
+};
 
 inline unsigned grid_for(i64 units, i64 per_block, i64 cap) {
   i64 g = (units + per_block - 1) / per_block;

@@ -7,7 +7,9 @@
 //                  RangePartitioner.scala:27-43, bit for bit incl. its Int truncations, or the
 //                  cyclic key % P of CyclicPartitioner.scala:19-22), stored
 //                  partition-major so that one exclusive scan yields every (partition, block) offset;
-//   (rocPRIM exclusive scan over the histogram)
+//   route_row_sums / route_row_scan
+//                  the (partition, block) offsets: each partition's total, then per partition its
+//                  first slot (the totals before it) plus the exclusive scan of its row;
 //   route_scatter  each block writes its record indices to their partition's range, in order: a
 //                  wave finds its same-owner lanes with one ballot per owner bit, the waves of a
 //                  256-record round then claim slots in wave order from per-owner LDS counters --
@@ -15,10 +17,11 @@
 // Out-of-range keys (IndexOutOfBoundsException in the reference, :30-32) are reported as the first
 // bad record index; the routing of the other records is unaffected.
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 #include <algorithm>
+#include <map>
 #include <mutex>
+#include <utility>
 #include "../../include/glint_gpu.h"
 
 namespace {
@@ -154,25 +157,134 @@ __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ key
   }
 }
 
-// records per partition: the distance between consecutive partitions' first offsets; the last
-// partition ends at the scan's total (its last block's offset + count)
-__global__ void route_counts(const u32* __restrict__ offs, const u32* __restrict__ hist, i64 nblocks,
-                             int32_t nparts, i64* __restrict__ counts) {
-  const i64 total = (i64)offs[(i64)nparts * nblocks - 1] + hist[(i64)nparts * nblocks - 1];
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < nparts; p += gridDim.x * blockDim.x) {
-    const i64 end = p + 1 < nparts ? (i64)offs[(i64)(p + 1) * nblocks] : total;
-    counts[p] = end - (i64)offs[(i64)p * nblocks];
+// ---- the (partition, block) offsets -------------------------------------------------------------
+// hist is partition-major: row p = the records of partition p in each block. The offset of (p, b) is
+// the records of partitions < p plus those of p in blocks < b: a row total per partition, then per
+// partition a base (the totals before it) and the exclusive scan of its row. Two small launches, no
+// scan library; every value stays on the device.
+constexpr int kST = 1024;  // threads of the offset kernels
+
+__device__ __forceinline__ u32 block_reduce_u32(u32 x) {
+  __shared__ u32 ws[kST / 64];
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  u32 t = 0;
+#pragma unroll
+  for (int w = 0; w < kST / 64; ++w) t += ws[w];
+  __syncthreads();
+  return t;
+}
+
+// tot[p] = records of partition p (the route's counts, too)
+__global__ __launch_bounds__(kST) void route_row_sums(const u32* __restrict__ hist, i64 nblocks, u32* __restrict__ tot,
+                                                      i64* __restrict__ counts) {
+  const u32* row = hist + (i64)blockIdx.x * nblocks;
+  u32 x = 0;
+  for (i64 b = threadIdx.x; b < nblocks; b += kST) x += row[b];
+  x = block_reduce_u32(x);
+  if (threadIdx.x == 0) {
+    tot[blockIdx.x] = x;
+    counts[blockIdx.x] = x;
   }
 }
 
-// route scratch, one per device (a process may route on several GPUs at once)
+// offs[p][b] = sum(tot[0..p)) + sum(hist[p][0..b)): one block per partition, the row in tiles of
+// kST x 4 values (each thread scans its 4, a wave scan, the waves' totals, then the carry)
+__global__ __launch_bounds__(kST) void route_row_scan(const u32* __restrict__ hist, i64 nblocks,
+                                                      const u32* __restrict__ tot, u32* __restrict__ offs) {
+  __shared__ u32 wt[kST / 64];
+  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  u32 base = 0;
+  for (int q = tid; q < p; q += kST) base += tot[q];
+  base = block_reduce_u32(base);
+  const u32* row = hist + (i64)p * nblocks;
+  u32* out = offs + (i64)p * nblocks;
+  constexpr int PER = 4;
+  u32 carry = base;
+  for (i64 t0 = 0; t0 < nblocks; t0 += (i64)kST * PER) {
+    const i64 b0 = t0 + (i64)tid * PER;
+    u32 v[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      v[j] = b0 + j < nblocks ? row[b0 + j] : 0u;
+      sum += v[j];
+    }
+    u32 incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wt[wid] = incl;
+    __syncthreads();
+    u32 run = carry + incl - sum, all = 0;
+#pragma unroll
+    for (int w = 0; w < kST / 64; ++w) {
+      const u32 y = wt[w];
+      run += w < wid ? y : 0u;
+      all += y;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (b0 + j < nblocks) out[b0 + j] = run;
+      run += v[j];
+    }
+    carry += all;
+    __syncthreads();
+  }
+}
+
+// ---- route scratch: one per (device, stream) ------------------------------------------------------
+// Routes on one stream run in stream order, so they can share a buffer; routes on different streams
+// of one device may run at the same time and get their own. A buffer grows only after its stream has
+// drained (the kernels that used the old one are done). At most kMaxScratch streams per device keep
+// a buffer: the least recently used one is released (after a device sync) to make room.
 constexpr int kMaxDevices = 64;
+constexpr size_t kMaxScratch = 64;
 struct RouteScratch {
-  std::mutex mu;
   void* tmp = nullptr;
   size_t bytes = 0;
+  u64 used = 0;  // last use (LRU)
 };
-RouteScratch g_scratch[kMaxDevices];
+std::mutex g_scratch_mu;
+std::map<std::pair<int, hipStream_t>, RouteScratch> g_scratch;
+u64 g_scratch_clock = 0;
+
+// a scratch buffer of at least `need` bytes for routes on (dev, st); nullptr on failure
+void* route_scratch(int dev, hipStream_t st, size_t need) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  RouteScratch& sc = g_scratch[{dev, st}];
+  sc.used = ++g_scratch_clock;
+  if (sc.bytes < need) {
+    if (sc.tmp) {  // earlier routes on this stream may still read the old buffer
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(sc.tmp);
+    }
+    sc.tmp = nullptr;
+    sc.bytes = 0;
+    if (hipMalloc(&sc.tmp, need) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    sc.bytes = need;
+  }
+  void* p = sc.tmp;
+  size_t on_dev = 0;
+  for (auto& kv : g_scratch) on_dev += kv.first.first == dev;
+  if (on_dev > kMaxScratch) {  // release the least recently used buffer of this device (not this one)
+    auto victim = g_scratch.end();
+    for (auto it = g_scratch.begin(); it != g_scratch.end(); ++it)
+      if (it->first.first == dev && it->second.tmp != p && (victim == g_scratch.end() || it->second.used < victim->second.used))
+        victim = it;
+    if (victim != g_scratch.end()) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(victim->second.tmp);
+      g_scratch.erase(victim);
+    }
+  }
+  return p;
+}
 
 struct DevGuard {
   int prev = -1;
@@ -243,26 +355,13 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   const i64 nblocks = std::max<i64>(1, (n + chunk - 1) / chunk);
   int nbits = 1;
   while ((1 << nbits) <= nparts) ++nbits;  // owners and the sentinel nparts fit in nbits
-  RouteScratch& sc = g_scratch[dev];
-  std::lock_guard<std::mutex> lk(sc.mu);
-  const size_t hist_bytes = (size_t)nparts * nblocks * 4;
-  size_t scan_bytes = 0;
-  if (rocprim::exclusive_scan(nullptr, scan_bytes, (u32*)nullptr, (u32*)nullptr, 0u, (size_t)nparts * nblocks,
-                              rocprim::plus<u32>(), st) != hipSuccess)
-    return GLINT_EDEVICE;
-  const size_t need = 2 * ((hist_bytes + 255) & ~(size_t)255) + scan_bytes;
-  if (sc.bytes < need) {
-    // the old buffer may still be read by kernels queued on another stream of this device
-    if (sc.tmp) { (void)hipDeviceSynchronize(); (void)hipFree(sc.tmp); }
-    sc.tmp = nullptr;
-    sc.bytes = 0;
-    if (hipMalloc(&sc.tmp, need) != hipSuccess) { (void)hipGetLastError(); return GLINT_ENOMEM; }
-    sc.bytes = need;
-  }
-  char* b = (char*)sc.tmp;
+  const size_t hist_bytes = ((size_t)nparts * nblocks * 4 + 255) & ~(size_t)255;
+  const size_t need = 2 * hist_bytes + (size_t)kMaxParts * 4;
+  char* b = (char*)route_scratch(dev, st, need);
+  if (!b) return GLINT_ENOMEM;
   u32* hist = (u32*)b;
-  u32* offs = (u32*)(b + ((hist_bytes + 255) & ~(size_t)255));
-  void* scan_tmp = b + 2 * ((hist_bytes + 255) & ~(size_t)255);
+  u32* offs = (u32*)(b + hist_bytes);
+  u32* tot = (u32*)(b + 2 * hist_bytes);
   if (hipMemsetAsync(bad_dev, 0, 8, st) != hipSuccess) return GLINT_EDEVICE;
   if (nparts == 1 && !out.order && !out.keys && !out.cols && !out.vals && n > 0 &&
       ((uintptr_t)keys & 15) == 0) {
@@ -274,14 +373,13 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
     if (hipMemsetAsync(counts, 0, (size_t)nparts * 8, st) != hipSuccess) return GLINT_EDEVICE;
   } else {
     route_hist<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, hist, nblocks, bad_dev);
-    if (rocprim::exclusive_scan(scan_tmp, scan_bytes, hist, offs, 0u, (size_t)nparts * nblocks,
-                                rocprim::plus<u32>(), st) != hipSuccess)
-      return GLINT_EDEVICE;
+    route_row_sums<<<(unsigned)nparts, kST, 0, st>>>(hist, nblocks, tot, counts);
     // no output requested (a single partition: the batch is its own send buffer): counts and the
     // status word only
-    if (out.order || out.keys || out.cols || out.vals)
+    if (out.order || out.keys || out.cols || out.vals) {
+      route_row_scan<<<(unsigned)nparts, kST, 0, st>>>(hist, nblocks, tot, offs);
       route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, offs, nblocks, out);
-    route_counts<<<(unsigned)((nparts + 255) / 256), 256, 0, st>>>(offs, hist, nblocks, nparts, counts);
+    }
   }
   if (hipGetLastError() != hipSuccess) return GLINT_EDEVICE;
   return GLINT_OK;

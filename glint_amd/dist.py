@@ -132,63 +132,58 @@ class Router:
 class _Exchange:
     """The all-to-all legs of one routed call (send splits, receive splits, local layout).
 
-    Device batches over RCCL: the (rank, partition) count matrix is built and exchanged on the
-    device, and the host reads it ONCE together with the route's status word; that single read gives
-    both the send and the receive splits. A batch with an out-of-range key sends nothing (every rank
-    still joins the collectives) and raises after them, so the other ranks' pushes complete."""
+    One code path for every backend: the (rank, partition) count matrix is built where the counts
+    are (on the device for a device route, on the host for the host route), exchanged with one
+    ``all_to_all_single``, and read by the host ONCE together with the route's status word; that
+    single read gives both the send and the receive splits. Only the transport differs (``_a2a``):
+    RCCL (``nccl``) exchanges device tensors, gloo host tensors. A batch with an out-of-range key
+    sends nothing (every rank still joins the collectives) and raises after them, so the other
+    ranks' pushes complete."""
 
-    def __init__(self, router: Router, rank: int, counts, group, device, bad=None):
+    def __init__(self, router: Router, rank: int, counts: torch.Tensor, group, comm_device, bad=None,
+                 bad_exc=None):
         W, maxp = router.world, router.maxp
-        self.group, self.device, self.world = group, device, W
+        self.group, self.comm, self.world = group, comm_device, W
         self.bad = -1
-        self.bad_exc = None
-        if isinstance(counts, torch.Tensor) and device.type == "cuda":
-            _, cell = router._device_tables(counts.device)
-            send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
+        self.bad_exc = bad_exc
+        _, cell = router._device_tables(counts.device)
+        send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
+        if bad_exc is None:
             send[cell] = counts
-            if bad is not None:
-                send = torch.where(bad == 0, send, torch.zeros_like(send))
-            recv = torch.empty_like(send)
-            if W > 1:
-                dist.all_to_all_single(recv, send, group=group)
-            else:
-                recv = send
-            parts = [send, recv] + ([bad] if bad is not None else [])
-            host = torch.cat(parts).cpu().numpy()  # the call's one host synchronisation
-            send_h, recv_h = host[:W * maxp].reshape(W, maxp), host[W * maxp:2 * W * maxp].reshape(W, maxp)
-            if bad is not None and host[-1] != 0:
-                self.bad = int(~host[-1])
-        else:
-            if isinstance(counts, torch.Tensor):  # device route, host (gloo) exchange
-                host = torch.cat([counts] + ([bad] if bad is not None else [])).cpu().numpy()
-                if bad is not None and host[-1] != 0:
-                    self.bad = int(~host[-1])
-                counts = host[:router.nparts]
-            send_h = np.zeros((W, maxp), dtype=np.int64)
-            if self.bad < 0:
-                send_h.reshape(-1)[router.slot_cell] = counts
-            recv = torch.empty((W, maxp), dtype=torch.int64, device=device)
-            dist.all_to_all_single(recv, torch.from_numpy(send_h).to(device), group=group)
-            recv_h = recv.cpu().numpy()
+        if bad is not None:
+            send = torch.where(bad == 0, send, torch.zeros_like(send))
+        recv = self._a2a(send) if W > 1 else send
+        parts = [send, recv] + ([bad] if bad is not None else [])
+        host = torch.cat(parts).cpu().numpy()  # the call's one host synchronisation
+        send_h, recv_h = host[:W * maxp].reshape(W, maxp), host[W * maxp:2 * W * maxp].reshape(W, maxp)
+        if bad is not None and host[-1] != 0:
+            self.bad = int(~host[-1])
         self.recv_counts = recv_h  # [source rank, local partition j]
         self.in_splits = send_h.sum(axis=1).tolist()
         self.out_splits = recv_h.sum(axis=1).tolist()
         self.nlocal = len(router.rank_parts[rank])
+        # start of each source rank's block in the received buffer, and of partition j inside it
+        self._src_off = np.concatenate([[0], np.cumsum(recv_h.sum(axis=1))])
+        self._part_off = np.concatenate([np.zeros((W, 1), np.int64), np.cumsum(recv_h, axis=1)], axis=1)
+
+    def _a2a(self, t: torch.Tensor, out_splits=None, in_splits=None) -> torch.Tensor:
+        """all_to_all_single on the backend's side of the bus, result on t's device: the only part
+        of the exchange that depends on the backend."""
+        src = t if t.device == self.comm else t.to(self.comm)
+        rows = sum(out_splits) if out_splits is not None else t.shape[0]
+        out = torch.empty((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.comm)
+        dist.all_to_all_single(out, src.contiguous(), out_splits, in_splits, group=self.group)
+        return out if out.device == t.device else out.to(t.device)
 
     def forward(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:  # a world of one exchanges with itself: the send buffer is the receive buffer
             return t[:self.out_splits[0]]
-        out = torch.empty((sum(self.out_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_to_all_single(out, t[:sum(self.in_splits)].contiguous(), self.out_splits, self.in_splits,
-                               group=self.group)
-        return out
+        return self._a2a(t[:sum(self.in_splits)], self.out_splits, self.in_splits)
 
     def backward(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return t
-        out = torch.empty((sum(self.in_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_to_all_single(out, t.contiguous(), self.in_splits, self.out_splits, group=self.group)
-        return out
+        return self._a2a(t, self.in_splits, self.out_splits)
 
     def raise_if_bad(self, keys: torch.Tensor, nkeys: int):
         if self.bad_exc is not None:
@@ -197,17 +192,33 @@ class _Exchange:
             i = self.bad
             raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {nkeys})")
 
-    def local_index(self, j: int) -> Optional[torch.Tensor]:
-        """Positions in the received buffer of local partition j's records (source-rank order);
-        None when the local shard owns the whole buffer."""
+    def local_ranges(self, j: int):
+        """Local partition j's records in the received buffer: one (start, length) range per source
+        rank, in source-rank order (each source's records in its caller's order)."""
+        return [(int(self._src_off[s] + self._part_off[s, j]), int(self.recv_counts[s, j]))
+                for s in range(self.recv_counts.shape[0]) if self.recv_counts[s, j]]
+
+    def take(self, buf: torch.Tensor, j: int) -> torch.Tensor:
+        """Local partition j's records of a received buffer: a view when they are one range (one
+        source, or one local partition), else the ranges concatenated -- no index array."""
         if self.nlocal == 1:
-            return None
-        seg = np.concatenate([[0], np.cumsum(self.recv_counts.sum(axis=1))])
-        parts = []
-        for s in range(self.recv_counts.shape[0]):
-            a = seg[s] + self.recv_counts[s, :j].sum()
-            parts.append(np.arange(a, a + self.recv_counts[s, j], dtype=np.int64))
-        return torch.from_numpy(np.concatenate(parts)).to(self.device)
+            return buf
+        rs = self.local_ranges(j)
+        if not rs:
+            return buf[:0]
+        if len(rs) == 1:
+            return buf[rs[0][0]:rs[0][0] + rs[0][1]]
+        return torch.cat([buf[a:a + c] for a, c in rs])
+
+    def put(self, resp: torch.Tensor, j: int, got: torch.Tensor) -> torch.Tensor:
+        """Writes local partition j's answers into the response buffer (the inverse of take)."""
+        if self.nlocal == 1:
+            return got
+        o = 0
+        for a, c in self.local_ranges(j):
+            resp[a:a + c] = got[o:o + c]
+            o += c
+        return resp
 
 
 class _Distributed:
@@ -224,18 +235,13 @@ class _Distributed:
     def nrOfPartitions(self) -> int:
         return self.router.nparts
 
-    def _comm_device(self, t: torch.Tensor) -> torch.Tensor:
-        # gloo exchanges host tensors; nccl (RCCL) device tensors
-        if dist.get_backend(self.group) == "gloo":
-            return t.cpu()
-        return t
-
-    def _nccl(self, keys: torch.Tensor) -> bool:
-        return keys.is_cuda and dist.get_backend(self.group) != "gloo"
+    def _comm(self, t: torch.Tensor) -> torch.device:
+        # the transport's side of the bus: gloo exchanges host tensors, RCCL (nccl) device tensors
+        return torch.device("cpu") if dist.get_backend(self.group) == "gloo" else t.device
 
     def _begin(self, keys: torch.Tensor):
-        """Host path (CPU tensors, or gloo): order + host counts, records gathered by index. A batch
-        with an out-of-range key sends nothing and raises after the collectives (raise_if_bad)."""
+        """Host route (CPU keys): order + counts on the host, records gathered by index. A batch with
+        an out-of-range key sends nothing and raises after the collectives (raise_if_bad)."""
         exc = None
         try:
             order, counts = self.router.group(keys)
@@ -243,16 +249,14 @@ class _Distributed:
             exc = e
             order = torch.zeros(0, dtype=torch.int64, device=keys.device)
             counts = np.zeros(self.router.nparts, dtype=np.int64)
-        comm = torch.device("cpu") if dist.get_backend(self.group) == "gloo" else keys.device
-        ex = _Exchange(self.router, self.rank, counts, self.group, comm)
-        ex.bad_exc = exc
+        ex = _Exchange(self.router, self.rank, torch.from_numpy(np.ascontiguousarray(counts, np.int64)), self.group,
+                       self._comm(keys), bad_exc=exc)
         return order, ex
 
     def _begin_fused(self, keys, cols=None, vals=None, want_order=False):
-        """Device path: the fused route writes the send buffers; one host read for the splits."""
+        """Device route: the fused route writes the send buffers; one host read for the splits."""
         counts, order, sk, sc, sv, bad = self.router.route(keys, cols, vals, want_order)
-        comm = keys.device if self._nccl(keys) else torch.device("cpu")
-        ex = _Exchange(self.router, self.rank, counts, self.group, comm, bad)
+        ex = _Exchange(self.router, self.rank, counts, self.group, self._comm(keys), bad)
         return ex, order, sk, sc, sv
 
     def _to_shard(self, t: torch.Tensor) -> torch.Tensor:
@@ -260,8 +264,7 @@ class _Distributed:
 
     def _split(self, ex: _Exchange, *bufs):
         for j, sh in enumerate(self.shards):
-            idx = ex.local_index(j)
-            yield j, sh, [b if idx is None else b.index_select(0, idx.to(b.device)) for b in bufs]
+            yield j, sh, [ex.take(b, j) for b in bufs]
 
     def destroy(self) -> bool:
         for sh in self.shards:
@@ -284,11 +287,11 @@ class DistributedBigVector(_Distributed):
             raise ValueError("keys and values differ in length")
         if keys.is_cuda and values.device == keys.device:
             ex, _, sk, _, sv = self._begin_fused(keys, vals=values.contiguous())
-            rk, rv = ex.forward(self._comm_device(sk)), ex.forward(self._comm_device(sv))
+            rk, rv = ex.forward(sk), ex.forward(sv)
         else:
             order, ex = self._begin(keys)
-            rk = ex.forward(self._comm_device(keys.index_select(0, order)))
-            rv = ex.forward(self._comm_device(values.index_select(0, order.to(values.device))))
+            rk = ex.forward(keys.index_select(0, order))
+            rv = ex.forward(values.index_select(0, order.to(values.device)))
         for _, sh, (k, v) in self._split(ex, rk, rv):
             if k.numel():
                 sh.update(self._to_shard(k), self._to_shard(v), deterministic=deterministic)
@@ -299,19 +302,14 @@ class DistributedBigVector(_Distributed):
         keys = keys.reshape(-1).to(torch.int64)
         if keys.is_cuda:
             ex, order, sk, _, _ = self._begin_fused(keys, want_order=True)
-            rk = ex.forward(self._comm_device(sk))
+            rk = ex.forward(sk)
         else:
             order, ex = self._begin(keys)
-            rk = ex.forward(self._comm_device(keys.index_select(0, order)))
+            rk = ex.forward(keys.index_select(0, order))
         resp = torch.empty(rk.numel(), dtype=self.dtype, device=rk.device)
         for j, sh, (k,) in self._split(ex, rk):
             if k.numel():
-                got = sh.get(self._to_shard(k)).to(resp.device)
-                idx = ex.local_index(j)
-                if idx is None:
-                    resp = got
-                else:
-                    resp.index_copy_(0, idx.to(resp.device), got)
+                resp = ex.put(resp, j, sh.get(self._to_shard(k)).to(resp.device))
         back = ex.backward(resp).to(keys.device)
         ex.raise_if_bad(keys, self.router.nkeys)  # after the collectives: this rank asked for nothing
         if order is None:  # one partition: the answer is already in the caller's order
@@ -338,12 +336,12 @@ class DistributedBigMatrix(_Distributed):
             raise ValueError("rows, cols and values differ in length")
         if rows.is_cuda and cols.device == rows.device and values.device == rows.device:
             ex, _, sr, sc, sv = self._begin_fused(rows, cols=cols.contiguous(), vals=values.contiguous())
-            rr, rc, rv = (ex.forward(self._comm_device(t)) for t in (sr, sc, sv))
+            rr, rc, rv = (ex.forward(t) for t in (sr, sc, sv))
         else:
             order, ex = self._begin(rows)
-            rr = ex.forward(self._comm_device(rows.index_select(0, order)))
-            rc = ex.forward(self._comm_device(cols.index_select(0, order.to(cols.device))))
-            rv = ex.forward(self._comm_device(values.index_select(0, order.to(values.device))))
+            rr = ex.forward(rows.index_select(0, order))
+            rc = ex.forward(cols.index_select(0, order.to(cols.device)))
+            rv = ex.forward(values.index_select(0, order.to(values.device)))
         for _, sh, (r, c, v) in self._split(ex, rr, rc, rv):
             if r.numel():
                 sh.update(self._to_shard(r), self._to_shard(c), self._to_shard(v), deterministic=deterministic)
@@ -359,12 +357,12 @@ class DistributedBigMatrix(_Distributed):
         if rows.is_cuda and (cols is None or cols.device == rows.device):
             ex, order, sr, sc, _ = self._begin_fused(rows, cols=None if cols is None else cols.contiguous(),
                                                      want_order=True)
-            rr = ex.forward(self._comm_device(sr))
-            rc = None if cols is None else ex.forward(self._comm_device(sc))
+            rr = ex.forward(sr)
+            rc = None if cols is None else ex.forward(sc)
         else:
             order, ex = self._begin(rows)
-            rr = ex.forward(self._comm_device(rows.index_select(0, order)))
-            rc = None if cols is None else ex.forward(self._comm_device(cols.index_select(0, order.to(cols.device))))
+            rr = ex.forward(rows.index_select(0, order))
+            rc = None if cols is None else ex.forward(cols.index_select(0, order.to(cols.device)))
         if cols is None:
             shape = (rr.numel(), self.cols)
             bufs = (rr,)
@@ -376,12 +374,7 @@ class DistributedBigMatrix(_Distributed):
             if parts[0].numel():
                 got = (sh.getRows(self._to_shard(parts[0])) if cols is None
                        else sh.get(self._to_shard(parts[0]), self._to_shard(parts[1])))
-                got = got.to(resp.device).reshape((-1,) + shape[1:])
-                idx = ex.local_index(j)
-                if idx is None:
-                    resp = got
-                else:
-                    resp.index_copy_(0, idx.to(resp.device), got)
+                resp = ex.put(resp, j, got.to(resp.device).reshape((-1,) + shape[1:]))
         back = ex.backward(resp).to(rows.device)
         ex.raise_if_bad(rows, self.router.nkeys)
         if order is None:  # one partition: the answer is already in the caller's order

@@ -132,7 +132,9 @@ class _Shard:
     # pipelined host ingest (include/glint_gpu.h): enqueue now, wait for the ticket before acknowledging
     def push_async(self, *arrays, deterministic: bool = False, unordered: bool = False) -> int:
         """Stage (keys, values) -- or (rows, cols, values) for a matrix -- in a pinned ring slot and
-        enqueue the push; returns its ticket (glint_stage_acquire + glint_push_staged)."""
+        enqueue the push; returns its ticket (glint_stage_acquire + glint_push_staged). A record outside
+        the partition raises ArrayIndexOutOfBoundsException here, at the message (as update() throws in
+        the reference), and nothing of the message is applied."""
         mat = self.cols != 0
         if len(arrays) != (3 if mat else 2):
             raise ValueError("push_async(keys, values) for vectors, (rows, cols, values) for matrices")
@@ -183,8 +185,8 @@ class _Shard:
         return ticket.value, out
 
     def wait(self, ticket: int) -> None:
-        """Until the push with this ticket (and every earlier one) is applied; raises if one of them
-        rejected a record (ArrayIndexOutOfBoundsException, as the actor's update would)."""
+        """Until the push with this ticket (and every earlier one) is applied; raises GlintDeviceError if
+        one of them failed to launch (rejected records raise at the enqueueing call instead)."""
         bad = C.c_int64(-1)
         rc = self.lib.glint_shard_wait(self.handle, ticket, C.byref(bad))
         if rc == N.GLINT_EOUTOFRANGE:

@@ -160,8 +160,12 @@ int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uin
  * pinned slot (no copy command); larger ones cross PCIe in one DMA. Tickets number the enqueued
  * pushes of a shard; glint_shard_wait(ticket) returns once that push and every push enqueued before
  * it are applied -- what the actor needs before it answers AcknowledgeReceipt
- * (PushLogic.scala:40-66) -- with GLINT_EOUTOFRANGE (first bad record via glint_shard_last_error) if
- * one of them rejected a record. Every other call on the shard is ordered after the enqueued pushes.
+ * (PushLogic.scala:40-66). Every other call on the shard is ordered after the enqueued pushes.
+ * Errors belong to the call that enqueues a message, as the reference's update/get throw while the
+ * actor handles the Push/Pull message itself (PartialVectorDouble.scala:17-23): the enqueueing call
+ * checks every record first and returns GLINT_EOUTOFRANGE (first bad record via
+ * glint_shard_last_error) with nothing of that message enqueued; a wait reports only a launch that
+ * failed on the device (GLINT_EDEVICE, once, to the first wait covering it).
  * Flags as for glint_vec_push (message order kept for Float/Double unless GLINT_PUSH_UNORDERED).
  * An entry of up to GLINT_ZERO_COPY_MAX records is ONE single-workgroup kernel that signals its own
  * completion through a host-mapped word (no event, no copy command): a few microseconds of stream
@@ -183,12 +187,14 @@ int glint_push_staged(glint_shard_t shard, int slot, int64_t n, int flags, uint6
 /* glint_push_wire, enqueued: the payload is copied into a slot before the call returns. */
 int glint_push_wire_async(glint_shard_t shard, const uint8_t* payload, size_t len, int32_t* id, int flags,
                           uint64_t* ticket);
-/* Waits for the entry with this ticket and every earlier one; reports their errors (a rejected key
- * of a pull included) and completes their pulls' answers. */
+/* Waits for the entry with this ticket and every earlier one and completes their pulls' answers;
+ * GLINT_EDEVICE if one of them failed to launch. */
 int glint_shard_wait(glint_shard_t shard, uint64_t ticket, int64_t* first_bad);
 /* glint_vec_pull (kind 0), glint_mat_pull (1) or glint_mat_pull_rows (2), enqueued: the keys (and
- * cols) are copied before the call returns; `out` receives the answer by the time
- * glint_shard_wait(*ticket) returns and must stay valid until then. n <= 2^20. */
+ * cols) are checked and copied before the call returns; `out` receives the answer by the time
+ * glint_shard_wait(*ticket) returns and must stay valid until then. n <= 2^20. An answer of more than
+ * 16 MiB (row pulls of wide matrices) is produced before the call returns instead, so the ring's pinned
+ * memory stays bounded. */
 int glint_pull_async(glint_shard_t shard, int kind, const int64_t* keys, const int32_t* cols, void* out,
                      int64_t n, uint64_t* ticket);
 /* glint_pull_wire, enqueued: the response header is written at once, its values by the time

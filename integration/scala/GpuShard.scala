@@ -73,9 +73,15 @@ object GpuShard {
   * -- which makes the id acknowledgeable -- runs when the AcknowledgeReceipt for it arrives, after
   * `await(ticket)`. The client's PushFSM (PushFSM.scala:88-120) sends that acknowledgement request
   * right after the push, so the actor answers it exactly as before, once the push is applied, and
-  * meanwhile takes the next messages. An out-of-partition key surfaces from that await as
-  * ArrayIndexOutOfBoundsException, Akka restarts the actor, and its constructor allocates a new,
-  * zeroed shard (the reference's restart re-creates `new Array[V](size)`).
+  * meanwhile takes the next messages. The await covers every push enqueued before it, so all of them
+  * become acknowledgeable then (`pending` holds only pushes newer than the last awaited one).
+  *
+  * Errors happen where the reference's happen: the library checks a message's keys when it is
+  * enqueued, so an out-of-partition key throws ArrayIndexOutOfBoundsException from the Push (or Pull)
+  * message itself, with nothing of it applied; Akka restarts the actor, postStop frees the shard and
+  * the new instance allocates a zeroed one (the reference's restart re-creates `new Array[V](size)`).
+  * The client's AcknowledgeReceipt then reaches the new actor and is answered NotAcknowledgeReceipt
+  * (PushLogic.scala:44-49), and a Pull after the restart is answered from the zeroed shard.
   */
 trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
   protected def shard: Long
@@ -83,12 +89,14 @@ trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
 
   protected def enqueued(id: Int, ticket: Long): Unit = pending.put(id, ticket)
 
-  /** AcknowledgeReceipt(id) of an enqueued push: wait for it, then mark it received (PushLogic). */
+  /** AcknowledgeReceipt(id) of an enqueued push: wait for it, then mark it -- and every push enqueued
+    * before it, which the same wait covers -- received (PushLogic.updateFinished). */
   protected def settle(message: Any, finished: Int => Unit): Unit = message match {
     case AcknowledgeReceipt(id) =>
-      pending.remove(id).foreach { ticket =>
+      pending.get(id).foreach { ticket =>
         GpuShard.await(shard, ticket)
-        finished(id)
+        val done = pending.collect { case (i, t) if t <= ticket => i }.toList
+        done.foreach { i => pending.remove(i); finished(i) }
       }
     case _ =>
   }

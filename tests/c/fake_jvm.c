@@ -1,7 +1,9 @@
 /* The JNIEnv of tests/c/jni.h over plain C arrays, plus a driver that calls the shim's native
  * methods in the order the GPU actors (integration/scala/GpuShard.scala) call them:
  * create -> push (ticket) -> await -> pull; an order-sensitive Double push; an out-of-partition
- * push -> await throws ArrayIndexOutOfBoundsException -> zero (the Akka restart) -> push again;
+ * push throws ArrayIndexOutOfBoundsException at the Push message itself (as update() throws inside
+ * receive, PartialVectorDouble.scala:17-23) and applies nothing, while earlier pushes' awaits and a
+ * pull stay clean; an out-of-partition pull throws the same way; zero (the Akka restart) -> push again;
  * argument errors (value type, short arrays); a matrix shard's element and row pulls; destroy.
  * Exit status 0 and "ok" on stdout when every check passes. */
 #include <math.h>
@@ -117,14 +119,32 @@ int main(int argc, char** argv) {
   seq = seq + 1.0;
   seq = seq + 1.0;
   CHECK(((jdouble*)o1->data)[0] == seq && ((jdouble*)o1->data)[2] == seq, "sequential Double order");
-  /* an out-of-partition key: the await throws ArrayIndexOutOfBoundsException; restart = zero */
+  /* an out-of-partition key: the Push itself throws ArrayIndexOutOfBoundsException and nothing of it
+   * is applied; a push enqueued before it and a pull after it are clean; restart = zero */
   Arr* kb = arr(2, 8);
   Arr* vb = arr(2, 8);
   ((jlong*)kb->data)[0] = 1001;
   ((jlong*)kb->data)[1] = 2000;
-  t = NAT(vecPushD)(env, NULL, h, kb, vb, 0);
-  NAT(await)(env, NULL, h, t);
-  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "out-of-partition key raises");
+  ((jdouble*)vb->data)[0] = 7.0;
+  Arr* k1 = arr(1, 8);
+  Arr* v1 = arr(1, 8);
+  ((jlong*)k1->data)[0] = 1002;
+  ((jdouble*)v1->data)[0] = 0.25;
+  const jlong t_before = NAT(vecPushD)(env, NULL, h, k1, v1, 0);
+  CHECK(t_before > 0 && !pending[0], "push before the bad one");
+  NAT(vecPushD)(env, NULL, h, kb, vb, 0);
+  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "out-of-partition key raises at the Push");
+  NAT(await)(env, NULL, h, t_before);
+  CHECK(!pending[0], "the earlier push's await is clean");
+  Arr* k2 = arr(2, 8);
+  ((jlong*)k2->data)[0] = 1001;
+  ((jlong*)k2->data)[1] = 1002;
+  Arr* o2 = arr(2, 8);
+  NAT(vecPullD)(env, NULL, h, k2, o2);
+  CHECK(!pending[0] && ((jdouble*)o2->data)[0] == 0.5 && ((jdouble*)o2->data)[1] == 1.0 + 0.25,
+        "clean pull after the bad push; the bad push applied nothing");
+  NAT(vecPullD)(env, NULL, h, kb, o2);
+  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "out-of-partition pull raises");
   NAT(zero)(env, NULL, h);
   NAT(await)(env, NULL, h, NAT(vecPushD)(env, NULL, h, k3, v3, 0));
   NAT(vecPullD)(env, NULL, h, k3, o1);

@@ -178,3 +178,52 @@ CASES = {
     "mat_range": _matrix_case(1_003, 17, 1),
     "mat_range_mps2": _matrix_case(1_003, 17, 2),
 }
+
+
+def run_cfg4(rank, world, port, backend, nbatch, log2_batch):
+    """BASELINE.json configs[3] at its own key space on one GPU: RangePartitioner(8, 2^31) -- eight
+    2^28-key Long shards (modelsPerServer = 8 on one server) behind DistributedClient -- fed `nbatch`
+    client batches of 2^log2_batch uniform keys (the 64 loopback clients of cfg4), each routed to the
+    8 shards by glint_route_gather_dev (AsyncBigVector.scala:96-121). Long sums are exact in any
+    order, so every shard must equal a torch.index_add_ int64 reference bit for bit; two sampled key
+    ranges are replayed through the oracle's sequential update loop as well."""
+    _init(rank, world, port, backend)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        from glint_amd.dist import DistributedClient
+        nkeys = 1 << 31
+        client = DistributedClient(device=dev)
+        vec = client.vector(nkeys, "long", modelsPerServer=8)
+        parts = vec.partitioner.all()
+        assert vec.nrOfPartitions == 8 and all(p.size == 1 << 28 for p in parts)
+        ref = torch.zeros(nkeys, dtype=torch.int64, device=dev)
+        # oracle replay windows: 2^20 keys inside partitions 2 and 7 (the last key of the space included)
+        windows = [(parts[2].start + 12_345, parts[2].start + 12_345 + (1 << 20)), (nkeys - (1 << 20), nkeys)]
+        orc = [O.OracleVector(O.part_range(a, b), O.O_I64) for a, b in windows]
+        n = 1 << log2_batch
+        for c in range(nbatch):
+            g = torch.Generator(device=dev)
+            g.manual_seed(4000 + c)
+            k = torch.randint(0, nkeys, (n,), dtype=torch.int64, device=dev, generator=g)
+            v = torch.randint(-(1 << 40), 1 << 40, (n,), dtype=torch.int64, device=dev, generator=g)
+            assert vec.push(k, v)
+            ref.index_add_(0, k, v)
+            for (a, b), o in zip(windows, orc):
+                m = (k >= a) & (k < b)
+                assert o.update(k[m].cpu().numpy(), v[m].cpu().numpy()) == -1
+        torch.cuda.synchronize(dev)
+        for p, sh in zip(parts, vec.shards):
+            got = sh.get(torch.arange(p.start, p.end, dtype=torch.int64, device=dev))
+            assert torch.equal(got, ref[p.start:p.end]), f"partition {p.index} differs from index_add_"
+            del got
+        for (a, b), o in zip(windows, orc):
+            got = vec.pull(torch.arange(a, b, dtype=torch.int64, device=dev)).cpu().numpy()
+            np.testing.assert_array_equal(got, o.data)
+        # pulls of random keys over all 8 shards come back in the caller's order
+        q = torch.randint(0, nkeys, (1 << 20,), dtype=torch.int64, device=dev)
+        assert torch.equal(vec.pull(q), ref[q])
+        vec.destroy()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

@@ -161,3 +161,36 @@ def test_route_one_partition_validates_only(gpu, n):
             assert int(bad.item()) != 0 and ~int(bad.item()) == min(bad_at)
         else:
             assert int(bad.item()) == 0 and int(counts.item()) == n
+
+
+def test_routes_on_two_streams_at_once(gpu):
+    """Two routes on two streams of one device run concurrently: each keeps its own scratch
+    (histogram, offsets), so both equal the oracle's bucketing."""
+    import torch
+    d = torch.device("cuda", gpu)
+    lib = N.load()
+    nkeys, n = 1 << 30, 1 << 23
+    cases = []
+    for j, nparts in enumerate((8, 1000)):
+        rng = np.random.default_rng(500 + j)
+        keys = rng.integers(0, nkeys, n).astype(np.int64)
+        cases.append((nparts, keys, torch.from_numpy(keys).to(d)))
+    torch.cuda.synchronize(d)
+    streams = [torch.cuda.Stream(d), torch.cuda.Stream(d)]
+    outs = []
+    for (nparts, _, kt), st in zip(cases, streams):
+        with torch.cuda.stream(st):
+            counts = torch.full((nparts,), -7, dtype=torch.int64, device=d)
+            order = torch.full((n,), -7, dtype=torch.int64, device=d)
+            bad = torch.full((1,), -7, dtype=torch.int64, device=d)
+            rc = lib.glint_route_gather_dev(kt.data_ptr(), None, None, 0, n, N.GLINT_ROUTE_RANGE, nparts, nkeys,
+                                            None, counts.data_ptr(), order.data_ptr(), None, None, None,
+                                            bad.data_ptr(), st.cuda_stream)
+            assert rc == N.GLINT_OK
+            outs.append((counts, order, bad))
+    torch.cuda.synchronize(d)
+    for (nparts, keys, _), (counts, order, bad) in zip(cases, outs):
+        c_ref, _, o_ref = O.bucket_range(keys, nparts, nkeys)
+        assert int(bad.item()) == 0
+        np.testing.assert_array_equal(counts.cpu().numpy(), c_ref)
+        np.testing.assert_array_equal(order.cpu().numpy(), o_ref)

@@ -529,6 +529,45 @@ def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
         assert cnt.value == 0
 
 
+def test_adaptive_switch_decides_at_sync_points(gpu, monkeypatch):
+    """The binned/scatter choice of a device-resident push comes from the previous pushes' tails as
+    of the shard's last sync point, never from a word the device may or may not have written yet:
+    unsynchronised pushes keep the path they started with, and the same sequence of pushes and
+    syncs takes the same paths on every run."""
+    import torch
+    lib = N.load()
+    d = torch.device("cuda", gpu)
+    size = 1 << 22
+    part = RangePartition(0, 0, size)
+    rng = np.random.default_rng(31)
+    keys = torch.from_numpy(rng.integers(0, size, 1 << 21).astype(np.int64)).to(d)
+    vals = torch.from_numpy(rng.integers(-5, 5, 1 << 21).astype(np.int64)).to(d)
+    monkeypatch.delenv("GLINT_BINNED", raising=False)
+
+    def binned_launches(sh):
+        ms, cnt = C.c_double(), C.c_int64()
+        lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
+        return cnt.value
+
+    runs = []
+    for _ in range(2):
+        with PartialVector(part, "long", gpu) as sh:
+            lib.glint_prof_enable(sh.handle, 1)
+            seq = []
+            for _ in range(3):  # no sync in between: no history is taken up, the scatter every time
+                sh.update(keys, vals, sync=False)
+                seq.append(binned_launches(sh))
+            sh.sync()
+            for _ in range(2):  # after the sync point: the large unordered tail is known -> binned
+                sh.update(keys, vals, sync=False)
+                seq.append(binned_launches(sh))
+            sh.sync()
+            np.testing.assert_array_equal(sh.to_numpy(), 5 * np.bincount(keys.cpu().numpy(), vals.cpu().numpy(),
+                                                                              minlength=size).astype(np.int64))
+            runs.append(seq)
+    assert runs[0] == [0, 0, 0, 1, 2] and runs[1] == runs[0]
+
+
 @pytest.mark.parametrize("dtype", ["double", "int"])
 def test_binned_matrix_push(gpu, dtype):
     rng = np.random.default_rng(11)

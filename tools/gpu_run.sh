@@ -1,0 +1,78 @@
+# One gpurun session, by stages (run from the repo root through gpurun):
+#   STAGES="tests bench prof2p30 binned pmc" bash tools/gpu_run.sh
+# Every GPU step has its own time limit; the first failing step ends the session (its log stays
+# under gpurun_out/$TAG). Stages:
+#   tests     python -m pytest tests -m gpu, then smoke()
+#   bench     the driver's default line (cfg2 with the CPU baseline) and the other bench lines
+#   prof2p30  rocprofv3 kernel stats of the dense push at 2^28 and at 2^30 (north-star size)
+#   binned    rocprofv3 kernel stats of the binned patterns (zipf, matrix, exchange)
+#   micro     tools/microbench_stream mode 6: the dense sweep at 2^26..2^30, chunked and shifted
+#   pmc       FETCH_SIZE / WRITE_SIZE passes (separate runs) of the dense, zipf and matrix lines
+set -o pipefail
+TAG=${TAG:-r03}
+R=$(pwd)
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <command...>: output to $OUT/<name>.log
+  local name=$1 secs=$2
+  shift 2
+  echo "[$(date +%T)] $name" >&2
+  timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >&2
+  if [ $rc -ne 0 ]; then tail -30 $OUT/$name.log >&2; exit $rc; fi
+}
+kstats() {  # kstats <name> <seconds> <bench args...>: kernel stats CSV of one bench command
+  local name=$1 secs=$2
+  shift 2
+  echo "[$(date +%T)] kstats $name" >&2
+  (cd /tmp && timeout -k 10 $secs rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$name -o run \
+     -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/prof_$name.log 2>&1) || { tail -30 $OUT/prof_$name.log >&2; exit 1; }
+  find /tmp/prof_$name -name "*kernel_stats.csv" -exec cp {} $OUT/kstats_$name.csv \;
+}
+pmc() {  # pmc <name> <bench args...>: FETCH_SIZE and WRITE_SIZE in two separate passes
+  local name=$1
+  shift
+  for c in FETCH_SIZE WRITE_SIZE; do
+    echo "[$(date +%T)] pmc $name $c" >&2
+    (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d /tmp/pmc_${name}_$c -o run \
+       -- python3 $R/bench.py --no-cpu-baseline --no-check --steps 5 --warmup 2 "$@" > $OUT/pmc_${name}_$c.log 2>&1) \
+       || { tail -30 $OUT/pmc_${name}_$c.log >&2; exit 1; }
+    find /tmp/pmc_${name}_$c -name "*counter_collection.csv" -exec cp {} $OUT/pmc_${name}_$c.csv \;
+  done
+}
+for s in ${STAGES:-tests bench}; do
+  case $s in
+    tests)
+      step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+      ;;
+    bench)
+      step bench_default 400 python3 bench.py
+      for pat in zipf matrix exchange pull rowpull; do
+        step bench_$pat 300 python3 bench.py --no-cpu-baseline --pattern $pat
+      done
+      ;;
+    prof2p30)
+      kstats dense_2p28 300
+      kstats dense_2p30 400 --log2-keys 30 --steps 10
+      ;;
+    binned)
+      for pat in zipf matrix exchange; do kstats $pat 300 --pattern $pat; done
+      ;;
+    pmc)
+      pmc dense_2p28
+      pmc zipf_2p28 --pattern zipf
+      pmc matrix_2p17x512 --pattern matrix
+      ;;
+    micro)
+      step micro_stream_2p30 300 tools/microbench_stream 30 9 6
+      ;;
+    *)
+      echo "unknown stage $s" >&2
+      exit 2
+      ;;
+  esac
+done
+echo "session done" >&2

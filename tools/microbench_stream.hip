@@ -266,6 +266,44 @@ int main(int argc, char** argv) {
     printf("done\n");
     return 0;
   }
+  if (mode == 6) {
+    // the push_apply sweep's shape (2 pairs per lane, all non-temporal, one 256-thread block per
+    // CU) at 2^26..2^lg records: whole, in 2^28-record launches, and with the value stream shifted
+    // against the shard stream -- why does 2^30 run slower per byte than 2^28?
+    double *v2, *d2;
+    CK(hipMalloc(&v2, n * 8 + (64 << 20)));
+    CK(hipMalloc(&d2, n * 8 + (64 << 20)));
+    CK(hipMemset(v2, 0, n * 8 + (64 << 20)));
+    CK(hipMemset(d2, 0, n * 8 + (64 << 20)));
+    CK(hipDeviceSynchronize());
+    printf("vals %p data %p (delta %lld MiB)\n", (void*)v2, (void*)d2, (long long)(((char*)d2 - (char*)v2) >> 20));
+    for (int l = 26; l <= lg; ++l) {
+      const i64 m2 = (1ll << l) / 2;
+      const float ms = timeit([&] { k_apply<2, 0, 1, 1, 1, 256><<<cus, 256>>>((const D2*)v2, (D2*)d2, m2); }, reps);
+      printf("sweep 2^%d whole: %7.3f ms %6.0f GB/s\n", l, ms, 24.0 * (2 * m2) / ms / 1e6);
+    }
+    for (int cl : {26, 27, 28, 29}) {
+      if (cl >= lg) continue;
+      const i64 c2 = (1ll << cl) / 2;
+      const float ms = timeit([&] {
+        for (i64 o = 0; o < n2; o += c2)
+          k_apply<2, 0, 1, 1, 1, 256><<<cus, 256>>>((const D2*)v2 + o, (D2*)d2 + o, std::min(c2, n2 - o));
+      }, reps);
+      printf("sweep 2^%d in 2^%d launches: %7.3f ms %6.0f GB/s\n", lg, cl, ms, 24.0 * n / ms / 1e6);
+    }
+    for (i64 shift : {4096ll, 65536ll, 1ll << 20, (2ll << 20) + 4096, (16ll << 20) + 65536}) {
+      const float ms = timeit([&] {
+        k_apply<2, 0, 1, 1, 1, 256><<<cus, 256>>>((const D2*)((char*)v2 + shift), (D2*)d2, n2);
+      }, reps);
+      printf("sweep 2^%d vals shifted +%lld B: %7.3f ms %6.0f GB/s\n", lg, (long long)shift, ms, 24.0 * n / ms / 1e6);
+    }
+    for (int g : {cus / 2, cus, cus * 2}) {
+      const float ms = timeit([&] { k_apply<4, 0, 1, 1, 1, 256><<<g, 256>>>((const D2*)v2, (D2*)d2, n2); }, reps);
+      printf("sweep 2^%d U4 grid %d: %7.3f ms %6.0f GB/s\n", lg, g, ms, 24.0 * n / ms / 1e6);
+    }
+    printf("done\n");
+    return 0;
+  }
   if (mode == 1) {
     APPLY2(2, 0, 256) APPLY2(4, 0, 256) APPLY2(8, 0, 256) APPLY2(16, 0, 256)
     APPLY2(4, 1, 256) APPLY2(8, 1, 256) APPLY2(16, 1, 256)
