@@ -165,6 +165,19 @@ def zipf_rows(rng, n: int, count: int):
     return np.minimum(np.floor(np.power(float(n), rng.random(count))).astype(np.int64) - 1, n - 1)
 
 
+def segment_sums(v, counts, chunk: int = 1 << 22):
+    """torch.segment_reduce(v, "sum", lengths=counts), in pieces of at most 2^22 segments: on this
+    ROCm build one call over ~59 M segments (cfg4b) returned zeros past the first ~9 M."""
+    import torch
+    out, o = [], 0
+    for i in range(0, counts.numel(), chunk):
+        c = counts[i:i + chunk]
+        m = int(c.sum())
+        out.append(torch.segment_reduce(v[o:o + m], "sum", lengths=c))
+        o += m
+    return torch.cat(out) if out else v[:0]
+
+
 def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: int, check: bool) -> dict:
     """Builds the workload of one bench line, times `steps` pushes (or pulls) after `warmup`, checks
     the shard afterwards and returns the line's fields (without the CPU baseline)."""
@@ -382,10 +395,18 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             # segment sums over the sorted addresses (an atomic index_add_ serialises on Zipf's hot key)
             a, order = torch.sort(addr)
             uq, counts = torch.unique_consecutive(a, return_counts=True)
-            sums = torch.segment_reduce(v_all[order], "sum", lengths=counts) * reps
-            ok = bool(torch.allclose(got[uq], sums, rtol=1e-6, atol=1e-9 * reps))
+            sums = segment_sums(v_all[order], counts) * reps
+            close = torch.isclose(got[uq], sums, rtol=1e-6, atol=1e-9 * reps)
+            ok = bool(close.all())
+            if not ok:
+                bad = (~close).nonzero().reshape(-1)[:5]
+                print(f"check: {int((~close).sum())} of {uq.numel()} elements differ, e.g. addr "
+                      f"{uq[bad].tolist()} got {got[uq[bad]].tolist()} want {sums[bad].tolist()}", file=sys.stderr)
             got[uq] = 0
-            ok = ok and not bool(got.any())  # nothing outside the pushed addresses
+            if bool(got.any()):  # nothing outside the pushed addresses
+                ok = False
+                print(f"check: {int((got != 0).sum())} elements outside the pushed addresses are nonzero",
+                      file=sys.stderr)
             if exch:
                 uniq, u_note = int(uq.numel()), ""
                 bytes_per_step = 16.0 * recv + 16.0 * uniq

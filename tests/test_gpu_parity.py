@@ -534,6 +534,7 @@ def test_adaptive_switch_decides_at_sync_points(gpu, monkeypatch):
     of the shard's last sync point, never from a word the device may or may not have written yet:
     unsynchronised pushes keep the path they started with, and the same sequence of pushes and
     syncs takes the same paths on every run."""
+    import ctypes as C
     import torch
     lib = N.load()
     d = torch.device("cuda", gpu)

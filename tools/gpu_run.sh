@@ -45,7 +45,7 @@ pmc() {  # pmc <name> <bench args...>: FETCH_SIZE and WRITE_SIZE in two separate
 for s in ${STAGES:-tests bench}; do
   case $s in
     tests)
-      step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+      step pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
       ;;
     bench)
