@@ -589,7 +589,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
-  if (binned && unordered) return push_binned<V, MAT>(s, a, false, st);
+  if (binned && unordered) return push_binned_tail<V, MAT>(s, a, false, st);
   // Small pushes (an Akka message is ~1000 records, GranularBigVectorSpec.scala:21) are one launch:
   // the scatter handles every record, instead of check + apply + scatter. Launch latency is the
   // whole cost at this size, so two fewer launches is the win; results are those of the scatter
@@ -618,7 +618,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     HIPCHK(launch_k(s, GLINT_K_PUSH_APPLY, push_apply_kernel<V, MAT>, ga, kTPB, st, a, (const i64*)desc));
   }
   if (det) return push_det_tail<V, MAT>(s, a, true, st);
-  if (binned) return push_binned<V, MAT>(s, a, true, st);
+  if (binned) return push_binned_tail<V, MAT>(s, a, true, st);
   const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
   HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 0));
   return GLINT_OK;

@@ -6,6 +6,8 @@
 #   bench     the driver's default line (cfg2 with the CPU baseline) and the other bench lines
 #   prof2p30  rocprofv3 kernel stats of the dense push at 2^28 and at 2^30 (north-star size)
 #   binned    rocprofv3 kernel stats of the binned patterns (zipf, matrix, exchange)
+#   bintests  the GPU tests of the binned path, the full-size cases, cfg4 and the exchange
+#   ab        bench zipf / matrix / exchange with the previous binned pipeline and the current one
 #   micro     tools/microbench_stream mode 6: the dense sweep at 2^26..2^30, chunked and shifted
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (separate runs) of the dense, zipf and matrix lines
 set -o pipefail
@@ -65,6 +67,16 @@ for s in ${STAGES:-tests bench}; do
       pmc dense_2p28
       pmc zipf_2p28 --pattern zipf
       pmc matrix_2p17x512 --pattern matrix
+      ;;
+    bintests)
+      step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
+        -k "binned or fullsize or adaptive or cfg4 or exchange"
+      ;;
+    ab)  # the binned patterns, previous pipeline (GLINT_BIN_IMPL=v1) and current, back to back
+      for pat in zipf matrix exchange; do
+        step ab_v1_$pat 300 env GLINT_BIN_IMPL=v1 python3 bench.py --no-cpu-baseline --pattern $pat
+        step ab_new_$pat 300 python3 bench.py --no-cpu-baseline --pattern $pat
+      done
       ;;
     micro)
       step micro_stream_2p30 300 tools/microbench_stream 30 9 6
