@@ -711,3 +711,27 @@ def test_loopback_concurrent_clients_gpu_backend(gpu, args):
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
     assert d["check"] is True and d["resends"] == 0
+
+
+def test_loopback_client_bucketing_offloaded(gpu):
+    """the clients' mapPartitions step (AsyncBigVector.scala:96-98) once per batch,
+    either as the reference's groupBy restated on the host or offloaded to the GPU (glint_route_dev,
+    one stable route of the whole batch). Both send the same messages; with Long values the shards end
+    bit-identical (each run's pulled values equal the exact sums), and each run reports its bucketing
+    time per client."""
+    import json
+    import subprocess
+    from glint_amd.build import LIB, LOOPBACK_BIN
+    out = {}
+    for mode in ("groupby", "device"):
+        r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--device", str(gpu),
+                            "--clients", "64", "--servers", "8", "--keys", str(1 << 22), "--pattern", "uniform",
+                            "--records", "32768", "--dtype", "long", "--bucket", mode],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        d = json.loads(r.stdout)
+        assert d["check"] is True and d["resends"] == 0 and d["bucket"] == mode
+        assert all(x > 0 for x in d["bucket_s_per_client"])
+        out[mode] = d
+    assert out["groupby"]["push_messages"] == out["device"]["push_messages"]
+    assert out["groupby"]["pull_messages"] == out["device"]["pull_messages"]

@@ -38,6 +38,14 @@
  * clients' records (Long: bit-exact; Double: within 1e-9 of the sum of magnitudes, since concurrent
  * clients' messages reach a server in no fixed order, as with Akka).
  *
+ * Client bucketing (--bucket), the mapPartitions step (AsyncBigVector.scala:96-98) in front of the
+ * links, done once per client batch for the push and again for the pull, and timed on its own:
+ *   groupby  the reference's algorithm restated: per GranularBigVector slice, one pass over its
+ *            records appending each index to its partition's list (keys.indices.groupBy(partition));
+ *   device   offloaded: the client's whole batch routed on the GPU by glint_route_dev (a stable
+ *            counting sort by partition, one launch), then each partition's ordered index list is cut
+ *            at the slice boundaries. Both give the same messages, record for record.
+ *
  * Output: one JSON line.
  */
 #define _GNU_SOURCE
@@ -461,6 +469,12 @@ static int32_t owner_of(int64_t k) {
 }
 
 typedef struct {
+  int32_t id;
+  int32_t n;
+  int64_t* idx; /* record positions of the message */
+} fsm;
+
+typedef struct {
   int c;               /* client index */
   int part;            /* server / partition */
   int fd;
@@ -470,42 +484,124 @@ typedef struct {
   void* pulled;        /* values pulled back, at the records' positions */
   int mode;            /* 0 push, 1 pull */
   int64_t messages, resends;
+  fsm* msgs;           /* this link's messages, in slice order (set by the client's bucketing) */
+  int64_t nmsg;
 } link_arg;
 
-/* one message of this link: the records of slice i (GranularBigVector) owned by `part` */
-static int32_t gather(const link_arg* l, int64_t i0, int64_t* idx) {
-  const int64_t i1 = i0 + M < l->n ? i0 + M : l->n;
-  int32_t m = 0;
-  for (int64_t j = i0; j < i1; ++j)
-    if (owner_of(l->keys[j]) == l->part) idx[m++] = j;
-  return m;
+/* ---- client bucketing (mapPartitions, AsyncBigVector.scala:96-98) ------------------------------------ */
+static int bucket_device;  /* --bucket device */
+static void* hip_dl;
+static int (*hip_malloc)(void**, size_t);
+static int (*hip_free)(void*);
+static int (*hip_memcpy)(void*, const void*, size_t, int);
+static int (*route_dev)(const int64_t*, int64_t, int, int32_t, int64_t, int64_t*, int64_t*, int64_t*, void*);
+
+/* per partition: its record indices in record order (idx[p][0..cnt[p])) -> the link's messages, cut at
+ * the GranularBigVector slice boundaries (every M records) */
+static void cut_messages(link_arg* l, int64_t* idx, int64_t cnt) {
+  const int64_t nslices = (l->n + M - 1) / M;
+  l->msgs = (fsm*)calloc((size_t)(nslices > 0 ? nslices : 1), sizeof(fsm));
+  l->nmsg = 0;
+  int64_t a = 0;
+  while (a < cnt) {
+    const int64_t slice = idx[a] / M;
+    int64_t b = a;
+    while (b < cnt && idx[b] / M == slice) ++b;
+    l->msgs[l->nmsg].n = (int32_t)(b - a);
+    l->msgs[l->nmsg].idx = idx + a;
+    ++l->nmsg;
+    a = b;
+  }
+}
+
+/* Buckets client c's batch for its S links; returns the seconds it took. `store` receives the S
+ * index arrays (freed by the caller). */
+static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int64_t** store) {
+  const double t0 = now_s();
+  int64_t* cnt = (int64_t*)calloc((size_t)S, 8);
+  if (bucket_device && n > 0) {
+    /* offloaded: one stable route of the whole batch on the GPU (glint_route_dev) */
+    void *dk = NULL, *dc = NULL, *dord = NULL;
+    if (hip_malloc(&dk, (size_t)n * 8) || hip_malloc(&dc, (size_t)S * 8) || hip_malloc(&dord, (size_t)n * 8))
+      die("hipMalloc");
+    if (hip_memcpy(dk, keys, (size_t)n * 8, 1 /* hipMemcpyHostToDevice */)) die("hipMemcpy");
+    int64_t bad = -1;
+    if (route_dev((const int64_t*)dk, n, 0 /* GLINT_ROUTE_RANGE */, S, N, (int64_t*)dc, (int64_t*)dord, &bad, NULL))
+      die("glint_route_dev");
+    int64_t* order = (int64_t*)malloc((size_t)n * 8);
+    if (hip_memcpy(order, dord, (size_t)n * 8, 2 /* DeviceToHost */) || hip_memcpy(cnt, dc, (size_t)S * 8, 2))
+      die("hipMemcpy");
+    hip_free(dk);
+    hip_free(dc);
+    hip_free(dord);
+    int64_t o = 0;
+    for (int p = 0; p < S; ++p) {
+      store[p] = (int64_t*)malloc((size_t)(cnt[p] > 0 ? cnt[p] : 1) * 8);
+      memcpy(store[p], order + o, (size_t)cnt[p] * 8);
+      o += cnt[p];
+    }
+    free(order);
+  } else {
+    /* the reference's groupBy, slice by slice: one pass per slice, each index appended to its
+     * partition's list (lists grow as the groupBy's buffers do) */
+    int64_t* capv = (int64_t*)calloc((size_t)S, 8);
+    for (int p = 0; p < S; ++p) {
+      capv[p] = 1024;
+      store[p] = (int64_t*)malloc((size_t)capv[p] * 8);
+    }
+    for (int64_t s0 = 0; s0 < n; s0 += M) {
+      const int64_t s1 = s0 + M < n ? s0 + M : n;
+      for (int64_t j = s0; j < s1; ++j) {
+        const int32_t p = owner_of(keys[j]);
+        if (cnt[p] == capv[p]) {
+          capv[p] *= 2;
+          store[p] = (int64_t*)realloc(store[p], (size_t)capv[p] * 8);
+          if (!store[p]) die("realloc");
+        }
+        store[p][cnt[p]++] = j;
+      }
+    }
+    free(capv);
+  }
+  for (int p = 0; p < S; ++p) cut_messages(&links[p], store[p], cnt[p]);
+  free(cnt);
+  return now_s() - t0;
 }
 
 typedef struct {
-  int32_t id;
-  int32_t n;
-  int64_t* idx; /* record positions of the message */
-} fsm;
+  link_arg* links; /* this client's S links */
+  double bucket_s;
+} client_arg;
+
+static void* link_main(void* p);
+
+/* one client: bucket its batch (timed), then run its S links (one connection per server) */
+static void* client_main(void* p) {
+  client_arg* ca = (client_arg*)p;
+  link_arg* l = ca->links;
+  int64_t** store = (int64_t**)calloc((size_t)S, sizeof(int64_t*));
+  ca->bucket_s = bucket_client(l, l[0].keys, l[0].n, store);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)S);
+  for (int i = 0; i < S; ++i) pthread_create(&th[i], NULL, link_main, &l[i]);
+  for (int i = 0; i < S; ++i) pthread_join(th[i], NULL);
+  for (int i = 0; i < S; ++i) {
+    free(l[i].msgs);
+    l[i].msgs = NULL;
+    free(store[i]);
+  }
+  free(store);
+  free(th);
+  return NULL;
+}
 
 static void* link_main(void* p) {
   link_arg* l = (link_arg*)p;
   uint8_t* buf = NULL;
   size_t cap = 0;
   obuf out = {0};
-  const int64_t nslices = (l->n + M - 1) / M;
-  /* the messages of this link, in slice order (empty slices send nothing) */
-  fsm* msgs = (fsm*)calloc((size_t)(nslices > 0 ? nslices : 1), sizeof(fsm));
-  int64_t nmsg = 0;
-  int64_t* scratch = (int64_t*)malloc((size_t)M * 8);
-  for (int64_t s = 0; s < nslices; ++s) {
-    const int32_t m = gather(l, s * M, scratch);
-    if (!m) continue;
-    msgs[nmsg].n = m;
-    msgs[nmsg].idx = (int64_t*)malloc((size_t)m * 8);
-    memcpy(msgs[nmsg].idx, scratch, (size_t)m * 8);
-    ++nmsg;
-  }
-  free(scratch);
+  /* the messages of this link, in slice order (empty slices send nothing), from the client's bucketing */
+  fsm* msgs = l->msgs;
+  const int64_t nmsg = l->nmsg;
   uint8_t* m = (uint8_t*)malloc(9 + (size_t)M * 16);
   /* replies come back in request order on a connection: a FIFO of (kind, message) */
   int64_t* fifo_msg = (int64_t*)malloc(sizeof(int64_t) * (size_t)(4 * W + 8));
@@ -578,8 +674,6 @@ static void* link_main(void* p) {
     FPUSH(L_ACK, mi);
   }
   ob_flush(&out, l->fd);
-  for (int64_t i = 0; i < nmsg; ++i) free(msgs[i].idx);
-  free(msgs);
   free(m);
   free(fifo_msg);
   free(fifo_kind);
@@ -610,10 +704,11 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--pattern") && i + 1 < argc) pattern = argv[++i];
     else if (!strcmp(argv[i], "--dtype") && i + 1 < argc) dtype_long = !strcmp(argv[++i], "long");
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) gpu_device = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--bucket") && i + 1 < argc) bucket_device = !strcmp(argv[++i], "device");
     else {
       fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--clients C] [--keys N] "
                       "[--pattern dense|uniform] [--records R] [--msg M] [--window W] [--dtype double|long] "
-                      "[--device D]\n", argv[0]);
+                      "[--device D] [--bucket groupby|device]\n", argv[0]);
       return 2;
     }
   }
@@ -621,6 +716,17 @@ int main(int argc, char** argv) {
   if (!lib || S <= 0 || C <= 0 || N <= 0 || M <= 0 || W <= 0) { fprintf(stderr, "glint_loopback: bad arguments\n"); return 2; }
   if (uniform && R <= 0) R = N / C;
   backend_open(kind, lib);
+  if (bucket_device) { /* the device route of libglint_gpu.so and the HIP runtime it runs on */
+    if (!use_gpu) { fprintf(stderr, "glint_loopback: --bucket device needs --backend gpu\n"); return 2; }
+    hip_dl = dlopen("libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
+    if (!hip_dl) hip_dl = dlopen("/opt/rocm/lib/libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
+    if (!hip_dl) { fprintf(stderr, "glint_loopback: dlopen libamdhip64.so: %s\n", dlerror()); return 2; }
+    *(void**)&hip_malloc = dlsym(hip_dl, "hipMalloc");
+    *(void**)&hip_free = dlsym(hip_dl, "hipFree");
+    *(void**)&hip_memcpy = dlsym(hip_dl, "hipMemcpy");
+    *(void**)&route_dev = dlsym(dl, "glint_route_dev");
+    if (!hip_malloc || !hip_free || !hip_memcpy || !route_dev) die("dlsym hip*/glint_route_dev");
+  }
 
   /* RangePartitioner.apply(S, N) (RangePartitioner.scala:62-84) and partition() (:27-43) */
   const int32_t n_large = (int32_t)(N % S);
@@ -702,18 +808,26 @@ int main(int argc, char** argv) {
       l->n = cn[c];
       l->pulled = cp[c];
     }
-  pthread_t* lt = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)L);
-  double t[3];
+  pthread_t* ct = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)C);
+  client_arg* cargs = (client_arg*)calloc((size_t)C, sizeof(client_arg));
+  double t[3], bucket_s[2] = {0, 0}, bucket_max[2] = {0, 0};
   int64_t msgs[2] = {0, 0}, resends = 0;
   for (int mode = 0; mode < 2; ++mode) {
     t[mode] = now_s();
-    for (int x = 0; x < L; ++x) {
-      la[x].mode = mode;
-      la[x].messages = 0;
-      pthread_create(&lt[x], NULL, link_main, &la[x]);
+    for (int c = 0; c < C; ++c) {
+      for (int i = 0; i < S; ++i) {
+        la[c * S + i].mode = mode;
+        la[c * S + i].messages = 0;
+      }
+      cargs[c].links = &la[c * S];
+      pthread_create(&ct[c], NULL, client_main, &cargs[c]);
+    }
+    for (int c = 0; c < C; ++c) {
+      pthread_join(ct[c], NULL);
+      bucket_s[mode] += cargs[c].bucket_s / C;
+      if (cargs[c].bucket_s > bucket_max[mode]) bucket_max[mode] = cargs[c].bucket_s;
     }
     for (int x = 0; x < L; ++x) {
-      pthread_join(lt[x], NULL);
       msgs[mode] += la[x].messages;
       resends += la[x].resends;
     }
@@ -761,10 +875,12 @@ int main(int argc, char** argv) {
          "\"keys\": %lld, \"records\": %lld, \"max_records_per_message\": %d, \"window\": %d, "
          "\"push_messages\": %lld, \"pull_messages\": %lld, \"resends\": %lld, \"push_s\": %.6f, \"pull_s\": %.6f, "
          "\"push_records_per_s\": %.1f, \"pull_records_per_s\": %.1f, \"push_payload_MBps\": %.2f, "
-         "\"pull_payload_MBps\": %.2f, \"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
+         "\"pull_payload_MBps\": %.2f, \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
+         "\"bucket_s_max\": [%.6f, %.6f], \"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
          kind, pattern, dtype_long ? "long" : "double", S, C, (long long)N, (long long)total, M, W,
          (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl, (double)total / tp, (double)total / tl,
          16.0 * (double)total / tp / 1e6, 16.0 * (double)total / tl / 1e6,
+         bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
          dtype_long ? 0.0 : ((double*)cv[0])[0], (!dtype_long && cn[0] > 1) ? ((double*)cv[0])[1] : 0.0,
          (!dtype_long && cn[0] > 2) ? ((double*)cv[0])[2] : 0.0, ok ? "true" : "false");
   return ok ? 0 : 1;
