@@ -347,9 +347,11 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         dt = float(t.item())
 
     def kernel_avg(kid):
+        """Device time of one kernel kind per step (a large push runs its check and apply as one
+        launch per window of records: the launches of a step are summed) and its launch count."""
         ms, cnt = C.c_double(), C.c_int64()
         lib.glint_prof_read(h, kid, C.byref(ms), C.byref(cnt))
-        return (ms.value / cnt.value if cnt.value else 0.0), cnt.value
+        return ms.value / steps, cnt.value
 
     # post-run check. Dense push: the shard holds (W+K) additions of each record, bit-exact (each
     # key once per push, the ordered path). Zipf / matrix / exchange: repeated keys sum in an
@@ -428,9 +430,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         apply_ms, apply_n = kernel_avg(N.GLINT_K_PUSH_APPLY)
         check_ms, _ = kernel_avg(N.GLINT_K_PUSH_CHECK)
         scat_ms, _ = kernel_avg(N.GLINT_K_PUSH_SCATTER)
-        bin_ms, bin_n = kernel_avg(N.GLINT_K_PUSH_BINNED)
-        if apply_n:
-            bin_ms = bin_ms * bin_n / apply_n  # per push (the binned pipeline may skip pushes)
+        bin_ms, _ = kernel_avg(N.GLINT_K_PUSH_BINNED)
         kern = "push_check+push_apply+push_scatter+push_binned"
         kern_ms = check_ms + apply_ms + scat_ms + bin_ms
         launches = apply_n

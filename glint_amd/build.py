@@ -23,7 +23,7 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "build" / "libglint_oracle.so"
 
 CSRC = PKG / "csrc"
-HIP_SOURCES = [CSRC / "glint_gpu.hip", CSRC / "glint_sort.hip", CSRC / "glint_route.hip", CSRC / "glint_ordered.hip", CSRC / "glint_bin.hip", CSRC / "glint_page.hip"]
+HIP_SOURCES = [CSRC / "glint_gpu.hip", CSRC / "glint_sort.hip", CSRC / "glint_route.hip", CSRC / "glint_ordered.hip", CSRC / "glint_bin.hip"]
 HIP_HEADERS = [CSRC / "glint_kernels.h", CSRC / "glint_device.h", CSRC / "glint_host.h", ROOT / "include" / "glint_gpu.h"]
 HIP_DEPS = HIP_SOURCES + HIP_HEADERS
 OBJ_DIR = ROOT / "build" / "obj"

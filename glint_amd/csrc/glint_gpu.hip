@@ -112,19 +112,22 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   return true;
 }
 
+// One launch covers the wave tiles [t_begin, t_end) (a push is checked in windows of tiles, see
+// sweep_window_tiles); the first window's launch also zeroes the next push's control words.
 template <bool MAT, int KIND>
 __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict__ keys,
                                                           const int32_t* __restrict__ cols, i64 n,
                                                           PartDesc part, LaunchCtl* ctl, LaunchCtl* next,
-                                                          i64* __restrict__ desc, u32 ntiles) {
+                                                          i64* __restrict__ desc, u32 ntiles, u32 t_begin,
+                                                          u32 t_end) {
   const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next push's control words (no kernel of this push reads them)
+  if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // the next push's control words (no kernel of this push reads them)
     next->brk_enc = 0u;
     next->nonaffine = 0u;
   }
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const u32 nw = gridDim.x * (kTPB / 64);
-  for (u32 t = w0; t < ntiles; t += nw) {
+  for (u32 t = t_begin + w0; t < t_end; t += nw) {
     const bool full = 2 * ((i64)t * (kTile / 2)) + kTile <= n;
     const bool go = full ? check_tile<MAT, true, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane)
                          : check_tile<MAT, false, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane);
@@ -236,13 +239,13 @@ __device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, i
 // 6.2 TB/s, against 5.7 TB/s at twice the waves with cached shard accesses).
 constexpr int kSweepU = 2;  // record pairs per lane per iteration
 template <typename V, bool EVEN>
-__device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta) {
+__device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta, i64 p_begin, i64 p_end) {
   typedef typename Vec2<V>::T V2;
   if (blockIdx.x >= a.sweep_blocks) return;
-  const i64 npairs = a.n >> 1;
+  const i64 npairs = p_end;
   const i64 stride = (i64)a.sweep_blocks * kTPB;
   const V2* vp = reinterpret_cast<const V2*>(a.vals);
-  i64 p = (i64)blockIdx.x * kTPB + threadIdx.x;
+  i64 p = p_begin + (i64)blockIdx.x * kTPB + threadIdx.x;
   if (EVEN) {
     V2* dp = reinterpret_cast<V2*>(a.data + delta);  // pair p -> element pair delta + 2p
     for (; p + (kSweepU - 1) * stride < npairs; p += kSweepU * stride) {
@@ -270,30 +273,33 @@ __device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta) {
       a.data[e + 1] = vadd(d1, (V)v.y);
     }
   }
-  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+  if ((a.n & 1) && p_end == (a.n >> 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // the last window: odd record
     const i64 e = a.n - 1 + delta;
     a.data[e] = vadd(a.data[e], a.vals[a.n - 1]);
   }
 }
 
+// One launch covers the wave tiles [t_begin, t_end) of the push (a window, see sweep_window_tiles).
 template <typename V, bool MAT>
-__global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i64* __restrict__ desc) {
+__global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i64* __restrict__ desc, u32 t_begin,
+                                                          u32 t_end) {
   const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
-  if (blockIdx.x == 0 && threadIdx.x == 0 && a.hint)  // for the host's next push: how unordered was this one?
+  if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0 && a.hint)  // for the host's next push: how unordered was this one?
     __hip_atomic_store(a.hint, brk == 0u ? 0ull : (u64)(a.n - (i64)(a.ntiles - brk) * kTile), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (brk == 0u && a.ctl->nonaffine == 0u) {
     const i64 delta = desc[0];  // tile 0 starts the run at record 0
-    if ((delta & 1) == 0) apply_sweep<V, true>(a, delta);
-    else apply_sweep<V, false>(a, delta);
+    const i64 p0 = (i64)t_begin * (kTile / 2), p1 = min((i64)t_end * (kTile / 2), a.n >> 1);
+    if ((delta & 1) == 0) apply_sweep<V, true>(a, delta, p0, p1);
+    else apply_sweep<V, false>(a, delta, p0, p1);
     return;
   }
-  const u32 tiles = brk == 0u ? a.ntiles : a.ntiles - brk;
+  const u32 tiles = min(t_end, brk == 0u ? a.ntiles : a.ntiles - brk);
   const int lane = threadIdx.x & 63;
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const u32 nw = gridDim.x * (kTPB / 64);
   i64 dbatch = kNotAffine;  // descriptors of this wave's next 64 tiles, one per lane
-  for (u32 t = w0, it = 0; t < tiles; t += nw, ++it) {
+  for (u32 t = t_begin + w0, it = 0; t < tiles; t += nw, ++it) {
     if ((it & 63) == 0) {  // one load per 64 tiles instead of a dependent load per tile
       const i64 tt = (i64)t + (i64)lane * nw;
       dbatch = tt < (i64)tiles ? desc[tt] : kNotAffine;
@@ -521,6 +527,21 @@ int sweep_blocks_per_cu() {
   return v;
 }
 
+// The apply of a large push runs as one launch per window of 2^26 records (GLINT_SWEEP_WINDOW =
+// log2 records overrides; 0 = one launch). A grid-stride sweep over a whole 2^30-record push lets its
+// blocks drift apart across gigabytes, and the 2-read + 1-write stream then runs 6-11 % slower than
+// the same bytes swept window by window (tools/microbench_stream.hip mode 6: 2^30 records whole
+// 5.90 TB/s, in 2^26-record launches 6.56 TB/s; 2^28 whole 6.21 TB/s; profiles/r03/micro_stream_2p30.txt).
+u32 sweep_window_tiles() {
+  static const u32 v = [] {
+    const char* e = getenv("GLINT_SWEEP_WINDOW");
+    const int lg = e ? atoi(e) : 26;
+    if (lg <= 10 || lg >= 42) return 0xFFFFFFFFu;
+    return (u32)(((i64)1 << lg) / kTile);
+  }();
+  return v;
+}
+
 // GLINT_BINNED: 0 = never bin, 1 = bin every large push, unset = bin when the previous push on the
 // shard left a large unordered tail (read from the host-mapped word push_apply writes)
 int binned_mode() {
@@ -589,7 +610,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
-  if (binned && unordered) return push_binned_tail<V, MAT>(s, a, false, st);
+  if (binned && unordered) return push_binned<V, MAT>(s, a, false, st);
   // Small pushes (an Akka message is ~1000 records, GranularBigVectorSpec.scala:21) are one launch:
   // the scatter handles every record, instead of check + apply + scatter. Launch latency is the
   // whole cost at this size, so two fewer launches is the win; results are those of the scatter
@@ -601,24 +622,29 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 1));
     return GLINT_OK;
   }
+  const u64 win = std::min<u64>(sweep_window_tiles(), a.ntiles);
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
+    // one launch: the key stream alone lost 3-6 % when windowed (each short launch ramps up and drains)
     const unsigned gc =
-        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT, 0>, 2, "GLINT_CHECK_BPC"));
+        grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT, 0>, 2, "GLINT_CHECK_BPC"));
     HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
-                                       a.part, a.ctl, next, desc, a.ntiles)
+                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles)
                             : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
-                                       a.part, a.ctl, next, desc, a.ntiles));
+                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles));
     s->ctl_par ^= 1;  // only once the check that zeroes the other slot is on the stream
   }
   {
-    const unsigned ga =
-        grid_for(ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_apply_kernel<V, MAT>, 2, "GLINT_APPLY_BPC"));
-    a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * sweep_blocks_per_cu()));
-    HIPCHK(launch_k(s, GLINT_K_PUSH_APPLY, push_apply_kernel<V, MAT>, ga, kTPB, st, a, (const i64*)desc));
+    const i64 bpc = blocks_per_cu(push_apply_kernel<V, MAT>, 2, "GLINT_APPLY_BPC");
+    for (u64 t0 = 0; t0 < a.ntiles; t0 += win) {
+      const u32 t1 = (u32)std::min<u64>(a.ntiles, t0 + win);
+      const unsigned ga = grid_for(t1 - t0, kTPB / 64, (i64)s->cus * bpc);
+      a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * sweep_blocks_per_cu()));
+      HIPCHK(launch_k(s, GLINT_K_PUSH_APPLY, push_apply_kernel<V, MAT>, ga, kTPB, st, a, (const i64*)desc, (u32)t0, t1));
+    }
   }
   if (det) return push_det_tail<V, MAT>(s, a, true, st);
-  if (binned) return push_binned_tail<V, MAT>(s, a, true, st);
+  if (binned) return push_binned<V, MAT>(s, a, true, st);
   const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
   HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 0));
   return GLINT_OK;

@@ -305,10 +305,6 @@ template <typename V, bool MAT>
 int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
 template <typename V, bool MAT>
 int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
-// the binned tail the push takes: paged (glint_page.hip) where the shard's geometry allows, else the
-// two-level partition of glint_bin.hip
-template <typename V, bool MAT>
-int push_binned_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
 // one-launch order-preserving push (glint_ordered.hip): n <= kOrderedMax, elems < 2^32
 template <typename V, bool MAT>
 int push_ordered(glint_shard* s, const PushArgs<V>& a, hipStream_t st);

@@ -20,6 +20,7 @@
 #include <stdint.h>
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <utility>
 #include "../../include/glint_gpu.h"
@@ -236,54 +237,68 @@ __global__ __launch_bounds__(kST) void route_row_scan(const u32* __restrict__ hi
 }
 
 // ---- route scratch: one per (device, stream) ------------------------------------------------------
-// Routes on one stream run in stream order, so they can share a buffer; routes on different streams
-// of one device may run at the same time and get their own. A buffer grows only after its stream has
-// drained (the kernels that used the old one are done). At most kMaxScratch streams per device keep
-// a buffer: the least recently used one is released (after a device sync) to make room.
+// Routes on one stream run in stream order, so they can share a buffer once their kernels are on the
+// stream; routes on different streams of one device may run at the same time and get their own. A
+// caller holds its buffer's lock from taking it until its kernels are enqueued (host threads sharing
+// a stream would otherwise interleave their launches on one buffer). A buffer grows only after its
+// stream has drained. At most kMaxScratch streams per device keep a buffer: the least recently used
+// idle one is released (after a device sync) to make room.
 constexpr int kMaxDevices = 64;
 constexpr size_t kMaxScratch = 64;
+constexpr size_t kBadWordOffset = 0;  // the synchronous route's status word: the buffer's first 256 B
 struct RouteScratch {
+  std::mutex use;  // held while a caller enqueues work on this buffer
   void* tmp = nullptr;
   size_t bytes = 0;
-  u64 used = 0;  // last use (LRU)
+  u64 used = 0;    // last use (LRU)
 };
 std::mutex g_scratch_mu;
-std::map<std::pair<int, hipStream_t>, RouteScratch> g_scratch;
+std::map<std::pair<int, hipStream_t>, std::unique_ptr<RouteScratch>> g_scratch;
 u64 g_scratch_clock = 0;
 
-// a scratch buffer of at least `need` bytes for routes on (dev, st); nullptr on failure
-void* route_scratch(int dev, hipStream_t st, size_t need) {
-  std::lock_guard<std::mutex> lk(g_scratch_mu);
-  RouteScratch& sc = g_scratch[{dev, st}];
-  sc.used = ++g_scratch_clock;
-  if (sc.bytes < need) {
-    if (sc.tmp) {  // earlier routes on this stream may still read the old buffer
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(sc.tmp);
+// The scratch of (dev, st), at least `need` bytes past its status word, LOCKED for the caller (who
+// unlocks it once its kernels are enqueued); nullptr on failure (unlocked).
+RouteScratch* route_scratch(int dev, hipStream_t st, size_t need) {
+  RouteScratch* sc;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto& slot = g_scratch[{dev, st}];
+    if (!slot) slot.reset(new RouteScratch());
+    sc = slot.get();
+    sc->used = ++g_scratch_clock;
+    size_t on_dev = 0;
+    for (auto& kv : g_scratch) on_dev += kv.first.first == dev;
+    if (on_dev > kMaxScratch) {  // release the least recently used idle buffer of this device
+      auto victim = g_scratch.end();
+      for (auto it = g_scratch.begin(); it != g_scratch.end(); ++it)
+        if (it->first.first == dev && it->second.get() != sc &&
+            (victim == g_scratch.end() || it->second->used < victim->second->used))
+          victim = it;
+      if (victim != g_scratch.end() && victim->second->use.try_lock()) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(victim->second->tmp);
+        victim->second->use.unlock();
+        g_scratch.erase(victim);
+      }
     }
-    sc.tmp = nullptr;
-    sc.bytes = 0;
-    if (hipMalloc(&sc.tmp, need) != hipSuccess) {
+  }
+  sc->use.lock();
+  need += 256;  // the status word
+  if (sc->bytes < need) {
+    if (sc->tmp) {  // earlier routes on this stream may still read the old buffer
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(sc->tmp);
+    }
+    sc->tmp = nullptr;
+    sc->bytes = 0;
+    if (hipMalloc(&sc->tmp, need) != hipSuccess) {
       (void)hipGetLastError();
+      sc->use.unlock();
       return nullptr;
     }
-    sc.bytes = need;
+    sc->bytes = need;
   }
-  void* p = sc.tmp;
-  size_t on_dev = 0;
-  for (auto& kv : g_scratch) on_dev += kv.first.first == dev;
-  if (on_dev > kMaxScratch) {  // release the least recently used buffer of this device (not this one)
-    auto victim = g_scratch.end();
-    for (auto it = g_scratch.begin(); it != g_scratch.end(); ++it)
-      if (it->first.first == dev && it->second.tmp != p && (victim == g_scratch.end() || it->second.used < victim->second.used))
-        victim = it;
-    if (victim != g_scratch.end()) {
-      (void)hipDeviceSynchronize();
-      (void)hipFree(victim->second.tmp);
-      g_scratch.erase(victim);
-    }
-  }
-  return p;
+  return sc;
 }
 
 struct DevGuard {
@@ -323,11 +338,14 @@ __global__ __launch_bounds__(256) void route_validate(const i64* __restrict__ ke
 }
 
 // Launches the route (histogram, scan, scatter, counts) on `st`; the first bad record (~index, 0 =
-// none) lands in the device word *bad_dev. No host synchronisation.
+// none) lands in the device word *bad_dev (nullptr: the scratch's own status word, and the scratch
+// stays locked for the caller, who reads the word after a sync and unlocks `*held`). No host
+// synchronisation.
 int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of,
-                 int64_t* counts, const RouteOut& out, uint64_t* bad_dev, hipStream_t st) {
+                 int64_t* counts, const RouteOut& out, uint64_t* bad_dev, hipStream_t st,
+                 RouteScratch** held = nullptr) {
   if (kind != GLINT_ROUTE_RANGE && kind != GLINT_ROUTE_CYCLIC) return GLINT_EINVAL;
-  if (nparts <= 0 || nparts > kMaxParts || n < 0 || nkeys < 0 || !counts || !bad_dev) return GLINT_EINVAL;
+  if (nparts <= 0 || nparts > kMaxParts || n < 0 || nkeys < 0 || !counts || (!bad_dev && !held)) return GLINT_EINVAL;
   if (n > 0 && !keys) return GLINT_EINVAL;
   if (n >= ((i64)1 << 32)) return GLINT_EINVAL;  // 32-bit offsets
   if (out.vals && out.vsize != 4 && out.vsize != 8) return GLINT_EINVAL;
@@ -357,8 +375,17 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   while ((1 << nbits) <= nparts) ++nbits;  // owners and the sentinel nparts fit in nbits
   const size_t hist_bytes = ((size_t)nparts * nblocks * 4 + 255) & ~(size_t)255;
   const size_t need = 2 * hist_bytes + (size_t)kMaxParts * 4;
-  char* b = (char*)route_scratch(dev, st, need);
-  if (!b) return GLINT_ENOMEM;
+  RouteScratch* sc = route_scratch(dev, st, need);
+  if (!sc) return GLINT_ENOMEM;
+  // the buffer stays locked until this call's kernels are on the stream (or, held, for the caller)
+  struct Unlock {
+    RouteScratch* sc;
+    bool keep;
+    ~Unlock() { if (!keep) sc->use.unlock(); }
+  } unlock{sc, held != nullptr};
+  if (held) *held = sc;
+  char* b = (char*)sc->tmp + 256;
+  if (!bad_dev) bad_dev = (uint64_t*)((char*)sc->tmp + kBadWordOffset);
   u32* hist = (u32*)b;
   u32* offs = (u32*)(b + hist_bytes);
   u32* tot = (u32*)(b + 2 * hist_bytes);
@@ -393,35 +420,18 @@ extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t
   hipStream_t st = (hipStream_t)stream;
   RouteOut out{};
   out.order = order;
-  // a per-device status word in device memory (read back with the call's synchronisation)
-  static std::mutex mu;
-  static uint64_t* bad_words[kMaxDevices] = {};
-  int dev = 0;
-  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return GLINT_EDEVICE;
-  }
-  if (dev < 0 || dev >= kMaxDevices) return GLINT_EDEVICE;
-  uint64_t* bad_dev = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (!bad_words[dev]) {
-      DevGuard guard(dev);
-      // one word per 256 B so concurrent callers on one device do not share it
-      if (!guard.ok || hipMalloc((void**)&bad_words[dev], 256 * 64) != hipSuccess) {
-        (void)hipGetLastError();
-        bad_words[dev] = nullptr;
-        return GLINT_ENOMEM;
-      }
-    }
-    static int next_slot = 0;
-    bad_dev = bad_words[dev] + 32 * (next_slot++ & 63);
-  }
-  int rc = route_launch(keys, n, kind, nparts, nkeys, nullptr, counts, out, bad_dev, st);
-  if (rc) return rc;
+  // the status word is the scratch's own; the scratch stays locked until the call has read it
+  RouteScratch* held = nullptr;
+  int rc = route_launch(keys, n, kind, nparts, nkeys, nullptr, counts, out, nullptr, st, &held);
+  if (!held) return rc;
   uint64_t enc = 0;
-  if (hipMemcpyAsync(&enc, bad_dev, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return GLINT_EDEVICE;
-  if (hipStreamSynchronize(st) != hipSuccess) return GLINT_EDEVICE;
+  if (rc == GLINT_OK && (hipMemcpyAsync(&enc, held->tmp, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                         hipStreamSynchronize(st) != hipSuccess)) {
+    (void)hipGetLastError();
+    rc = GLINT_EDEVICE;
+  }
+  held->use.unlock();
+  if (rc) return rc;
   *first_bad = enc ? (int64_t)~enc : -1;
   return enc ? GLINT_EOUTOFRANGE : GLINT_OK;
 }

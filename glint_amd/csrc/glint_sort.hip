@@ -1,13 +1,10 @@
 // glint_sort.hip -- the deterministic tail of a large push: a stable
-// rocPRIM radix sort by address, then an in-order fold per address starting from the shard's value --
-// PartialVector.update's sequential `+=` order (src/main/scala/glint/models/server/
-// PartialVector.scala:35-43), bit for bit. (Pushes of up to kOrderedMax records take the one-launch
-// fold of glint_ordered.hip instead; the binned unordered path is glint_bin.hip.)
-// Kept apart from glint_gpu.hip so that the rocPRIM instantiations compile once.
+// radix sort by address (hand-written, LSD, 8-bit digits), then an in-order fold per address starting
+// from the shard's value -- PartialVector.update's sequential `+=` order (src/main/scala/glint/models/
+// server/PartialVector.scala:35-43), bit for bit. (Pushes of up to kOrderedMax records take the
+// one-launch fold of glint_ordered.hip instead; the binned unordered path is glint_bin.hip.)
 #include "glint_device.h"
 #include "glint_host.h"
-
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <cstring>
 
@@ -19,10 +16,10 @@ namespace glint {
 // ------------------------------------------------------------------------------------------------
 // Records before the tail start (push_check's break, read here on the device: no host round trip)
 // and rejected records get the sentinel address, which sorts behind every element and is skipped.
-template <typename V, bool MAT>
+template <typename K, typename V, bool MAT>
 __global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, const int32_t* cols, const V* vals, i64 m,
                                                            const LaunchCtl* ctl, u32 ntiles, int from_break,
-                                                           PartDesc part, u64 sentinel, u64* addr, V* val,
+                                                           PartDesc part, K sentinel, K* addr, V* val,
                                                            ErrState* err) {
   i64 r0 = 0;
   if (from_break) {
@@ -30,10 +27,10 @@ __global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, cons
     r0 = brk == 0u ? m : (i64)(ntiles - brk) * kTile;
   }
   for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
-    u64 out = sentinel;
+    K out = sentinel;
     if (i >= r0) {
       i64 ad;
-      if (rec_addr<MAT>(part, keys[i], MAT ? cols[i] : 0, ad)) out = (u64)ad;
+      if (rec_addr<MAT>(part, keys[i], MAT ? cols[i] : 0, ad)) out = (K)ad;
       else record_error(err, i);
     }
     addr[i] = out;
@@ -46,11 +43,11 @@ __global__ __launch_bounds__(kTPB) void det_prepare_kernel(const i64* keys, cons
 // current value -- the reference's `data(k) += v` sequence, rounding for rounding.
 constexpr int kDetShort = 64;  // runs up to this length: one thread; longer: one wave
 
-template <typename V>
-__global__ __launch_bounds__(kTPB) void det_fold_short_kernel(const u64* addr, const V* val, i64 m, u64 sentinel,
+template <typename K, typename V>
+__global__ __launch_bounds__(kTPB) void det_fold_short_kernel(const K* addr, const V* val, i64 m, K sentinel,
                                                               V* data, u32* long_count, u32* long_list) {
   for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < m; i += (i64)gridDim.x * kTPB) {
-    const u64 ad = addr[i];
+    const K ad = addr[i];
     if (ad == sentinel) continue;
     if (i > 0 && addr[i - 1] == ad) continue;  // not the head of its run
     i64 j = i;
@@ -82,7 +79,8 @@ __device__ __forceinline__ int lane_value(int x, int l) { return __builtin_amdgc
 
 // End (exclusive) of the run of `ad` that starts at i in the sorted addresses: a 64-way gallop,
 // then 64-way refinement -- O(log64 len) dependent probe rounds instead of a compare per element.
-__device__ __forceinline__ i64 run_end(const u64* addr, i64 m, i64 i, u64 ad, int lane) {
+template <typename K>
+__device__ __forceinline__ i64 run_end(const K* addr, i64 m, i64 i, K ad, int lane) {
   i64 lo = i, hi;  // addr[lo] == ad; the end lies in (lo, hi]
   for (i64 step = 1;; step *= 64) {
     const i64 p = lo + (i64)(lane + 1) * step;
@@ -138,8 +136,8 @@ __device__ __forceinline__ V det_fold(const V (&x)[kDetK], V acc, i64 start, i64
   return acc;
 }
 
-template <typename V>
-__global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, const V* val, i64 m,
+template <typename K, typename V>
+__global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const K* addr, const V* val, i64 m,
                                                              const u32* long_count, const u32* long_list, V* data) {
   const int lane = threadIdx.x & 63;
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
@@ -148,7 +146,7 @@ __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, co
   constexpr i64 kB = 64 * kDetK;
   for (u32 w = w0; w < cnt; w += nw) {
     const i64 i = long_list[w];
-    const u64 ad = addr[i];
+    const K ad = addr[i];
     const i64 e = run_end(addr, m, i, ad, lane);
     V acc = data[ad];
     V A[kDetK], B[kDetK];
@@ -163,44 +161,270 @@ __global__ __launch_bounds__(kTPB) void det_fold_long_kernel(const u64* addr, co
   }
 }
 
+// ---- stable LSD radix sort of (address, value) pairs --------------------------------------------
+// One pass per 8-bit digit, three launches each:
+//   rs_hist     per 2048-key tile, the digit counts -> hist[digit][tile];
+//   rs_sums / rs_scan  per digit its total, then offs[digit][tile] = keys of smaller digits + keys of
+//               this digit in earlier tiles (the route's offset kernels, one block per digit);
+//   rs_scatter  per tile, stable ranks (lanes and waves in key order: one ballot per digit bit, then
+//               per-(round, wave) counts), the tile staged in LDS grouped by digit, and written out
+//               in runs -- consecutive threads, consecutive slots.
+constexpr int kST = 256;               // threads of the sort kernels
+constexpr int kSPer = 8;               // keys per thread per tile
+constexpr int kSTile = kST * kSPer;    // 2048
+constexpr int kSSegs = kSPer * (kST / 64);  // (round, wave) segments of a tile: 32
+
+template <typename K>
+__global__ __launch_bounds__(kST) void rs_hist(const K* __restrict__ keys, i64 n, int shift, u32* __restrict__ hist,
+                                               u32 ntiles) {
+  __shared__ u32 h[kST / 64][256];
+  const int tid = threadIdx.x, wid = tid >> 6;
+  for (int d = tid; d < 4 * 256; d += kST) (&h[0][0])[d] = 0;
+  __syncthreads();
+  const i64 t0 = (i64)blockIdx.x * kSTile;
+  K k[kSPer];
+#pragma unroll
+  for (int j = 0; j < kSPer; ++j) {
+    const i64 i = t0 + j * kST + tid;
+    k[j] = keys[i < n ? i : n - 1];
+  }
+  const int lane = tid & 63;
+#pragma unroll
+  for (int j = 0; j < kSPer; ++j) {  // one LDS add per distinct digit of the wave (a hot key is one)
+    const u32 d = t0 + j * kST + tid < n ? ((u32)(k[j] >> shift) & 255u) : 256u;
+    u64 m = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const u64 bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    if (d < 256u && (m & ((1ull << lane) - 1ull)) == 0) h[wid][d] += (u32)__popcll(m);
+  }
+  __syncthreads();
+  hist[(i64)tid * ntiles + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+__device__ __forceinline__ u32 rs_block_sum(u32 x) {
+  __shared__ u32 ws[1024 / 64];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  u32 t = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += ws[w];
+  __syncthreads();
+  return t;
+}
+
+// tot[d] = keys with digit d (one block per digit)
+__global__ __launch_bounds__(1024) void rs_sums(const u32* __restrict__ hist, u32 ntiles, u32* __restrict__ tot) {
+  const u32* row = hist + (i64)blockIdx.x * ntiles;
+  u32 x = 0;
+  for (u32 b = threadIdx.x; b < ntiles; b += 1024) x += row[b];
+  x = rs_block_sum(x);
+  if (threadIdx.x == 0) tot[blockIdx.x] = x;
+}
+
+// offs[d][t] = sum(tot[0..d)) + sum(hist[d][0..t)) (one block per digit)
+__global__ __launch_bounds__(1024) void rs_scan(const u32* __restrict__ hist, u32 ntiles, const u32* __restrict__ tot,
+                                                u32* __restrict__ offs) {
+  __shared__ u32 wt[16];
+  const int d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  u32 base = tid < d ? tot[tid] : 0u;
+  base = rs_block_sum(base);
+  const u32* row = hist + (i64)d * ntiles;
+  u32* out = offs + (i64)d * ntiles;
+  u32 carry = base;
+  for (u32 t0 = 0; t0 < ntiles; t0 += 1024 * 4) {
+    const u32 b0 = t0 + (u32)tid * 4;
+    u32 v[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = b0 + j < ntiles ? row[b0 + j] : 0u;
+      sum += v[j];
+    }
+    u32 incl = sum;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const u32 y = __shfl_up(incl, s);
+      if (lane >= s) incl += y;
+    }
+    if (lane == 63) wt[wid] = incl;
+    __syncthreads();
+    u32 run = carry + incl - sum, all = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const u32 y = wt[w];
+      run += w < wid ? y : 0u;
+      all += y;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (b0 + j < ntiles) out[b0 + j] = run;
+      run += v[j];
+    }
+    carry += all;
+    __syncthreads();
+  }
+}
+
+template <typename K, typename V>
+__global__ __launch_bounds__(kST) void rs_scatter(const K* __restrict__ kin, const V* __restrict__ vin, i64 n, int shift,
+                                                  const u32* __restrict__ offs, u32 ntiles, K* __restrict__ kout,
+                                                  V* __restrict__ vout) {
+  __shared__ uint16_t seg[256][kSSegs];  // per digit: counts, then first staging slot, of each segment
+  __shared__ u32 dbase[256];             // per digit: first staging slot
+  __shared__ u32 wt[kST / 64];
+  __shared__ K sk[kSTile];
+  __shared__ V sv[kSTile];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u64 below = (1ull << lane) - 1ull;
+  const i64 t0 = (i64)blockIdx.x * kSTile;
+  K k[kSPer];
+  V v[kSPer];
+  u32 d[kSPer], wr[kSPer];
+#pragma unroll
+  for (int j = 0; j < kSPer; ++j) {  // clamped, branch-free loads; key order = (round j, thread)
+    const i64 i = t0 + j * kST + tid;
+    const i64 ii = i < n ? i : n - 1;
+    k[j] = kin[ii];
+    v[j] = vin[ii];
+    d[j] = i < n ? ((u32)(k[j] >> shift) & 255u) : 256u;  // 256: past the end
+  }
+  for (int x = tid; x < 256 * kSSegs / 2; x += kST) reinterpret_cast<u32*>(&seg[0][0])[x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSPer; ++j) {  // lanes with equal digits: one ballot per digit bit
+    u64 m = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const bool bit = (d[j] >> b) & 1u;
+      const u64 bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    wr[j] = (u32)__popcll(m & below);
+    if (d[j] < 256u && wr[j] == 0) seg[d[j]][j * (kST / 64) + wid] = (uint16_t)__popcll(m);
+  }
+  __syncthreads();
+  // per digit (one thread each): segment prefixes in key order, then the digits' bases
+  u32 tot = 0;
+  {
+    for (int q = 0; q < kSSegs; ++q) {
+      const u32 c = seg[tid][q];
+      seg[tid][q] = (uint16_t)tot;
+      tot += c;
+    }
+    u32 incl = tot;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const u32 y = __shfl_up(incl, s);
+      if (lane >= s) incl += y;
+    }
+    if (lane == 63) wt[wid] = incl;
+    __syncthreads();
+    u32 ex = incl - tot;
+#pragma unroll
+    for (int w = 0; w < kST / 64; ++w) ex += w < wid ? wt[w] : 0u;
+    dbase[tid] = ex;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSPer; ++j) {
+    if (d[j] < 256u) {
+      const u32 p = dbase[d[j]] + seg[d[j]][j * (kST / 64) + wid] + wr[j];
+      sk[p] = k[j];
+      sv[p] = v[j];
+    }
+  }
+  __syncthreads();
+  const i64 valid = n - t0 < kSTile ? n - t0 : kSTile;
+#pragma unroll
+  for (int j = 0; j < kSPer; ++j) {
+    const int p = tid + j * kST;
+    if (p < valid) {
+      const K kk = sk[p];
+      const u32 dd = (u32)(kk >> shift) & 255u;
+      const u32 dst = offs[(i64)dd * ntiles + blockIdx.x] + ((u32)p - dbase[dd]);
+      kout[dst] = kk;
+      vout[dst] = sv[p];
+    }
+  }
+}
+
+// Sorts m (key, value) pairs by the low end_bit bits of the key, stably; the result is in (k1, v1)
+// when the number of passes is odd, else back in (k0, v0). Returns the buffer index (0 or 1).
+template <typename K, typename V>
+int rs_sort(K* k0, V* v0, K* k1, V* v1, i64 m, int end_bit, u32* hist, u32* offs, u32* tot, hipStream_t st,
+            int* where) {
+  const u32 ntiles = (u32)((m + kSTile - 1) / kSTile);
+  int cur = 0;
+  for (int shift = 0; shift < end_bit; shift += 8) {
+    const K* ki = cur ? k1 : k0;
+    const V* vi = cur ? v1 : v0;
+    K* ko = cur ? k0 : k1;
+    V* vo = cur ? v0 : v1;
+    rs_hist<K><<<ntiles, kST, 0, st>>>(ki, m, shift, hist, ntiles);
+    rs_sums<<<256, 1024, 0, st>>>(hist, ntiles, tot);
+    rs_scan<<<256, 1024, 0, st>>>(hist, ntiles, tot, offs);
+    rs_scatter<K, V><<<ntiles, kST, 0, st>>>(ki, vi, m, shift, offs, ntiles, ko, vo);
+    HIPCHK(hipGetLastError());
+    cur ^= 1;
+  }
+  *where = cur;
+  return GLINT_OK;
+}
+
 // ---- host side ----------------------------------------------------------------------------------
-template <typename V, bool MAT>
-int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
+template <typename K, typename V, bool MAT>
+int det_tail_k(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
   // the whole push is sorted; records before push_check's break are masked on the device, so the
   // call stays stream-ordered with no host synchronisation
   const i64 m = a.n;
-  const u64 sentinel = (u64)s->elems;
+  const K sentinel = (K)s->elems;
   int end_bit = 1;
-  while (end_bit < 64 && ((u64)1 << end_bit) <= sentinel) ++end_bit;
-  size_t tmp_bytes = 0;
-  u64* nul64 = nullptr;
-  V* nulv = nullptr;
-  HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, nul64, nul64, nulv, nulv, (size_t)m, 0, end_bit, st));
-  const size_t b_addr = pad256((size_t)m * 8), b_val = pad256((size_t)m * sizeof(V));
+  while (end_bit < (int)(8 * sizeof(K)) && ((u64)1 << end_bit) <= (u64)sentinel) ++end_bit;
+  const u32 ntiles = (u32)((m + kSTile - 1) / kSTile);
+  const size_t b_addr = pad256((size_t)m * sizeof(K)), b_val = pad256((size_t)m * sizeof(V));
   const size_t b_list = pad256(((size_t)m / kDetShort + 2) * 4);
-  const size_t need = 2 * b_addr + 2 * b_val + b_list + pad256(tmp_bytes);
+  const size_t b_hist = pad256((size_t)ntiles * 256 * 4);
+  const size_t need = 2 * b_addr + 2 * b_val + b_list + 2 * b_hist + 1024;
   int rc = grow(&s->d_det, &s->det_bytes, need);
   if (rc) return rc;
   char* base = (char*)s->d_det;
-  u64* addr_in = (u64*)base;
-  u64* addr_out = (u64*)(base + b_addr);
-  V* val_in = (V*)(base + 2 * b_addr);
-  V* val_out = (V*)(base + 2 * b_addr + b_val);
+  K* addr0 = (K*)base;
+  K* addr1 = (K*)(base + b_addr);
+  V* val0 = (V*)(base + 2 * b_addr);
+  V* val1 = (V*)(base + 2 * b_addr + b_val);
   u32* long_count = (u32*)(base + 2 * b_addr + 2 * b_val);
   u32* long_list = long_count + 1;
-  void* tmp = base + 2 * b_addr + 2 * b_val + b_list;
+  u32* hist = (u32*)(base + 2 * b_addr + 2 * b_val + b_list);
+  u32* offs = (u32*)((char*)hist + b_hist);
+  u32* tot = (u32*)((char*)offs + b_hist);
   const unsigned g = grid_for(m, kTPB, (i64)s->cus * 8);
-  det_prepare_kernel<V, MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, a.vals, m, a.ctl, a.ntiles, from_break ? 1 : 0,
-                                                 a.part, sentinel, addr_in, val_in, a.err);
+  det_prepare_kernel<K, V, MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, a.vals, m, a.ctl, a.ntiles, from_break ? 1 : 0,
+                                                    a.part, sentinel, addr0, val0, a.err);
   HIPCHK(hipGetLastError());
   // stable LSD radix sort: equal addresses keep their push order
-  HIPCHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, addr_in, addr_out, val_in, val_out, (size_t)m, 0, end_bit, st));
+  int where = 0;
+  rc = rs_sort<K, V>(addr0, val0, addr1, val1, m, end_bit, hist, offs, tot, st, &where);
+  if (rc) return rc;
+  const K* addr = where ? addr1 : addr0;
+  const V* val = where ? val1 : val0;
   HIPCHK(hipMemsetAsync(long_count, 0, 4, st));
-  det_fold_short_kernel<V><<<g, kTPB, 0, st>>>(addr_out, val_out, m, sentinel, a.data, long_count, long_list);
+  det_fold_short_kernel<K, V><<<g, kTPB, 0, st>>>(addr, val, m, sentinel, a.data, long_count, long_list);
   HIPCHK(hipGetLastError());
-  det_fold_long_kernel<V><<<(unsigned)s->cus * 2, kTPB, 0, st>>>(addr_out, val_out, m, long_count, long_list, a.data);
+  det_fold_long_kernel<K, V><<<(unsigned)s->cus * 2, kTPB, 0, st>>>(addr, val, m, long_count, long_list, a.data);
   HIPCHK(hipGetLastError());
   return GLINT_OK;
+}
+
+template <typename V, bool MAT>
+int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
+  // 32-bit addresses (and 32-bit offsets) while the shard's element count and the push fit them
+  if (s->elems < ((i64)1 << 32) - 1 && a.n < ((i64)1 << 32) - kSTile) return det_tail_k<u32, V, MAT>(s, a, from_break, st);
+  if (a.n >= ((i64)1 << 32) - kSTile) return GLINT_EINVAL;
+  return det_tail_k<u64, V, MAT>(s, a, from_break, st);
 }
 
 #define GLINT_INST(V, MAT) template int push_det_tail<V, MAT>(glint_shard*, const PushArgs<V>&, bool, hipStream_t);

@@ -7,7 +7,9 @@
 #   prof2p30  rocprofv3 kernel stats of the dense push at 2^28 and at 2^30 (north-star size)
 #   binned    rocprofv3 kernel stats of the binned patterns (zipf, matrix, exchange)
 #   bintests  the GPU tests of the binned path, the full-size cases, cfg4 and the exchange
-#   ab        bench zipf / matrix / exchange with the previous binned pipeline and the current one
+#   ab        bench zipf / matrix / exchange with a previous library (AB_LIB) and the current one
+#   dettests  the deterministic / message-order / full-size GPU tests
+#   det       tools/det_probe.py (cfg3 deterministic push), timed and under rocprofv3 kernel stats
 #   micro     tools/microbench_stream mode 6: the dense sweep at 2^26..2^30, chunked and shifted
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (separate runs) of the dense, zipf and matrix lines
 set -o pipefail
@@ -61,7 +63,7 @@ for s in ${STAGES:-tests bench}; do
       kstats dense_2p30 400 --log2-keys 30 --steps 10
       ;;
     binned)
-      for pat in zipf matrix exchange; do kstats $pat 300 --pattern $pat; done
+      for pat in ${PATTERNS:-zipf matrix exchange}; do kstats $pat 300 --pattern $pat --steps 10 --warmup 2; done
       ;;
     pmc)
       pmc dense_2p28
@@ -72,10 +74,26 @@ for s in ${STAGES:-tests bench}; do
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
         -k "binned or fullsize or adaptive or cfg4 or exchange"
       ;;
-    ab)  # the binned patterns, previous pipeline (GLINT_BIN_IMPL=v1) and current, back to back
-      for pat in zipf matrix exchange; do
-        step ab_v1_$pat 300 env GLINT_BIN_IMPL=v1 python3 bench.py --no-cpu-baseline --pattern $pat
+    ab)  # the binned patterns: the previous build's library (GLINT_GPU_LIB=$AB_LIB) and this one, back to back
+      for pat in ${PATTERNS:-zipf matrix exchange}; do
+        step ab_old_$pat 300 env GLINT_GPU_LIB=$AB_LIB python3 bench.py --no-cpu-baseline --pattern $pat
         step ab_new_$pat 300 python3 bench.py --no-cpu-baseline --pattern $pat
+      done
+      ;;
+    dettests)
+      step pytest_det 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
+        -k "determin or order or fullsize or det"
+      ;;
+    det)  # the deterministic cfg3 push (sort + in-order fold), timed and with kernel stats
+      step det_probe 300 python3 tools/det_probe.py
+      echo "[$(date +%T)] kstats det" >&2
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_det -o run \
+         -- python3 $R/tools/det_probe.py > $OUT/prof_det.log 2>&1) || { tail -30 $OUT/prof_det.log >&2; exit 1; }
+      find /tmp/prof_det -name "*kernel_stats.csv" -exec cp {} $OUT/kstats_det.csv \;
+      ;;
+    win)  # the dense push by sweep window (GLINT_SWEEP_WINDOW = log2 records; 0 = one launch)
+      for w in ${WINDOWS:-0 24 25 26 27}; do
+        step win_$w 300 env GLINT_SWEEP_WINDOW=$w python3 bench.py --no-cpu-baseline
       done
       ;;
     micro)
