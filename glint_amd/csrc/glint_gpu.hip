@@ -386,14 +386,15 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
 // pulls
 // ------------------------------------------------------------------------------------------------
 // PartialVector.get (PartialVector.scala:51-60): out[i] = data(globalToLocal(keys(i)))
+// PAIRS: records [2 * p_begin, min(n, 2 * p_end)) (a large pull runs one launch per window)
 template <typename V, bool PAIRS>
 __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, const V* data, PartDesc part,
-                                                        V* out, ErrState* err, MsgSig sig) {
+                                                        V* out, ErrState* err, MsgSig sig, i64 p_begin, i64 p_end) {
   typedef typename Vec2<V>::T V2;
   const i64 stride = (i64)gridDim.x * kTPB;
   if (PAIRS) {
-    const i64 npairs = (n + 1) >> 1;
-    for (i64 p = (i64)blockIdx.x * kTPB + threadIdx.x; p < npairs; p += stride) {
+    const i64 npairs = p_end;
+    for (i64 p = p_begin + (i64)blockIdx.x * kTPB + threadIdx.x; p < npairs; p += stride) {
       const i64 r = 2 * p;
       if (r + 1 < n) {
         const K2 k = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p);
@@ -664,14 +665,20 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   }
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
   if (pairs) {
-    // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5)
-    const unsigned g = sig.done ? 1u : grid_for((n + 1) / 2, kTPB, (i64)s->cus * 4);
-    HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, true>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
-                    (V*)out, err_of(s), sig));
+    // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5); one launch per
+    // window of records, as the push's apply sweep (sweep_window_tiles)
+    const i64 npairs = (n + 1) / 2;
+    const i64 win = sig.done ? npairs : std::min<i64>(npairs, (i64)sweep_window_tiles() * (kTile / 2));
+    for (i64 p0 = 0; p0 < npairs; p0 += win) {
+      const i64 p1 = std::min<i64>(npairs, p0 + win);
+      const unsigned g = sig.done ? 1u : grid_for(p1 - p0, kTPB, (i64)s->cus * 4);
+      HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, true>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
+                      (V*)out, err_of(s), sig, p0, p1));
+    }
   } else {
     const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, false>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
-                    (V*)out, err_of(s), sig));
+                    (V*)out, err_of(s), sig, (i64)0, (i64)0));
   }
   return GLINT_OK;
 }

@@ -32,7 +32,7 @@ kstats() {  # kstats <name> <seconds> <bench args...>: kernel stats CSV of one b
   shift 2
   echo "[$(date +%T)] kstats $name" >&2
   (cd /tmp && timeout -k 10 $secs rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$name -o run \
-     -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/prof_$name.log 2>&1) || { tail -30 $OUT/prof_$name.log >&2; exit 1; }
+     -- python3 $R/bench.py --no-cpu-baseline --no-north-star "$@" > $OUT/prof_$name.log 2>&1) || { tail -30 $OUT/prof_$name.log >&2; exit 1; }
   find /tmp/prof_$name -name "*kernel_stats.csv" -exec cp {} $OUT/kstats_$name.csv \;
 }
 pmc() {  # pmc <name> <bench args...>: FETCH_SIZE and WRITE_SIZE in two separate passes
@@ -41,7 +41,7 @@ pmc() {  # pmc <name> <bench args...>: FETCH_SIZE and WRITE_SIZE in two separate
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "[$(date +%T)] pmc $name $c" >&2
     (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d /tmp/pmc_${name}_$c -o run \
-       -- python3 $R/bench.py --no-cpu-baseline --no-check --steps 5 --warmup 2 "$@" > $OUT/pmc_${name}_$c.log 2>&1) \
+       -- python3 $R/bench.py --no-cpu-baseline --no-north-star --no-check --steps 5 --warmup 2 "$@" > $OUT/pmc_${name}_$c.log 2>&1) \
        || { tail -30 $OUT/pmc_${name}_$c.log >&2; exit 1; }
     find /tmp/pmc_${name}_$c -name "*counter_collection.csv" -exec cp {} $OUT/pmc_${name}_$c.csv \;
   done
@@ -66,9 +66,15 @@ for s in ${STAGES:-tests bench}; do
       for pat in ${PATTERNS:-zipf matrix exchange}; do kstats $pat 300 --pattern $pat --steps 10 --warmup 2; done
       ;;
     pmc)
-      pmc dense_2p28
-      pmc zipf_2p28 --pattern zipf
-      pmc matrix_2p17x512 --pattern matrix
+      for w in ${PMC:-dense_2p28 dense_2p30 zipf_2p28 matrix_2p17x512}; do
+        case $w in
+          dense_2p28) pmc $w ;;
+          dense_2p30) pmc $w --log2-keys 30 ;;
+          zipf_2p28) pmc $w --pattern zipf ;;
+          matrix_2p17x512) pmc $w --pattern matrix ;;
+          exchange_2p28) pmc $w --pattern exchange ;;
+        esac
+      done
       ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
@@ -95,6 +101,9 @@ for s in ${STAGES:-tests bench}; do
       for w in ${WINDOWS:-0 24 25 26 27}; do
         step win_$w 300 env GLINT_SWEEP_WINDOW=$w python3 bench.py --no-cpu-baseline
       done
+      ;;
+    pullwin)
+      for w in 0 26; do step pullwin_$w 300 env GLINT_SWEEP_WINDOW=$w python3 bench.py --no-cpu-baseline --pattern pull; done
       ;;
     micro)
       step micro_stream_2p30 300 tools/microbench_stream 30 9 6
