@@ -809,6 +809,12 @@ void free_shard(glint_shard* s) {
     if (s->d_ctl) (void)hipFree(s->d_ctl);
     if (s->d_scratch) (void)hipFree(s->d_scratch);
     if (s->d_det) (void)hipFree(s->d_det);
+    if (s->det_stream) {
+      (void)hipStreamSynchronize(s->det_stream);
+      (void)hipStreamDestroy(s->det_stream);
+    }
+    for (auto& e : s->det_ev)
+      if (e) (void)hipEventDestroy(e);
     if (s->d_bin) (void)hipFree(s->d_bin);
     if (s->h_hint) (void)hipHostFree(s->h_hint);
     if (s->h_stage) (void)hipHostFree(s->h_stage);

@@ -35,6 +35,10 @@ struct glint_shard {
   size_t scratch_bytes = 0;
   void* d_det = nullptr;
   size_t det_bytes = 0;
+  // the deterministic tail folds the chains of its hottest elements on a second stream while the rest
+  // of the push is sorted (glint_sort.hip); created on first use
+  hipStream_t det_stream = nullptr;
+  hipEvent_t det_ev[2] = {nullptr, nullptr};
   void* d_bin = nullptr;  // binned-push scratch
   size_t bin_bytes = 0;
   double bin_dedup_ratio = 0.0;  // distinct/records of the last deduplicating binned push

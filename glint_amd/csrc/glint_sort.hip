@@ -375,6 +375,184 @@ int rs_sort(K* k0, V* v0, K* k1, V* v1, i64 m, int end_bit, u32* hist, u32* offs
   return GLINT_OK;
 }
 
+// ---- hot chains ---------------------------------------------------------------------------------
+// An element with hundreds of thousands of records is a fold chain of that many dependent adds (the
+// cfg3 batch's hottest key: 7.3 M records, ~33 ms); nothing can shorten it, but nothing needs to wait
+// for it either. The elements with the most records in a sample are split off first: their records,
+// in push order, go to one buffer per element (a stable compaction) and leave the main sort (their
+// address becomes the sentinel). One wave per hot element folds its chain on a second stream while
+// the main stream sorts and folds everything else.
+constexpr int kHotMax = 8;          // hot elements split off, at most
+constexpr int kHotSample = 65536;   // records sampled
+constexpr i64 kHotMinRecords = 1 << 16;  // estimated records an element needs to be split off
+constexpr int kHotTile = 4096;      // records per block of the compaction
+
+// One block: sample every (m / kHotSample)-th address, count them in an LDS hash table, keep the up
+// to kHotMax most frequent ones whose estimated record count reaches kHotMinRecords.
+template <typename K>
+__global__ __launch_bounds__(1024) void det_hot_pick(const K* __restrict__ addr, i64 m, K sentinel, u32 thresh,
+                                                     K* __restrict__ hot, u32* __restrict__ nhot) {
+  constexpr int kSlots = sizeof(K) == 4 ? 16384 : 8192;
+  constexpr int kSlotShift = sizeof(K) == 4 ? 50 : 51;
+  __shared__ K hk[kSlots];
+  __shared__ u32 hc[kSlots];
+  __shared__ u32 best_c[1024 / 64];
+  __shared__ int best_i[1024 / 64];
+  __shared__ u32 taken;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int i = tid; i < kSlots; i += 1024) {
+    hk[i] = sentinel;
+    hc[i] = 0;
+  }
+  if (tid == 0) taken = 0;
+  __syncthreads();
+  const i64 stride = m / kHotSample > 0 ? m / kHotSample : 1;
+  for (i64 j = tid; j < kHotSample && j * stride < m; j += 1024) {
+    const K a = addr[j * stride];
+    if (a == sentinel) continue;
+    u32 h = (u32)(((u64)a * 0x9E3779B97F4A7C15ull) >> kSlotShift);
+    // bounded probing: with more distinct samples than slots a sample may go uncounted -- a hot
+    // element is among the first ones seen and is counted
+    for (int probe = 0; probe < 64; ++probe) {
+      const K prev = atomicCAS(&hk[h], sentinel, a);
+      if (prev == sentinel || prev == a) {
+        atomicAdd(&hc[h], 1u);
+        break;
+      }
+      h = (h + 1) & (kSlots - 1);
+    }
+  }
+  __syncthreads();
+  for (int r = 0; r < kHotMax; ++r) {  // repeated block-wide arg-max
+    u32 c = 0;
+    int idx = -1;
+    for (int i = tid; i < kSlots; i += 1024)
+      if (hc[i] > c) { c = hc[i]; idx = i; }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      const u32 oc = __shfl_xor(c, d);
+      const int oi = __shfl_xor(idx, d);
+      if (oc > c || (oc == c && oi > idx)) { c = oc; idx = oi; }
+    }
+    if (lane == 0) { best_c[wid] = c; best_i[wid] = idx; }
+    __syncthreads();
+    if (tid == 0) {
+      u32 bc = 0;
+      int bi = -1;
+      for (int w = 0; w < 1024 / 64; ++w)
+        if (best_c[w] > bc) { bc = best_c[w]; bi = best_i[w]; }
+      if (bi >= 0 && bc >= thresh) {
+        hot[taken++] = hk[bi];
+        hc[bi] = 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *nhot = taken;
+}
+
+__device__ __forceinline__ int hot_index(u64 a, const u64* hot, u32 nh) {
+  int h = -1;
+#pragma unroll
+  for (int q = 0; q < kHotMax; ++q) h = ((u32)q < nh && a == hot[q]) ? q : h;
+  return h;
+}
+
+// per block (kHotTile records): records of each hot element -> cnt[h * nblocks + block]
+template <typename K>
+__global__ __launch_bounds__(kTPB) void det_hot_count(const K* __restrict__ addr, i64 m, const K* __restrict__ hot,
+                                                      const u32* __restrict__ nhot, u32* __restrict__ cnt, u32 nblocks) {
+  __shared__ u32 c[kHotMax];
+  const u32 nh = *nhot;
+  if (threadIdx.x < kHotMax) c[threadIdx.x] = 0;
+  __syncthreads();
+  if (nh == 0) return;
+  u64 hv[kHotMax];
+#pragma unroll
+  for (int q = 0; q < kHotMax; ++q) hv[q] = (u32)q < nh ? (u64)hot[q] : ~0ull;
+  const i64 t0 = (i64)blockIdx.x * kHotTile;
+  u32 mine[kHotMax] = {0};
+  for (int j = threadIdx.x; j < kHotTile; j += kTPB) {
+    const i64 i = t0 + j;
+    if (i >= m) break;
+    const int h = hot_index((u64)addr[i], hv, nh);
+    if (h >= 0) ++mine[h];
+  }
+#pragma unroll
+  for (int q = 0; q < kHotMax; ++q)
+    if (mine[q]) atomicAdd(&c[q], mine[q]);
+  __syncthreads();
+  if (threadIdx.x < kHotMax) cnt[(i64)threadIdx.x * nblocks + blockIdx.x] = c[threadIdx.x];
+}
+
+// per block, in record order: each hot record's value to the hot buffer at offs[h][block] (the
+// element's run, then its block) + its rank among the block's earlier records of that element (waves
+// in order, lanes in order); its address becomes the sentinel, so the main sort leaves it out
+template <typename K, typename V>
+__global__ __launch_bounds__(kTPB) void det_hot_scatter(K* __restrict__ addr, const V* __restrict__ val, i64 m,
+                                                        K sentinel, const K* __restrict__ hot,
+                                                        const u32* __restrict__ nhot, const u32* __restrict__ offs,
+                                                        u32 nblocks, V* __restrict__ hbuf) {
+  __shared__ u32 base[kHotMax];
+  __shared__ u32 wc[kTPB / 64][kHotMax];
+  const u32 nh = *nhot;
+  if (nh == 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u64 below = (1ull << lane) - 1ull;
+  u64 hv[kHotMax];
+#pragma unroll
+  for (int q = 0; q < kHotMax; ++q) hv[q] = (u32)q < nh ? (u64)hot[q] : ~0ull;
+  if (tid < kHotMax) base[tid] = (u32)tid < nh ? offs[(i64)tid * nblocks + blockIdx.x] : 0u;
+  const i64 t0 = (i64)blockIdx.x * kHotTile;
+  for (int r0 = 0; r0 < kHotTile; r0 += kTPB) {  // rounds of kTPB records
+    const i64 i = t0 + r0 + tid;
+    const int h = i < m ? hot_index((u64)addr[i], hv, nh) : -1;
+    u32 rank = 0;
+#pragma unroll
+    for (int q = 0; q < kHotMax; ++q) {
+      const u64 b = __ballot(h == q);
+      if (h == q) rank = (u32)__popcll(b & below);
+      if (lane == 0) wc[wid][q] = (u32)__popcll(b);
+    }
+    __syncthreads();
+    if (h >= 0) {
+      u32 pos = base[h] + rank;
+      for (int w = 0; w < wid; ++w) pos += wc[w][h];
+      hbuf[pos] = val[i];
+      addr[i] = sentinel;
+    }
+    __syncthreads();
+    if (tid < kHotMax)
+      for (int w = 0; w < kTPB / 64; ++w) base[tid] += wc[w][tid];
+    __syncthreads();
+  }
+}
+
+// one wave per hot element: its whole chain, starting from the shard's value (det_fold's transposed
+// loads and lane hand-off)
+template <typename K, typename V>
+__global__ __launch_bounds__(kTPB) void det_fold_hot(const K* __restrict__ hot, const u32* __restrict__ nhot,
+                                                     const u32* __restrict__ tot, const u32* __restrict__ offs,
+                                                     u32 nblocks, const V* __restrict__ hbuf, V* data) {
+  const int lane = threadIdx.x & 63;
+  const u32 w = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
+  if (w >= *nhot) return;
+  const K ad = hot[w];
+  const V* v = hbuf + offs[(i64)w * nblocks];  // the element's run starts at its first block's offset
+  const i64 e = tot[w];
+  constexpr i64 kB = 64 * kDetK;
+  V acc = data[ad];
+  V A[kDetK], B[kDetK];
+  det_load(A, v, 0, e, lane);
+  for (i64 b = 0; b < e; b += 2 * kB) {
+    det_load(B, v, b + kB, e, lane);
+    acc = det_fold(A, acc, b, e, lane);
+    det_load(A, v, b + 2 * kB, e, lane);
+    acc = det_fold(B, acc, b + kB, e, lane);
+  }
+  if (lane == 0) data[ad] = acc;
+}
+
 // ---- host side ----------------------------------------------------------------------------------
 template <typename K, typename V, bool MAT>
 int det_tail_k(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
@@ -388,7 +566,11 @@ int det_tail_k(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_
   const size_t b_addr = pad256((size_t)m * sizeof(K)), b_val = pad256((size_t)m * sizeof(V));
   const size_t b_list = pad256(((size_t)m / kDetShort + 2) * 4);
   const size_t b_hist = pad256((size_t)ntiles * 256 * 4);
-  const size_t need = 2 * b_addr + 2 * b_val + b_list + 2 * b_hist + 1024;
+  // hot chains: up to kHotMax buffers of m values each (a hot element may own any share of the push)
+  const bool split = m >= 8 * kHotMinRecords;
+  const u32 hblocks = (u32)((m + kHotTile - 1) / kHotTile);
+  const size_t b_hot = split ? pad256((size_t)m * sizeof(V)) + 2 * pad256((size_t)kHotMax * hblocks * 4) + 1024 : 0;
+  const size_t need = 2 * b_addr + 2 * b_val + b_list + 2 * b_hist + 1024 + b_hot;
   int rc = grow(&s->d_det, &s->det_bytes, need);
   if (rc) return rc;
   char* base = (char*)s->d_det;
@@ -405,6 +587,38 @@ int det_tail_k(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_
   det_prepare_kernel<K, V, MAT><<<g, kTPB, 0, st>>>(a.keys, a.cols, a.vals, m, a.ctl, a.ntiles, from_break ? 1 : 0,
                                                     a.part, sentinel, addr0, val0, a.err);
   HIPCHK(hipGetLastError());
+  if (split) {
+    if (!s->det_stream) {
+      if (hipStreamCreateWithFlags(&s->det_stream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&s->det_ev[0], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s->det_ev[1], hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return GLINT_EDEVICE;
+      }
+    }
+    char* hb = (char*)tot + 1024;
+    V* hbuf = (V*)hb;
+    u32* hcnt = (u32*)(hb + pad256((size_t)m * sizeof(V)));
+    u32* hoffs = hcnt + pad256((size_t)kHotMax * hblocks * 4) / 4;
+    K* hot = (K*)(hoffs + pad256((size_t)kHotMax * hblocks * 4) / 4);
+    u32* nhot = (u32*)(hot + kHotMax);
+    u32* htot = nhot + 1;
+    const u32 thresh = (u32)std::max<i64>(2, kHotMinRecords * kHotSample / m);
+    det_hot_pick<K><<<1, 1024, 0, st>>>(addr0, m, sentinel, thresh, hot, nhot);
+    det_hot_count<K><<<hblocks, kTPB, 0, st>>>(addr0, m, hot, nhot, hcnt, hblocks);
+    // per hot element its records, then per block its offset (the elements' runs one after another)
+    rs_sums<<<kHotMax, 1024, 0, st>>>(hcnt, hblocks, htot);
+    rs_scan<<<kHotMax, 1024, 0, st>>>(hcnt, hblocks, htot, hoffs);
+    det_hot_scatter<K, V><<<hblocks, kTPB, 0, st>>>(addr0, val0, m, sentinel, hot, nhot, hoffs, hblocks, hbuf);
+    HIPCHK(hipGetLastError());
+    // the hot chains on the second stream, from here; the push's stream joins them at its end
+    HIPCHK(hipEventRecord(s->det_ev[0], st));
+    HIPCHK(hipStreamWaitEvent(s->det_stream, s->det_ev[0], 0));
+    det_fold_hot<K, V><<<(kHotMax + kTPB / 64 - 1) / (kTPB / 64), kTPB, 0, s->det_stream>>>(hot, nhot, htot, hoffs,
+                                                                                              hblocks, hbuf, a.data);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(s->det_ev[1], s->det_stream));
+  }
   // stable LSD radix sort: equal addresses keep their push order
   int where = 0;
   rc = rs_sort<K, V>(addr0, val0, addr1, val1, m, end_bit, hist, offs, tot, st, &where);
@@ -416,6 +630,7 @@ int det_tail_k(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_
   HIPCHK(hipGetLastError());
   det_fold_long_kernel<K, V><<<(unsigned)s->cus * 2, kTPB, 0, st>>>(addr, val, m, long_count, long_list, a.data);
   HIPCHK(hipGetLastError());
+  if (split) HIPCHK(hipStreamWaitEvent(st, s->det_ev[1], 0));  // the push ends when its hot chains have
   return GLINT_OK;
 }
 
