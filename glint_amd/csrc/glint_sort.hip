@@ -383,7 +383,7 @@ int rs_sort(K* k0, V* v0, K* k1, V* v1, i64 m, int end_bit, u32* hist, u32* offs
 // address becomes the sentinel). One wave per hot element folds its chain on a second stream while
 // the main stream sorts and folds everything else.
 constexpr int kHotMax = 8;          // hot elements split off, at most
-constexpr int kHotSample = 65536;   // records sampled
+constexpr int kHotSample = 16384;   // records sampled
 constexpr i64 kHotMinRecords = 1 << 16;  // estimated records an element needs to be split off
 constexpr int kHotTile = 4096;      // records per block of the compaction
 
