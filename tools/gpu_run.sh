@@ -12,6 +12,9 @@
 #   det       tools/det_probe.py (cfg3 deterministic push), timed and under rocprofv3 kernel stats
 #   micro     tools/microbench_stream mode 6: the dense sweep at 2^26..2^30, chunked and shifted
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (separate runs) of the dense, zipf and matrix lines
+#   latency   tools/host_latency.py (per-call cost of the host-pointer entry points)
+#   ring      tools/ring_probe.py: pipelined message-sized wire pushes, timed and with kernel stats
+#   loopback  tools/loopback/build/glint_loopback, HBM shards vs the oracle's CPU loop (cfg1, cfg4 shapes)
 set -o pipefail
 TAG=${TAG:-r03}
 R=$(pwd)
@@ -107,6 +110,33 @@ for s in ${STAGES:-tests bench}; do
       ;;
     micro)
       step micro_stream_2p30 300 tools/microbench_stream 30 9 6
+      ;;
+    latency)  # per-call cost of the host-pointer entry points, and the box's launch / mapped-wait floor
+      step host_latency 300 python3 tools/host_latency.py --reps 300
+      ;;
+    ring)  # pipelined message-sized wire pushes (4000 x 1000 random keys), timed and under kernel stats
+      step ring_probe 300 python3 tools/ring_probe.py 1000 4000
+      echo "[$(date +%T)] kstats ring" >&2
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_ring -o run \
+         -- python3 $R/tools/ring_probe.py 1000 4000 > $OUT/prof_ring.log 2>&1) || { tail -30 $OUT/prof_ring.log >&2; exit 1; }
+      find /tmp/prof_ring -name "*kernel_stats.csv" -exec cp {} $OUT/kstats_ring.csv \;
+      ;;
+    loopback)  # cfg1 / window 1 / 79 999-record messages / cfg4a / cfg4b over loopback TCP, both backends;
+               # the cfg4 shapes also with the client bucketing offloaded to the device route
+      LB=tools/loopback/build/glint_loopback
+      G="--backend gpu --lib glint_amd/lib/libglint_gpu.so"
+      O="--backend oracle --lib oracle/build/libglint_oracle.so"
+      i=0
+      for args in "" "--window 1" "--keys 16777216 --msg 79999" "--clients 64 --servers 8 --keys 33554432" \
+                  "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
+        step lb_gpu_$i 200 $LB $G $args
+        step lb_oracle_$i 200 $LB $O $args
+        case "$args" in *--clients*) step lb_gpudev_$i 200 $LB $G $args --bucket device ;; esac
+        i=$((i + 1))
+      done
+      cat $OUT/lb_gpu_*.log | grep '^{' > $OUT/loopback_gpu.jsonl || true
+      cat $OUT/lb_gpudev_*.log | grep '^{' > $OUT/loopback_gpu_bucket_device.jsonl || true
+      cat $OUT/lb_oracle_*.log | grep '^{' > $OUT/loopback_oracle.jsonl || true
       ;;
     *)
       echo "unknown stage $s" >&2
