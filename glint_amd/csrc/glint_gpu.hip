@@ -1822,9 +1822,25 @@ int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, i
   if (n < 0) return GLINT_EINVAL;
   if (len != 9 + (size_t)n * (8 + (mat ? 4 : 0) + s->vsize)) return GLINT_EINVAL;
   if (id) *id = mid;
+  const uint8_t* kp = payload + 9;  // unaligned sections, copied as they lie
+  if (!batchable(s, n) && stage_layout(s, n).total > kSlotKeepBytes) {
+    // larger than a ring slot is kept at (never an Akka message: the frame cap is 79 999 records):
+    // applied now through the staged copies, so no pinned slot is allocated and released per message.
+    // Checked on the host first, so a rejected message applies nothing, as every enqueued one; the
+    // ticket is that of everything enqueued so far (complete on return).
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      const int rc = reject_if_bad(s, kp, mat ? kp + (size_t)n * 8 : nullptr, n);
+      if (rc) return rc;
+    }
+    const int rc = host_push(s, mat, (const int64_t*)kp, (const int32_t*)(kp + (size_t)n * 8),
+                             kp + (size_t)n * (8 + (mat ? 4 : 0)), n, flags);
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (ticket) *ticket = s->ticket_next;
+    return rc;
+  }
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
-  const uint8_t* kp = payload + 9;  // unaligned sections, copied as they lie
   if (batchable(s, n))
     return ring_append_locked(s, n, flags, kp, kp + (size_t)n * 8, kp + (size_t)n * (8 + (mat ? 4 : 0)),
                               (u64*)ticket);

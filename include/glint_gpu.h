@@ -184,7 +184,9 @@ int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uin
 int glint_stage_acquire(glint_shard_t shard, int64_t n, void** keys, void** cols, void** vals, int* slot);
 /* Enqueues the push of the n records staged in `slot`; *ticket receives its ticket. */
 int glint_push_staged(glint_shard_t shard, int slot, int64_t n, int flags, uint64_t* ticket);
-/* glint_push_wire, enqueued: the payload is copied into a slot before the call returns. */
+/* glint_push_wire, enqueued: the payload is copied into a slot before the call returns. A push of more
+ * than 4 MiB of records (far above the 79 999-record frame cap) is applied before the call returns
+ * instead, through the staged copies, so the ring's pinned memory stays bounded. */
 int glint_push_wire_async(glint_shard_t shard, const uint8_t* payload, size_t len, int32_t* id, int flags,
                           uint64_t* ticket);
 /* Waits for the entry with this ticket and every earlier one and completes their pulls' answers;

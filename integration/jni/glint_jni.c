@@ -105,9 +105,10 @@ JNIEXPORT void JNICALL Java_glint_models_server_gpu_GpuShard_await(JNIEnv* env, 
   raise(env, glint_shard_wait(SHARD(h), (uint64_t)ticket, &bad), SHARD(h));
 }
 
-/* Pushes of more records than a ring slot holds (never an Akka message: the frame cap is 79 999)
- * go through the synchronous host-pointer entry points with a private copy of the arrays. */
-#define RING_MAX ((jsize)1 << 20)
+/* Pushes of more records than a ring slot is kept at (a few MiB; never an Akka message: the frame cap
+ * is 79 999) go through the synchronous host-pointer entry points with a private copy of the arrays,
+ * so no pinned slot is allocated and released per message. */
+#define RING_MAX ((jsize)1 << 17)
 
 /* ---- typed pushes: PartialVector.update / PartialMatrix.update -> ticket ------------------------- */
 #define VEC_PUSH(SUF, JT, JARR, REGION, GLDT)                                                              \
@@ -231,6 +232,97 @@ JNIEXPORT void JNICALL Java_glint_models_server_gpu_GpuShard_await(JNIEnv* env, 
     free(o);                                                                                                \
     raise(env, rc, s);                                                                                      \
   }
+
+/* ---- pipelined pulls: the actor enqueues a Pull and answers the burst's pulls after one wait -------
+ * pullAsync copies the keys (and cols) out of the JVM arrays and enqueues the pull (glint_pull_async)
+ * into a native answer buffer; it returns a handle. pullFinish<T> waits for that pull's ticket, copies
+ * the answer into the result array and frees the handle. kind: 0 PartialVector.get, 1
+ * PartialMatrix.get, 2 PartialMatrix.getRows (flattened rows x cols). An out-of-partition key throws
+ * from pullAsync (the Pull message itself), with nothing enqueued. */
+typedef struct {
+  glint_shard_t s;
+  uint64_t ticket;
+  int64_t count; /* answer elements */
+  int dtype;
+  void* buf;
+} pending_pull;
+
+#define PULL_ASYNC_MAX ((jsize)1 << 20) /* glint_pull_async's bound; larger pulls are answered at once */
+
+JNIEXPORT jlong JNICALL Java_glint_models_server_gpu_GpuShard_pullAsync(JNIEnv* env, jclass c, jlong h, jint kind,
+                                                                        jlongArray rows, jintArray cols) {
+  glint_shard_t s = SHARD(h);
+  int dt = -1;
+  int32_t ncols = 0;
+  if (raise(env, glint_shard_info(s, NULL, &ncols, &dt, NULL), s)) return 0;
+  if (kind < 0 || kind > 2 || (kind == 0) != (ncols == 0)) {
+    throw_named(env, "java/lang/IllegalArgumentException", "pull kind does not match the shard");
+    return 0;
+  }
+  const jsize n = (*env)->GetArrayLength(env, rows);
+  if (kind == 1 && check_len(env, cols, n, "cols shorter than rows")) return 0;
+  const int64_t count = kind == 2 ? (int64_t)n * ncols : (int64_t)n;
+  if (count > 0x7fffffff) {
+    throw_named(env, "java/lang/IllegalArgumentException", "answer larger than a JVM array");
+    return 0;
+  }
+  const size_t vsize = (dt == GLINT_F64 || dt == GLINT_I64) ? 8 : 4;
+  pending_pull* p = (pending_pull*)calloc(1, sizeof(pending_pull));
+  jlong* r = (jlong*)malloc((size_t)n * 8 + 8);
+  jint* cc = kind == 1 ? (jint*)malloc((size_t)n * 4 + 8) : NULL;
+  void* buf = malloc((size_t)count * vsize + 8);
+  if (!p || !r || (kind == 1 && !cc) || !buf) {
+    free(p); free(r); free(cc); free(buf);
+    raise(env, GLINT_ENOMEM, s);
+    return 0;
+  }
+  (*env)->GetLongArrayRegion(env, rows, 0, n, r);
+  if (kind == 1) (*env)->GetIntArrayRegion(env, cols, 0, n, cc);
+  int rc;
+  uint64_t ticket = 0;
+  if (n > PULL_ASYNC_MAX) {
+    rc = kind == 0   ? glint_vec_pull(s, (const int64_t*)r, buf, n)
+         : kind == 1 ? glint_mat_pull(s, (const int64_t*)r, (const int32_t*)cc, buf, n)
+                     : glint_mat_pull_rows(s, (const int64_t*)r, buf, n);
+  } else {
+    rc = glint_pull_async(s, kind, (const int64_t*)r, (const int32_t*)cc, buf, n, &ticket);
+  }
+  free(r);
+  free(cc);
+  if (raise(env, rc, s)) {
+    free(buf);
+    free(p);
+    return 0;
+  }
+  p->s = s;
+  p->ticket = ticket;
+  p->count = count;
+  p->dtype = dt;
+  p->buf = buf;
+  return (jlong)(intptr_t)p;
+}
+
+#define PULL_FINISH(SUF, JT, JARR, REGION, GLDT)                                                           \
+  JNIEXPORT void JNICALL Java_glint_models_server_gpu_GpuShard_pullFinish##SUF(JNIEnv* env, jclass c,         \
+                                                                             jlong pending, JARR out) {    \
+    pending_pull* p = (pending_pull*)(intptr_t)pending;                                                     \
+    if (!p) return;                                                                                         \
+    int rc = glint_shard_wait(p->s, p->ticket, NULL);                                                       \
+    if (rc == GLINT_OK && p->dtype != GLDT) {                                                               \
+      throw_named(env, "java/lang/IllegalArgumentException", "value type does not match the shard");       \
+    } else if (rc == GLINT_OK && !check_len(env, out, (jsize)p->count, "result array shorter than answer")) { \
+      (*env)->Set##REGION##ArrayRegion(env, out, 0, (jsize)p->count, (const JT*)p->buf);                    \
+    }                                                                                                       \
+    const glint_shard_t s = p->s;                                                                           \
+    free(p->buf);                                                                                           \
+    free(p);                                                                                                \
+    raise(env, rc, s);                                                                                      \
+  }
+
+PULL_FINISH(D, jdouble, jdoubleArray, Double, GLINT_F64)
+PULL_FINISH(F, jfloat, jfloatArray, Float, GLINT_F32)
+PULL_FINISH(L, jlong, jlongArray, Long, GLINT_I64)
+PULL_FINISH(I, jint, jintArray, Int, GLINT_I32)
 
 VEC_PUSH(D, jdouble, jdoubleArray, Double, GLINT_F64)
 VEC_PUSH(F, jfloat, jfloatArray, Float, GLINT_F32)

@@ -54,6 +54,17 @@ object GpuShard {
   @native def matPullRowsL(handle: Long, rows: Array[Long], out: Array[Long]): Unit
   @native def matPullRowsI(handle: Long, rows: Array[Long], out: Array[Int]): Unit
 
+  /** Pipelined pulls: `pullAsync` enqueues a pull (kind 0 get, 1 matrix get, 2 getRows) behind every
+    * enqueued push and returns a handle; `pullFinish*` waits for it and fills the result array. */
+  @native def pullAsync(handle: Long, kind: Int, rows: Array[Long], cols: Array[Int]): Long
+  @native def pullFinishD(pending: Long, out: Array[Double]): Unit
+  @native def pullFinishF(pending: Long, out: Array[Float]): Unit
+  @native def pullFinishL(pending: Long, out: Array[Long]): Unit
+  @native def pullFinishI(pending: Long, out: Array[Int]): Unit
+
+  /** Sent by an actor to itself behind a burst of Pull messages (see GpuShardActor). */
+  private[gpu] case object FlushPulls
+
   /** The shard of `partition` on GPU `device` (range or cyclic layout, as the partitioner chose). */
   def create(partition: Partition, dtype: Int, cols: Int, device: Int): Long = partition match {
     case p: RangePartition => createRange(device, dtype, p.start, p.end, cols)
@@ -82,10 +93,32 @@ object GpuShard {
   * the new instance allocates a zeroed one (the reference's restart re-creates `new Array[V](size)`).
   * The client's AcknowledgeReceipt then reaches the new actor and is answered NotAcknowledgeReceipt
   * (PushLogic.scala:44-49), and a Pull after the restart is answered from the zeroed shard.
+  *
+  * Pulls are pipelined the same way: a Pull enqueues its gather (pullAsync; it sees every push
+  * enqueued before it, as get() sees every update before it) and its answer is held. The first held
+  * pull sends FlushPulls to the actor itself; that message queues behind everything already in the
+  * mailbox, so when it arrives the burst has been taken, and the held pulls are answered in arrival
+  * order after their waits (the first wait covers most of the burst). The reference answers each Pull
+  * in `receive` (PartialVectorDouble.scala:18); here a burst of Pulls costs one GPU round trip instead
+  * of one per message. A restart answers the held pulls first (postStop).
   */
 trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
   protected def shard: Long
   private val pending = mutable.HashMap.empty[Int, Long]  // push id -> ticket
+  private val held = mutable.ArrayBuffer.empty[() => Unit]  // answers of enqueued pulls, in arrival order
+
+  /** Holds the answer of an enqueued pull (`answer` finishes it and replies to its sender). */
+  protected def hold(answer: () => Unit): Unit = {
+    held += answer
+    if (held.size == 1) self ! GpuShard.FlushPulls
+  }
+
+  /** Answers every held pull, in arrival order. */
+  protected def flushPulls(): Unit = {
+    val answers = held.toList
+    held.clear()
+    answers.foreach(_())
+  }
 
   protected def enqueued(id: Int, ticket: Long): Unit = pending.put(id, ticket)
 
@@ -101,7 +134,9 @@ trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
     case _ =>
   }
 
-  override def postStop(): Unit = GpuShard.destroy(shard)
+  override def postStop(): Unit = {
+    try flushPulls() finally GpuShard.destroy(shard)
+  }
 }
 
 // ---- vectors: PartialVector{Double,Float,Long,Int}.scala --------------------------------------------
@@ -115,7 +150,11 @@ class GpuPartialVectorDouble(partition: Partition) extends PartialVector[Double]
     val out = new Array[Double](keys.length); GpuShard.vecPullD(shard, keys, out); out
   }
   override def receive: Receive = {
-    case pull: PullVector => sender ! ResponseDouble(get(pull.keys))
+    case pull: PullVector =>
+      val to = sender(); val out = new Array[Double](pull.keys.length)
+      val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
+      hold(() => { GpuShard.pullFinishD(p, out); to ! ResponseDouble(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorDouble => enqueued(push.id, GpuShard.vecPushD(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -131,7 +170,11 @@ class GpuPartialVectorFloat(partition: Partition) extends PartialVector[Float](p
     val out = new Array[Float](keys.length); GpuShard.vecPullF(shard, keys, out); out
   }
   override def receive: Receive = {
-    case pull: PullVector => sender ! ResponseFloat(get(pull.keys))
+    case pull: PullVector =>
+      val to = sender(); val out = new Array[Float](pull.keys.length)
+      val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
+      hold(() => { GpuShard.pullFinishF(p, out); to ! ResponseFloat(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorFloat => enqueued(push.id, GpuShard.vecPushF(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -147,7 +190,11 @@ class GpuPartialVectorLong(partition: Partition) extends PartialVector[Long](par
     val out = new Array[Long](keys.length); GpuShard.vecPullL(shard, keys, out); out
   }
   override def receive: Receive = {
-    case pull: PullVector => sender ! ResponseLong(get(pull.keys))
+    case pull: PullVector =>
+      val to = sender(); val out = new Array[Long](pull.keys.length)
+      val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
+      hold(() => { GpuShard.pullFinishL(p, out); to ! ResponseLong(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorLong => enqueued(push.id, GpuShard.vecPushL(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -163,7 +210,11 @@ class GpuPartialVectorInt(partition: Partition) extends PartialVector[Int](parti
     val out = new Array[Int](keys.length); GpuShard.vecPullI(shard, keys, out); out
   }
   override def receive: Receive = {
-    case pull: PullVector => sender ! ResponseInt(get(pull.keys))
+    case pull: PullVector =>
+      val to = sender(); val out = new Array[Int](pull.keys.length)
+      val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
+      hold(() => { GpuShard.pullFinishI(p, out); to ! ResponseInt(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorInt => enqueued(push.id, GpuShard.vecPushI(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -186,8 +237,15 @@ class GpuPartialMatrixDouble(partition: Partition, cols: Int) extends PartialMat
     val out = new Array[Double](rows.length * cols); GpuShard.matPullRowsD(shard, rows, out); out
   }
   override def receive: Receive = {
-    case pull: PullMatrix => sender ! ResponseDouble(get(pull.rows, pull.cols))
-    case pull: PullMatrixRows => sender ! ResponseDouble(getRowsFlat(pull.rows))
+    case pull: PullMatrix =>
+      val to = sender(); val out = new Array[Double](pull.rows.length)
+      val p = GpuShard.pullAsync(shard, 1, pull.rows, pull.cols)
+      hold(() => { GpuShard.pullFinishD(p, out); to ! ResponseDouble(out) })
+    case pull: PullMatrixRows =>
+      val to = sender(); val out = new Array[Double](pull.rows.length * cols)
+      val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
+      hold(() => { GpuShard.pullFinishD(p, out); to ! ResponseDouble(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixDouble => enqueued(push.id, GpuShard.matPushD(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -207,8 +265,15 @@ class GpuPartialMatrixFloat(partition: Partition, cols: Int) extends PartialMatr
     val out = new Array[Float](rows.length * cols); GpuShard.matPullRowsF(shard, rows, out); out
   }
   override def receive: Receive = {
-    case pull: PullMatrix => sender ! ResponseFloat(get(pull.rows, pull.cols))
-    case pull: PullMatrixRows => sender ! ResponseFloat(getRowsFlat(pull.rows))
+    case pull: PullMatrix =>
+      val to = sender(); val out = new Array[Float](pull.rows.length)
+      val p = GpuShard.pullAsync(shard, 1, pull.rows, pull.cols)
+      hold(() => { GpuShard.pullFinishF(p, out); to ! ResponseFloat(out) })
+    case pull: PullMatrixRows =>
+      val to = sender(); val out = new Array[Float](pull.rows.length * cols)
+      val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
+      hold(() => { GpuShard.pullFinishF(p, out); to ! ResponseFloat(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixFloat => enqueued(push.id, GpuShard.matPushF(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -228,8 +293,15 @@ class GpuPartialMatrixLong(partition: Partition, cols: Int) extends PartialMatri
     val out = new Array[Long](rows.length * cols); GpuShard.matPullRowsL(shard, rows, out); out
   }
   override def receive: Receive = {
-    case pull: PullMatrix => sender ! ResponseLong(get(pull.rows, pull.cols))
-    case pull: PullMatrixRows => sender ! ResponseLong(getRowsFlat(pull.rows))
+    case pull: PullMatrix =>
+      val to = sender(); val out = new Array[Long](pull.rows.length)
+      val p = GpuShard.pullAsync(shard, 1, pull.rows, pull.cols)
+      hold(() => { GpuShard.pullFinishL(p, out); to ! ResponseLong(out) })
+    case pull: PullMatrixRows =>
+      val to = sender(); val out = new Array[Long](pull.rows.length * cols)
+      val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
+      hold(() => { GpuShard.pullFinishL(p, out); to ! ResponseLong(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixLong => enqueued(push.id, GpuShard.matPushL(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -249,8 +321,15 @@ class GpuPartialMatrixInt(partition: Partition, cols: Int) extends PartialMatrix
     val out = new Array[Int](rows.length * cols); GpuShard.matPullRowsI(shard, rows, out); out
   }
   override def receive: Receive = {
-    case pull: PullMatrix => sender ! ResponseInt(get(pull.rows, pull.cols))
-    case pull: PullMatrixRows => sender ! ResponseInt(getRowsFlat(pull.rows))
+    case pull: PullMatrix =>
+      val to = sender(); val out = new Array[Int](pull.rows.length)
+      val p = GpuShard.pullAsync(shard, 1, pull.rows, pull.cols)
+      hold(() => { GpuShard.pullFinishI(p, out); to ! ResponseInt(out) })
+    case pull: PullMatrixRows =>
+      val to = sender(); val out = new Array[Int](pull.rows.length * cols)
+      val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
+      hold(() => { GpuShard.pullFinishI(p, out); to ! ResponseInt(out) })
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixInt => enqueued(push.id, GpuShard.matPushI(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }

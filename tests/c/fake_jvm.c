@@ -3,7 +3,8 @@
  * create -> push (ticket) -> await -> pull; an order-sensitive Double push; an out-of-partition
  * push throws ArrayIndexOutOfBoundsException at the Push message itself (as update() throws inside
  * receive, PartialVectorDouble.scala:17-23) and applies nothing, while earlier pushes' awaits and a
- * pull stay clean; an out-of-partition pull throws the same way; zero (the Akka restart) -> push again;
+ * pull stay clean; an out-of-partition pull throws the same way; pipelined pulls (pullAsync, then
+ * pullFinish after the burst) see the pushes enqueued before them; zero (the Akka restart) -> push again;
  * argument errors (value type, short arrays); a matrix shard's element and row pulls; destroy.
  * Exit status 0 and "ok" on stdout when every check passes. */
 #include <math.h>
@@ -71,6 +72,9 @@ void NAT(vecPullD)(JNIEnv*, jclass, jlong, jlongArray, jdoubleArray);
 jlong NAT(matPushI)(JNIEnv*, jclass, jlong, jlongArray, jintArray, jintArray, jint);
 void NAT(matPullI)(JNIEnv*, jclass, jlong, jlongArray, jintArray, jintArray);
 void NAT(matPullRowsI)(JNIEnv*, jclass, jlong, jlongArray, jintArray);
+jlong NAT(pullAsync)(JNIEnv*, jclass, jlong, jint, jlongArray, jintArray);
+void NAT(pullFinishD)(JNIEnv*, jclass, jlong, jdoubleArray);
+void NAT(pullFinishI)(JNIEnv*, jclass, jlong, jintArray);
 
 static int failures = 0;
 #define CHECK(cond, what)                                            \
@@ -145,6 +149,21 @@ int main(int argc, char** argv) {
         "clean pull after the bad push; the bad push applied nothing");
   NAT(vecPullD)(env, NULL, h, kb, o2);
   CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "out-of-partition pull raises");
+  /* pipelined pulls (the actor's burst): a push enqueued, two pulls enqueued behind it, then answered */
+  const jlong tp = NAT(vecPushD)(env, NULL, h, k1, v1, 0);
+  const jlong pa = NAT(pullAsync)(env, NULL, h, 0, k2, NULL);
+  const jlong pb = NAT(pullAsync)(env, NULL, h, 0, k, NULL);
+  CHECK(tp > 0 && pa != 0 && pb != 0 && !pending[0], "pulls enqueued behind a push");
+  Arr* oa = arr(2, 8);
+  NAT(pullFinishD)(env, NULL, pa, oa);
+  NAT(pullFinishD)(env, NULL, pb, out);
+  CHECK(!pending[0] && ((jdouble*)oa->data)[0] == 0.5 && ((jdouble*)oa->data)[1] == 1.0 + 0.5,
+        "async pull sees the push enqueued before it");
+  CHECK(((jdouble*)out->data)[0] == seq && ((jdouble*)out->data)[999] == 0.5 * 999, "async pull of 1000 keys");
+  CHECK(NAT(pullAsync)(env, NULL, h, 0, kb, NULL) == 0 && took("java/lang/ArrayIndexOutOfBoundsException"),
+        "out-of-partition async pull raises at the Pull");
+  NAT(pullAsync)(env, NULL, h, 2, k2, NULL);
+  CHECK(took("java/lang/IllegalArgumentException"), "row pull of a vector shard");
   NAT(zero)(env, NULL, h);
   NAT(await)(env, NULL, h, NAT(vecPushD)(env, NULL, h, k3, v3, 0));
   NAT(vecPullD)(env, NULL, h, k3, o1);
@@ -177,6 +196,14 @@ int main(int argc, char** argv) {
   Arr* ro = arr(70, 4);
   NAT(matPullRowsI)(env, NULL, m, rows, ro);
   CHECK(!memcmp(ro->data, mv->data, 280) && !pending[0], "matrix row pull (flattened)");
+  const jlong pr = NAT(pullAsync)(env, NULL, m, 2, rows, NULL);
+  const jlong pe = NAT(pullAsync)(env, NULL, m, 1, r, c);
+  Arr* ro2 = arr(70, 4);
+  Arr* mo2 = arr(70, 4);
+  NAT(pullFinishI)(env, NULL, pr, ro2);
+  NAT(pullFinishI)(env, NULL, pe, mo2);
+  CHECK(!pending[0] && !memcmp(ro2->data, mv->data, 280) && !memcmp(mo2->data, mv->data, 280),
+        "async matrix row and element pulls");
   Arr* cs = arr(69, 4);
   NAT(matPushI)(env, NULL, m, r, cs, mv, 0);
   CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "short cols");

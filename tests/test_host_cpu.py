@@ -138,7 +138,7 @@ def test_jni_shim_compiles_and_links():
     scala = (Path(__file__).resolve().parent.parent / "integration" / "scala" / "GpuShard.scala").read_text()
     import re
     natives = re.findall(r"@native def (\w+)", scala)
-    assert len(natives) == 25  # lifetime 5, typed pushes 8, typed pulls 12
+    assert len(natives) == 30  # lifetime 5, typed pushes 8, typed pulls 12, pipelined pulls 5
     for name in natives:
         assert f"Java_glint_models_server_gpu_GpuShard_{name}" in syms, name
 

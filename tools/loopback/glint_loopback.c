@@ -44,7 +44,8 @@
  *            records appending each index to its partition's list (keys.indices.groupBy(partition));
  *   device   offloaded: the client's whole batch routed on the GPU by glint_route_dev (a stable
  *            counting sort by partition, one launch), then each partition's ordered index list is cut
- *            at the slice boundaries. Both give the same messages, record for record.
+ *            at the slice boundaries. Each client holds its device buffers, pinned read-back memory and
+ *            its own stream from before the timed region. Both give the same messages, record for record.
  *
  * Output: one JSON line.
  */
@@ -493,7 +494,10 @@ static int bucket_device;  /* --bucket device */
 static void* hip_dl;
 static int (*hip_malloc)(void**, size_t);
 static int (*hip_free)(void*);
-static int (*hip_memcpy)(void*, const void*, size_t, int);
+static int (*hip_memcpy_async)(void*, const void*, size_t, int, void*);
+static int (*hip_stream_create)(void**, unsigned);
+static int (*hip_stream_sync)(void*);
+static int (*hip_host_malloc)(void**, size_t, unsigned);
 static int (*route_dev)(const int64_t*, int64_t, int, int32_t, int64_t, int64_t*, int64_t*, int64_t*, void*);
 
 /* per partition: its record indices in record order (idx[p][0..cnt[p])) -> the link's messages, cut at
@@ -514,33 +518,46 @@ static void cut_messages(link_arg* l, int64_t* idx, int64_t cnt) {
   }
 }
 
+/* A client's device context for the offloaded bucketing, set up before the timed region (a client
+ * process holds its GPU buffers and stream for its lifetime): keys in, counts and order out, the order
+ * read back into pinned host memory, all on the client's own stream. */
+typedef struct {
+  void *dk, *dc, *dord, *stream;
+  int64_t* order; /* pinned */
+  int64_t* cnt;   /* pinned */
+} client_dev;
+
+static void client_dev_init(client_dev* d, int64_t n) {
+  const size_t b = (size_t)(n > 0 ? n : 1) * 8;
+  if (hip_malloc(&d->dk, b) || hip_malloc(&d->dc, (size_t)S * 8) || hip_malloc(&d->dord, b)) die("hipMalloc");
+  if (hip_stream_create(&d->stream, 1 /* hipStreamNonBlocking */)) die("hipStreamCreateWithFlags");
+  if (hip_host_malloc((void**)&d->order, b, 0) || hip_host_malloc((void**)&d->cnt, (size_t)S * 8, 0))
+    die("hipHostMalloc");
+}
+
 /* Buckets client c's batch for its S links; returns the seconds it took. `store` receives the S
  * index arrays (freed by the caller). */
-static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int64_t** store) {
+static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int64_t** store, client_dev* d) {
   const double t0 = now_s();
   int64_t* cnt = (int64_t*)calloc((size_t)S, 8);
   if (bucket_device && n > 0) {
-    /* offloaded: one stable route of the whole batch on the GPU (glint_route_dev) */
-    void *dk = NULL, *dc = NULL, *dord = NULL;
-    if (hip_malloc(&dk, (size_t)n * 8) || hip_malloc(&dc, (size_t)S * 8) || hip_malloc(&dord, (size_t)n * 8))
-      die("hipMalloc");
-    if (hip_memcpy(dk, keys, (size_t)n * 8, 1 /* hipMemcpyHostToDevice */)) die("hipMemcpy");
+    /* offloaded: one stable route of the whole batch on the GPU (glint_route_dev), on the client's stream */
+    if (hip_memcpy_async(d->dk, keys, (size_t)n * 8, 1 /* hipMemcpyHostToDevice */, d->stream)) die("hipMemcpyAsync");
     int64_t bad = -1;
-    if (route_dev((const int64_t*)dk, n, 0 /* GLINT_ROUTE_RANGE */, S, N, (int64_t*)dc, (int64_t*)dord, &bad, NULL))
+    if (route_dev((const int64_t*)d->dk, n, 0 /* GLINT_ROUTE_RANGE */, S, N, (int64_t*)d->dc, (int64_t*)d->dord, &bad,
+                  d->stream))
       die("glint_route_dev");
-    int64_t* order = (int64_t*)malloc((size_t)n * 8);
-    if (hip_memcpy(order, dord, (size_t)n * 8, 2 /* DeviceToHost */) || hip_memcpy(cnt, dc, (size_t)S * 8, 2))
-      die("hipMemcpy");
-    hip_free(dk);
-    hip_free(dc);
-    hip_free(dord);
+    if (hip_memcpy_async(d->order, d->dord, (size_t)n * 8, 2 /* DeviceToHost */, d->stream) ||
+        hip_memcpy_async(d->cnt, d->dc, (size_t)S * 8, 2, d->stream) || hip_stream_sync(d->stream))
+      die("hipMemcpyAsync");
+    memcpy(cnt, d->cnt, (size_t)S * 8);
+    const int64_t* order = d->order;
     int64_t o = 0;
     for (int p = 0; p < S; ++p) {
       store[p] = (int64_t*)malloc((size_t)(cnt[p] > 0 ? cnt[p] : 1) * 8);
       memcpy(store[p], order + o, (size_t)cnt[p] * 8);
       o += cnt[p];
     }
-    free(order);
   } else {
     /* the reference's groupBy, slice by slice: one pass per slice, each index appended to its
      * partition's list (lists grow as the groupBy's buffers do) */
@@ -571,6 +588,7 @@ static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int
 typedef struct {
   link_arg* links; /* this client's S links */
   double bucket_s;
+  client_dev dev;  /* --bucket device */
 } client_arg;
 
 static void* link_main(void* p);
@@ -580,7 +598,7 @@ static void* client_main(void* p) {
   client_arg* ca = (client_arg*)p;
   link_arg* l = ca->links;
   int64_t** store = (int64_t**)calloc((size_t)S, sizeof(int64_t*));
-  ca->bucket_s = bucket_client(l, l[0].keys, l[0].n, store);
+  ca->bucket_s = bucket_client(l, l[0].keys, l[0].n, store, &ca->dev);
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)S);
   for (int i = 0; i < S; ++i) pthread_create(&th[i], NULL, link_main, &l[i]);
   for (int i = 0; i < S; ++i) pthread_join(th[i], NULL);
@@ -723,9 +741,14 @@ int main(int argc, char** argv) {
     if (!hip_dl) { fprintf(stderr, "glint_loopback: dlopen libamdhip64.so: %s\n", dlerror()); return 2; }
     *(void**)&hip_malloc = dlsym(hip_dl, "hipMalloc");
     *(void**)&hip_free = dlsym(hip_dl, "hipFree");
-    *(void**)&hip_memcpy = dlsym(hip_dl, "hipMemcpy");
+    *(void**)&hip_memcpy_async = dlsym(hip_dl, "hipMemcpyAsync");
+    *(void**)&hip_stream_create = dlsym(hip_dl, "hipStreamCreateWithFlags");
+    *(void**)&hip_stream_sync = dlsym(hip_dl, "hipStreamSynchronize");
+    *(void**)&hip_host_malloc = dlsym(hip_dl, "hipHostMalloc");
     *(void**)&route_dev = dlsym(dl, "glint_route_dev");
-    if (!hip_malloc || !hip_free || !hip_memcpy || !route_dev) die("dlsym hip*/glint_route_dev");
+    if (!hip_malloc || !hip_free || !hip_memcpy_async || !hip_stream_create || !hip_stream_sync || !hip_host_malloc ||
+        !route_dev)
+      die("dlsym hip*/glint_route_dev");
   }
 
   /* RangePartitioner.apply(S, N) (RangePartitioner.scala:62-84) and partition() (:27-43) */
@@ -810,6 +833,8 @@ int main(int argc, char** argv) {
     }
   pthread_t* ct = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)C);
   client_arg* cargs = (client_arg*)calloc((size_t)C, sizeof(client_arg));
+  if (bucket_device)
+    for (int c = 0; c < C; ++c) client_dev_init(&cargs[c].dev, cn[c]);
   double t[3], bucket_s[2] = {0, 0}, bucket_max[2] = {0, 0};
   int64_t msgs[2] = {0, 0}, resends = 0;
   for (int mode = 0; mode < 2; ++mode) {
