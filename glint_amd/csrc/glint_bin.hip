@@ -1079,9 +1079,17 @@ BinGeom bin_geometry(i64 elems) {
   const i64 slabs = (elems + kSlab - 1) / kSlab;
   u32 sb = 0;
   while (((i64)1 << sb) < slabs) ++sb;
-  // up to 256 coarse buckets (few enough that a partition chunk's records form runs per bucket), more
-  // only when the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses)
-  const u32 cb = std::min<u32>(sb, std::max<u32>(8u, sb > 10u ? sb - 10u : 0u));
+  // 128 coarse buckets (few enough that a partition chunk's records form runs per bucket, and a
+  // fine-partition item's runs per slab stay as long: 32 records each way for uniform keys into
+  // 2^28), more only when the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses).
+  // Same box, two runs each (profiles/r03/bench_binned_cb.txt): 2^7 against 2^8 buckets cfg5
+  // 0.418 -> 0.398 ms, cfg3 1.648 -> 1.636 ms, cfg4b exchange 3.005 -> 3.005 ms; 2^6 slower on all
+  static const u32 cb_min = [] {  // GLINT_BIN_CB: coarse digit bits at least (tuning knob, 4..10)
+    const char* e = getenv("GLINT_BIN_CB");
+    const int v = e ? atoi(e) : 0;
+    return (u32)(v >= 4 && v <= 10 ? v : 7);
+  }();
+  const u32 cb = std::min<u32>(sb, std::max<u32>(cb_min, sb > 10u ? sb - 10u : 0u));
   BinGeom g;
   g.fb = sb - cb;
   g.nb = 1u << cb;

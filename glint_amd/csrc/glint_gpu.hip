@@ -17,6 +17,7 @@
 #include <vector>
 #include <utility>
 #include <new>
+#include <chrono>
 #include <cstring>
 #include <sched.h>
 #include <cstdio>
@@ -1194,14 +1195,33 @@ StageLayout stage_layout(const glint_shard* s, i64 n) {
   return L;
 }
 
-// Waits until the launch that carries `ticket` has written it to h_done (tickets complete in stream
-// order, so a later ticket there covers this one). Spins briefly -- a message-sized launch is a few
-// microseconds -- then lets HIP block on the stream, which also surfaces a device error.
-int wait_done(glint_shard* s, u64 ticket) {
-  for (int i = 0; i < (1 << 16); ++i) {
-    if (__atomic_load_n(s->h_done, __ATOMIC_ACQUIRE) >= ticket) return GLINT_OK;
+// Polls a host-mapped ticket word until it reaches `ticket` or `budget_us` has passed: a busy spin
+// for the first few microseconds (a message-sized launch completes in about that), then
+// sched_yield between polls, so that a server with many more waiting threads than cores (one
+// thread per client connection) hands the CPU to the threads that have work instead of spinning
+// against them.
+bool poll_word(const u64* word, u64 ticket, double budget_us) {
+  constexpr double kSpinUs = 4.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (u32 i = 0;; ++i) {
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) >= ticket) return true;
+    if ((i & 15) == 15) {
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (us > budget_us) return false;
+      if (us > kSpinUs) {
+        sched_yield();
+        continue;
+      }
+    }
     __builtin_ia32_pause();
   }
+}
+
+// Waits until the launch that carries `ticket` has written it to h_done (tickets complete in stream
+// order, so a later ticket there covers this one). Polls briefly, then lets HIP block on the
+// stream, which also surfaces a device error.
+int wait_done(glint_shard* s, u64 ticket) {
+  if (poll_word(s->h_done, ticket, 200.0)) return GLINT_OK;
   HIPCHK(hipStreamSynchronize(s->stream));
   return __atomic_load_n(s->h_done, __ATOMIC_ACQUIRE) >= ticket ? GLINT_OK : GLINT_EDEVICE;
 }
@@ -1857,22 +1877,33 @@ int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, i
 
 int glint_shard_wait(glint_shard_t s, uint64_t ticket, int64_t* first_bad) {
   if (!s) return GLINT_EINVAL;
-  {  // launch the open batch if it holds this ticket, then wait WITHOUT the shard lock, so other
-     // threads of the server keep enqueueing meanwhile (one connection per client in the actor model)
+  // Launch the open batch if it holds this ticket, then wait WITHOUT the shard lock, so other
+  // threads of the server keep enqueueing meanwhile (one connection per client in the actor
+  // model): on the ticket word when the entry carrying the ticket signals it, else on its event.
+  bool sig = false;
+  hipEvent_t ev = nullptr;
+  {
     std::lock_guard<std::mutex> lk(s->mu);
     DeviceGuard g(s->device);
     if (s->open_slot >= 0 && s->ring[s->open_slot].msgs.front().ticket <= ticket) {
       const int rc = ring_flush_locked(s);
       if (rc) return rc;
     }
-  }
-  const u64* done = s->h_done;  // written once, before the first ticket exists
-  if (done) {
-    // bounded: an entry that completes by event (a DMA'd push) never moves the word
-    for (int i = 0; i < (1 << 14) && __atomic_load_n(done, __ATOMIC_ACQUIRE) < ticket; ++i) {
-      if ((i & 255) == 255) sched_yield();
-      else __builtin_ia32_pause();
+    const glint_shard::RingSlot* cover = nullptr;  // the newest in-flight entry at or below the ticket
+    for (const auto& r : s->ring)
+      if (r.inflight && r.ticket_lo <= ticket && (!cover || r.ticket_lo > cover->ticket_lo)) cover = &r;
+    if (cover) {
+      sig = cover->sig;
+      ev = cover->done;
     }
+  }
+  if (sig) {
+    (void)poll_word(s->h_done, ticket, 5000.0);
+  } else if (ev) {
+    // a DMA'd entry completes by its event; a slot reused meanwhile only re-records it later, so
+    // this never returns early (the locked wait below settles the entries either way)
+    (void)hipEventSynchronize(ev);
+    (void)hipGetLastError();
   }
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
