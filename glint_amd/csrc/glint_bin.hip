@@ -500,20 +500,127 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   ph.flush(8);
 }
 
+// ---- hot elements ----------------------------------------------------------------------------------
+// A Zipf-like tail sends its most frequent elements through every partition chunk: the dedup table
+// merges them within a chunk, but each chunk still emits one record per hot element, and those
+// records cross both partition levels and the apply. The hot elements are picked per push from a
+// sample of the tail (bin_hot_pick) into a direct-mapped table of kHotSlots elements; the dedup
+// front end sums their records in per-workgroup LDS accumulators over ALL its chunks and adds each
+// sum to the shard once at the end (one device atomic per hot element per workgroup), so only the
+// cold elements are partitioned. Any choice of hot set gives the same sums; the sample only decides
+// how much work moves off the partition path.
+constexpr int kHotSlots = 2048;     // direct-mapped hot table (per dedup workgroup: tags + sums in LDS)
+constexpr int kHotSample = 16384;   // records sampled per push, as kHotRuns runs of kHotRun records
+constexpr int kHotRun = 128;
+constexpr int kHotRuns = kHotSample / kHotRun;
+constexpr int kHotCount = 16384;    // sampler's LDS count table (load <= ~0.5: short probe chains)
+constexpr int kHotTPB = 1024;
+
+__device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ u32 hot_slot(u32 a) { return hot_mix(a) & (kHotSlots - 1); }
+
+// One workgroup: kHotSample records (kHotRuns runs spread evenly over the tail) are counted per
+// element in LDS; every element seen at least min_count times (2: frequency >= ~2 / kHotSample of
+// the tail) competes for its direct-mapped slot, the most frequent one wins. Writes hot_tags[kHotSlots] (kEmptySlot = none).
+template <bool MAT>
+__global__ __launch_bounds__(kHotTPB) void bin_hot_pick_kernel(const i64* __restrict__ keys,
+                                                               const int32_t* __restrict__ cols, i64 n,
+                                                               PartDesc part, const LaunchCtl* lctl, u32 ntiles,
+                                                               int from_break, u32 min_count,
+                                                               u32* __restrict__ hot_tags) {
+  __shared__ u32 ck[kHotCount];
+  __shared__ u32 cc[kHotCount];
+  __shared__ unsigned long long best[kHotSlots];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kHotCount; i += kHotTPB) {
+    ck[i] = kEmptySlot;
+    cc[i] = 0;
+  }
+  for (int i = tid; i < kHotSlots; i += kHotTPB) best[i] = 0ull;
+  __syncthreads();
+  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
+  const i64 m = n - r0;
+  if (m > 0) {
+    // kHotRuns runs of kHotRun consecutive records, spread evenly over the tail: whole-line reads
+    // (one workgroup reading 32768 scattered 8-B keys took ~150 us, bound by its lines in flight;
+    // 32768 samples in this table took 87 us, bound by divergent probe chains at load ~0.75)
+    const i64 ns = min((i64)kHotSample, m);
+    const i64 run_stride = m >= (i64)kHotSample ? m / kHotRuns : kHotRun;  // a short tail: read it all
+    auto rec_of = [&](i64 sidx) { return r0 + (sidx / kHotRun) * run_stride + (sidx % kHotRun); };
+    constexpr int kBatch = 16;  // samples per thread whose loads are in flight together
+    for (i64 s0 = 0; s0 < ns; s0 += (i64)kBatch * kHotTPB) {
+      i64 k[kBatch];
+      int32_t c[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {  // clamped, branch-free loads
+        const i64 i = rec_of(min(s0 + (i64)j * kHotTPB + tid, ns - 1));
+        k[j] = keys[i];
+        c[j] = MAT ? cols[i] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        i64 a64;
+        if (s0 + (i64)j * kHotTPB + tid >= ns || !rec_addr<MAT>(part, k[j], c[j], a64)) continue;
+        const u32 a = (u32)a64;
+        u32 h = hot_mix(a * 0x9E3779B1u) & (kHotCount - 1);
+        for (int probe = 0; probe < 64; ++probe) {  // bounded: a full neighbourhood drops the sample
+          const u32 prev = atomicCAS(&ck[h], kEmptySlot, a);
+          if (prev == kEmptySlot || prev == a) {
+            atomicAdd(&cc[h], 1u);
+            break;
+          }
+          h = (h + 1) & (kHotCount - 1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int h = tid; h < kHotCount; h += kHotTPB)
+    if (cc[h] >= min_count) atomicMax(&best[hot_slot(ck[h])], ((unsigned long long)cc[h] << 32) | ck[h]);
+  __syncthreads();
+  for (int i = tid; i < kHotSlots; i += kHotTPB) hot_tags[i] = best[i] ? (u32)best[i] : kEmptySlot;
+}
+
+// a hot sum's initial value: adding it to the first record is exact (x + -0.0 == x), and a slot still
+// holding it at the end got no record (or only -0.0 ones, which leave the element as it is)
+template <typename A> __device__ __forceinline__ A hot_zero() { return A(0); }
+template <> __device__ __forceinline__ double hot_zero<double>() { return -0.0; }
+template <typename A> __device__ __forceinline__ bool hot_untouched(A x) { return x == A(0); }
+template <> __device__ __forceinline__ bool hot_untouched<double>(double x) {
+  return __double_as_longlong(x) == (long long)0x8000000000000000ull;
+}
+__device__ __forceinline__ void hot_flush(double* p, double x) { gadd(p, x); }
+__device__ __forceinline__ void hot_flush(float* p, double x) { gadd(p, (float)x); }
+__device__ __forceinline__ void hot_flush(long long* p, long long x) { gadd(p, x); }
+__device__ __forceinline__ void hot_flush(int* p, int x) { gadd(p, x); }
+
 // Dedup front end for duplicate-heavy tails: per chunk, equal elements are summed in an LDS hash
 // table first, so one record per distinct element of the chunk moves on. The staging buffer of the
-// append overlays the table's value array.
-template <typename V, bool MAT>
+// append overlays the table's value array. Records of the push's hot elements (hot_tags) are summed
+// in LDS across all of the workgroup's chunks instead and added to the shard at the end.
+
+// KIND: the partition layout (0 range: only the keys' low words are loaded, as in bin_count -- the
+// register budget of this kernel is tight; -1 read at run time)
+template <typename V, bool MAT, int KIND>
 __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     const i64* __restrict__ keys, const int32_t* __restrict__ cols, const V* __restrict__ vals, i64 n, PartDesc part,
     const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, const u32* __restrict__ R,
     u32* __restrict__ segoff, u32* __restrict__ seglen, u32* __restrict__ addr_out,
     typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc, const u32* __restrict__ T,
-    uint2* __restrict__ fitems) {
+    uint2* __restrict__ fitems, const u32* __restrict__ hot_tags, V* __restrict__ data) {
   typedef typename LdsAcc<V>::T A;
   static_assert(kAChunk * (4 + sizeof(A)) <= kASlots * sizeof(A), "staging must fit the value table");
   __shared__ u32 hk[kASlots];
   __shared__ A hv[kASlots];
+  __shared__ u32 htag[kHotSlots];
+  __shared__ A hacc[kHotSlots];
   __shared__ uint16_t used[kAChunk];
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
   __shared__ u32 nused;
@@ -527,6 +634,10 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   for (int sl = tid; sl < kASlots; sl += kATPB) {
     hk[sl] = kEmptySlot;
     hv[sl] = A(0);
+  }
+  for (int sl = tid; sl < kHotSlots; sl += kATPB) {
+    htag[sl] = hot_tags ? hot_tags[sl] : kEmptySlot;
+    hacc[sl] = hot_zero<A>();
   }
   if (tid == 0) nused = 0;
   PhaseClock ph(8);
@@ -544,30 +655,62 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   // compiler can wait for one chunk's loads while the next chunk's stay in flight
   auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 cc = min(c, nchunks - 1);
-    load_recs<V, MAT>(keys, cols, vals, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+    const i64 c0 = r0 + cc * kAChunk, c1 = min(n, r0 + (cc + 1) * kAChunk);
+    if constexpr (KIND == 0) {  // (key - start).toInt needs the low words only
+#pragma unroll
+      for (int q = 0; q < kAPer; ++q) {
+        const i64 i = c0 + q * kATPB + threadIdx.x;
+        const i64 ii = i < c1 ? i : c1 - 1;
+        r.k[q] = (i64)(u64)reinterpret_cast<const u32*>(keys)[2 * ii];
+        r.cl[q] = MAT ? cols[ii] : 0;
+        r.v[q] = vals[ii];
+      }
+    } else {
+      load_recs<V, MAT>(keys, cols, vals, c0, c1, r);
+    }
   };
   auto step = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
+    // the chunk's addresses, rejected records and hot hits first: the hot-table reads of all kAPer
+    // records are in flight together, and a hot record is summed here and leaves the chunk
+    u32 ca[kAPer];
+    u32 cold = 0;
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       const i64 i = c0 + q * kATPB + tid;
+      i64 a64;
+      ca[q] = 0;
+      if (i < c1) {
+        if (rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64)) {
+          ca[q] = (u32)a64;
+          cold |= 1u << q;
+        } else {
+          bad.add(i);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kAPer; ++q) {
+      const u32 hs = hot_slot(ca[q]);
+      if ((cold & (1u << q)) && htag[hs] == ca[q]) {  // hot: summed over all of this workgroup's chunks
+        lds_add(&hacc[hs], (A)r.v[q]);
+        cold &= ~(1u << q);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kAPer; ++q) {
       bool claimed = false;
       u32 h = 0;
-      if (i < c1) {
-        i64 a64;
-        if (!rec_addr<MAT>(part, r.k[q], r.cl[q], a64)) {
-          bad.add(i);
-        } else {
-          const u32 a = (u32)a64;
-          h = (a * 0x9E3779B1u) >> (32 - kASlotBits);
-          for (;;) {  // the compare-and-swap is the probe: one LDS round trip per slot tried
-            const u32 prev = atomicCAS(&hk[h], kEmptySlot, a);
-            if (prev == kEmptySlot) { claimed = true; break; }
-            if (prev == a) break;
-            h = (h + 1) & (kASlots - 1);
-          }
-          lds_add(&hv[h], (A)r.v[q]);
+      if (cold & (1u << q)) {
+        const u32 a = ca[q];
+        h = (a * 0x9E3779B1u) >> (32 - kASlotBits);
+        for (;;) {  // the compare-and-swap is the probe: one LDS round trip per slot tried
+          const u32 prev = atomicCAS(&hk[h], kEmptySlot, a);
+          if (prev == kEmptySlot) { claimed = true; break; }
+          if (prev == a) break;
+          h = (h + 1) & (kASlots - 1);
         }
+        lds_add(&hv[h], (A)r.v[q]);
       }
       const u64 b = __ballot(claimed);  // the wave's new slots join the list with one LDS atomic
       if (b) {
@@ -626,6 +769,11 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
   bad.report(err);
+  __syncthreads();  // every chunk's hot sums are in
+  for (int sl = tid; sl < kHotSlots; sl += kATPB) {
+    const u32 a = htag[sl];
+    if (a != kEmptySlot && !hot_untouched<A>(hacc[sl])) hot_flush(data + a, hacc[sl]);
+  }
   ph.flush(10);
 }
 
@@ -1138,7 +1286,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const size_t cap_a = (size_t)nchunks_max * kAChunk;  // the partition's capacity (every chunk full)
   const size_t b_a = pad256(cap_a * 4), b_v = pad256(cap_a * sizeof(A));
   const size_t b_zero = b_ctl + b_T + 2 * b_H;
-  const size_t need = b_zero + 3 * b_seg + b_cd + 2 * (b_a + b_v);
+  const size_t b_hot = pad256((size_t)kHotSlots * 4);
+  const size_t need = b_zero + 3 * b_seg + b_cd + b_hot + 2 * (b_a + b_v);
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   char* p = (char*)s->d_bin;
@@ -1155,6 +1304,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   uint2* fitems = (uint2*)(p + pad256((size_t)nslots * 16));
   u32* IH = (u32*)(p + pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8));
   p += b_cd;
+  u32* hot_tags = (u32*)p;
+  p += b_hot;
   u32* addr_a = (u32*)p;
   A* val_a = (A*)(p + b_a);
   u32* addr_b = (u32*)(p + b_a + b_v);
@@ -1163,14 +1314,28 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
+  static const bool hot_on = [] {  // GLINT_BIN_HOT=0: no hot-element split (A/B, tests)
+    const char* e = getenv("GLINT_BIN_HOT");
+    return !(e && atoi(e) == 0);
+  }();
+  if (dedup && hot_on) {
+    static const u32 hot_min = [] {  // GLINT_BIN_HOT_MIN: sample count that makes an element hot (tuning)
+      const char* e = getenv("GLINT_BIN_HOT_MIN");
+      return (u32)(e && atoi(e) > 0 ? atoi(e) : 2);
+    }();
+    bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, hot_min,
+                                                    hot_tags);
+    HIPCHK(hipGetLastError());
+  }
   if (a.part.kind == 0)
     bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
   else
     bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
   HIPCHK(hipGetLastError());
   if (dedup) {
-    bin_part_dedup_kernel<V, MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R,
-                                                       segoff, seglen, addr_a, val_a, a.err, bc, T, fitems);
+    auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
+                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data);
   } else {
     bin_part_kernel<V, MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff,
                                                  seglen, addr_a, val_a, a.err, bc, T, fitems);
