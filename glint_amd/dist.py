@@ -146,16 +146,25 @@ class _Exchange:
         self.group, self.comm, self.world = group, comm_device, W
         self.bad = -1
         self.bad_exc = bad_exc
-        _, cell = router._device_tables(counts.device)
-        send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
-        if bad_exc is None:
-            send[cell] = counts
-        if bad is not None:
-            send = torch.where(bad == 0, send, torch.zeros_like(send))
-        recv = self._a2a(send) if W > 1 else send
-        parts = [send, recv] + ([bad] if bad is not None else [])
-        host = torch.cat(parts).cpu().numpy()  # the call's one host synchronisation
-        send_h, recv_h = host[:W * maxp].reshape(W, maxp), host[W * maxp:2 * W * maxp].reshape(W, maxp)
+        if W == 1:
+            # a world of one exchanges nothing: the counts (and the status word) are read as they are,
+            # one small copy, and the send matrix is built on the host
+            host = (torch.cat([counts, bad]) if bad is not None else counts).cpu().numpy()
+            send_h = np.zeros((1, maxp), dtype=np.int64)
+            if bad_exc is None and (bad is None or host[-1] == 0):
+                send_h[0, router.slot_cell] = host[:counts.numel()]
+            recv_h = send_h
+        else:
+            _, cell = router._device_tables(counts.device)
+            send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
+            if bad_exc is None:
+                send[cell] = counts
+            if bad is not None:
+                send = torch.where(bad == 0, send, torch.zeros_like(send))
+            recv = self._a2a(send)
+            parts = [send, recv] + ([bad] if bad is not None else [])
+            host = torch.cat(parts).cpu().numpy()  # the call's one host synchronisation
+            send_h, recv_h = host[:W * maxp].reshape(W, maxp), host[W * maxp:2 * W * maxp].reshape(W, maxp)
         if bad is not None and host[-1] != 0:
             self.bad = int(~host[-1])
         self.recv_counts = recv_h  # [source rank, local partition j]

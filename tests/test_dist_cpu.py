@@ -1,4 +1,4 @@
-"""Multi-process tests of the exchange layer (glint_amd.dist) on CPU: world_size 2 and 3 over gloo,
+"""Multi-process tests of the exchange layer (glint_amd.dist) on CPU: world_size 1, 2 and 3 over gloo,
 with oracle-backed shards standing in for the HBM shards (tests/dist_workers.py). Covers range and
 cyclic placement, several partitions per rank (Client.scala:63, 75-84), fewer keys than partitions,
 matrices, out-of-range keys and empty batches."""
@@ -16,7 +16,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 @pytest.mark.parametrize("case", sorted(dist_workers.CASES))
 def test_exchange_matches_sequential_oracle(case, world):
     mp.spawn(dist_workers.run_case, args=(world, free_port(), "gloo", case, False), nprocs=world, join=True)
