@@ -80,6 +80,7 @@ struct BinCtl {
   u32 nslots;  // apply item slots written by bin_fpart (the last bucket's first item knows the total)
   u32 nfitems; // fine-partition items (written by bin_part's workgroup 0)
   u32 fnext;   // bin_fpart's item queue: the next item to take
+  u32 cold;    // valid records that were not hot (the dedup front end's input; m for the others)
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -113,6 +114,21 @@ struct PhaseClock {
   __device__ void flush(int) {}
 };
 #endif
+
+// Streaming inputs (records read once by a pass) load non-temporally (GLINT_BIN_NT, default 1), so
+// they do not evict the partially written output runs and slab lines the passes revisit. Same box,
+// two runs each (profiles/r03/ab_nt.txt): cfg3 1.43-1.50 -> 1.33-1.40 ms, cfg4b exchange -2-4 %.
+#ifndef GLINT_BIN_NT
+#define GLINT_BIN_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_in(const T* p) {
+#if GLINT_BIN_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 
 // ---- counted memory operations --------------------------------------------------------------------
 // On gfx9 loads and stores share one counter (vmcnt), and the compiler can keep loads of a later
@@ -247,9 +263,9 @@ __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const in
   for (int q = 0; q < kAPer; ++q) {  // clamped, branch-free loads
     const i64 i = c0 + q * kATPB + threadIdx.x;
     const i64 ii = i < c1 ? i : c1 - 1;
-    r.k[q] = keys[ii];
-    r.cl[q] = MAT ? cols[ii] : 0;
-    if (VALS) r.v[q] = vals[ii];
+    r.k[q] = ld_in(keys + ii);
+    r.cl[q] = MAT ? ld_in(cols + ii) : 0;
+    if (VALS) r.v[q] = ld_in(vals + ii);
   }
 }
 
@@ -289,8 +305,8 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
       for (int q = 0; q < kAPer; ++q) {
         const i64 i = c0 + q * kATPB + threadIdx.x;
         const i64 ii = i < c1 ? i : c1 - 1;
-        r.k[q] = (i64)(u64)reinterpret_cast<const u32*>(keys)[2 * ii];
-        r.cl[q] = MAT ? cols[ii] : 0;
+        r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
+        r.cl[q] = MAT ? ld_in(cols + ii) : 0;
       }
     } else {
       load_recs<double, MAT, false>(keys, cols, nullptr, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
@@ -334,170 +350,6 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   }
   const u32 tot = block_sum<kATPB>(nvalid);
   if (tid == 0 && tot) atomicAdd(&bc->tail, tot);
-}
-
-// ---- bin_part -------------------------------------------------------------------------------------
-// Appends a chunk's records (P per thread in registers, `valid` bit mask) to this workgroup's bucket
-// ranges: cur[b] = next free slot of bucket b. dcnt and gpos are scratch (dcnt zero on entry/exit).
-template <typename A, int P>
-__device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u32 valid, const BinGeom& g,
-                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v, const BufOut& oa,
-                                         const BufOut& ov, u32 wbase, PhaseClock& ph, int pb) {
-  const int tid = threadIdx.x;
-  u32 rank[P];
-#pragma unroll
-  for (int j = 0; j < P; ++j)
-    if (valid & (1u << j)) rank[j] = atomicAdd(&dcnt[bucket_of(ad[j], g)], 1u);
-  __syncthreads();
-  ph.mark(pb);
-  const u32 total = block_scan<kATPB, 1>(
-      g.nb, [&](u32 d) { return dcnt[d]; },
-      [&](u32 d, u32 excl) {
-        const u32 c = dcnt[d];
-        gpos[d] = cur[d] - excl;  // slot of local staging position p (bucket d) = gpos[d] + p
-        cur[d] += c;
-        dcnt[d] = excl;
-      });
-  ph.mark(pb + 1);
-#pragma unroll
-  for (int j = 0; j < P; ++j) {
-    if (valid & (1u << j)) {
-      const u32 p = dcnt[bucket_of(ad[j], g)] + rank[j];
-      st_a[p] = ad[j];
-      st_v[p] = va[j];
-    }
-  }
-  __syncthreads();
-  ph.mark(pb + 2);
-  static_assert(P * kATPB == kAChunk, "the store loop covers a whole chunk");
-#pragma unroll
-  for (int j = 0; j < P; ++j) {  // consecutive threads: consecutive slots of one run
-    if ((u32)(j * kATPB) >= total) break;  // workgroup-uniform: no store instructions past the chunk
-    const u32 p = tid + j * kATPB;
-    const bool on = p < total;
-    const u32 a = st_a[p];
-    const u32 rel = gpos[on ? bucket_of(a, g) : 0u] + p - wbase;  // within this workgroup's range
-#ifdef GLINT_BIN_NOSTORE  // timing experiment only: every partition store dropped
-    bput(oa, rel * 4u, false, a);
-    bput(ov, rel * (u32)sizeof(A), false, st_v[p]);
-#else
-    bput(oa, rel * 4u, on, a);
-    bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
-#endif
-  }
-  __syncthreads();
-  ph.mark(pb + 3);
-  for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
-  __syncthreads();
-  ph.mark(pb + 4);
-  return total;
-}
-
-// Workgroup w's bucket ranges: cur[b] = chunk_base(w) * kAChunk + exclusive scan of R[w][*], also
-// published bucket-major as segoff[b][w] for the fine partition.
-__device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks, const u32* __restrict__ R,
-                                           u32* __restrict__ segoff, u32* cur, u32* dcnt) {
-  const u32 base = chunk_base(w, gridDim.x, nchunks) * (u32)kAChunk;
-  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return R[w * g.nb + b]; },
-                       [&](u32 b, u32 excl) {
-                         cur[b] = base + excl;
-                         segoff[b * gridDim.x + w] = base + excl;  // bucket-major: bin_fpart reads a row
-                         dcnt[b] = 0;
-                       });
-}
-
-// Workgroup 0 of bin_part: the fine-partition items -- bucket b gets max(1, ceil(T[b] / kFItem))
-// of them ({b, j}: its records [j * kFItem, (j + 1) * kFItem) in segment order).
-__device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
-                                           BinCtl* bc) {
-  const u32 tot = block_scan<kATPB, 1>(
-      g.nb, [&](u32 b) { return max(1u, (T[b] + kFItem - 1) / kFItem); },
-      [&](u32 b, u32 excl) {
-        const u32 J = max(1u, (T[b] + kFItem - 1) / kFItem);
-        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
-      });
-  if (threadIdx.x == 0) bc->nfitems = tot;
-}
-
-__device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
-                                            u32* __restrict__ seglen, u32 emitted, BinCtl* bc) {
-  for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[b * gridDim.x + w] = cur[b] - segoff[b * gridDim.x + w];
-  if (threadIdx.x == 0 && emitted) atomicAdd(&bc->m, emitted);
-}
-
-// Plain front end: every valid record is appended as it is.
-template <typename V, bool MAT>
-__global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
-                                                         const V* __restrict__ vals, i64 n, PartDesc part,
-                                                         const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
-                                                         const u32* __restrict__ R, u32* __restrict__ segoff,
-                                                         u32* __restrict__ seglen, u32* __restrict__ addr_out,
-                                                         typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
-                                                         BinCtl* bc, const u32* __restrict__ T,
-                                                         uint2* __restrict__ fitems) {
-  typedef typename LdsAcc<V>::T A;
-  __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
-  __shared__ u32 st_a[kAChunk];
-  __shared__ A st_v[kAChunk];
-  const int tid = threadIdx.x;
-  const u32 w = blockIdx.x;
-  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
-  const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
-  PhaseClock ph(0);
-  if (w == 0) part_items(g, T, fitems, bc);
-  part_setup(g, w, nchunks, R, segoff, cur, dcnt);
-  ph.mark(0);
-  const i64 G = gridDim.x;
-  const u32 wbase = chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
-  const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
-  const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
-  BadRecs bad;
-  u32 emitted = 0;
-  // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
-  // compiler can wait for one chunk's loads while the next chunk's stay in flight
-  auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
-    const i64 cc = min(c, nchunks - 1);
-    load_recs<V, MAT>(keys, cols, vals, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
-  };
-  auto step = [&](i64 c, RecRegs<V, MAT>& r) {
-    const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
-    u32 ad[kAPer];
-    A va[kAPer];
-    u32 valid = 0;
-#pragma unroll
-    for (int q = 0; q < kAPer; ++q) {
-      const i64 i = c0 + q * kATPB + tid;
-      i64 a64;
-      ad[q] = 0;
-      va[q] = (A)r.v[q];
-      if (i < c1) {
-        if (rec_addr<MAT>(part, r.k[q], r.cl[q], a64)) {
-          ad[q] = (u32)a64;
-          valid |= 1u << q;
-        } else {
-          bad.add(i);
-        }
-      }
-    }
-    ph.mark(1);
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 3);
-    // two chunks ahead, into the registers just consumed: in flight across the next chunk's work
-    load_chunk(c + 2 * G, r);
-    ph.mark(2);
-  };
-  RecRegs<V, MAT> ra, rb;
-  i64 c = w;
-  if (c < nchunks) {
-    load_chunk(c, ra);
-    load_chunk(c + G, rb);
-    for (; c < nchunks; c += 2 * G) {
-      step(c, ra);
-      step(c + G, rb);  // past the end: no valid record, nothing stored
-    }
-  }
-  part_finish(g, w, segoff, cur, seglen, emitted, bc);
-  bad.report(err);
-  ph.flush(8);
 }
 
 // ---- hot elements ----------------------------------------------------------------------------------
@@ -601,6 +453,202 @@ __device__ __forceinline__ void hot_flush(float* p, double x) { gadd(p, (float)x
 __device__ __forceinline__ void hot_flush(long long* p, long long x) { gadd(p, x); }
 __device__ __forceinline__ void hot_flush(int* p, int x) { gadd(p, x); }
 
+// ---- bin_part -------------------------------------------------------------------------------------
+// Appends a chunk's records (P per thread in registers, `valid` bit mask) to this workgroup's bucket
+// ranges: cur[b] = next free slot of bucket b. dcnt and gpos are scratch (dcnt zero on entry/exit).
+template <typename A, int P>
+__device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u32 valid, const BinGeom& g,
+                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v, const BufOut& oa,
+                                         const BufOut& ov, u32 wbase, PhaseClock& ph, int pb) {
+  const int tid = threadIdx.x;
+  u32 rank[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j)
+    if (valid & (1u << j)) rank[j] = atomicAdd(&dcnt[bucket_of(ad[j], g)], 1u);
+  __syncthreads();
+  ph.mark(pb);
+  const u32 total = block_scan<kATPB, 1>(
+      g.nb, [&](u32 d) { return dcnt[d]; },
+      [&](u32 d, u32 excl) {
+        const u32 c = dcnt[d];
+        gpos[d] = cur[d] - excl;  // slot of local staging position p (bucket d) = gpos[d] + p
+        cur[d] += c;
+        dcnt[d] = excl;
+      });
+  ph.mark(pb + 1);
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    if (valid & (1u << j)) {
+      const u32 p = dcnt[bucket_of(ad[j], g)] + rank[j];
+      st_a[p] = ad[j];
+      st_v[p] = va[j];
+    }
+  }
+  __syncthreads();
+  ph.mark(pb + 2);
+  static_assert(P * kATPB == kAChunk, "the store loop covers a whole chunk");
+#pragma unroll
+  for (int j = 0; j < P; ++j) {  // consecutive threads: consecutive slots of one run
+    if ((u32)(j * kATPB) >= total) break;  // workgroup-uniform: no store instructions past the chunk
+    const u32 p = tid + j * kATPB;
+    const bool on = p < total;
+    const u32 a = st_a[p];
+    const u32 rel = gpos[on ? bucket_of(a, g) : 0u] + p - wbase;  // within this workgroup's range
+#ifdef GLINT_BIN_NOSTORE  // timing experiment only: every partition store dropped
+    bput(oa, rel * 4u, false, a);
+    bput(ov, rel * (u32)sizeof(A), false, st_v[p]);
+#else
+    bput(oa, rel * 4u, on, a);
+    bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
+#endif
+  }
+  __syncthreads();
+  ph.mark(pb + 3);
+  for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
+  __syncthreads();
+  ph.mark(pb + 4);
+  return total;
+}
+
+// Workgroup w's bucket ranges: cur[b] = chunk_base(w) * kAChunk + exclusive scan of R[w][*], also
+// published bucket-major as segoff[b][w] for the fine partition.
+__device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks, const u32* __restrict__ R,
+                                           u32* __restrict__ segoff, u32* cur, u32* dcnt) {
+  const u32 base = chunk_base(w, gridDim.x, nchunks) * (u32)kAChunk;
+  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return R[w * g.nb + b]; },
+                       [&](u32 b, u32 excl) {
+                         cur[b] = base + excl;
+                         segoff[b * gridDim.x + w] = base + excl;  // bucket-major: bin_fpart reads a row
+                         dcnt[b] = 0;
+                       });
+}
+
+// Workgroup 0 of bin_part: the fine-partition items -- bucket b gets max(1, ceil(T[b] / kFItem))
+// of them ({b, j}: its records [j * kFItem, (j + 1) * kFItem) in segment order).
+__device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
+                                           BinCtl* bc) {
+  const u32 tot = block_scan<kATPB, 1>(
+      g.nb, [&](u32 b) { return max(1u, (T[b] + kFItem - 1) / kFItem); },
+      [&](u32 b, u32 excl) {
+        const u32 J = max(1u, (T[b] + kFItem - 1) / kFItem);
+        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
+      });
+  if (threadIdx.x == 0) bc->nfitems = tot;
+}
+
+__device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
+                                            u32* __restrict__ seglen, u32 emitted, BinCtl* bc) {
+  for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[b * gridDim.x + w] = cur[b] - segoff[b * gridDim.x + w];
+  if (threadIdx.x == 0 && emitted) atomicAdd(&bc->m, emitted);
+}
+
+// Plain front end: every valid record is appended as it is. HOT: the push's hot elements (hot_tags,
+// bin_hot_pick) are summed in LDS over all of the workgroup's chunks and added to the shard at the
+// end, as the dedup front end does; only the cold records are appended. Once the hot elements are off,
+// a Zipf-like tail has almost no duplicates left inside a chunk (cfg3: the chunk dedup would merge
+// 0.6 % of the cold records), so the hash table is not worth its time there.
+template <typename V, bool MAT, bool HOT>
+__global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
+                                                         const V* __restrict__ vals, i64 n, PartDesc part,
+                                                         const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
+                                                         const u32* __restrict__ R, u32* __restrict__ segoff,
+                                                         u32* __restrict__ seglen, u32* __restrict__ addr_out,
+                                                         typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
+                                                         BinCtl* bc, const u32* __restrict__ T,
+                                                         uint2* __restrict__ fitems, const u32* __restrict__ hot_tags,
+                                                         V* __restrict__ data) {
+  typedef typename LdsAcc<V>::T A;
+  __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
+  __shared__ u32 st_a[kAChunk];
+  __shared__ A st_v[kAChunk];
+  constexpr int kHS = HOT ? kHotSlots : 1;
+  __shared__ u32 htag[kHS];
+  __shared__ A hacc[kHS];
+  const int tid = threadIdx.x;
+  const u32 w = blockIdx.x;
+  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
+  const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
+  if constexpr (HOT) {
+    for (int sl = tid; sl < kHotSlots; sl += kATPB) {
+      htag[sl] = hot_tags[sl];
+      hacc[sl] = hot_zero<A>();
+    }
+  }
+  PhaseClock ph(0);
+  if (w == 0) part_items(g, T, fitems, bc);
+  part_setup(g, w, nchunks, R, segoff, cur, dcnt);
+  ph.mark(0);
+  const i64 G = gridDim.x;
+  const u32 wbase = chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
+  const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
+  const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
+  BadRecs bad;
+  u32 emitted = 0;
+  // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
+  // compiler can wait for one chunk's loads while the next chunk's stay in flight
+  auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
+    const i64 cc = min(c, nchunks - 1);
+    load_recs<V, MAT>(keys, cols, vals, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+  };
+  auto step = [&](i64 c, RecRegs<V, MAT>& r) {
+    const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
+    u32 ad[kAPer];
+    A va[kAPer];
+    u32 valid = 0;
+#pragma unroll
+    for (int q = 0; q < kAPer; ++q) {
+      const i64 i = c0 + q * kATPB + tid;
+      i64 a64;
+      ad[q] = 0;
+      va[q] = (A)r.v[q];
+      if (i < c1) {
+        if (rec_addr<MAT>(part, r.k[q], r.cl[q], a64)) {
+          ad[q] = (u32)a64;
+          valid |= 1u << q;
+        } else {
+          bad.add(i);
+        }
+      }
+    }
+    if constexpr (HOT) {
+#pragma unroll
+      for (int q = 0; q < kAPer; ++q) {
+        const u32 hs = hot_slot(ad[q]);
+        if ((valid & (1u << q)) && htag[hs] == ad[q]) {  // hot: summed over all of this workgroup's chunks
+          lds_add(&hacc[hs], va[q]);
+          valid &= ~(1u << q);
+        }
+      }
+    }
+    ph.mark(1);
+    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 3);
+    // two chunks ahead, into the registers just consumed: in flight across the next chunk's work
+    load_chunk(c + 2 * G, r);
+    ph.mark(2);
+  };
+  RecRegs<V, MAT> ra, rb;
+  i64 c = w;
+  if (c < nchunks) {
+    load_chunk(c, ra);
+    load_chunk(c + G, rb);
+    for (; c < nchunks; c += 2 * G) {
+      step(c, ra);
+      step(c + G, rb);  // past the end: no valid record, nothing stored
+    }
+  }
+  part_finish(g, w, segoff, cur, seglen, emitted, bc);
+  if (tid == 0 && emitted) atomicAdd(&bc->cold, emitted);  // cold records: all of them were appended
+  bad.report(err);
+  if constexpr (HOT) {
+    __syncthreads();  // every chunk's hot sums are in
+    for (int sl = tid; sl < kHotSlots; sl += kATPB) {
+      const u32 a = htag[sl];
+      if (a != kEmptySlot && !hot_untouched<A>(hacc[sl])) hot_flush(data + a, hacc[sl]);
+    }
+  }
+  ph.flush(8);
+}
+
 // Dedup front end for duplicate-heavy tails: per chunk, equal elements are summed in an LDS hash
 // table first, so one record per distinct element of the chunk moves on. The staging buffer of the
 // append overlays the table's value array. Records of the push's hot elements (hot_tags) are summed
@@ -650,7 +698,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
   const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
   BadRecs bad;
-  u32 emitted = 0;
+  u32 emitted = 0, ncold = 0;
   // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
   // compiler can wait for one chunk's loads while the next chunk's stay in flight
   auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
@@ -661,9 +709,9 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
       for (int q = 0; q < kAPer; ++q) {
         const i64 i = c0 + q * kATPB + threadIdx.x;
         const i64 ii = i < c1 ? i : c1 - 1;
-        r.k[q] = (i64)(u64)reinterpret_cast<const u32*>(keys)[2 * ii];
-        r.cl[q] = MAT ? cols[ii] : 0;
-        r.v[q] = vals[ii];
+        r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
+        r.cl[q] = MAT ? ld_in(cols + ii) : 0;
+        r.v[q] = ld_in(vals + ii);
       }
     } else {
       load_recs<V, MAT>(keys, cols, vals, c0, c1, r);
@@ -697,6 +745,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
         cold &= ~(1u << q);
       }
     }
+    ncold += (u32)__popc(cold);
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       bool claimed = false;
@@ -769,6 +818,10 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
   bad.report(err);
+  {  // records that entered the hash table (valid, not hot): the host's measure of what chunk dedup merges
+    const u32 tot = block_sum<kATPB>(ncold);
+    if (tid == 0 && tot) atomicAdd(&bc->cold, tot);
+  }
   __syncthreads();  // every chunk's hot sums are in
   for (int sl = tid; sl < kHotSlots; sl += kATPB) {
     const u32 a = htag[sl];
@@ -794,7 +847,7 @@ __device__ __forceinline__ void fetch_addr(u32 t0, u32 v1, u32& s, const u32* se
 #pragma unroll
   for (int q = 0; q < kFPer; ++q) {
     const u32 v = t0 + q * TPB + threadIdx.x;
-    const u32 x = addr_in[seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst)];
+    const u32 x = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
     a[q] = v < v1 ? x : kEmptySlot;
   }
 }
@@ -881,7 +934,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
   __shared__ A st_v[(TPB * kFPer)];
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0 && hint)  // for the host's next binned push: how much did dedup keep?
+  {
     __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hint + 1, (u64)bc->cold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const u32 nit = bc->nfitems;
   PhaseClock ph(20);
   // items are taken from a queue (one returning atomic per item, fetched one item ahead): the grid
@@ -943,8 +999,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
       for (int q = 0; q < kFPer; ++q) {
         const u32 v = t0 + q * TPB + tid;
         const u32 r = seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst);
-        const u32 x = addr_in[r];
-        nv[q] = val_in[r];
+        const u32 x = ld_in(addr_in + r);
+        nv[q] = ld_in(val_in + r);
         na[q] = v < v1 ? x : kEmptySlot;
       }
     };
@@ -1024,8 +1080,8 @@ __device__ __forceinline__ void apply_fetch(const uint4& d, const u32* __restric
     ad[q] = kEmptySlot;
     v[q] = A(0);
     if (d.w != kItemEmpty && d.z > d.y) {
-      ad[q] = addr[jj];
-      v[q] = val[jj];
+      ad[q] = ld_in(addr + jj);
+      v[q] = ld_in(val + jj);
       if (j >= d.z) ad[q] = kEmptySlot;
     }
   }
@@ -1252,21 +1308,35 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const i64 n = a.n;
   if (n >= ((i64)1 << 32) - 2 * kAChunk || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
   const BinGeom g = bin_geometry(s->elems);
-  // front end: dedup when the last probe kept < 60 % of the records (the device reports m and the
-  // tail size of each push through a host-mapped word, taken at the shard's last sync point, so the
-  // choice does not depend on timing); re-probe every 16 pushes. GLINT_BIN_FRONT = dedup | prep
-  // forces one (tests, tuning).
+  // Front end, from what the last dedup push measured (the device reports m, the tail size and the
+  // cold records of each push through host-mapped words, taken at the shard's last sync point, so the
+  // choice does not depend on timing): chunk dedup when it kept < 80 % of the cold records it saw;
+  // otherwise the plain front end, with the hot-element split when the hot elements took >= 25 % of
+  // the tail (cfg3 ~65 %; cfg5's ~10 % does not pay for the sampling launch and the per-record check).
+  // A dedup push re-measures every 16 pushes (and the first one).
+  // GLINT_BIN_FRONT = dedup | hot | prep forces one (tests, tuning).
+  static const bool hot_on = [] {  // GLINT_BIN_HOT=0: no hot-element split (A/B, tests)
+    const char* e = getenv("GLINT_BIN_HOT");
+    return !(e && atoi(e) == 0);
+  }();
   {
     const u64 w = s->hint_bin;
     const u32 m = (u32)(w >> 32), tail = (u32)w;
-    if (tail > 0 && s->hint_bin_dedup) s->bin_dedup_ratio = (double)m / (double)tail;
+    const u32 cold = (u32)s->hint_bin_cold;
+    if (tail > 0 && s->hint_bin_front == 2) {
+      s->bin_chunk_ratio = cold ? (double)m / (double)cold : 1.0;
+      s->bin_hot_frac = 1.0 - (double)cold / (double)tail;
+    }
   }
-  bool dedup = s->bin_dedup_ratio < 0.6 || (++s->bin_pushes & 15) == 0;
+  const bool probe = (s->bin_pushes++ & 15) == 0;
+  int front = probe || s->bin_chunk_ratio < 0.8 ? 2 : (hot_on && s->bin_hot_frac >= 0.25 ? 1 : 0);
   if (const char* e = getenv("GLINT_BIN_FRONT")) {
-    if (!strcmp(e, "dedup")) dedup = true;
-    else if (!strcmp(e, "prep")) dedup = false;
+    if (!strcmp(e, "dedup")) front = 2;
+    else if (!strcmp(e, "hot")) front = hot_on ? 1 : 0;
+    else if (!strcmp(e, "prep")) front = 0;
   }
-  s->bin_last_dedup = dedup;
+  const bool dedup = front == 2;
+  s->bin_last_front = front;
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
@@ -1314,11 +1384,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
-  static const bool hot_on = [] {  // GLINT_BIN_HOT=0: no hot-element split (A/B, tests)
-    const char* e = getenv("GLINT_BIN_HOT");
-    return !(e && atoi(e) == 0);
-  }();
-  if (dedup && hot_on) {
+  if ((dedup && hot_on) || front == 1) {
     static const u32 hot_min = [] {  // GLINT_BIN_HOT_MIN: sample count that makes an element hot (tuning)
       const char* e = getenv("GLINT_BIN_HOT_MIN");
       return (u32)(e && atoi(e) > 0 ? atoi(e) : 2);
@@ -1337,8 +1403,9 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
                               val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data);
   } else {
-    bin_part_kernel<V, MAT><<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff,
-                                                 seglen, addr_a, val_a, a.err, bc, T, fitems);
+    auto kern = front == 1 ? bin_part_kernel<V, MAT, true> : bin_part_kernel<V, MAT, false>;
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
+                              val_a, a.err, bc, T, fitems, hot_tags, a.data);
   }
   HIPCHK(hipGetLastError());
   static const int fcount_rpc = resident_per_cu(bin_fcount_kernel, kFCTPB, "GLINT_FCOUNT_BPC");

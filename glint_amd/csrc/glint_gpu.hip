@@ -780,7 +780,8 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   }
   if (hipHostMalloc((void**)&s->h_hint, 64, hipHostMallocMapped) == hipSuccess) {
     s->h_hint[0] = 0;  // unordered-tail size of the last push (push_apply)
-    s->h_hint[1] = 0;  // (m << 32 | tail) of the last binned push (bin_bitems)
+    s->h_hint[1] = 0;  // (m << 32 | tail) of the last binned push (bin_fpart)
+    s->h_hint[2] = 0;  // cold records of the last binned push (bin_fpart)
     if (hipHostGetDevicePointer((void**)&s->d_hint, s->h_hint, 0) != hipSuccess) s->d_hint = nullptr;
   } else {
     s->h_hint = nullptr;

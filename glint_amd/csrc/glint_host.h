@@ -41,9 +41,14 @@ struct glint_shard {
   hipEvent_t det_ev[2] = {nullptr, nullptr};
   void* d_bin = nullptr;  // binned-push scratch
   size_t bin_bytes = 0;
-  double bin_dedup_ratio = 0.0;  // distinct/records of the last deduplicating binned push
+  // binned front end (glint_bin.hip push_binned): 0 plain, 1 plain + hot-element split, 2 chunk dedup
+  // (+ hot split). What the last dedup push measured decides: chunk_ratio = records it kept of the cold
+  // records that entered its hash table (1.0 = dedup merged nothing), hot_frac = share of the tail
+  // taken by the hot elements. A dedup push re-measures every 16 pushes.
+  double bin_chunk_ratio = 0.0;
+  double bin_hot_frac = 0.0;
   uint32_t bin_pushes = 0;
-  bool bin_last_dedup = false;   // whether the last binned push ran the dedup front end
+  int bin_last_front = 0;        // the front end of the last binned push
   // pinned host staging for host-pointer calls (grow-only, <= pinned_stage_max()): the caller's
   // arrays are memcpy'd in and cross PCIe in one DMA; pull answers come back the same way
   void* h_stage = nullptr;
@@ -103,7 +108,8 @@ struct glint_shard {
   // syncs takes the same path every run
   u64 hint_tail = 0;  // h_hint[0]
   u64 hint_bin = 0;   // h_hint[1]
-  bool hint_bin_dedup = false;  // whether the binned push that wrote hint_bin ran the dedup front end
+  u64 hint_bin_cold = 0;  // h_hint[2]
+  int hint_bin_front = -1;  // the front end of the binned push that wrote hint_bin (-1: none yet)
   i64 last_bad = -1;
   // ordering of host-pointer calls (private stream) after device-resident calls (caller's stream):
   // the last stream a *_dev call used; a host call records an event there and waits on it
@@ -264,7 +270,8 @@ inline void latch_hints(glint_shard* s) {
   if (!s->h_hint) return;
   s->hint_tail = __atomic_load_n(s->h_hint, __ATOMIC_ACQUIRE);
   s->hint_bin = __atomic_load_n(s->h_hint + 1, __ATOMIC_ACQUIRE);
-  s->hint_bin_dedup = s->bin_last_dedup;  // the stream has drained: the hint is the last binned push's
+  s->hint_bin_cold = __atomic_load_n(s->h_hint + 2, __ATOMIC_ACQUIRE);
+  s->hint_bin_front = s->bin_last_front;  // the stream has drained: the hint is the last binned push's
 }
 
 // The error state a launch of this call records into: a host-pointer call's own, or the one

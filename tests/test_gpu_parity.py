@@ -606,12 +606,12 @@ def test_binned_dedup_policy(gpu):
             np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
-@pytest.mark.parametrize("front", ["dedup", "prep"])
+@pytest.mark.parametrize("front", ["dedup", "hot", "prep"])
 @pytest.mark.parametrize("dtype", ["double", "float", "long"])
 @pytest.mark.parametrize("pattern", ["zipf", "hot_slab", "uniform", "with_prefix", "one_key", "unique"])
 def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
-    """Both front ends of the binned tail (GLINT_BIN_FRONT: per-chunk LDS dedup, plain address
-    prepare) against the oracle, on skewed and flat tails; Long is bit-exact, and so is Float when
+    """Every front end of the binned tail (GLINT_BIN_FRONT: per-chunk LDS dedup, plain with the
+    hot-element split, plain address prepare) against the oracle, on skewed and flat tails; Long is bit-exact, and so is Float when
     every key occurs once per push (its LDS partial sums are double, LdsAcc in glint_device.h).
     Float sums over duplicates are checked against the exact (float64) sum within 1e-6 of the sum
     of magnitudes per element -- the reference's sequential float order is one rounding of many."""
@@ -663,7 +663,7 @@ def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
         assert ei.value.record == 777
 
 
-@pytest.mark.parametrize("front", ["dedup", "prep"])
+@pytest.mark.parametrize("front", ["dedup", "hot", "prep"])
 def test_binned_fronts_matrix(gpu, monkeypatch, front):
     monkeypatch.setenv("GLINT_BIN_FRONT", front)
     rng = np.random.default_rng(23)
