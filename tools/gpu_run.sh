@@ -8,7 +8,7 @@
 #   binned    rocprofv3 kernel stats of the binned patterns (zipf, matrix, exchange)
 #   bintests  the GPU tests of the binned path, the full-size cases, cfg4 and the exchange
 #   ab        bench zipf / matrix / exchange with a previous library (AB_LIB) and the current one
-#   abn       the same over several libraries (LIBS="tag=path ..."; tools/variant.py builds variants)
+#   abn       the same over several libraries (LIBS="tag=path[,VAR=VALUE...] ..."; tools/variant.py builds variants)
 #   dettests  the deterministic / message-order / full-size GPU tests
 #   det       tools/det_probe.py (cfg3 deterministic push), timed and under rocprofv3 kernel stats
 #   micro     tools/microbench_stream mode 6: the dense sweep at 2^26..2^30, chunked and shifted
@@ -93,8 +93,11 @@ for s in ${STAGES:-tests bench}; do
     abn)  # LIBS="tag=path ...": each binned pattern on each library, ROUNDS rounds interleaved (one box)
       for r in $(seq ${ROUNDS:-2}); do
         for pat in ${PATTERNS:-zipf matrix exchange}; do
-          for lv in $LIBS; do
-            step ab_${lv%%=*}_${pat}_$r 300 env GLINT_GPU_LIB=${lv#*=} python3 bench.py --no-cpu-baseline --no-north-star --pattern $pat
+          for lv in $LIBS; do  # tag=path[,VAR=VALUE...]
+            spec=${lv#*=}
+            extra=""
+            case $spec in *,*) extra=$(echo ${spec#*,} | tr ',' ' ') ;; esac
+            step ab_${lv%%=*}_${pat}_$r 300 env GLINT_GPU_LIB=${spec%%,*} $extra python3 bench.py --no-cpu-baseline --no-north-star --pattern $pat
           done
         done
       done
