@@ -270,8 +270,188 @@ static int readable_now(int fd) {
   return avail > 0;
 }
 
+/* --replies async (the GPU backend's default): a connection's receive loop never waits for the GPU.
+ * It enqueues every push and pull on the shard and hands each reply, in request order, to the
+ * connection's reply thread; that thread takes whatever has queued up, waits ONCE for the highest
+ * ticket among it (tickets complete in order), then writes the replies with one send. The actor
+ * equivalent answers from a completion callback (pipeTo) instead of blocking its mailbox on a
+ * FlushPulls wait, so the mailbox keeps feeding the GPU while earlier messages are in flight.
+ * --replies burst keeps the previous server: one blocking wait per drained burst. */
+static int replies_async = 1;
+
+enum { R_FRAME, R_ACK, R_RESP, R_STOP };
+typedef struct {
+  int kind;
+  int32_t id;       /* R_ACK */
+  uint64_t ticket;  /* R_ACK (0: not a push of this connection), R_RESP */
+  uint8_t* buf;     /* R_FRAME / R_RESP payload (owned) */
+  uint32_t len;
+} rentry;
+typedef struct {
+  server* s;
+  int fd;
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  rentry* q;
+  size_t n, cap;
+} rqueue;
+
+static void rq_put(rqueue* r, rentry e) {
+  pthread_mutex_lock(&r->mu);
+  if (r->n == r->cap) {
+    r->cap = r->cap ? 2 * r->cap : 256;
+    r->q = (rentry*)realloc(r->q, r->cap * sizeof(rentry));
+    if (!r->q) die("realloc");
+  }
+  r->q[r->n++] = e;
+  pthread_cond_signal(&r->cv);
+  pthread_mutex_unlock(&r->mu);
+}
+static void rq_frame_logic(rqueue* r, uint8_t type, int32_t id) {
+  rentry e = {R_FRAME, 0, 0, (uint8_t*)malloc(5), 5};
+  e.buf[0] = type;
+  memcpy(e.buf + 1, &id, 4);
+  rq_put(r, e);
+}
+
+static void* reply_main(void* p) {
+  rqueue* r = (rqueue*)p;
+  server* s = r->s;
+  obuf out = {0};
+  rentry* batch = NULL;
+  size_t bcap = 0;
+  for (int stop = 0; !stop;) {
+    pthread_mutex_lock(&r->mu);
+    while (r->n == 0) pthread_cond_wait(&r->cv, &r->mu);
+    /* swap the queue out: the receive loop keeps appending to the (empty) other array */
+    rentry* q = r->q;
+    const size_t n = r->n, qcap = r->cap;
+    r->q = batch;
+    r->cap = bcap;
+    r->n = 0;
+    pthread_mutex_unlock(&r->mu);
+    batch = q;
+    bcap = qcap;
+    uint64_t tmax = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (batch[i].ticket > tmax) tmax = batch[i].ticket;
+    const int rc = tmax ? s->b.g_wait(s->b.shard, tmax, NULL) : 0;
+    pthread_mutex_lock(&s->mu);
+    if (rc != 0) s->errors++;
+    for (size_t i = 0; i < n; ++i) {
+      rentry* e = &batch[i];
+      if (e->kind == R_FRAME || e->kind == R_RESP) {
+        ob_frame(&out, e->buf, e->len);
+        free(e->buf);
+      } else if (e->kind == R_ACK) {
+        if (e->ticket && rc == 0) receipt_set(s, e->id, 1); /* updateFinished(id), once the push ran */
+        ob_logic(&out, receipt_has(s, e->id) ? L_ACK : L_NACK, e->id);
+      } else {
+        stop = 1;
+      }
+    }
+    pthread_mutex_unlock(&s->mu);
+    ob_flush(&out, r->fd);
+  }
+  free(out.p);
+  free(batch);
+  return NULL;
+}
+
+static void* conn_main_async(conn_arg* a) {
+  server* s = a->s;
+  const int fd = a->fd;
+  rqueue r;
+  memset(&r, 0, sizeof(r));
+  r.s = s;
+  r.fd = fd;
+  pthread_mutex_init(&r.mu, NULL);
+  pthread_cond_init(&r.cv, NULL);
+  pthread_t th;
+  if (pthread_create(&th, NULL, reply_main, &r)) die("pthread_create");
+  uint8_t* buf = NULL;
+  size_t cap = 0;
+  struct { int32_t id; uint64_t ticket; }* pend = NULL; /* this connection's pushes, not acked yet */
+  size_t npend = 0, pcap = 0;
+  for (;;) {
+    const uint32_t len = recv_frame(fd, &buf, &cap);
+    if (len == 0) break;
+    const uint8_t t = buf[0];
+    int32_t id = 0;
+    if (len >= 5 && t >= L_GET_UID && t <= L_FORGET) memcpy(&id, buf + 1, 4);
+    if (t == W_PUSH_VEC_D || t == W_PUSH_VEC_L) {
+      int32_t mid = 0;
+      uint64_t ticket = 0;
+      if (s->b.g_push_async(s->b.shard, buf, len, &mid, 0, &ticket) != 0) {
+        pthread_mutex_lock(&s->mu);
+        s->errors++;
+        pthread_mutex_unlock(&s->mu);
+        continue; /* rejected: never updateFinished, the ack becomes a NotAcknowledgeReceipt */
+      }
+      if (npend == pcap) {
+        pcap = pcap ? 2 * pcap : 64;
+        pend = realloc(pend, pcap * sizeof(*pend));
+        if (!pend) die("realloc");
+      }
+      pend[npend].id = mid;
+      pend[npend].ticket = ticket;
+      ++npend;
+    } else if (t == W_PULL_VECTOR) {
+      int32_t n;
+      memcpy(&n, buf + 1, 4);
+      const size_t need = 5 + (size_t)n * 8;
+      rentry e = {R_RESP, 0, 0, (uint8_t*)malloc(need), 0};
+      size_t olen = 0;
+      if (s->b.g_pull_async(s->b.shard, buf, len, e.buf, need, &olen, &e.ticket) != 0) {
+        pthread_mutex_lock(&s->mu);
+        s->errors++;
+        pthread_mutex_unlock(&s->mu);
+      }
+      e.len = (uint32_t)olen;
+      rq_put(&r, e);
+    } else if (t == L_GET_UID) {
+      pthread_mutex_lock(&s->mu);
+      const int32_t u = ++s->uid; /* sender ! UniqueID(nextId()) */
+      pthread_mutex_unlock(&s->mu);
+      rq_frame_logic(&r, L_UID, u);
+    } else if (t == L_ACK) {
+      rentry e = {R_ACK, id, 0, NULL, 0};
+      for (size_t i = 0; i < npend; ++i)
+        if (pend[i].id == id) {
+          e.ticket = pend[i].ticket;
+          pend[i] = pend[--npend];
+          break;
+        }
+      rq_put(&r, e);
+    } else if (t == L_FORGET) {
+      pthread_mutex_lock(&s->mu);
+      if (receipt_has(s, id)) receipt_set(s, id, 0);
+      pthread_mutex_unlock(&s->mu);
+      rq_frame_logic(&r, L_FORGET, id);
+    } else if (t == L_STOP) {
+      break;
+    } else {
+      pthread_mutex_lock(&s->mu);
+      s->errors++;
+      pthread_mutex_unlock(&s->mu);
+    }
+  }
+  rentry stop = {R_STOP, 0, 0, NULL, 0};
+  rq_put(&r, stop);
+  pthread_join(th, NULL);
+  close(fd);
+  free(buf);
+  free(pend);
+  free(r.q);
+  pthread_mutex_destroy(&r.mu);
+  pthread_cond_destroy(&r.cv);
+  free(a);
+  return NULL;
+}
+
 static void* conn_main(void* p) {
   conn_arg* a = (conn_arg*)p;
+  if (use_gpu && replies_async) return conn_main_async(a);
   server* s = a->s;
   const int fd = a->fd;
   uint8_t* buf = NULL;
@@ -723,10 +903,11 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--dtype") && i + 1 < argc) dtype_long = !strcmp(argv[++i], "long");
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) gpu_device = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--bucket") && i + 1 < argc) bucket_device = !strcmp(argv[++i], "device");
+    else if (!strcmp(argv[i], "--replies") && i + 1 < argc) replies_async = !strcmp(argv[++i], "async");
     else {
       fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--clients C] [--keys N] "
                       "[--pattern dense|uniform] [--records R] [--msg M] [--window W] [--dtype double|long] "
-                      "[--device D] [--bucket groupby|device]\n", argv[0]);
+                      "[--device D] [--bucket groupby|device] [--replies async|burst]\n", argv[0]);
       return 2;
     }
   }
@@ -900,12 +1081,12 @@ int main(int argc, char** argv) {
          "\"keys\": %lld, \"records\": %lld, \"max_records_per_message\": %d, \"window\": %d, "
          "\"push_messages\": %lld, \"pull_messages\": %lld, \"resends\": %lld, \"push_s\": %.6f, \"pull_s\": %.6f, "
          "\"push_records_per_s\": %.1f, \"pull_records_per_s\": %.1f, \"push_payload_MBps\": %.2f, "
-         "\"pull_payload_MBps\": %.2f, \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
+         "\"pull_payload_MBps\": %.2f, \"replies\": \"%s\", \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
          "\"bucket_s_max\": [%.6f, %.6f], \"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
          kind, pattern, dtype_long ? "long" : "double", S, C, (long long)N, (long long)total, M, W,
          (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl, (double)total / tp, (double)total / tl,
          16.0 * (double)total / tp / 1e6, 16.0 * (double)total / tl / 1e6,
-         bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
+         !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
          dtype_long ? 0.0 : ((double*)cv[0])[0], (!dtype_long && cn[0] > 1) ? ((double*)cv[0])[1] : 0.0,
          (!dtype_long && cn[0] > 2) ? ((double*)cv[0])[2] : 0.0, ok ? "true" : "false");
   return ok ? 0 : 1;
