@@ -699,18 +699,20 @@ def test_loopback_harness_gpu_backend(gpu):
      "--dtype", "long"],
     ["--clients", "16", "--servers", "4", "--keys", str(1 << 20), "--pattern", "uniform", "--records", "65536"],
 ])
-def test_loopback_concurrent_clients_gpu_backend(gpu, args):
+@pytest.mark.parametrize("replies", ["async", "burst"])
+def test_loopback_concurrent_clients_gpu_backend(gpu, args, replies):
     """configs[3]'s shape (64 concurrent loopback clients, 8 range-sharded servers -- here all on one
-    GPU) with HBM shards: pushes enqueued through the pinned ring and acknowledged after one wait per
-    burst; Long sums bit-exact, dense ranges bit-exact."""
+    GPU) with HBM shards: pushes enqueued through the pinned ring and acknowledged once applied, the
+    replies written by each connection's reply thread (async) or after one wait per drained burst;
+    Long sums bit-exact, dense ranges bit-exact."""
     import json
     import subprocess
     from glint_amd.build import LIB, LOOPBACK_BIN
-    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--device", str(gpu)] + args,
-                       capture_output=True, text=True, timeout=300)
+    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--device", str(gpu),
+                        "--replies", replies] + args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
-    assert d["check"] is True and d["resends"] == 0
+    assert d["check"] is True and d["resends"] == 0 and d["replies"] == replies
 
 
 def test_loopback_client_bucketing_offloaded(gpu):

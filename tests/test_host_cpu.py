@@ -163,3 +163,19 @@ def test_loopback_concurrent_clients_cpu_backend(args):
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
     assert d["check"] is True and d["resends"] == 0
+
+
+@pytest.mark.parametrize("args", [[], ["--clients", "8", "--servers", "3", "--keys", "100003", "--pattern", "uniform",
+                                       "--records", "20000", "--dtype", "long"]])
+def test_loopback_harness_oracle_backend(args):
+    """The loopback harness (tools/loopback/glint_loopback.c) with the oracle's CPU loop as the server
+    backend: the message flow, PushLogic's exactly-once protocol and the harness's own checks run on
+    the CPU (the GPU backend is exercised by the -m gpu tests)."""
+    import json
+    import subprocess
+    from glint_amd.build import LOOPBACK_BIN, ORACLE_LIB
+    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "oracle", "--lib", str(ORACLE_LIB)] + args,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["check"] is True and d["resends"] == 0 and d["replies"] == "inline"
