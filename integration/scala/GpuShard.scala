@@ -62,8 +62,8 @@ object GpuShard {
   @native def pullFinishL(pending: Long, out: Array[Long]): Unit
   @native def pullFinishI(pending: Long, out: Array[Int]): Unit
 
-  /** Sent by an actor's reply thread to the actor when finishing a pull failed (see GpuShardActor). */
-  private[gpu] final case class ReplyFailed(e: Throwable)
+  /** Sent by an actor to itself behind a burst of Pull messages (see GpuShardActor). */
+  private[gpu] case object FlushPulls
 
   /** The shard of `partition` on GPU `device` (range or cyclic layout, as the partitioner chose). */
   def create(partition: Partition, dtype: Int, cols: Int, device: Int): Long = partition match {
@@ -95,30 +95,29 @@ object GpuShard {
   * (PushLogic.scala:44-49), and a Pull after the restart is answered from the zeroed shard.
   *
   * Pulls are pipelined the same way: a Pull enqueues its gather (pullAsync; it sees every push
-  * enqueued before it, as get() sees every update before it) and hands the answer to the actor's
-  * reply thread, which finishes the pulls in arrival order (pullFinish waits for the pull's ticket,
-  * and one wait covers every pull enqueued before it) and sends each Response to the sender captured
-  * when the Pull arrived. The mailbox never blocks on a pull: it keeps taking messages, and feeding
-  * the GPU, while earlier pulls are in flight -- the pipeTo pattern, as the loopback servers do it
-  * (tools/loopback/glint_loopback.c, --replies async). The reference answers each Pull in `receive`
-  * (PartialVectorDouble.scala:18); its asks are independent futures, so answering from another
-  * thread changes no ordering a client can observe. A failure while finishing a pull is sent back
-  * to the actor, which rethrows it (the reference's actor would have failed in `receive`); a restart
-  * first lets the reply thread answer what it holds (postStop), then frees the shard.
+  * enqueued before it, as get() sees every update before it) and its answer is held. The first held
+  * pull sends FlushPulls to the actor itself; that message queues behind everything already in the
+  * mailbox, so when it arrives the burst has been taken, and the held pulls are answered in arrival
+  * order after their waits (the first wait covers most of the burst). The reference answers each Pull
+  * in `receive` (PartialVectorDouble.scala:18); here a burst of Pulls costs one GPU round trip instead
+  * of one per message. A restart answers the held pulls first (postStop).
   */
 trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
   protected def shard: Long
   private val pending = mutable.HashMap.empty[Int, Long]  // push id -> ticket
-  // answers of enqueued pulls, run in arrival order off the actor's thread
-  private val replier = java.util.concurrent.Executors.newSingleThreadExecutor()
+  private val held = mutable.ArrayBuffer.empty[() => Unit]  // answers of enqueued pulls, in arrival order
 
-  /** Hands the answer of an enqueued pull to the reply thread (`answer` finishes it and replies to
-    * its sender). */
+  /** Holds the answer of an enqueued pull (`answer` finishes it and replies to its sender). */
   protected def hold(answer: () => Unit): Unit = {
-    val me = self
-    replier.execute(new Runnable {
-      def run(): Unit = try answer() catch { case e: Throwable => me ! GpuShard.ReplyFailed(e) }
-    })
+    held += answer
+    if (held.size == 1) self ! GpuShard.FlushPulls
+  }
+
+  /** Answers every held pull, in arrival order. */
+  protected def flushPulls(): Unit = {
+    val answers = held.toList
+    held.clear()
+    answers.foreach(_())
   }
 
   protected def enqueued(id: Int, ticket: Long): Unit = pending.put(id, ticket)
@@ -136,10 +135,7 @@ trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
   }
 
   override def postStop(): Unit = {
-    try {
-      replier.shutdown()
-      replier.awaitTermination(1, java.util.concurrent.TimeUnit.MINUTES)
-    } finally GpuShard.destroy(shard)
+    try flushPulls() finally GpuShard.destroy(shard)
   }
 }
 
@@ -158,7 +154,7 @@ class GpuPartialVectorDouble(partition: Partition) extends PartialVector[Double]
       val to = sender(); val out = new Array[Double](pull.keys.length)
       val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
       hold(() => { GpuShard.pullFinishD(p, out); to ! ResponseDouble(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorDouble => enqueued(push.id, GpuShard.vecPushD(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -178,7 +174,7 @@ class GpuPartialVectorFloat(partition: Partition) extends PartialVector[Float](p
       val to = sender(); val out = new Array[Float](pull.keys.length)
       val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
       hold(() => { GpuShard.pullFinishF(p, out); to ! ResponseFloat(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorFloat => enqueued(push.id, GpuShard.vecPushF(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -198,7 +194,7 @@ class GpuPartialVectorLong(partition: Partition) extends PartialVector[Long](par
       val to = sender(); val out = new Array[Long](pull.keys.length)
       val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
       hold(() => { GpuShard.pullFinishL(p, out); to ! ResponseLong(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorLong => enqueued(push.id, GpuShard.vecPushL(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -218,7 +214,7 @@ class GpuPartialVectorInt(partition: Partition) extends PartialVector[Int](parti
       val to = sender(); val out = new Array[Int](pull.keys.length)
       val p = GpuShard.pullAsync(shard, 0, pull.keys, null)
       hold(() => { GpuShard.pullFinishI(p, out); to ! ResponseInt(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushVectorInt => enqueued(push.id, GpuShard.vecPushI(shard, push.keys, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -249,7 +245,7 @@ class GpuPartialMatrixDouble(partition: Partition, cols: Int) extends PartialMat
       val to = sender(); val out = new Array[Double](pull.rows.length * cols)
       val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
       hold(() => { GpuShard.pullFinishD(p, out); to ! ResponseDouble(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixDouble => enqueued(push.id, GpuShard.matPushD(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -277,7 +273,7 @@ class GpuPartialMatrixFloat(partition: Partition, cols: Int) extends PartialMatr
       val to = sender(); val out = new Array[Float](pull.rows.length * cols)
       val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
       hold(() => { GpuShard.pullFinishF(p, out); to ! ResponseFloat(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixFloat => enqueued(push.id, GpuShard.matPushF(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -305,7 +301,7 @@ class GpuPartialMatrixLong(partition: Partition, cols: Int) extends PartialMatri
       val to = sender(); val out = new Array[Long](pull.rows.length * cols)
       val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
       hold(() => { GpuShard.pullFinishL(p, out); to ! ResponseLong(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixLong => enqueued(push.id, GpuShard.matPushL(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
@@ -333,7 +329,7 @@ class GpuPartialMatrixInt(partition: Partition, cols: Int) extends PartialMatrix
       val to = sender(); val out = new Array[Int](pull.rows.length * cols)
       val p = GpuShard.pullAsync(shard, 2, pull.rows, null)
       hold(() => { GpuShard.pullFinishI(p, out); to ! ResponseInt(out) })
-    case GpuShard.ReplyFailed(e) => throw e
+    case GpuShard.FlushPulls => flushPulls()
     case push: PushMatrixInt => enqueued(push.id, GpuShard.matPushI(shard, push.rows, push.cols, push.values, 0))
     case x => settle(x, updateFinished); handleLogic(x, sender)
   }
