@@ -142,16 +142,16 @@ for s in ${STAGES:-tests bench}; do
       i=0
       for args in "" "--window 1" "--keys 16777216 --msg 79999" "--clients 64 --servers 8 --keys 33554432" \
                   "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
-        for r in 1 2; do  # the GPU server both ways (replies from a reply thread / one wait per burst), twice
+        for r in 1 2; do  # the GPU server twice (one wait per drained burst; LB_ASYNC=1: also with reply threads)
           step lb_gpu_${i}_$r 200 $LB $G $args
-          step lb_gpuburst_${i}_$r 200 $LB $G $args --replies burst
+          [ -n "$LB_ASYNC" ] && step lb_gpuasync_${i}_$r 200 $LB $G $args --replies async
         done
         step lb_oracle_$i 200 $LB $O $args
         case "$args" in *--clients*) step lb_gpudev_$i 200 $LB $G $args --bucket device ;; esac
         i=$((i + 1))
       done
       cat $OUT/lb_gpu_*.log | grep '^{' > $OUT/loopback_gpu.jsonl || true
-      cat $OUT/lb_gpuburst_*.log | grep '^{' > $OUT/loopback_gpu_burst.jsonl || true
+      cat $OUT/lb_gpuasync_*.log 2>/dev/null | grep '^{' > $OUT/loopback_gpu_async.jsonl || true
       cat $OUT/lb_gpudev_*.log | grep '^{' > $OUT/loopback_gpu_bucket_device.jsonl || true
       cat $OUT/lb_oracle_*.log | grep '^{' > $OUT/loopback_oracle.jsonl || true
       ;;

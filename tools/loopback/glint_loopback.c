@@ -270,14 +270,16 @@ static int readable_now(int fd) {
   return avail > 0;
 }
 
-/* --replies async (the GPU backend's default): a connection's receive loop never waits for the GPU.
- * It enqueues every push and pull on the shard and hands each reply, in request order, to the
- * connection's reply thread; that thread takes whatever has queued up, waits ONCE for the highest
- * ticket among it (tickets complete in order), then writes the replies with one send. The actor
- * equivalent answers from a completion callback (pipeTo) instead of blocking its mailbox on a
- * FlushPulls wait, so the mailbox keeps feeding the GPU while earlier messages are in flight.
- * --replies burst keeps the previous server: one blocking wait per drained burst. */
-static int replies_async = 1;
+/* --replies async: a connection's receive loop never waits for the GPU. It enqueues every push and
+ * pull on the shard and hands each reply, in request order, to the connection's reply thread; that
+ * thread takes whatever has queued up, waits ONCE for the highest ticket among it (tickets complete
+ * in order), then writes the replies with one send (the actor equivalent: pipeTo from a completion
+ * thread). --replies burst (the default): one blocking wait per drained burst, then the replies.
+ * Measured on one box (profiles/r03/loopback_gpu_async.jsonl against loopback_gpu.jsonl): async loses
+ * everywhere there are many connections (cfg4b push 48 -> 23 M, pull 108 -> 24-30 M records/s): a
+ * reply thread per connection doubles the threads on the box's CPU share, and each waits on a
+ * smaller batch. Kept as an option for the comparison. */
+static int replies_async = 0;
 
 enum { R_FRAME, R_ACK, R_RESP, R_STOP };
 typedef struct {
