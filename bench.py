@@ -84,6 +84,26 @@ def pmc_traffic(workload_tag: str):
         return None, None
 
 
+def sparse_floor(workload_tag: str, ms_per_step: float):
+    """The practical floor of a binned line, REPLAYED from the newest committed
+    tools/microbench_sparse measurement (profiles/<round>/micro_sparse_floor.json): the time to stream
+    the records once plus read-modify-write each distinct element once in ascending order, as if
+    partitioning were free. frac = floor / ms_per_step; None for lines without one."""
+    case = {"zipf_2p28": "cfg3", "exchange_2p28": "cfg4b", "matrix_2p17x512": "cfg5"}.get(workload_tag)
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*" / "micro_sparse_floor.json")))
+    if not case or not files:
+        return None
+    try:
+        for d in json.loads(Path(files[-1]).read_text())["cases"]:
+            if d.get("case") == case:
+                return {"floor_ms": d["floor_ms"], "frac": round(d["floor_ms"] / ms_per_step, 4),
+                        "read_ms": d["read_ms"], "rmw_sorted_ms": d["rmw_sorted_ms"],
+                        "source": "replayed from " + str(Path(files[-1]).relative_to(ROOT))}
+    except Exception:
+        return None
+    return None
+
+
 def cpu_baseline(log2_keys: int, seconds: float):
     """The oracle's scalar PartialVector.update loop (one thread = one actor) on a bounded sample of
     the same dense workload, timed on this host."""
@@ -470,6 +490,9 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
                      "launches_timed": launches, "kernels_ms": shares},
         "check": ok,
     }
+    floor = sparse_floor(tag, dt / steps * 1e3)
+    if floor is not None:
+        line["practical_floor"] = floor
     shard.destroy()
     return line
 
