@@ -378,6 +378,8 @@ __device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
 }
 __device__ __forceinline__ u32 hot_slot(u32 a) { return hot_mix(a) & (kHotSlots - 1); }
 
+
+
 // One workgroup: kHotSample records (kHotRuns runs spread evenly over the tail) are counted per
 // element in LDS; every element seen at least min_count times (2: frequency >= ~2 / kHotSample of
 // the tail) competes for its direct-mapped slot, the most frequent one wins. Writes hot_tags[kHotSlots] (kEmptySlot = none).
@@ -542,9 +544,137 @@ __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* 
   if (threadIdx.x == 0 && emitted) atomicAdd(&bc->m, emitted);
 }
 
-// Plain front end: every valid record is appended as it is. HOT: the push's hot elements (hot_tags,
-// bin_hot_pick) are summed in LDS over all of the workgroup's chunks and added to the shard at the
-// end, as the dedup front end does; only the cold records are appended. Once the hot elements are off,
+// The plain + hot front end keeps a wider hot table (kWideSlots tags + sums fit the plain partition
+// kernel's LDS next to its staging). Its hot elements come from a sample 16x larger than
+// bin_hot_pick's, counted in a global hash table by many workgroups (bin_hot_sample) and picked per
+// slot by bin_hot_select; the partition workgroups' per-slot sums are stored (not added with atomics:
+// kWideSlots x G of them would cost more than the split saves) and bin_hot_reduce adds each hot
+// element's sum over the workgroups to the shard in workgroup order.
+constexpr int kWideSlots = 8192;
+constexpr int kWideHashBits = 20;           // global count table: 2^20 slots
+constexpr int kWideRunsPerWg = 8;           // sampled runs of kHotRun records per sampling workgroup
+constexpr int kWideSampleWgs = 256;         // 256 x 8 x 128 = 262 144 sampled records per push
+__device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
+
+// Each workgroup reads kWideRunsPerWg runs of kHotRun consecutive records (spread evenly over the
+// tail), counts them in LDS, then adds its (element, count) pairs to the global hash table.
+template <bool MAT>
+__global__ __launch_bounds__(256) void bin_hot_sample_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
+                                                             i64 n, PartDesc part, const LaunchCtl* lctl, u32 ntiles,
+                                                             int from_break, u32* __restrict__ gkey,
+                                                             u32* __restrict__ gcnt) {
+  constexpr int kLocal = 2048;  // LDS count table (1024 samples per workgroup: load <= 0.5)
+  __shared__ u32 lk[kLocal], lc[kLocal];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kLocal; i += 256) {
+    lk[i] = kEmptySlot;
+    lc[i] = 0;
+  }
+  __syncthreads();
+  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
+  const i64 m = n - r0;
+  const i64 runs = (i64)kWideSampleWgs * kWideRunsPerWg;
+  if (m > 0) {
+    const i64 stride = m >= runs * kHotRun ? m / runs : kHotRun;
+    constexpr int kPer = kWideRunsPerWg * kHotRun / 256;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int s = j * 256 + tid;  // sample s of this workgroup: run s / kHotRun, offset s % kHotRun
+      const i64 run = (i64)blockIdx.x * kWideRunsPerWg + s / kHotRun;
+      const i64 i = r0 + run * stride + s % kHotRun;
+      if (i >= n) continue;
+      i64 a64;
+      if (!rec_addr<MAT>(part, keys[i], MAT ? cols[i] : 0, a64)) continue;
+      const u32 a = (u32)a64;
+      u32 h = hot_mix(a * 0x9E3779B1u) & (kLocal - 1);
+      for (int probe = 0; probe < 64; ++probe) {
+        const u32 prev = atomicCAS(&lk[h], kEmptySlot, a);
+        if (prev == kEmptySlot || prev == a) {
+          atomicAdd(&lc[h], 1u);
+          break;
+        }
+        h = (h + 1) & (kLocal - 1);
+      }
+    }
+  }
+  __syncthreads();
+  constexpr u32 kMask = (1u << kWideHashBits) - 1u;
+  for (int i = tid; i < kLocal; i += 256) {
+    const u32 a = lk[i];
+    if (a == kEmptySlot) continue;
+    u32 h = hot_mix(a) & kMask;
+    for (int probe = 0; probe < 64; ++probe) {
+      const u32 prev = atomicCAS(&gkey[h], kEmptySlot, a);
+      if (prev == kEmptySlot || prev == a) {
+        atomicAdd(&gcnt[h], lc[i]);
+        break;
+      }
+      h = (h + 1) & kMask;
+    }
+  }
+}
+
+// Every counted element with >= min_count samples competes for its wide slot; the most sampled wins
+// (best[slot] = count << 32 | element; zeroed per push). The partition kernel reads the tags from it.
+__global__ __launch_bounds__(256) void bin_hot_select_kernel(const u32* __restrict__ gkey, const u32* __restrict__ gcnt,
+                                                             u32 min_count, unsigned long long* __restrict__ best) {
+  const u32 i = blockIdx.x * 256u + threadIdx.x;
+  const u32 a = gkey[i], c = gcnt[i];
+  if (a != kEmptySlot && c >= min_count) atomicMax(&best[wide_slot(a)], ((unsigned long long)c << 32) | a);
+}
+
+// Each hot element's sum over the partition workgroups (partial[w][slot]), added to the shard once: a
+// plain read-modify-write (the element's records all went to the hot sums, so no other kernel of the
+// push touches it). A workgroup of kRedTPB threads takes kRedSlots slots; its kRedGroups lane groups
+// each sum a contiguous range of workgroups (coalesced rows, loads issued back to back), then the
+// group sums are added in group order -- the result is the same on every run.
+constexpr int kRedSlots = 64, kRedTPB = 1024, kRedGroups = kRedTPB / kRedSlots;
+template <typename V>
+__global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned long long* __restrict__ best, u32 G,
+                                                                 const typename LdsAcc<V>::T* __restrict__ partial,
+                                                                 V* __restrict__ data) {
+  typedef typename LdsAcc<V>::T A;
+  __shared__ A gs[kRedGroups][kRedSlots];
+  __shared__ u32 gany[kRedGroups][kRedSlots];
+  const int tid = threadIdx.x, ls = tid % kRedSlots, grp = tid / kRedSlots;
+  const u32 sl = blockIdx.x * (u32)kRedSlots + (u32)ls;
+  const u32 per = (G + kRedGroups - 1) / kRedGroups;
+  const u32 w0 = grp * per, w1 = min(G, w0 + per);
+  A sum = hot_zero<A>();
+  u32 any = 0;
+  constexpr int kUnroll = 8;
+  for (u32 w = w0; w < w1; w += kUnroll) {
+    A x[kUnroll];
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) x[j] = partial[(size_t)min(w + (u32)j, w1 - 1u) * kWideSlots + sl];
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      if (w + (u32)j < w1 && !hot_untouched<A>(x[j])) {
+        sum = any ? vadd(sum, x[j]) : x[j];
+        any = 1;
+      }
+    }
+  }
+  gs[grp][ls] = sum;
+  gany[grp][ls] = any;
+  __syncthreads();
+  if (grp != 0) return;
+  const unsigned long long b = best[sl];
+  if (!b) return;
+  A tot = hot_zero<A>();
+  bool seen = false;
+  for (int q = 0; q < kRedGroups; ++q) {
+    if (!gany[q][ls]) continue;
+    tot = seen ? vadd(tot, gs[q][ls]) : gs[q][ls];
+    seen = true;
+  }
+  const u32 a = (u32)b;
+  if (seen) data[a] = acc_add(data[a], tot);
+}
+
+// Plain front end: every valid record is appended as it is. HOT: the push's hot elements (the wide
+// table, bin_hot_select) are summed in LDS over all of the workgroup's chunks and stored per
+// workgroup for bin_hot_reduce; only the cold records are appended. Once the hot elements are off,
 // a Zipf-like tail has almost no duplicates left inside a chunk (cfg3: the chunk dedup would merge
 // 0.6 % of the cold records), so the hash table is not worth its time there.
 template <typename V, bool MAT, bool HOT>
@@ -555,13 +685,14 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
                                                          u32* __restrict__ seglen, u32* __restrict__ addr_out,
                                                          typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
                                                          BinCtl* bc, const u32* __restrict__ T,
-                                                         uint2* __restrict__ fitems, const u32* __restrict__ hot_tags,
-                                                         V* __restrict__ data) {
+                                                         uint2* __restrict__ fitems,
+                                                         const unsigned long long* __restrict__ hot_best,
+                                                         typename LdsAcc<V>::T* __restrict__ hot_partial) {
   typedef typename LdsAcc<V>::T A;
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
   __shared__ u32 st_a[kAChunk];
   __shared__ A st_v[kAChunk];
-  constexpr int kHS = HOT ? kHotSlots : 1;
+  constexpr int kHS = HOT ? kWideSlots : 1;
   __shared__ u32 htag[kHS];
   __shared__ A hacc[kHS];
   const int tid = threadIdx.x;
@@ -569,8 +700,9 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
   if constexpr (HOT) {
-    for (int sl = tid; sl < kHotSlots; sl += kATPB) {
-      htag[sl] = hot_tags[sl];
+    for (int sl = tid; sl < kWideSlots; sl += kATPB) {
+      const unsigned long long b = hot_best[sl];
+      htag[sl] = b ? (u32)b : kEmptySlot;
       hacc[sl] = hot_zero<A>();
     }
   }
@@ -613,7 +745,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
     if constexpr (HOT) {
 #pragma unroll
       for (int q = 0; q < kAPer; ++q) {
-        const u32 hs = hot_slot(ad[q]);
+        const u32 hs = wide_slot(ad[q]);
         if ((valid & (1u << q)) && htag[hs] == ad[q]) {  // hot: summed over all of this workgroup's chunks
           lds_add(&hacc[hs], va[q]);
           valid &= ~(1u << q);
@@ -640,11 +772,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   if (tid == 0 && emitted) atomicAdd(&bc->cold, emitted);  // cold records: all of them were appended
   bad.report(err);
   if constexpr (HOT) {
-    __syncthreads();  // every chunk's hot sums are in
-    for (int sl = tid; sl < kHotSlots; sl += kATPB) {
-      const u32 a = htag[sl];
-      if (a != kEmptySlot && !hot_untouched<A>(hacc[sl])) hot_flush(data + a, hacc[sl]);
-    }
+    __syncthreads();  // every chunk's hot sums are in; bin_hot_reduce adds them up
+    for (int sl = tid; sl < kWideSlots; sl += kATPB) hot_partial[(size_t)w * kWideSlots + sl] = hacc[sl];
   }
   ph.flush(8);
 }
@@ -1357,7 +1486,12 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const size_t b_a = pad256(cap_a * 4), b_v = pad256(cap_a * sizeof(A));
   const size_t b_zero = b_ctl + b_T + 2 * b_H;
   const size_t b_hot = pad256((size_t)kHotSlots * 4);
-  const size_t need = b_zero + 3 * b_seg + b_cd + b_hot + 2 * (b_a + b_v);
+  // the wide hot table of the plain + hot front end: global count table (keys, counts), the picked
+  // elements per slot, the partition workgroups' per-slot sums
+  const size_t b_wk = front == 1 ? pad256(((size_t)4 << kWideHashBits)) : 0;
+  const size_t b_wbest = front == 1 ? pad256((size_t)kWideSlots * 8) : 0;
+  const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
+  const size_t need = b_zero + 3 * b_seg + b_cd + b_hot + 2 * b_wk + b_wbest + b_wpart + 2 * (b_a + b_v);
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   char* p = (char*)s->d_bin;
@@ -1376,6 +1510,11 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   p += b_cd;
   u32* hot_tags = (u32*)p;
   p += b_hot;
+  u32* wkey = (u32*)p;
+  u32* wcnt = (u32*)(p + b_wk);
+  unsigned long long* wbest = (unsigned long long*)(p + 2 * b_wk);
+  A* wpart = (A*)(p + 2 * b_wk + b_wbest);
+  p += 2 * b_wk + b_wbest + b_wpart;
   u32* addr_a = (u32*)p;
   A* val_a = (A*)(p + b_a);
   u32* addr_b = (u32*)(p + b_a + b_v);
@@ -1384,7 +1523,20 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
-  if ((dedup && hot_on) || front == 1) {
+  if (front == 1) {  // the wide hot table: sample, count, pick
+    static const u32 wide_min = [] {  // GLINT_BIN_WIDE_MIN: sample count that makes an element hot (tuning)
+      const char* e = getenv("GLINT_BIN_WIDE_MIN");
+      return (u32)(e && atoi(e) > 0 ? atoi(e) : 3);
+    }();
+    HIPCHK(hipMemsetAsync(wkey, 0xFF, b_wk, st));
+    HIPCHK(hipMemsetAsync(wcnt, 0, b_wk + b_wbest, st));  // counts and picks
+    bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
+                                                                wcnt);
+    HIPCHK(hipGetLastError());
+    bin_hot_select_kernel<<<(1u << kWideHashBits) / 256u, 256, 0, st>>>(wkey, wcnt, wide_min, wbest);
+    HIPCHK(hipGetLastError());
+  }
+  if (dedup && hot_on) {
     static const u32 hot_min = [] {  // GLINT_BIN_HOT_MIN: sample count that makes an element hot (tuning)
       const char* e = getenv("GLINT_BIN_HOT_MIN");
       return (u32)(e && atoi(e) > 0 ? atoi(e) : 2);
@@ -1405,9 +1557,13 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   } else {
     auto kern = front == 1 ? bin_part_kernel<V, MAT, true> : bin_part_kernel<V, MAT, false>;
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
-                              val_a, a.err, bc, T, fitems, hot_tags, a.data);
+                              val_a, a.err, bc, T, fitems, wbest, wpart);
   }
   HIPCHK(hipGetLastError());
+  if (front == 1) {
+    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
+    HIPCHK(hipGetLastError());
+  }
   static const int fcount_rpc = resident_per_cu(bin_fcount_kernel, kFCTPB, "GLINT_FCOUNT_BPC");
   const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
   bin_fcount_kernel<<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
