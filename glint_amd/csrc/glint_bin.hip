@@ -967,18 +967,21 @@ __device__ __forceinline__ u32 seg_addr(u32 v, u32& s, const u32* segpre, const 
   return segst[s] + (v - segpre[s]);
 }
 
-// the addresses of records [t0, t0 + TPB * kFPer) of a bucket (kEmptySlot past v1); s is the thread's
-// segment cursor (its records only move forward)
+// the addresses of records [t0, t0 + TPB * kFPer) of a bucket; returns which are valid (< v1) as a
+// mask (selecting on the loaded registers would make the compiler wait for the loads at once); s is
+// the thread's segment cursor (its records only move forward)
 // (clamped and branch-free: every lane issues kFPer loads; needs v1 > 0)
 template <int TPB>
-__device__ __forceinline__ void fetch_addr(u32 t0, u32 v1, u32& s, const u32* segpre, const u32* segst,
-                                           const u32* __restrict__ addr_in, u32 (&a)[kFPer]) {
+__device__ __forceinline__ u32 fetch_addr(u32 t0, u32 v1, u32& s, const u32* segpre, const u32* segst,
+                                          const u32* __restrict__ addr_in, u32 (&a)[kFPer]) {
+  u32 valid = 0;
 #pragma unroll
   for (int q = 0; q < kFPer; ++q) {
     const u32 v = t0 + q * TPB + threadIdx.x;
-    const u32 x = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
-    a[q] = v < v1 ? x : kEmptySlot;
+    a[q] = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
+    valid |= (v < v1 ? 1u : 0u) << q;
   }
+  return valid;
 }
 
 // bucket b's segment table into LDS; returns M_b
@@ -1013,16 +1016,17 @@ __global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, co
     const u32 M = load_segments<kFCTPB>(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
     u32 s = 0;
-    u32 a[kFPer];
-    if (v1 > v0) fetch_addr<kFCTPB>(v0, v1, s, segpre, segst, addr_in, a);
+    u32 a[kFPer], avalid = 0;
+    if (v1 > v0) avalid = fetch_addr<kFCTPB>(v0, v1, s, segpre, segst, addr_in, a);
     for (u32 t0 = v0; t0 < v1; t0 += kFCTPB * kFPer) {
       u32 cur[kFPer];
+      const u32 cvalid = avalid;
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) cur[q] = a[q];
-      fetch_addr<kFCTPB>(t0 + kFCTPB * kFPer, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
+      avalid = fetch_addr<kFCTPB>(t0 + kFCTPB * kFPer, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
 #pragma unroll
       for (int q = 0; q < kFPer; ++q)
-        if (cur[q] != kEmptySlot) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
+        if ((cvalid >> q) & 1u) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
     }
     __syncthreads();
     for (u32 f = tid; f < g.nf; f += kFCTPB) {
@@ -1121,16 +1125,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
     ph.mark(24);
     // pass 2: tiles moved to their slab ranges
     u32 s = 0;
-    u32 na[kFPer];
+    u32 na[kFPer], nvalid = 0;
     A nv[kFPer];
-    auto fetch = [&](u32 t0) {  // a tile's addresses and values (clamped, branch-free)
+    // a tile's addresses and values (clamped, branch-free); which are valid goes to a separate mask
+    // (selecting on a loaded register would make the compiler wait for the load at once)
+    auto fetch = [&](u32 t0) {
+      nvalid = 0;
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
         const u32 v = t0 + q * TPB + tid;
         const u32 r = seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst);
-        const u32 x = ld_in(addr_in + r);
+        na[q] = ld_in(addr_in + r);
         nv[q] = ld_in(val_in + r);
-        na[q] = v < v1 ? x : kEmptySlot;
+        nvalid |= (v < v1 ? 1u : 0u) << q;
       }
     };
     // the bucket's output range as buffer descriptors (counted stores)
@@ -1139,6 +1146,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
     for (u32 t0 = v0; t0 < v1; t0 += (TPB * kFPer)) {
       u32 a[kFPer], rank[kFPer];
       A val[kFPer];
+      const u32 valid = nvalid;
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
         a[q] = na[q];
@@ -1148,7 +1156,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
       ph.mark(25);
 #pragma unroll
       for (int q = 0; q < kFPer; ++q)
-        if (a[q] != kEmptySlot) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
+        if ((valid >> q) & 1u) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
       __syncthreads();
       ph.mark(26);
       const u32 total = block_scan<TPB, 4>(
@@ -1161,7 +1169,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
       ph.mark(27);
 #pragma unroll
       for (int q = 0; q < kFPer; ++q) {
-        if (a[q] != kEmptySlot) {
+        if ((valid >> q) & 1u) {
           const u32 p = tcnt[fine_of(a[q], g)] + rank[q];
           st_a[p] = a[q];
           st_v[p] = val[q];
