@@ -677,7 +677,7 @@ __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned 
 // workgroup for bin_hot_reduce; only the cold records are appended. Once the hot elements are off,
 // a Zipf-like tail has almost no duplicates left inside a chunk (cfg3: the chunk dedup would merge
 // 0.6 % of the cold records), so the hash table is not worth its time there.
-template <typename V, bool MAT, bool HOT>
+template <typename V, bool MAT, bool HOT, int KIND>
 __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                          const V* __restrict__ vals, i64 n, PartDesc part,
                                                          const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
@@ -720,7 +720,19 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   // compiler can wait for one chunk's loads while the next chunk's stay in flight
   auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 cc = min(c, nchunks - 1);
-    load_recs<V, MAT>(keys, cols, vals, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+    const i64 c0 = r0 + cc * kAChunk, c1 = min(n, r0 + (cc + 1) * kAChunk);
+    if constexpr (KIND == 0) {  // (key - start).toInt needs the low words only (as bin_count loads them)
+#pragma unroll
+      for (int q = 0; q < kAPer; ++q) {
+        const i64 i = c0 + q * kATPB + threadIdx.x;
+        const i64 ii = i < c1 ? i : c1 - 1;
+        r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
+        r.cl[q] = MAT ? ld_in(cols + ii) : 0;
+        r.v[q] = ld_in(vals + ii);
+      }
+    } else {
+      load_recs<V, MAT>(keys, cols, vals, c0, c1, r);
+    }
   };
   auto step = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
@@ -734,7 +746,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
       ad[q] = 0;
       va[q] = (A)r.v[q];
       if (i < c1) {
-        if (rec_addr<MAT>(part, r.k[q], r.cl[q], a64)) {
+        if (rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64)) {
           ad[q] = (u32)a64;
           valid |= 1u << q;
         } else {
@@ -1563,7 +1575,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
                               val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data);
   } else {
-    auto kern = front == 1 ? bin_part_kernel<V, MAT, true> : bin_part_kernel<V, MAT, false>;
+    auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
+                                 : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
                               val_a, a.err, bc, T, fitems, wbest, wpart);
   }
