@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 2^30 leg of the default 1-GPU run")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run shard check")
+    ap.add_argument("--parts-per-gpu", type=int, default=1,
+                    help="exchange only: range partitions hosted per GPU (modelsPerServer, Client.scala:63); "
+                         "8 at one GPU is cfg4's own key space, RangePartitioner(8, 2^31)")
     return ap.parse_args()
 
 
@@ -198,7 +201,8 @@ def segment_sums(v, counts, chunk: int = 1 << 22):
     return torch.cat(out) if out else v[:0]
 
 
-def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: int, check: bool) -> dict:
+def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: int, check: bool,
+             mps: int = 1) -> dict:
     """Builds the workload of one bench line, times `steps` pushes (or pulls) after `warmup`, checks
     the shard afterwards and returns the line's fields (without the CPU baseline)."""
     import numpy as np
@@ -215,12 +219,21 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     cols_n = 512
     if mat:
         partitioner = RangePartitioner.apply(world, world * (1 << 17))
+    elif exch:  # modelsPerServer partitions per rank (rank r hosts r, r + W, ...: Client.scala:71-85)
+        partitioner = RangePartitioner.apply(world * mps, world * mps * (1 << log2_keys))
     elif strong:  # total work fixed: one 2^k-key vector range-sharded over the ranks
         partitioner = RangePartitioner.apply(world, 1 << log2_keys)
     else:
         partitioner = RangePartitioner.apply(world, world * (1 << log2_keys))
-    part = partitioner.all()[rank]
-    shard = PartialMatrix(part, cols_n, "double", device=local) if mat else PartialVector(part, "double", device=local)
+    if exch:
+        from glint_amd.dist import Router
+        my_parts = [partitioner.all()[p] for p in Router(partitioner, world).rank_parts[rank]]
+    else:
+        my_parts = [partitioner.all()[rank]]
+    part = my_parts[0]
+    shards = [PartialMatrix(p, cols_n, "double", device=local) if mat else PartialVector(p, "double", device=local)
+              for p in my_parts]
+    shard = shards[0]
     n = part.size
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
@@ -266,7 +279,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         # space), so each push is route + gather (glint_route_gather_dev) + all_to_all_single + the
         # local push. Keys and values come from per-rank generators that every rank can replay.
         from glint_amd.dist import DistributedBigVector
-        dv = DistributedBigVector(partitioner, [shard], partitioner.size, np.float64, None, dev)
+        dv = DistributedBigVector(partitioner, shards, partitioner.size, np.float64, None, dev)
         nrec = 1 << 26
 
         def batch(src):
@@ -280,12 +293,14 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         keys, vals = batch(rank)
         # distinct elements a rank receives per push: counted over all ranks' batches by the check,
         # the expected value until then
-        uniq = int(n * (1.0 - np.exp(-nrec / n)))
+        P = world * mps
+        uniq = int(mps * n * (1.0 - np.exp(-nrec / (P * n) * world)))
         u_note = " (U estimated)"
-        tag = f"exchange_2p{log2_keys}"
+        tag = f"exchange_2p{log2_keys}" + (f"_mps{mps}" if mps > 1 else "")
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
-        workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({world}, "
-                    f"{partitioner.size}); route + gather + RCCL all-to-all + local push")
+        workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({P}, "
+                    f"{partitioner.size}), {mps} partition(s) per GPU; route + gather + RCCL all-to-all + "
+                    f"local push" + ("es" if mps > 1 else ""))
     elif pat in ("dense", "pull"):
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
         vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
@@ -345,10 +360,12 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         # one push at a time, each ended by the shard's sync point: the adaptive tail switch decides
         # from the previous push's tail as published at its sync, so the timed pushes take the path
         # the warm-up settled on (and its one-time scratch allocation lands in the warm-up)
-        shard.sync(stream)
-    shard.sync(stream)
-    lib.glint_prof_reset(h)
-    lib.glint_prof_enable(h, 1)
+        for sh in shards:
+            sh.sync(stream)
+    for sh in shards:
+        sh.sync(stream)
+        lib.glint_prof_reset(sh.handle)
+        lib.glint_prof_enable(sh.handle, 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -359,8 +376,9 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    lib.glint_prof_enable(h, 0)
-    shard.sync(stream)
+    for sh in shards:
+        lib.glint_prof_enable(sh.handle, 0)
+        sh.sync(stream)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -369,9 +387,12 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     def kernel_avg(kid):
         """Device time of one kernel kind per step (a large push runs its check and apply as one
         launch per window of records: the launches of a step are summed) and its launch count."""
-        ms, cnt = C.c_double(), C.c_int64()
-        lib.glint_prof_read(h, kid, C.byref(ms), C.byref(cnt))
-        return ms.value / steps, cnt.value
+        tot_ms, tot_n = 0.0, 0
+        for sh in shards:  # every local shard's launches of this kind (the exchange line may host several)
+            ms, cnt = C.c_double(), C.c_int64()
+            lib.glint_prof_read(sh.handle, kid, C.byref(ms), C.byref(cnt))
+            tot_ms, tot_n = tot_ms + ms.value, tot_n + cnt.value
+        return tot_ms / steps, tot_n
 
     # post-run check. Dense push: the shard holds (W+K) additions of each record, bit-exact (each
     # key once per push, the ordered path). Zipf / matrix / exchange: repeated keys sum in an
@@ -394,18 +415,21 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             ok = bool(torch.equal(out, fill_v.view(n, cols_n)[keys - part.start]))
         else:
             if exch:
-                # every rank's batch, replayed: the records of this rank's range, in local addresses
+                # every rank's batch, replayed: the records of this rank's partitions, in addresses local
+                # to the concatenation of its shards (shard j's elements at j * n ...)
                 addr_l, val_l = [], []
                 for src in range(world):
                     k_s, v_s = (keys, vals) if src == rank else batch(src)
-                    m = (k_s >= part.start) & (k_s < part.end)
-                    addr_l.append(k_s[m] - part.start)
-                    val_l.append(v_s[m])
+                    for j, p in enumerate(my_parts):
+                        m = (k_s >= p.start) & (k_s < p.end)
+                        addr_l.append(k_s[m] - p.start + j * n)
+                        val_l.append(v_s[m])
                     del k_s, v_s, m
                 addr, v_all = torch.cat(addr_l), torch.cat(val_l)
                 del addr_l, val_l
                 recv = int(addr.numel())
-                got = shard.get(torch.arange(part.start, part.end, dtype=torch.int64, device=dev))
+                got = torch.cat([sh.get(torch.arange(p.start, p.end, dtype=torch.int64, device=dev))
+                                 for sh, p in zip(shards, my_parts)])
             elif mat:
                 addr = (keys - part.start) * cols_n + cols.to(torch.int64)
                 v_all = vals
@@ -418,7 +442,11 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             a, order = torch.sort(addr)
             uq, counts = torch.unique_consecutive(a, return_counts=True)
             sums = segment_sums(v_all[order], counts) * reps
-            close = torch.isclose(got[uq], sums, rtol=1e-6, atol=1e-9 * reps)
+            # the north star's 1e-6 relative, relative to each element's sum of magnitudes: the scale
+            # any summation order of a Double sum is accurate to (equal to the plain relative error
+            # where the terms do not cancel)
+            mags = segment_sums(v_all[order].abs(), counts) * reps
+            close = (got[uq] - sums).abs() <= 1e-6 * mags
             ok = bool(close.all())
             if not ok:
                 bad = (~close).nonzero().reshape(-1)[:5]
@@ -432,7 +460,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             if exch:
                 uniq, u_note = int(uq.numel()), ""
                 bytes_per_step = 16.0 * recv + 16.0 * uniq
-            del a, order, uq, counts, sums, addr, v_all, got
+            del a, order, uq, counts, sums, mags, addr, v_all, got
         if not ok:
             raise SystemExit(f"post-run shard check FAILED ({pat}, 2^{log2_keys})")
 
@@ -478,7 +506,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (keys per BASELINE.md config, values U[-1,1) seed 42+rank), resident in HBM",
-        "config": {"workload": workload + u_note, "keys_per_gpu": n * (cols_n if mat else 1),
+        "config": {"workload": workload + u_note, "keys_per_gpu": n * (cols_n if mat else 1) * len(shards),
                    "records_per_step_per_gpu": nrec, "records_received_per_step_per_gpu": recv,
                    "distinct_keys_per_step_per_gpu": uniq, "key_dtype": "i64", "value_dtype": "f64",
                    "parallelism": f"range-sharded x{world}, " + ("route + all-to-all exchange" if exch else "no exchange")},
@@ -493,7 +521,8 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     floor = sparse_floor(tag, dt / steps * 1e3)
     if floor is not None:
         line["practical_floor"] = floor
-    shard.destroy()
+    for sh in shards:
+        sh.destroy()
     return line
 
 
@@ -529,7 +558,10 @@ def main():
         else:
             dist.init_process_group(backend)
     ctx = {"lib": N.load(), "dev": dev, "world": world, "rank": rank, "backend": backend}
-    line = run_line(ctx, args.pattern, args.log2_keys, args.scaling, args.steps, args.warmup, not args.no_check)
+    if args.parts_per_gpu > 1 and not exch:
+        raise SystemExit("--parts-per-gpu applies to --pattern exchange")
+    line = run_line(ctx, args.pattern, args.log2_keys, args.scaling, args.steps, args.warmup, not args.no_check,
+                    args.parts_per_gpu)
     # the north star's own size (BASELINE.json north_star: >= 70 % of HBM roofline at 1 GPU over a
     # 2^30-key Double vector) beside the driver's cfg2 line, with its own roofline and check
     if (world == 1 and args.pattern == "dense" and args.scaling == "weak" and args.log2_keys == 28

@@ -58,12 +58,15 @@ SIGNATURES = {
     "glint_pull_wire": (_I, [_P, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     "glint_route_dev": (_I, [_P, _I64, _I, _I32, _I64, _P, _P, C.POINTER(_I64), _P]),
     "glint_route_gather_dev": (_I, [_P, _P, _P, _I, _I64, _I, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "glint_scatter_rows_dev": (_I, [_P, _P, _I64, _I64, _P, _P]),
+    "glint_copy_segments_dev": (_I, [_P, _P, C.POINTER(_I64), _I, _P]),
     "glint_prof_enable": (_I, [_P, _I]),
     "glint_prof_read": (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(_I64)]),
     "glint_prof_reset": (_I, [_P]),
     "glint_strerror": (C.c_char_p, [_I]),
     "glint_device_count": (_I, []),
     "glint_version": (_I, []),
+    "glint_reload_env": (_I, []),
 }
 
 _lib = None
@@ -93,6 +96,11 @@ def load() -> C.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def reload_env() -> None:
+    """Make the library re-read its GLINT_* environment knobs (it caches them)."""
+    load().glint_reload_env()
 
 
 def strerror(code: int) -> str:

@@ -23,7 +23,8 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "build" / "libglint_oracle.so"
 
 CSRC = PKG / "csrc"
-HIP_SOURCES = [CSRC / "glint_gpu.hip", CSRC / "glint_sort.hip", CSRC / "glint_route.hip", CSRC / "glint_ordered.hip", CSRC / "glint_bin.hip"]
+HIP_SOURCES = [CSRC / "glint_gpu.hip", CSRC / "glint_sort.hip", CSRC / "glint_route.hip", CSRC / "glint_ordered.hip", CSRC / "glint_bin.hip",
+               CSRC / "glint_exchange.hip"]
 HIP_HEADERS = [CSRC / "glint_kernels.h", CSRC / "glint_device.h", CSRC / "glint_host.h", ROOT / "include" / "glint_gpu.h"]
 HIP_DEPS = HIP_SOURCES + HIP_HEADERS
 OBJ_DIR = ROOT / "build" / "obj"
@@ -47,8 +48,9 @@ def _stale(out: Path, deps) -> bool:
 
 
 def build_gpu_lib(force: bool = False, verbose: bool = False) -> Path:
-    """Compile libglint_gpu.so for gfx950 (no other target): one object per source (rebuilt when
-    it or a header changed; the rocPRIM-heavy glint_sort.hip rarely is), then one link."""
+    """Compile libglint_gpu.so for gfx950 (no other target): one object per source, rebuilt when
+    it or a header changed (sources compile in parallel), then one link. No library beyond the HIP
+    runtime is linked: every sort, scan and partition is hand-written."""
     if not force and not _stale(LIB, HIP_DEPS):
         return LIB
     OBJ_DIR.mkdir(parents=True, exist_ok=True)

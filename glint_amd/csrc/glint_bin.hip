@@ -1398,33 +1398,27 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
 // records per slab item from which bin_apply warms the whole slab into L2 (GLINT_BIN_PREFETCH_MIN;
 // 0xFFFFFFFF disables)
 u32 bin_prefetch_min() {
-  static const u32 v = [] {
-    const char* e = getenv("GLINT_BIN_PREFETCH_MIN");
-    return e ? (u32)strtoul(e, nullptr, 10) : (u32)(kSlab / 4);
-  }();
-  return v;
+  static EnvKnob k("GLINT_BIN_PREFETCH_MIN");
+  return (u32)k.get([](const char* e) -> long long { return e ? (long long)strtoul(e, nullptr, 10) : kSlab / 4; });
 }
 
 // records per exclusive slab item up to which bin_apply lists the touched elements instead of
 // sweeping the slab (GLINT_BIN_SPARSE_MAX; 0 disables; at most kSparseCap)
 u32 bin_sparse_max() {
-  static const u32 v = [] {
-    const char* e = getenv("GLINT_BIN_SPARSE_MAX");
+  static EnvKnob k("GLINT_BIN_SPARSE_MAX");
+  return (u32)k.get([](const char* e) -> long long {
     return std::min<u32>(kSparseCap, e ? (u32)strtoul(e, nullptr, 10) : 1024u);
-  }();
-  return v;
+  });
 }
 
-// resident blocks per CU of a kernel at its block size (occupancy query); `knob` overrides (tuning)
+// resident blocks per CU of a kernel at its block size (occupancy query)
 template <typename K>
-int resident_per_cu(K kernel, int tpb, const char* knob, size_t dyn_lds = 0) {
+int resident_per_cu(K kernel, int tpb, size_t dyn_lds = 0) {
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, tpb, dyn_lds) != hipSuccess || b < 1) {
     (void)hipGetLastError();
     b = 1;
   }
-  const char* env = getenv(knob);
-  if (env && atoi(env) > 0) b = atoi(env);
   return b;
 }
 
@@ -1437,11 +1431,11 @@ BinGeom bin_geometry(i64 elems) {
   // 2^28), more only when the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses).
   // Same box, two runs each (profiles/r03/bench_binned_cb.txt): 2^7 against 2^8 buckets cfg5
   // 0.418 -> 0.398 ms, cfg3 1.648 -> 1.636 ms, cfg4b exchange 3.005 -> 3.005 ms; 2^6 slower on all
-  static const u32 cb_min = [] {  // GLINT_BIN_CB: coarse digit bits at least (tuning knob, 4..10)
-    const char* e = getenv("GLINT_BIN_CB");
+  static EnvKnob cb_knob("GLINT_BIN_CB");  // coarse digit bits at least (tuning knob, 4..10)
+  const u32 cb_min = (u32)cb_knob.get([](const char* e) -> long long {
     const int v = e ? atoi(e) : 0;
-    return (u32)(v >= 4 && v <= 10 ? v : 7);
-  }();
+    return v >= 4 && v <= 10 ? v : 7;
+  });
   const u32 cb = std::min<u32>(sb, std::max<u32>(cb_min, sb > 10u ? sb - 10u : 0u));
   BinGeom g;
   g.fb = sb - cb;
@@ -1464,10 +1458,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // the tail (cfg3 ~65 %; cfg5's ~10 % does not pay for the sampling launch and the per-record check).
   // A dedup push re-measures every 16 pushes (and the first one).
   // GLINT_BIN_FRONT = dedup | hot | prep forces one (tests, tuning).
-  static const bool hot_on = [] {  // GLINT_BIN_HOT=0: no hot-element split (A/B, tests)
-    const char* e = getenv("GLINT_BIN_HOT");
-    return !(e && atoi(e) == 0);
-  }();
+  static EnvKnob hot_knob("GLINT_BIN_HOT");  // GLINT_BIN_HOT=0: no hot-element split (A/B, tests)
+  const bool hot_on = hot_knob.get([](const char* e) -> long long { return !(e && atoi(e) == 0); }) != 0;
   {
     const u64 w = s->hint_bin;
     const u32 m = (u32)(w >> 32), tail = (u32)w;
@@ -1479,20 +1471,23 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   }
   const bool probe = (s->bin_pushes++ & 15) == 0;
   int front = probe || s->bin_chunk_ratio < 0.8 ? 2 : (hot_on && s->bin_hot_frac >= 0.25 ? 1 : 0);
-  if (const char* e = getenv("GLINT_BIN_FRONT")) {
-    if (!strcmp(e, "dedup")) front = 2;
-    else if (!strcmp(e, "hot")) front = hot_on ? 1 : 0;
-    else if (!strcmp(e, "prep")) front = 0;
-  }
+  static EnvKnob front_knob("GLINT_BIN_FRONT");
+  const int forced = (int)front_knob.get([](const char* e) -> long long {
+    if (!e) return -1;
+    if (!strcmp(e, "dedup")) return 2;
+    if (!strcmp(e, "hot")) return 1;
+    if (!strcmp(e, "prep")) return 0;
+    return -1;
+  });
+  if (forced == 2 || forced == 0) front = forced;
+  else if (forced == 1) front = hot_on ? 1 : 0;
   const bool dedup = front == 2;
   s->bin_last_front = front;
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
-  static const int plain_wpc = [] {  // GLINT_PART_WPC: plain partition workgroups per CU (tuning knob)
-    const char* e = getenv("GLINT_PART_WPC");
-    return (e && atoi(e) > 0) ? atoi(e) : kPartWgPerCuPlain;
-  }();
+  static EnvKnob wpc_knob("GLINT_PART_WPC");  // plain partition workgroups per CU (tuning knob)
+  const int plain_wpc = (int)wpc_knob.pos_or(kPartWgPerCuPlain);
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : plain_wpc)));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
@@ -1544,10 +1539,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
   if (front == 1) {  // the wide hot table: sample, count, pick
-    static const u32 wide_min = [] {  // GLINT_BIN_WIDE_MIN: sample count that makes an element hot (tuning)
-      const char* e = getenv("GLINT_BIN_WIDE_MIN");
-      return (u32)(e && atoi(e) > 0 ? atoi(e) : 3);
-    }();
+    static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");  // sample count that makes an element hot (tuning)
+    const u32 wide_min = (u32)wide_knob.pos_or(3);
     HIPCHK(hipMemsetAsync(wkey, 0xFF, b_wk, st));
     HIPCHK(hipMemsetAsync(wcnt, 0, b_wk + b_wbest, st));  // counts and picks
     bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
@@ -1557,10 +1550,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     HIPCHK(hipGetLastError());
   }
   if (dedup && hot_on) {
-    static const u32 hot_min = [] {  // GLINT_BIN_HOT_MIN: sample count that makes an element hot (tuning)
-      const char* e = getenv("GLINT_BIN_HOT_MIN");
-      return (u32)(e && atoi(e) > 0 ? atoi(e) : 2);
-    }();
+    static EnvKnob hmin_knob("GLINT_BIN_HOT_MIN");  // sample count that makes an element hot (tuning)
+    const u32 hot_min = (u32)hmin_knob.pos_or(2);
     bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, hot_min,
                                                     hot_tags);
     HIPCHK(hipGetLastError());
@@ -1585,7 +1576,9 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
     HIPCHK(hipGetLastError());
   }
-  static const int fcount_rpc = resident_per_cu(bin_fcount_kernel, kFCTPB, "GLINT_FCOUNT_BPC");
+  static EnvKnob fcount_knob("GLINT_FCOUNT_BPC");
+  static const int fcount_occ = resident_per_cu(bin_fcount_kernel, kFCTPB);
+  const int fcount_rpc = (int)fcount_knob.pos_or(fcount_occ);
   const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
   bin_fcount_kernel<<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
   HIPCHK(hipGetLastError());
@@ -1593,13 +1586,14 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // workgroup size: 512 threads (4096-record tiles, whole-line runs) unless the push has no more
   // items than 256-thread blocks fit at once (small pushes: parallelism beats tile size)
   static std::atomic<int> fpart_rpc[2][kMaxSegs + 1][11] = {};  // resident blocks per CU by (TPB, G, log2 nf)
+  static EnvKnob fpart_knob("GLINT_FPART_BPC");
   auto rpc_of = [&](int w, auto kernel, int tpb) {
     int r = fpart_rpc[w][G][g.fb].load(std::memory_order_relaxed);
-    if (!r) {
-      r = resident_per_cu(kernel, tpb, "GLINT_FPART_BPC", fdyn);
+    if (!r) {  // the occupancy query once per geometry; the knob applies on top
+      r = resident_per_cu(kernel, tpb, fdyn);
       fpart_rpc[w][G][g.fb].store(r, std::memory_order_relaxed);
     }
-    return r;
+    return (int)fpart_knob.pos_or(r);
   };
   const int r256 = rpc_of(0, bin_fpart_kernel<A, 256>, 256);
   if (max_fitems <= (i64)s->cus * r256) {
@@ -1613,10 +1607,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
                                             val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
   }
   HIPCHK(hipGetLastError());
-  static const int apply_bpc = [] {  // GLINT_BIN_APPLY_BPC: work-item blocks per CU (tuning knob)
-    const char* e = getenv("GLINT_BIN_APPLY_BPC");
-    return (e && atoi(e) > 0) ? atoi(e) : 64;
-  }();
+  static EnvKnob apply_knob("GLINT_BIN_APPLY_BPC");  // work-item blocks per CU (tuning knob)
+  const int apply_bpc = (int)apply_knob.pos_or(64);
   bin_apply_kernel<V><<<(unsigned)std::min<i64>(nslots, (i64)s->cus * apply_bpc), kCTPB, 0, st>>>(
       addr_b, val_b, cdesc, bc, s->elems, a.data, bin_prefetch_min(), bin_sparse_max());
   HIPCHK(hipGetLastError());

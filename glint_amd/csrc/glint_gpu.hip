@@ -240,7 +240,7 @@ __device__ __forceinline__ void apply_general(const PushArgs<V>& a, i64 pbase, i
 // 6.2 TB/s, against 5.7 TB/s at twice the waves with cached shard accesses).
 constexpr int kSweepU = 2;  // record pairs per lane per iteration
 template <typename V, bool EVEN>
-__device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta, i64 p_begin, i64 p_end) {
+__device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta, i64 p_begin, i64 p_end, bool last) {
   typedef typename Vec2<V>::T V2;
   if (blockIdx.x >= a.sweep_blocks) return;
   const i64 npairs = p_end;
@@ -274,7 +274,9 @@ __device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta, i64
       a.data[e + 1] = vadd(d1, (V)v.y);
     }
   }
-  if ((a.n & 1) && p_end == (a.n >> 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // the last window: odd record
+  // the odd record belongs to the last window only: with n = k * 2^26 + 1 an earlier window also
+  // ends at pair n >> 1 (its tiles cover every pair), so p_end alone cannot tell them apart
+  if ((a.n & 1) && last && blockIdx.x == 0 && threadIdx.x == 0) {
     const i64 e = a.n - 1 + delta;
     a.data[e] = vadd(a.data[e], a.vals[a.n - 1]);
   }
@@ -291,8 +293,9 @@ __global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i
   if (brk == 0u && a.ctl->nonaffine == 0u) {
     const i64 delta = desc[0];  // tile 0 starts the run at record 0
     const i64 p0 = (i64)t_begin * (kTile / 2), p1 = min((i64)t_end * (kTile / 2), a.n >> 1);
-    if ((delta & 1) == 0) apply_sweep<V, true>(a, delta, p0, p1);
-    else apply_sweep<V, false>(a, delta, p0, p1);
+    const bool last = t_end >= a.ntiles;
+    if ((delta & 1) == 0) apply_sweep<V, true>(a, delta, p0, p1, last);
+    else apply_sweep<V, false>(a, delta, p0, p1, last);
     return;
   }
   const u32 tiles = min(t_end, brk == 0u ? a.ntiles : a.ntiles - brk);
@@ -522,11 +525,8 @@ namespace {
 // ---- push -------------------------------------------------------------------------------------
 // blocks per CU in the affine sweep (GLINT_SWEEP_BPC overrides; 1 measured best on MI355X)
 int sweep_blocks_per_cu() {
-  static const int v = [] {
-    const char* e = getenv("GLINT_SWEEP_BPC");
-    return (e && atoi(e) > 0) ? atoi(e) : 1;
-  }();
-  return v;
+  static EnvKnob k("GLINT_SWEEP_BPC");
+  return (int)k.pos_or(1);
 }
 
 // The apply of a large push runs as one launch per window of 2^26 records (GLINT_SWEEP_WINDOW =
@@ -535,31 +535,29 @@ int sweep_blocks_per_cu() {
 // the same bytes swept window by window (tools/microbench_stream.hip mode 6: 2^30 records whole
 // 5.90 TB/s, in 2^26-record launches 6.56 TB/s; 2^28 whole 6.21 TB/s; profiles/r03/micro_stream_2p30.txt).
 u32 sweep_window_tiles() {
-  static const u32 v = [] {
-    const char* e = getenv("GLINT_SWEEP_WINDOW");
+  static EnvKnob k("GLINT_SWEEP_WINDOW");
+  return (u32)k.get([](const char* e) -> long long {
     const int lg = e ? atoi(e) : 26;
-    if (lg <= 10 || lg >= 42) return 0xFFFFFFFFu;
-    return (u32)(((i64)1 << lg) / kTile);
-  }();
-  return v;
+    if (lg <= 10 || lg >= 42) return 0xFFFFFFFFll;
+    return ((i64)1 << lg) / kTile;
+  });
 }
 
 // GLINT_BINNED: 0 = never bin, 1 = bin every large push, unset = bin when the previous push on the
 // shard left a large unordered tail (read from the host-mapped word push_apply writes)
 int binned_mode() {
-  const char* e = getenv("GLINT_BINNED");
-  if (!e || !*e) return -1;
-  return atoi(e) != 0 ? 1 : 0;
+  static EnvKnob k("GLINT_BINNED");
+  return (int)k.get([](const char* e) -> long long {
+    if (!e || !*e) return -1;
+    return atoi(e) != 0 ? 1 : 0;
+  });
 }
 constexpr i64 kBinMin = (i64)1 << 20;  // records: below this the LDS-hash scatter wins
 // records: up to this many, a (non-deterministic) push is the single scatter launch.
 // GLINT_SMALL_PUSH overrides it (0 = always check + apply).
 i64 small_push_max() {
-  static const i64 v = [] {
-    const char* e = std::getenv("GLINT_SMALL_PUSH");
-    return e ? (i64)std::strtoll(e, nullptr, 10) : (i64)4096;
-  }();
-  return v;
+  static EnvKnob k("GLINT_SMALL_PUSH");
+  return k.get([](const char* e) -> long long { return e ? std::strtoll(e, nullptr, 10) : 4096ll; });
 }
 
 template <typename V, bool MAT>
@@ -627,9 +625,10 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   const u64 win = std::min<u64>(sweep_window_tiles(), a.ntiles);
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
+    static EnvKnob check_bpc("GLINT_CHECK_BPC");
     // one launch: the key stream alone lost 3-6 % when windowed (each short launch ramps up and drains)
     const unsigned gc =
-        grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu(push_check_kernel<MAT, 0>, 2, "GLINT_CHECK_BPC"));
+        grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu<push_check_kernel<MAT, 0>>(2, &check_bpc));
     HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
                                        a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles)
                             : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
@@ -637,7 +636,8 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     s->ctl_par ^= 1;  // only once the check that zeroes the other slot is on the stream
   }
   {
-    const i64 bpc = blocks_per_cu(push_apply_kernel<V, MAT>, 2, "GLINT_APPLY_BPC");
+    static EnvKnob apply_bpc("GLINT_APPLY_BPC");
+    const i64 bpc = blocks_per_cu<push_apply_kernel<V, MAT>>(2, &apply_bpc);
     for (u64 t0 = 0; t0 < a.ntiles; t0 += win) {
       const u32 t1 = (u32)std::min<u64>(a.ntiles, t0 + win);
       const unsigned ga = grid_for(t1 - t0, kTPB / 64, (i64)s->cus * bpc);
@@ -876,9 +876,16 @@ int ring_retire_through(glint_shard* s, u64 t);
 // ================================================================================================
 // C ABI
 // ================================================================================================
+std::atomic<unsigned> g_env_gen{1};
+
 extern "C" {
 
 int glint_version(void) { return 100; }
+
+int glint_reload_env(void) {
+  g_env_gen.fetch_add(1, std::memory_order_acq_rel);
+  return GLINT_OK;
+}
 
 int glint_device_count(void) {
   int n = 0;
@@ -1084,11 +1091,10 @@ namespace {
 // GranularBigVectorSpec.scala:21). Larger arrays go straight from pageable memory at PCIe rate.
 // GLINT_PINNED_STAGE_MAX (bytes) overrides the crossover; tools/host_latency.py measures it.
 size_t pinned_stage_max() {
-  static const size_t v = [] {
-    const char* e = std::getenv("GLINT_PINNED_STAGE_MAX");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : ((size_t)2 << 20);
-  }();
-  return v;
+  static EnvKnob k("GLINT_PINNED_STAGE_MAX");
+  return (size_t)k.get([](const char* e) -> long long {
+    return e ? (long long)std::strtoull(e, nullptr, 10) : (2ll << 20);
+  });
 }
 
 // stage host arrays into the shard's device scratch: returns device pointers to each section and,

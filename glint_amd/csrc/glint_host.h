@@ -7,6 +7,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <utility>
@@ -44,8 +45,11 @@ struct glint_shard {
   // binned front end (glint_bin.hip push_binned): 0 plain, 1 plain + hot-element split, 2 chunk dedup
   // (+ hot split). What the last dedup push measured decides: chunk_ratio = records it kept of the cold
   // records that entered its hash table (1.0 = dedup merged nothing), hot_frac = share of the tail
-  // taken by the hot elements. A dedup push re-measures every 16 pushes.
-  double bin_chunk_ratio = 0.0;
+  // taken by the hot elements. A dedup push re-measures every 16 pushes. The measurements reach the
+  // host only at sync points (latch_hints), so a device-resident caller that never calls
+  // glint_shard_sync keeps the no-history default: the plain front end (ratio 1.0: dedup merged
+  // nothing), with a dedup probe every 16 pushes.
+  double bin_chunk_ratio = 1.0;
   double bin_hot_frac = 0.0;
   uint32_t bin_pushes = 0;
   int bin_last_front = 0;        // the front end of the last binned push
@@ -122,6 +126,33 @@ struct glint_shard {
   double prof_ms[GLINT_K_COUNT] = {0};
   int64_t prof_n[GLINT_K_COUNT] = {0};
   std::mutex mu;
+};
+
+// ---- environment knobs ----------------------------------------------------------------------------
+// Tuning and test overrides (GLINT_BINNED, GLINT_BIN_FRONT, GLINT_SWEEP_WINDOW, ...) are read once per
+// generation, so the push paths that several actor threads reach never call getenv. A test that
+// changes the environment between calls starts a new generation with glint_reload_env().
+extern std::atomic<unsigned> g_env_gen;  // glint_gpu.hip
+
+struct EnvKnob {
+  const char* name;
+  std::atomic<unsigned> gen{0};
+  std::atomic<long long> val{0};
+  explicit EnvKnob(const char* n) : name(n) {}
+  // parse(getenv(name)) -- the string may be NULL -- cached until the next glint_reload_env()
+  template <typename F>
+  long long get(F parse) {
+    const unsigned g = g_env_gen.load(std::memory_order_acquire);
+    if (gen.load(std::memory_order_acquire) == g) return val.load(std::memory_order_relaxed);
+    const long long v = parse(getenv(name));
+    val.store(v, std::memory_order_relaxed);
+    gen.store(g, std::memory_order_release);
+    return v;
+  }
+  // an integer knob: its value if set to a positive integer, else dflt
+  long long pos_or(long long dflt) {
+    return get([dflt](const char* e) { return (e && atoll(e) > 0) ? atoll(e) : dflt; });
+  }
 };
 
 namespace {
@@ -294,16 +325,20 @@ inline unsigned grid_for(i64 units, i64 per_block, i64 cap) {
 
 // resident blocks per CU for a kernel (occupancy query), capped at the measured best; the
 // environment variable `knob` (e.g. GLINT_CHECK_BPC) overrides it for tuning sweeps
-template <typename K>
-inline int blocks_per_cu(K kernel, int cap, const char* knob = nullptr) {
-  int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kTPB, 0) != hipSuccess || b < 1) {
-    (void)hipGetLastError();
-    b = 2;
+// (the occupancy query runs once per kernel; `knob` is an EnvKnob the call site owns)
+template <auto Kernel>
+inline int blocks_per_cu(int cap, EnvKnob* knob = nullptr) {
+  static std::atomic<int> occ{0};  // one per kernel
+  int b = occ.load(std::memory_order_relaxed);
+  if (!b) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, Kernel, kTPB, 0) != hipSuccess || b < 1) {
+      (void)hipGetLastError();
+      b = 2;
+    }
+    occ.store(b, std::memory_order_relaxed);
   }
   b = std::min(b, cap);
-  const char* env = knob ? getenv(knob) : nullptr;
-  if (env && atoi(env) > 0) b = atoi(env);
+  if (knob) b = (int)knob->pos_or(b);
   return b;
 }
 

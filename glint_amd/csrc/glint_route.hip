@@ -242,7 +242,8 @@ __global__ __launch_bounds__(kST) void route_row_scan(const u32* __restrict__ hi
 // caller holds its buffer's lock from taking it until its kernels are enqueued (host threads sharing
 // a stream would otherwise interleave their launches on one buffer). A buffer grows only after its
 // stream has drained. At most kMaxScratch streams per device keep a buffer: the least recently used
-// idle one is released (after a device sync) to make room.
+// idle one is released to make room, after the event its last route recorded (never a device-wide
+// sync: that would stall every shard's pushes on the device, and the victim's stream may be gone).
 constexpr int kMaxDevices = 64;
 constexpr size_t kMaxScratch = 64;
 constexpr size_t kBadWordOffset = 0;  // the synchronous route's status word: the buffer's first 256 B
@@ -251,6 +252,8 @@ struct RouteScratch {
   void* tmp = nullptr;
   size_t bytes = 0;
   u64 used = 0;    // last use (LRU)
+  hipEvent_t done = nullptr;  // recorded after the last route's kernels on this buffer
+  bool recorded = false;
 };
 std::mutex g_scratch_mu;
 std::map<std::pair<int, hipStream_t>, std::unique_ptr<RouteScratch>> g_scratch;
@@ -275,9 +278,12 @@ RouteScratch* route_scratch(int dev, hipStream_t st, size_t need) {
             (victim == g_scratch.end() || it->second->used < victim->second->used))
           victim = it;
       if (victim != g_scratch.end() && victim->second->use.try_lock()) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(victim->second->tmp);
-        victim->second->use.unlock();
+        RouteScratch* v = victim->second.get();
+        if (v->recorded) (void)hipEventSynchronize(v->done);  // its last route has finished with it
+        (void)hipFree(v->tmp);
+        if (v->done) (void)hipEventDestroy(v->done);
+        (void)hipGetLastError();
+        v->use.unlock();
         g_scratch.erase(victim);
       }
     }
@@ -377,12 +383,19 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   const size_t need = 2 * hist_bytes + (size_t)kMaxParts * 4;
   RouteScratch* sc = route_scratch(dev, st, need);
   if (!sc) return GLINT_ENOMEM;
-  // the buffer stays locked until this call's kernels are on the stream (or, held, for the caller)
+  // the buffer stays locked until this call's kernels are on the stream (or, held, for the caller);
+  // its event marks the end of this call's use, for an eviction from another stream
   struct Unlock {
     RouteScratch* sc;
+    hipStream_t st;
     bool keep;
-    ~Unlock() { if (!keep) sc->use.unlock(); }
-  } unlock{sc, held != nullptr};
+    ~Unlock() {
+      if (!sc->done && hipEventCreateWithFlags(&sc->done, hipEventDisableTiming) != hipSuccess) sc->done = nullptr;
+      sc->recorded = sc->done && hipEventRecord(sc->done, st) == hipSuccess;
+      (void)hipGetLastError();
+      if (!keep) sc->use.unlock();
+    }
+  } unlock{sc, st, held != nullptr};
   if (held) *held = sc;
   char* b = (char*)sc->tmp + 256;
   if (!bad_dev) bad_dev = (uint64_t*)((char*)sc->tmp + kBadWordOffset);

@@ -129,6 +129,41 @@ class Router:
         return order, counts
 
 
+def _row_bytes(t: torch.Tensor) -> int:
+    return t.element_size() * (t[0].numel() if t.dim() > 1 else 1)
+
+
+def copy_ranges(src: torch.Tensor, dst: torch.Tensor, ranges) -> None:
+    """dst[d:d + c] = src[s:s + c] for every (s, d, c) in ranges (rows): one launch of
+    glint_copy_segments_dev for device tensors; plain slices on the host."""
+    ranges = [(int(a), int(b), int(c)) for a, b, c in ranges if c]
+    if not ranges:
+        return
+    if src.is_cuda:
+        rb = _row_bytes(src)
+        segs = np.array([(a * rb, b * rb, c * rb) for a, b, c in ranges], dtype=np.int64).reshape(-1)
+        check(N.load().glint_copy_segments_dev(src.data_ptr(), dst.data_ptr(),
+                                               segs.ctypes.data_as(N.C.POINTER(N.C.c_int64)), len(ranges),
+                                               torch.cuda.current_stream(src.device).cuda_stream))
+        return
+    for a, b, c in ranges:
+        dst[b:b + c] = src[a:a + c]
+
+
+def scatter_rows(src: torch.Tensor, order: torch.Tensor, out: torch.Tensor) -> None:
+    """out[order[i]] = src[i] (rows): the answer's way back to the caller's order
+    (AsyncBigVector.scala:61-79). Device tensors: one launch of glint_scatter_rows_dev; host tensors:
+    index_copy_."""
+    n = src.shape[0]
+    if n == 0:
+        return
+    if src.is_cuda:
+        check(N.load().glint_scatter_rows_dev(src.data_ptr(), order.data_ptr(), n, _row_bytes(src), out.data_ptr(),
+                                              torch.cuda.current_stream(src.device).cuda_stream))
+        return
+    out.index_copy_(0, order, src)
+
+
 class _Exchange:
     """The all-to-all legs of one routed call (send splits, receive splits, local layout).
 
@@ -209,7 +244,8 @@ class _Exchange:
 
     def take(self, buf: torch.Tensor, j: int) -> torch.Tensor:
         """Local partition j's records of a received buffer: a view when they are one range (one
-        source, or one local partition), else the ranges concatenated -- no index array."""
+        source, or one local partition), else the ranges gathered into one buffer by one
+        multi-range copy (glint_copy_segments_dev) -- no index array."""
         if self.nlocal == 1:
             return buf
         rs = self.local_ranges(j)
@@ -217,16 +253,24 @@ class _Exchange:
             return buf[:0]
         if len(rs) == 1:
             return buf[rs[0][0]:rs[0][0] + rs[0][1]]
-        return torch.cat([buf[a:a + c] for a, c in rs])
+        out = torch.empty((sum(c for _, c in rs),) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
+        copy_ranges(buf, out, [(a, o, c) for (a, c), o in zip(rs, np.cumsum([0] + [c for _, c in rs]))])
+        return out
+
+    def single_range(self, j: int):
+        """(start, length) of local partition j's records in the received buffer when they are one
+        range (their answers can then be written in place), else None."""
+        if self.nlocal == 1:
+            return (0, int(self._src_off[-1]))
+        rs = self.local_ranges(j)
+        return rs[0] if len(rs) == 1 else None
 
     def put(self, resp: torch.Tensor, j: int, got: torch.Tensor) -> torch.Tensor:
         """Writes local partition j's answers into the response buffer (the inverse of take)."""
         if self.nlocal == 1:
             return got
-        o = 0
-        for a, c in self.local_ranges(j):
-            resp[a:a + c] = got[o:o + c]
-            o += c
+        rs = self.local_ranges(j)
+        copy_ranges(got, resp, [(o, a, c) for (a, c), o in zip(rs, np.cumsum([0] + [c for _, c in rs]))])
         return resp
 
 
@@ -275,6 +319,66 @@ class _Distributed:
         for j, sh in enumerate(self.shards):
             yield j, sh, [ex.take(b, j) for b in bufs]
 
+    def _on_shard_device(self, t: torch.Tensor) -> bool:
+        return t.is_cuda and self.device.type == "cuda" and t.device == self.device
+
+    def _nosync(self, t: torch.Tensor, out=None) -> dict:
+        """Device-resident shard calls are enqueued without a wait (_sync waits once at the end), and
+        a pull may write its answer straight into `out`."""
+        kw = {"sync": False} if self._on_shard_device(t) else {}
+        if out is not None:
+            kw["out"] = out
+        return kw
+
+    @staticmethod
+    def _sync(touched) -> None:
+        for sh, t in touched:
+            if t.is_cuda and hasattr(sh, "sync"):
+                sh.sync(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def _answer(self, ex: _Exchange, order, bufs: tuple, caller: torch.Tensor, tail: tuple, get):
+        """The pull's answer path: each local shard answers its records (get(shard, parts, out)), the
+        answers travel back along the reversed splits and land in the caller's order
+        (AsyncBigVector.scala:61-79, AsyncBigMatrix.scala:53-86).
+        * world 1, device batch: each shard's answer is scattered straight to the caller's positions
+          (glint_scatter_rows_dev over its range of `order`): no response buffer, no collective;
+        * otherwise: answers are written into the response buffer (in place when a partition's records
+          are one range, else by one multi-range copy), sent back, and scattered by `order`."""
+        rk = bufs[0]
+        n = caller.shape[0]
+        out_shape = (n,) + tail
+        touched = []
+        if ex.world == 1 and order is not None and self._on_shard_device(rk):
+            out = torch.empty(out_shape, dtype=self.dtype, device=caller.device)
+            for j, sh, parts in self._split(ex, *bufs):
+                if parts[0].numel():
+                    a, c = ex.single_range(j)
+                    got = get(sh, parts, None)
+                    touched.append((sh, parts[0]))
+                    scatter_rows(got, order[a:a + c], out)
+            self._sync(touched)
+            ex.raise_if_bad(caller, self.router.nkeys)
+            return out
+        resp = torch.empty((rk.shape[0],) + tail, dtype=self.dtype, device=rk.device)
+        for j, sh, parts in self._split(ex, *bufs):
+            if parts[0].numel():
+                rng = ex.single_range(j)
+                k = [self._to_shard(p) for p in parts]
+                if rng is not None and self._on_shard_device(rk):  # answered in place
+                    get(sh, k, resp[rng[0]:rng[0] + rng[1]])
+                else:
+                    got = get(sh, k, None)
+                    resp = ex.put(resp, j, got.to(resp.device).reshape((-1,) + tail))
+                touched.append((sh, k[0]))
+        self._sync(touched)
+        back = ex.backward(resp).to(caller.device)
+        ex.raise_if_bad(caller, self.router.nkeys)  # after the collectives: this rank asked for nothing
+        if order is None:  # one partition: the answer is already in the caller's order
+            return back
+        out = torch.empty(out_shape, dtype=self.dtype, device=caller.device)
+        scatter_rows(back, order.to(caller.device), out)
+        return out
+
     def destroy(self) -> bool:
         for sh in self.shards:
             sh.destroy()
@@ -301,9 +405,14 @@ class DistributedBigVector(_Distributed):
             order, ex = self._begin(keys)
             rk = ex.forward(keys.index_select(0, order))
             rv = ex.forward(values.index_select(0, order.to(values.device)))
+        touched = []
         for _, sh, (k, v) in self._split(ex, rk, rv):
             if k.numel():
-                sh.update(self._to_shard(k), self._to_shard(v), deterministic=deterministic)
+                # every local push is enqueued before the first wait (keys are validated by the route)
+                sh.update(self._to_shard(k), self._to_shard(v), deterministic=deterministic,
+                          **self._nosync(k))
+                touched.append((sh, k))
+        self._sync(touched)
         ex.raise_if_bad(keys, self.router.nkeys)
         return True
 
@@ -315,17 +424,7 @@ class DistributedBigVector(_Distributed):
         else:
             order, ex = self._begin(keys)
             rk = ex.forward(keys.index_select(0, order))
-        resp = torch.empty(rk.numel(), dtype=self.dtype, device=rk.device)
-        for j, sh, (k,) in self._split(ex, rk):
-            if k.numel():
-                resp = ex.put(resp, j, sh.get(self._to_shard(k)).to(resp.device))
-        back = ex.backward(resp).to(keys.device)
-        ex.raise_if_bad(keys, self.router.nkeys)  # after the collectives: this rank asked for nothing
-        if order is None:  # one partition: the answer is already in the caller's order
-            return back
-        out = torch.empty(keys.numel(), dtype=self.dtype, device=keys.device)
-        out.index_copy_(0, order.to(keys.device), back)
-        return out
+        return self._answer(ex, order, (rk,), keys, (), lambda sh, p, out: sh.get(p[0], **self._nosync(p[0], out)))
 
 
 class DistributedBigMatrix(_Distributed):
@@ -351,9 +450,13 @@ class DistributedBigMatrix(_Distributed):
             rr = ex.forward(rows.index_select(0, order))
             rc = ex.forward(cols.index_select(0, order.to(cols.device)))
             rv = ex.forward(values.index_select(0, order.to(values.device)))
+        touched = []
         for _, sh, (r, c, v) in self._split(ex, rr, rc, rv):
             if r.numel():
-                sh.update(self._to_shard(r), self._to_shard(c), self._to_shard(v), deterministic=deterministic)
+                sh.update(self._to_shard(r), self._to_shard(c), self._to_shard(v), deterministic=deterministic,
+                          **self._nosync(r))
+                touched.append((sh, r))
+        self._sync(touched)
         ex.raise_if_bad(rows, self.router.nkeys)
         return True
 
@@ -373,24 +476,10 @@ class DistributedBigMatrix(_Distributed):
             rr = ex.forward(rows.index_select(0, order))
             rc = None if cols is None else ex.forward(cols.index_select(0, order.to(cols.device)))
         if cols is None:
-            shape = (rr.numel(), self.cols)
-            bufs = (rr,)
-        else:
-            shape = (rr.numel(),)
-            bufs = (rr, rc)
-        resp = torch.empty(shape, dtype=self.dtype, device=rr.device)
-        for j, sh, parts in self._split(ex, *bufs):
-            if parts[0].numel():
-                got = (sh.getRows(self._to_shard(parts[0])) if cols is None
-                       else sh.get(self._to_shard(parts[0]), self._to_shard(parts[1])))
-                resp = ex.put(resp, j, got.to(resp.device).reshape((-1,) + shape[1:]))
-        back = ex.backward(resp).to(rows.device)
-        ex.raise_if_bad(rows, self.router.nkeys)
-        if order is None:  # one partition: the answer is already in the caller's order
-            return back
-        out = torch.empty((rows.numel(),) + shape[1:], dtype=self.dtype, device=rows.device)
-        out.index_copy_(0, order.to(rows.device), back)
-        return out
+            return self._answer(ex, order, (rr,), rows, (self.cols,),
+                                lambda sh, p, out: sh.getRows(p[0], **self._nosync(p[0], out)))
+        return self._answer(ex, order, (rr, rc), rows, (),
+                            lambda sh, p, out: sh.get(p[0], p[1], **self._nosync(p[0], out)))
 
 
 class DistributedClient:

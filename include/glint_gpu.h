@@ -58,7 +58,10 @@ enum glint_push_flags {
    * device atomics; a host-pointer push takes the unordered LDS-hash scatter instead of the
    * order-preserving fold. Without the hint, a large push takes the binned path by itself when the
    * shard's previous push was unordered (environment GLINT_BINNED=0 disables that, =1 forces it
-   * for pushes >= 2^20 records). */
+   * for pushes >= 2^20 records). The adaptive choices (binned or not, and the binned front end)
+   * follow what earlier pushes measured on the device as of the shard's last sync point
+   * (glint_shard_sync, or the end of a host-pointer call): a device-resident caller that never
+   * syncs gets the no-history defaults. */
   GLINT_PUSH_UNORDERED = 2
 };
 
@@ -232,6 +235,21 @@ int glint_route_gather_dev(const int64_t* keys, const int32_t* cols, const void*
                            int64_t* order, int64_t* out_keys, int32_t* out_cols, void* out_vals,
                            uint64_t* bad_dev, void* stream);
 
+/* ---- exchange glue (device) ----------------------------------------------------------------- *
+ * The client side of a routed pull: AsyncBigVector.pull writes each partition's answer back to the
+ * positions its keys came from (`result(indices(i)) = values(i)`, AsyncBigVector.scala:61-79;
+ * whole rows in AsyncBigMatrix.pull(rows), AsyncBigMatrix.scala:53-86). Stream-ordered on `stream`,
+ * no host synchronisation; device pointers.
+ * dst[order[i]] = src[i] for i < n, rows of row_bytes bytes (a multiple of 4); order is the record
+ * index array glint_route_gather_dev wrote (or a sub-range of it). */
+int glint_scatter_rows_dev(const void* src, const int64_t* order, int64_t n, int64_t row_bytes, void* dst,
+                           void* stream);
+/* A multi-range copy in one launch: segs is a HOST array of nseg (src_offset, dst_offset, bytes)
+ * triples (byte offsets, multiples of 4); segment k copies src + src_offset to dst + dst_offset. Used to
+ * gather a local partition's records that arrived from several source ranks into one buffer, and to
+ * put its answers back into the response buffer's ranges. */
+int glint_copy_segments_dev(const void* src, void* dst, const int64_t* segs, int nseg, void* stream);
+
 /* ---- kernel timing ------------------------------------------------------------------------- *
  * With profiling on, every kernel launch of the shard is bracketed by HIP events recorded on the
  * stream it is launched on; glint_prof_read waits for them and returns the summed device time and
@@ -257,6 +275,9 @@ const char* glint_strerror(int status);
 int glint_device_count(void);
 /* Library version (major*10000 + minor*100 + patch). */
 int glint_version(void);
+/* The library reads its GLINT_* environment overrides (tuning and test knobs) once and caches them;
+ * this makes the next call re-read them (tests that change the environment between calls). */
+int glint_reload_env(void);
 
 #ifdef __cplusplus
 }

@@ -39,3 +39,14 @@ def gpu():
     if N.load().glint_device_count() < 1:
         pytest.fail("no GPU visible to libglint_gpu.so")
     return int(os.environ.get("GLINT_TEST_DEVICE", "0"))
+
+
+@pytest.fixture(autouse=True)
+def _glint_env_knobs():
+    """libglint_gpu.so caches its GLINT_* environment knobs; a test that sets one calls
+    ``N.reload_env()``, and every test ends with a reload (after monkeypatch has restored the
+    environment), so no knob leaks into the next test."""
+    yield
+    import glint_amd._native as N
+    if N._lib is not None:
+        N.reload_env()

@@ -180,50 +180,167 @@ CASES = {
 }
 
 
-def run_cfg4(rank, world, port, backend, nbatch, log2_batch):
+def _check_close(got, ref, mag, what):
+    """Default-mode Double sums of repeated keys are summed in no particular order. The bound is the
+    north star's 1e-6 relative, taken relative to each element's sum of magnitudes (sum |v|) -- the
+    scale every ordering of a floating-point sum is accurate to; it equals the plain relative error
+    wherever the terms do not cancel, and demands exact zeros where nothing was pushed."""
+    err = (got - ref).abs()
+    bad = err > 1e-6 * mag
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} elements off by more than 1e-6 of sum |v|"
+
+
+def run_cfg4(rank, world, port, backend, nbatch, log2_batch, dtype="long"):
     """BASELINE.json configs[3] at its own key space on one GPU: RangePartitioner(8, 2^31) -- eight
-    2^28-key Long shards (modelsPerServer = 8 on one server) behind DistributedClient -- fed `nbatch`
+    2^28-key shards (modelsPerServer = 8 on one server) behind DistributedClient -- fed `nbatch`
     client batches of 2^log2_batch uniform keys (the 64 loopback clients of cfg4), each routed to the
     8 shards by glint_route_gather_dev (AsyncBigVector.scala:96-121). Long sums are exact in any
-    order, so every shard must equal a torch.index_add_ int64 reference bit for bit; two sampled key
-    ranges are replayed through the oracle's sequential update loop as well."""
+    order, so every shard must equal a torch.index_add_ int64 reference bit for bit; Double shards
+    must be within 1e-6 of fp64 segment sums (relative to the sum of magnitudes, _check_close). Two
+    sampled key ranges are replayed through the oracle's sequential update loop as well."""
     _init(rank, world, port, backend)
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         from glint_amd.dist import DistributedClient
         nkeys = 1 << 31
+        fp = dtype == "double"
+        tdt = torch.float64 if fp else torch.int64
         client = DistributedClient(device=dev)
-        vec = client.vector(nkeys, "long", modelsPerServer=8)
+        vec = client.vector(nkeys, dtype, modelsPerServer=8)
         parts = vec.partitioner.all()
         assert vec.nrOfPartitions == 8 and all(p.size == 1 << 28 for p in parts)
-        ref = torch.zeros(nkeys, dtype=torch.int64, device=dev)
+        ref = torch.zeros(nkeys, dtype=tdt, device=dev)
+        mag = torch.zeros(nkeys, dtype=tdt, device=dev) if fp else None
         # oracle replay windows: 2^20 keys inside partitions 2 and 7 (the last key of the space included)
         windows = [(parts[2].start + 12_345, parts[2].start + 12_345 + (1 << 20)), (nkeys - (1 << 20), nkeys)]
-        orc = [O.OracleVector(O.part_range(a, b), O.O_I64) for a, b in windows]
+        orc = [O.OracleVector(O.part_range(a, b), O.O_F64 if fp else O.O_I64) for a, b in windows]
         n = 1 << log2_batch
         for c in range(nbatch):
             g = torch.Generator(device=dev)
             g.manual_seed(4000 + c)
             k = torch.randint(0, nkeys, (n,), dtype=torch.int64, device=dev, generator=g)
-            v = torch.randint(-(1 << 40), 1 << 40, (n,), dtype=torch.int64, device=dev, generator=g)
+            if fp:
+                v = torch.rand(n, dtype=torch.float64, device=dev, generator=g) * 2 - 1
+            else:
+                v = torch.randint(-(1 << 40), 1 << 40, (n,), dtype=torch.int64, device=dev, generator=g)
             assert vec.push(k, v)
             ref.index_add_(0, k, v)
+            if fp:
+                mag.index_add_(0, k, v.abs())
             for (a, b), o in zip(windows, orc):
                 m = (k >= a) & (k < b)
                 assert o.update(k[m].cpu().numpy(), v[m].cpu().numpy()) == -1
         torch.cuda.synchronize(dev)
         for p, sh in zip(parts, vec.shards):
             got = sh.get(torch.arange(p.start, p.end, dtype=torch.int64, device=dev))
-            assert torch.equal(got, ref[p.start:p.end]), f"partition {p.index} differs from index_add_"
+            if fp:
+                _check_close(got, ref[p.start:p.end], mag[p.start:p.end], f"partition {p.index}")
+            else:
+                assert torch.equal(got, ref[p.start:p.end]), f"partition {p.index} differs from index_add_"
             del got
         for (a, b), o in zip(windows, orc):
-            got = vec.pull(torch.arange(a, b, dtype=torch.int64, device=dev)).cpu().numpy()
-            np.testing.assert_array_equal(got, o.data)
-        # pulls of random keys over all 8 shards come back in the caller's order
+            got = vec.pull(torch.arange(a, b, dtype=torch.int64, device=dev))
+            if fp:
+                _check_close(got.cpu(), torch.from_numpy(o.data), mag[a:b].cpu(), "oracle window")
+            else:
+                np.testing.assert_array_equal(got.cpu().numpy(), o.data)
+        # pulls of random keys over all 8 shards come back in the caller's order, bit-equal to the shards
         q = torch.randint(0, nkeys, (1 << 20,), dtype=torch.int64, device=dev)
-        assert torch.equal(vec.pull(q), ref[q])
+        got = vec.pull(q)
+        own = torch.empty_like(got)
+        for p, sh in zip(parts, vec.shards):
+            m = (q >= p.start) & (q < p.end)
+            own[m] = sh.get(q[m].contiguous())
+        assert torch.equal(got, own)
+        if not fp:
+            assert torch.equal(got, ref[q])
         vec.destroy()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def zipf_rows(g, n, rows, dev):
+    """Zipf(1.0)-distributed row indices (P(rank r) ~ 1/r: floor(rows^u) for uniform u is log-uniform)
+    scattered over [0, rows) by an odd-multiplier bijection (rows a power of two)."""
+    u = torch.rand(n, dtype=torch.float64, device=dev, generator=g)
+    ranks = torch.clamp(torch.floor(torch.pow(float(rows), u)).to(torch.int64) - 1, 0, rows - 1)
+    return (ranks * 0x9E3779B1) & (rows - 1)
+
+
+def run_cfg5(rank, world, port, backend, dtype, log2_rows=20, ncols=512, nbatch=8, log2_batch=23, log2_pull=16):
+    """BASELINE.json configs[4] at its own shape on one GPU: a 2^20 x 512 matrix (4 GiB of Double) over
+    RangePartitioner(8, 2^20) -- modelsPerServer = 8 on one server, eight 2^17-row shards -- behind
+    DistributedClient / DistributedBigMatrix. 2^26 triplets (Zipf(1.0) rows x uniform cols) arrive as
+    8 client batches of 2^23, each routed to the 8 shards (AsyncBigMatrix.scala:141-156); then 2^16
+    Zipf rows are pulled back whole (AsyncBigMatrix.scala:53-86). Long: every shard and every pulled
+    row equal a torch.index_add_ int64 reference bit for bit; Double: within 1e-6 of fp64 segment sums
+    (_check_close), and the pulled rows bit-equal to the shards. Two row windows are replayed through
+    the oracle's PartialMatrix.update loop."""
+    _init(rank, world, port, backend)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        from glint_amd.dist import DistributedClient
+        nrows = 1 << log2_rows
+        fp = dtype == "double"
+        tdt = torch.float64 if fp else torch.int64
+        client = DistributedClient(device=dev)
+        mat = client.matrix(nrows, ncols, dtype, modelsPerServer=8)
+        parts = mat.partitioner.all()
+        assert mat.nrOfPartitions == 8 and all(p.size == nrows // 8 for p in parts)
+        ref = torch.zeros(nrows * ncols, dtype=tdt, device=dev)
+        mag = torch.zeros(nrows * ncols, dtype=tdt, device=dev) if fp else None
+        wins = [(parts[2].start + 777, parts[2].start + 777 + 64), (nrows - 64, nrows)]
+        orc = [O.OracleMatrix(O.part_range(a, b), ncols, O.O_F64 if fp else O.O_I64) for a, b in wins]
+        n = 1 << log2_batch
+        for c in range(nbatch):
+            g = torch.Generator(device=dev)
+            g.manual_seed(5000 + c)
+            r = zipf_rows(g, n, nrows, dev)
+            cl = torch.randint(0, ncols, (n,), dtype=torch.int32, device=dev, generator=g)
+            if fp:
+                v = torch.rand(n, dtype=torch.float64, device=dev, generator=g) * 2 - 1
+            else:
+                v = torch.randint(-(1 << 40), 1 << 40, (n,), dtype=torch.int64, device=dev, generator=g)
+            assert mat.push(r, cl, v)
+            flat = r * ncols + cl.to(torch.int64)
+            ref.index_add_(0, flat, v)
+            if fp:
+                mag.index_add_(0, flat, v.abs())
+            for (a, b), o in zip(wins, orc):
+                m = (r >= a) & (r < b)
+                assert o.update(r[m].cpu().numpy(), cl[m].cpu().numpy(), v[m].cpu().numpy()) == -1
+        torch.cuda.synchronize(dev)
+        ref = ref.view(nrows, ncols)
+        mag = mag.view(nrows, ncols) if fp else None
+        full = torch.empty((nrows, ncols), dtype=tdt, device=dev)
+        for p, sh in zip(parts, mat.shards):
+            sh.getRows(torch.arange(p.start, p.end, dtype=torch.int64, device=dev), out=full[p.start:p.end])
+            if fp:
+                _check_close(full[p.start:p.end], ref[p.start:p.end], mag[p.start:p.end], f"partition {p.index}")
+            else:
+                assert torch.equal(full[p.start:p.end], ref[p.start:p.end]), f"partition {p.index} differs"
+        for (a, b), o in zip(wins, orc):
+            want = torch.from_numpy(o.data.reshape(b - a, ncols))
+            if fp:
+                _check_close(full[a:b].cpu(), want, mag[a:b].cpu(), "oracle window")
+            else:
+                assert torch.equal(full[a:b].cpu(), want)
+        # the row pull: 2^16 Zipf rows through DistributedBigMatrix.pull(rows)
+        g = torch.Generator(device=dev)
+        g.manual_seed(6000)
+        q = zipf_rows(g, 1 << log2_pull, nrows, dev)
+        got = mat.pull(q)
+        assert got.shape == (q.numel(), ncols)
+        assert torch.equal(got, full[q])
+        if not fp:
+            assert torch.equal(got, ref[q])
+        # element pulls of the same rows at random cols, through DistributedBigMatrix.pull(rows, cols)
+        qc = torch.randint(0, ncols, (q.numel(),), dtype=torch.int32, device=dev, generator=g)
+        assert torch.equal(mat.pull(q, qc), full[q, qc.to(torch.int64)])
+        mat.destroy()
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -194,3 +194,64 @@ def test_routes_on_two_streams_at_once(gpu):
         assert int(bad.item()) == 0
         np.testing.assert_array_equal(counts.cpu().numpy(), c_ref)
         np.testing.assert_array_equal(order.cpu().numpy(), o_ref)
+
+
+@pytest.mark.parametrize("row_elems,dtype", [(1, "float64"), (1, "float32"), (1, "int64"), (512, "float64"),
+                                             (3, "float32"), (300, "float64"), (7, "int32")])
+@pytest.mark.parametrize("n", [0, 1, 4097, 100_003])
+def test_scatter_rows_matches_index_copy(gpu, row_elems, dtype, n):
+    """glint_scatter_rows_dev: the pull answer's way back to the caller's order
+    (AsyncBigVector.scala:61-79), out[order[i]] = src[i] for elements and whole rows, against
+    torch's index_copy_; a sub-range of order (a partition's range) lands only its rows."""
+    import torch
+    from glint_amd.dist import scatter_rows
+    d = torch.device("cuda", gpu)
+    g = torch.Generator(device=d)
+    g.manual_seed(n * 31 + row_elems)
+    dt = getattr(torch, dtype)
+    shape = (n,) if row_elems == 1 else (n, row_elems)
+    src = torch.randint(-1000, 1000, shape, generator=g, device=d).to(dt)
+    order = torch.randperm(n, generator=g, device=d)
+    out = torch.full(shape, -7, dtype=dt, device=d)
+    scatter_rows(src, order, out)
+    want = torch.full(shape, -7, dtype=dt, device=d)
+    want.index_copy_(0, order, src)
+    assert torch.equal(out, want)
+    if n > 10:  # a partition's sub-range of order
+        a, c = n // 3, n // 4
+        out2 = torch.full(shape, -7, dtype=dt, device=d)
+        scatter_rows(src[a:a + c], order[a:a + c], out2)
+        want2 = torch.full(shape, -7, dtype=dt, device=d)
+        want2.index_copy_(0, order[a:a + c], src[a:a + c])
+        assert torch.equal(out2, want2)
+
+
+@pytest.mark.parametrize("row_elems,dtype", [(1, "float64"), (1, "int32"), (512, "float64"), (3, "float32")])
+def test_copy_segments_gathers_and_puts_ranges(gpu, row_elems, dtype):
+    """glint_copy_segments_dev: a local partition's records from several source ranks gathered into
+    one buffer in one launch (the exchange's take), and its answers put back (put); more segments than
+    one launch carries (64) are split over launches."""
+    import torch
+    from glint_amd.dist import copy_ranges
+    d = torch.device("cuda", gpu)
+    g = torch.Generator(device=d)
+    g.manual_seed(row_elems)
+    dt = getattr(torch, dtype)
+    for nseg in (1, 3, 8, 150):
+        lens = torch.randint(0, 900, (nseg,), generator=g).tolist()
+        total = sum(lens) + 5000
+        shape = (total,) if row_elems == 1 else (total, row_elems)
+        src = torch.randint(-1000, 1000, shape, generator=g, device=d).to(dt)
+        starts = sorted(torch.randint(0, total - 900, (nseg,), generator=g).tolist())
+        ranges, o = [], 0
+        for a, c in zip(starts, lens):
+            ranges.append((a, o, c))
+            o += c
+        out = torch.full((o,) + tuple(shape[1:]), -7, dtype=dt, device=d)
+        copy_ranges(src, out, ranges)
+        want = torch.cat([src[a:a + c] for a, _, c in ranges]) if o else out
+        assert torch.equal(out, want)
+        back = torch.full(shape, -7, dtype=dt, device=d)
+        copy_ranges(out, back, [(b, a, c) for a, b, c in ranges])
+        for a, _, c in ranges:
+            assert torch.equal(back[a:a + c], src[a:a + c])

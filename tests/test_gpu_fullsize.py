@@ -7,8 +7,10 @@
 * cfg5 per GPU: 2^23 Zipf(1.0)-row x uniform-col triplets into a 2^17 x 512 shard
   (PartialMatrix.scala:74-83), same scheme.
 
-Long is bit-exact; Double in the default mode is within the north star's 1e-6 relative (plus an
-absolute floor for sums that cancel); Double with GLINT_PUSH_DETERMINISTIC is bit-exact.
+Long is bit-exact; Double in the default mode is within the north star's 1e-6 relative, taken
+relative to each element's sum of magnitudes (sum |v| over its records: the scale every summation
+order is accurate to; it is the plain relative error wherever the terms do not cancel, and it demands
+exact zeros where nothing was pushed); Double with GLINT_PUSH_DETERMINISTIC is bit-exact.
 Zipf ranks are scattered over the shard by an odd-multiplier bijection of [0, 2^k) (the bench uses
 a seeded permutation; the mapping does not matter for parity).
 """
@@ -42,6 +44,13 @@ def cfg5():
     return _scatter(ranks, 17), rng.integers(0, 512, nrec).astype(np.int32), rng
 
 
+def assert_close_mag(got, want, mag):
+    """|got - want| <= 1e-6 * sum |v| per element (see the module docstring)."""
+    err = np.abs(got.astype(np.float64) - want.astype(np.float64))
+    bad = err > 1e-6 * mag
+    assert not bad.any(), f"{int(bad.sum())} elements off by more than 1e-6 of sum |v|"
+
+
 def _push3(sh, torch, dev, *arrays, deterministic=False):
     t = [torch.from_numpy(a).to(dev) for a in arrays]
     if deterministic:
@@ -72,7 +81,8 @@ def test_cfg3_full_size(gpu, cfg3, mode):
     for _ in range(reps):
         assert ref.update(keys + start, vals) == -1
     if mode == "double":
-        np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9 * reps)
+        mag = reps * np.bincount(keys, np.abs(vals), minlength=1 << 28)
+        assert_close_mag(got, ref.data, mag)
     else:
         np.testing.assert_array_equal(got, ref.data)
 
@@ -96,6 +106,7 @@ def test_cfg5_slice_full_size(gpu, cfg5, mode):
     for _ in range(reps):
         assert ref.update(rows + start, cols, vals) == -1
     if mode == "double":
-        np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9 * reps)
+        mag = reps * np.bincount(rows * 512 + cols, np.abs(vals), minlength=(1 << 17) * 512).reshape(1 << 17, 512)
+        assert_close_mag(got, ref.data, mag)
     else:
         np.testing.assert_array_equal(got, ref.data)

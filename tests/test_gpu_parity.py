@@ -164,6 +164,71 @@ def test_deterministic_push_is_bit_exact(gpu, dtype):
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
+@pytest.mark.parametrize("dtype", ["double", "float"])
+@pytest.mark.parametrize("layout", ["range", "cyclic"])
+@pytest.mark.parametrize("head", [False, True])
+def test_deterministic_hot_chain_split(gpu, dtype, layout, head):
+    """The deterministic tail's hot-chain split (glint_sort.hip: det_hot_pick / det_hot_count /
+    det_hot_scatter and det_fold_hot on the second stream, joined by an event) engages for tails of
+    >= 2^19 records with elements of >= 2^16 estimated records. 2^21 records, three keys taking 40 %,
+    20 % and 10 % of them in push order, the rest over the partition: the result must be the
+    sequential loop's (PartialVector.scala:35-43) bit for bit, with and without a sorted head in front
+    (the tail then continues from the head's sums)."""
+    rng = np.random.default_rng(zlib.crc32(f"hotchain/{dtype}/{layout}/{head}".encode()))
+    n, size = 1 << 21, 1 << 20
+    if layout == "range":
+        start = 3 << 20
+        part = RangePartition(3, start, start + size)
+        owned = np.arange(start, start + size, dtype=np.int64)
+    else:
+        P, idx = 5, 2
+        part = CyclicPartition(idx, P, P * size)
+        owned = np.arange(idx, P * size, P, dtype=np.int64)
+    hot = owned[rng.choice(size, 3, replace=False)]
+    which = rng.random(n)
+    keys = owned[rng.integers(0, size, n)]
+    keys[which < 0.4] = hot[0]
+    keys[(which >= 0.4) & (which < 0.6)] = hot[1]
+    keys[(which >= 0.6) & (which < 0.7)] = hot[2]
+    vals = rand_vals(rng, dtype, n)
+    if head:  # strictly increasing head (plain-RMW prefix), then the unordered tail
+        keys = np.concatenate([owned, keys])
+        vals = np.concatenate([rand_vals(rng, dtype, size), vals])
+    ref = oracle_vec(part, dtype)
+    assert ref.update(keys, vals) == -1
+    import torch
+    d = torch.device("cuda", gpu)
+    with PartialVector(part, dtype, gpu) as sh:
+        sh.update(torch.from_numpy(keys).to(d), torch.from_numpy(vals).to(d), deterministic=True)
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+@pytest.mark.parametrize("n,window", [(2 * 2048 + 1, "11"), (3 * 2048 + 1, "11"), ((1 << 26) + 1, None)])
+def test_windowed_sweep_odd_record_once(gpu, monkeypatch, n, window):
+    """A dense push is applied in windows of 2^GLINT_SWEEP_WINDOW records; with n = k * 2^w + 1 the
+    window before the last also ends at pair n >> 1, and the odd last record must still be added once
+    (it was added by both windows before the fix)."""
+    import torch
+    if window is not None:
+        monkeypatch.setenv("GLINT_SWEEP_WINDOW", window)
+        N.reload_env()
+    d = torch.device("cuda", gpu)
+    for dtype in ("long", "double"):
+        part = RangePartition(0, 0, n + 5)
+        with PartialVector(part, dtype, gpu) as sh:
+            keys = torch.arange(n, dtype=torch.int64, device=d)
+            if dtype == "long":
+                vals = torch.arange(1, n + 1, dtype=torch.int64, device=d)
+            else:
+                vals = torch.arange(1, n + 1, dtype=torch.float64, device=d) * 0.5
+            sh.update(keys, vals)
+            sh.update(keys, vals)
+            got = sh.get(torch.arange(n + 5, dtype=torch.int64, device=d))
+            want = torch.zeros(n + 5, dtype=vals.dtype, device=d)
+            want[:n] = 2 * vals
+            assert torch.equal(got, want), f"{dtype} n={n}"
+
+
 def test_zipf_fixture_default_mode(gpu):
     z = np.load(GOLD / "zipf_push.npz")
     start, size = int(z["start"]), int(z["size"])
@@ -496,6 +561,7 @@ def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
     vals = rng.integers(-5, 5, keys.size).astype(np.int64)
     ref = oracle_vec(part, "long")
     monkeypatch.delenv("GLINT_BINNED", raising=False)
+    N.reload_env()
     with PartialVector(part, "long", gpu) as sh:
         lib.glint_prof_enable(sh.handle, 1)
         counts = []
@@ -520,6 +586,7 @@ def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
             sh.update(bad, vals, unordered=True)
         assert ei.value.record == 1234
     monkeypatch.setenv("GLINT_BINNED", "0")
+    N.reload_env()
     with PartialVector(part, "long", gpu) as sh:
         lib.glint_prof_enable(sh.handle, 1)
         for _ in range(2):
@@ -544,6 +611,7 @@ def test_adaptive_switch_decides_at_sync_points(gpu, monkeypatch):
     keys = torch.from_numpy(rng.integers(0, size, 1 << 21).astype(np.int64)).to(d)
     vals = torch.from_numpy(rng.integers(-5, 5, 1 << 21).astype(np.int64)).to(d)
     monkeypatch.delenv("GLINT_BINNED", raising=False)
+    N.reload_env()
 
     def binned_launches(sh):
         ms, cnt = C.c_double(), C.c_int64()
@@ -616,6 +684,7 @@ def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
     Float sums over duplicates are checked against the exact (float64) sum within 1e-6 of the sum
     of magnitudes per element -- the reference's sequential float order is one rounding of many."""
     monkeypatch.setenv("GLINT_BIN_FRONT", front)
+    N.reload_env()
     rng = np.random.default_rng(zlib.crc32(f"fronts/{front}/{dtype}/{pattern}".encode()))
     start, size = 1 << 33, 2_000_003
     part = RangePartition(2, start, start + size)
@@ -666,6 +735,7 @@ def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
 @pytest.mark.parametrize("front", ["dedup", "hot", "prep"])
 def test_binned_fronts_matrix(gpu, monkeypatch, front):
     monkeypatch.setenv("GLINT_BIN_FRONT", front)
+    N.reload_env()
     rng = np.random.default_rng(23)
     rows_n, cols_n = 30_011, 129  # pitch 130: row padding stays untouched
     part = RangePartition(0, 0, rows_n)

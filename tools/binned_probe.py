@@ -35,6 +35,7 @@ for name, keys in (("zipf1.1", torch.from_numpy(zipf_keys(rng, n, n // 4, 1.1)).
                    ("uniform", torch.randint(0, n, (n // 4,), dtype=torch.int64, device=dev))):
     for front in fronts:
         os.environ["GLINT_BIN_FRONT"] = front
+        glint_amd._native.reload_env()  # the library caches its knobs
         ts = []
         for _ in range(4):
             torch.cuda.synchronize()

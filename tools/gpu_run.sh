@@ -6,6 +6,7 @@
 #   bench     the driver's default line (cfg2 with the CPU baseline) and the other bench lines
 #   prof2p30  rocprofv3 kernel stats of the dense push at 2^28 and at 2^30 (north-star size)
 #   binned    rocprofv3 kernel stats of the binned patterns (zipf, matrix, exchange)
+#   newtests  this round's new GPU tests, then the config-shape tests (cfg4 Long/Double, cfg5 full shape)
 #   bintests  the GPU tests of the binned path, the full-size cases, cfg4 and the exchange
 #   ab        bench zipf / matrix / exchange with a previous library (AB_LIB) and the current one
 #   abn       the same over several libraries (LIBS="tag=path[,VAR=VALUE...] ..."; tools/variant.py builds variants)
@@ -17,7 +18,7 @@
 #   ring      tools/ring_probe.py: pipelined message-sized wire pushes, timed and with kernel stats
 #   loopback  tools/loopback/build/glint_loopback, HBM shards vs the oracle's CPU loop (cfg1, cfg4 shapes)
 set -o pipefail
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
@@ -61,6 +62,7 @@ for s in ${STAGES:-tests bench}; do
       for pat in zipf matrix exchange pull rowpull; do
         step bench_$pat 300 python3 bench.py --no-cpu-baseline --pattern $pat
       done
+      step bench_exchange_mps8 300 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
       ;;
     prof2p30)
       kstats dense_2p28 300
@@ -79,6 +81,11 @@ for s in ${STAGES:-tests bench}; do
           exchange_2p28) pmc $w --pattern exchange ;;
         esac
       done
+      ;;
+    newtests)  # this round's new GPU tests first (fast feedback), then the config-shape tests
+      step pytest_new 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -k "hot_chain or odd_record or scatter_rows or copy_segments or dist_exchange"
+      step pytest_configs 1100 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread
       ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \

@@ -140,6 +140,7 @@ def main():
         for mode, flags, env in (("atomic", 0, "0"), ("binned (UNORDERED hint)", N.GLINT_PUSH_UNORDERED, ""),
                                  ("adaptive (no hint)", 0, "")):
             os.environ["GLINT_BINNED"] = env
+            glint_amd._native.reload_env()  # the library caches its knobs
             dt = timed(lambda: lib.glint_vec_push_dev(h, kt.data_ptr(), zvals.data_ptr(), nz, flags, stream), 5, h)
             rec = dict(op="vec_push_dev", pattern=pat, path=mode, records=nz, ms=dt * 1e3,
                        Grecords_per_s=nz / dt / 1e9,
@@ -151,6 +152,7 @@ def main():
                 rec.update(algorithmic_GBps=32.0 * nz / dt / 1e9)
             emit(**rec)
         os.environ["GLINT_BINNED"] = ""
+        glint_amd._native.reload_env()  # the library caches its knobs
     dt = timed(lambda: lib.glint_vec_push_dev(h, zkeys.data_ptr(), zvals.data_ptr(), zk.size, 1, stream), 2, h)
     emit(op="vec_push_dev", mode="deterministic", pattern="zipf1.1", records=int(zk.size), ms=dt * 1e3,
          algorithmic_GBps=(16.0 * zk.size + 16.0 * U) / dt / 1e9)
@@ -176,11 +178,13 @@ def main():
          Grecords_per_s=r.size / dt / 1e9)
     for mode, flags, env in (("atomic", 0, "0"), ("binned (UNORDERED hint)", N.GLINT_PUSH_UNORDERED, "")):
         os.environ["GLINT_BINNED"] = env
+        glint_amd._native.reload_env()  # the library caches its knobs
         dt = timed(lambda: lib.glint_mat_push_dev(h, mr.data_ptr(), mc.data_ptr(), mv.data_ptr(), r.size, flags,
                                                   stream), 5, h)
         emit(op="mat_push_dev", pattern="zipf1.0 rows x uniform cols", path=mode, records=int(r.size), distinct=U,
              ms=dt * 1e3, algorithmic_GBps=(20.0 * r.size + 16.0 * U) / dt / 1e9, Grecords_per_s=r.size / dt / 1e9)
     os.environ["GLINT_BINNED"] = ""
+    glint_amd._native.reload_env()  # the library caches its knobs
     nrow = (1 << 16) // 8
     qr = torch.from_numpy(zipf_keys(rng, shard_rows, nrow, 1.0)).to(dev)
     rout = torch.empty((qr.numel(), cols), dtype=torch.float64, device=dev)
