@@ -113,11 +113,19 @@ trait GpuShardActor extends ActorLogging { this: akka.actor.Actor =>
     if (held.size == 1) self ! GpuShard.FlushPulls
   }
 
-  /** Answers every held pull, in arrival order. */
+  /** Answers every held pull, in arrival order. Every held answer runs even if an earlier one throws
+    * (its pullFinish frees its native handle on every path, and the other senders still get their
+    * replies); the first exception is rethrown afterwards, so the actor fails on it as the
+    * reference's get() would inside `receive`. */
   protected def flushPulls(): Unit = {
     val answers = held.toList
     held.clear()
-    answers.foreach(_())
+    var first: Throwable = null
+    answers.foreach { a =>
+      try a()
+      catch { case t: Throwable => if (first == null) first = t }
+    }
+    if (first != null) throw first
   }
 
   protected def enqueued(id: Int, ticket: Long): Unit = pending.put(id, ticket)

@@ -234,14 +234,14 @@ def test_copy_segments_gathers_and_puts_ranges(gpu, row_elems, dtype):
     import torch
     from glint_amd.dist import copy_ranges
     d = torch.device("cuda", gpu)
-    g = torch.Generator(device=d)
+    g = torch.Generator()
     g.manual_seed(row_elems)
     dt = getattr(torch, dtype)
     for nseg in (1, 3, 8, 150):
         lens = torch.randint(0, 900, (nseg,), generator=g).tolist()
         total = sum(lens) + 5000
         shape = (total,) if row_elems == 1 else (total, row_elems)
-        src = torch.randint(-1000, 1000, shape, generator=g, device=d).to(dt)
+        src = torch.randint(-1000, 1000, shape, generator=g).to(dt).to(d)
         starts = sorted(torch.randint(0, total - 900, (nseg,), generator=g).tolist())
         ranges, o = [], 0
         for a, c in zip(starts, lens):

@@ -20,8 +20,8 @@ PHASES = {
                              "clear+sync"]),
     "bin_part (dedup)": (8, ["setup", "hash insert", "issue loads", "sync+extract+sync", "rank+sync", "scan",
                              "stage+sync", "store+sync", "clear+sync", "hv clear+sync"]),
-    "bin_fpart": (20, ["T/H scans", "item descs", "segments", "pass1 count", "reserve", "p2 fetch issue",
-                       "p2 rank+sync", "p2 scan", "p2 stage+sync", "p2 store+sync", "p2 clear+sync"]),
+    "bin_fpart": (20, ["T/H scans", "item descs", "segments", "sync", "reserve", "fetch issue",
+                       "rank+sync", "scan", "stage+sync", "store+sync", "clear+sync"]),
     "bin_apply": (40, ["desc/warm", "clear+sync", "records", "sync", "rmw", "sync"]),
 }
 

@@ -7,6 +7,7 @@
 #   prof2p30  rocprofv3 kernel stats of the dense push at 2^28 and at 2^30 (north-star size)
 #   binned    rocprofv3 kernel stats of the binned patterns (zipf, matrix, exchange)
 #   newtests  this round's new GPU tests, then the config-shape tests (cfg4 Long/Double, cfg5 full shape)
+#   pmccal    PMC calibration per access shape (tools/microbench_pmc.hip, tools/pmc_calibrate.py)
 #   bintests  the GPU tests of the binned path, the full-size cases, cfg4 and the exchange
 #   ab        bench zipf / matrix / exchange with a previous library (AB_LIB) and the current one
 #   abn       the same over several libraries (LIBS="tag=path[,VAR=VALUE...] ..."; tools/variant.py builds variants)
@@ -84,8 +85,31 @@ for s in ${STAGES:-tests bench}; do
       ;;
     newtests)  # this round's new GPU tests first (fast feedback), then the config-shape tests
       step pytest_new 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-        -k "hot_chain or odd_record or scatter_rows or copy_segments or dist_exchange"
+        -k "hot_chain or odd_record or scatter_rows or copy_segments or dist_exchange or bucket_apply or cfg5_slice"
       step pytest_configs 1100 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread
+      ;;
+    pmccal)  # FETCH_SIZE / WRITE_SIZE per access shape against known byte counts (tools/microbench_pmc.hip)
+      step pmccal_known 120 tools/build/microbench_pmc
+      for c in FETCH_SIZE WRITE_SIZE; do
+        echo "[$(date +%T)] pmccal $c" >&2
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d /tmp/pmccal_$c -o run \
+           -- $R/tools/build/microbench_pmc > $OUT/pmccal_$c.log 2>&1) || { tail -30 $OUT/pmccal_$c.log >&2; exit 1; }
+        find /tmp/pmccal_$c -name "*counter_collection.csv" -exec cp {} $OUT/pmccal_$c.csv \;
+      done
+      python3 tools/pmc_calibrate.py $OUT/pmccal_known.log $OUT/pmccal_FETCH_SIZE.csv $OUT/pmccal_WRITE_SIZE.csv \
+        $OUT/pmc_calibration.json >&2
+      ;;
+    quickbench)  # the binned lines only, no CPU baseline
+      for pat in ${PATTERNS:-matrix zipf exchange}; do
+        step qb_$pat 300 python3 bench.py --no-cpu-baseline --no-north-star --pattern $pat
+      done
+      ;;
+    bapstats)  # kernel stats of the cfg5 line with the bucket apply on and off
+      GLINT_BIN_BAPPLY=1 kstats matrix_bap1 300 --pattern matrix --steps 10 --warmup 2
+      GLINT_BIN_BAPPLY=0 kstats matrix_bap0 300 --pattern matrix --steps 10 --warmup 2
+      ;;
+    phases)  # phase clocks of the binned kernels (tools/bin_phases.py, a -DGLINT_BIN_PROF build)
+      step bin_phases 300 python3 tools/bin_phases.py
       ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
