@@ -41,6 +41,8 @@ SIGNATURES = {
     "glint_mat_pull_rows": (_I, [_P, _P, _P, _I64]),
     "glint_shard_last_error": (_I, [_P, C.POINTER(_I64)]),
     "glint_vec_push_dev": (_I, [_P, _P, _P, _I64, _I, _P]),
+    "glint_vec_push_dev_gated": (_I, [_P, _P, _P, _I64, _I, _P, _P]),
+    "glint_mat_push_dev_gated": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P]),
     "glint_vec_pull_dev": (_I, [_P, _P, _P, _I64, _P]),
     "glint_mat_push_dev": (_I, [_P, _P, _P, _P, _I64, _I, _P]),
     "glint_mat_pull_dev": (_I, [_P, _P, _P, _P, _I64, _P]),
@@ -90,7 +92,10 @@ def load() -> C.CDLL:
     except Exception:
         pass
     lib = C.CDLL(str(path))
+    ab = "GLINT_GPU_LIB" in os.environ  # an older library loaded for a same-box A/B may lack newer symbols
     for name, (res, args) in SIGNATURES.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -55,8 +55,9 @@ constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments
 #endif
 constexpr int kFPer = 8;               // records per thread per fine-partition tile (tile = TPB * kFPer;
                                        // bin_fpart runs at 256 or 512 threads, chosen per push)
-constexpr int kFCTPB = 256;            // bin_fcount's workgroup size (512 measured slower there)
 constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
+constexpr int kFCTPB = 512;            // bin_fcount's workgroup size: a whole item's addresses in flight
+constexpr int kFCPer = (int)kFItem / kFCTPB;  // at once, kFCPer per thread
 #ifndef GLINT_APPLY_TPB
 #define GLINT_APPLY_TPB 256
 #endif
@@ -1036,18 +1037,19 @@ __global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, co
     for (u32 f = tid; f < g.nf; f += kFCTPB) fh[f] = 0;
     const u32 M = load_segments<kFCTPB>(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
-    u32 s = 0;
-    u32 a[kFPer], avalid = 0;
-    if (v1 > v0) avalid = fetch_addr<kFCTPB>(v0, v1, s, segpre, segst, addr_in, a);
-    for (u32 t0 = v0; t0 < v1; t0 += kFCTPB * kFPer) {
-      u32 cur[kFPer];
-      const u32 cvalid = avalid;
+    if (v1 > v0) {
+      // the whole item's addresses are loaded at once (one memory round trip per item; with 256-thread
+      // workgroups walking 2048-record tiles a small push's item was 8 dependent round trips)
+      u32 s = 0;
+      u32 a[kFCPer];
 #pragma unroll
-      for (int q = 0; q < kFPer; ++q) cur[q] = a[q];
-      avalid = fetch_addr<kFCTPB>(t0 + kFCTPB * kFPer, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
+      for (int q = 0; q < kFCPer; ++q) {
+        const u32 v = v0 + (u32)q * kFCTPB + (u32)tid;
+        a[q] = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
+      }
 #pragma unroll
-      for (int q = 0; q < kFPer; ++q)
-        if ((cvalid >> q) & 1u) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
+      for (int q = 0; q < kFCPer; ++q)
+        if (v0 + (u32)q * kFCTPB + (u32)tid < v1) atomicAdd(&fh[fine_of(a[q], g)], 1u);
     }
     __syncthreads();
     for (u32 f = tid; f < g.nf; f += kFCTPB) {

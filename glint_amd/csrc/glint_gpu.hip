@@ -125,7 +125,9 @@ __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict_
   if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // the next push's control words (no kernel of this push reads them)
     next->brk_enc = 0u;
     next->nonaffine = 0u;
+    next->cancel = 0u;
   }
+  if (ctl->cancel) return;  // a cancelled gated push: brk_enc stays 0, so no tail either
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const u32 nw = gridDim.x * (kTPB / 64);
   for (u32 t = t_begin + w0; t < t_end; t += nw) {
@@ -286,6 +288,7 @@ __device__ __forceinline__ void apply_sweep(const PushArgs<V>& a, i64 delta, i64
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i64* __restrict__ desc, u32 t_begin,
                                                           u32 t_end) {
+  if (a.ctl->cancel) return;  // a gated push whose gate was set applies nothing (and leaves the hint)
   const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
   if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0 && a.hint)  // for the host's next push: how unordered was this one?
     __hip_atomic_store(a.hint, brk == 0u ? 0ull : (u64)(a.n - (i64)(a.ntiles - brk) * kTile), __ATOMIC_RELAXED,
@@ -384,6 +387,12 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
     }
     __syncthreads();
   }
+}
+
+// A gated push (glint_vec_push_dev_gated): its LaunchCtl learns, on the device, whether the gate word
+// is set; push_check and push_apply then do nothing, and the tail is empty (brk_enc stays 0).
+__global__ void push_gate_kernel(const u64* gate, LaunchCtl* ctl) {
+  if (threadIdx.x == 0) ctl->cancel = *gate != 0ull ? 1u : 0u;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -608,14 +617,18 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
 
   const int bmode = binned_mode();
   const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
+  const bool gated = s->gate != nullptr;
+  // a gated push takes check + apply (+ its tail from the break): those kernels read the gate's
+  // verdict from the LaunchCtl (the unordered hint and the one-launch small push have no such step)
+  if (gated && (det || !vec_ok)) return GLINT_EINVAL;
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
-  if (binned && unordered) return push_binned<V, MAT>(s, a, false, st);
+  if (binned && unordered && !gated) return push_binned<V, MAT>(s, a, false, st);
   // Small pushes (an Akka message is ~1000 records, GranularBigVectorSpec.scala:21) are one launch:
   // the scatter handles every record, instead of check + apply + scatter. Launch latency is the
   // whole cost at this size, so two fewer launches is the win; results are those of the scatter
   // path (bit-exact for unique keys and for Int/Long, unordered sums otherwise).
-  const bool small = !det && n <= small_push_max();
+  const bool small = !det && !gated && n <= small_push_max();
   if (!vec_ok || small) {  // unaligned caller pointers or a small push: the scatter for everything
     if (det) return push_det_tail<V, MAT>(s, a, false, st);
     const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
@@ -626,6 +639,10 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
     static EnvKnob check_bpc("GLINT_CHECK_BPC");
+    if (gated) {
+      push_gate_kernel<<<1, 64, 0, st>>>(s->gate, a.ctl);
+      HIPCHK(hipGetLastError());
+    }
     // one launch: the key stream alone lost 3-6 % when windowed (each short launch ramps up and drains)
     const unsigned gc =
         grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu<push_check_kernel<MAT, 0>>(2, &check_bpc));
@@ -1049,6 +1066,36 @@ int glint_mat_push_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
+  GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
+}
+
+int glint_vec_push_dev_gated(glint_shard_t s, const int64_t* keys, const void* vals, int64_t n, int flags,
+                             const uint64_t* gate, void* stream) {
+  if (!s || n < 0 || !gate) return GLINT_EINVAL;
+  if (s->part.cols != 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
+  struct Gate {
+    glint_shard* s;
+    ~Gate() { s->gate = nullptr; }
+  } reset{s};
+  s->gate = (const u64*)gate;
+  GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)keys, nullptr, vals, n, flags, pick(s, stream));
+}
+
+int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t* cols, const void* vals, int64_t n,
+                             int flags, const uint64_t* gate, void* stream) {
+  if (!s || n < 0 || !gate) return GLINT_EINVAL;
+  if (s->part.cols == 0) return GLINT_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
+  struct Gate {
+    glint_shard* s;
+    ~Gate() { s->gate = nullptr; }
+  } reset{s};
+  s->gate = (const u64*)gate;
   GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
 }
 

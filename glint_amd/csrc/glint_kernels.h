@@ -53,7 +53,8 @@ constexpr int kPushHostSequential = 1 << 16;
 struct LaunchCtl {
   u32 brk_enc;    // max over tiles that break the increasing order of (ntiles - t); 0 = none
   u32 nonaffine;  // some tile is not affine or does not continue its predecessor's affine run
-  u32 pad_[2];
+  u32 cancel;     // a gated push whose gate word was set: it applies nothing (push_gate_kernel)
+  u32 pad_;
 };
 
 // persistent error state, cleared by glint_shard_sync / host-pointer calls

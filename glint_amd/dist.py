@@ -336,6 +336,29 @@ class _Distributed:
             if t.is_cuda and hasattr(sh, "sync"):
                 sh.sync(torch.cuda.current_stream(t.device).cuda_stream)
 
+    def _push_gated(self, keys: torch.Tensor, args: tuple, deterministic: bool) -> bool:
+        """A world of one with one partition: the batch is the shard's push as it is. The key check
+        (the route's validation pass) and the push are enqueued back to back -- the push gated on the
+        route's status word on the device (glint_*_push_dev_gated: a batch with an out-of-range key
+        applies nothing, as mapPartitions throws before sending, AsyncBigVector.scala:96-98) -- and the
+        host reads the word after the one wait, so no synchronisation sits between them. Returns False
+        when the call does not qualify (the general path then runs)."""
+        if not (self.world == 1 and self.router.nparts == 1 and keys.is_cuda and not deterministic
+                and self._on_shard_device(keys) and hasattr(self.shards[0], "handle")):
+            return False
+        esz = args[-1].element_size()
+        if keys.data_ptr() % 16 or args[-1].data_ptr() % (2 * esz) or (len(args) == 3 and args[1].data_ptr() % 8):
+            return False
+        _, _, _, _, _, bad = self.router.route(keys)
+        sh = self.shards[0]
+        sh.update(*args, gate=bad, sync=False)
+        sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
+        b = int(bad.cpu()[0])
+        if b != 0:
+            i = ~b
+            raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.router.nkeys})")
+        return True
+
     def _answer(self, ex: _Exchange, order, bufs: tuple, caller: torch.Tensor, tail: tuple, get):
         """The pull's answer path: each local shard answers its records (get(shard, parts, out)), the
         answers travel back along the reversed splits and land in the caller's order
@@ -398,6 +421,8 @@ class DistributedBigVector(_Distributed):
         values = values.reshape(-1).to(self.dtype)
         if keys.numel() != values.numel():
             raise ValueError("keys and values differ in length")
+        if values.device == keys.device and self._push_gated(keys, (keys, values.contiguous()), deterministic):
+            return True
         if keys.is_cuda and values.device == keys.device:
             ex, _, sk, _, sv = self._begin_fused(keys, vals=values.contiguous())
             rk, rv = ex.forward(sk), ex.forward(sv)
@@ -442,6 +467,9 @@ class DistributedBigMatrix(_Distributed):
         values = values.reshape(-1).to(self.dtype)
         if not rows.numel() == cols.numel() == values.numel():
             raise ValueError("rows, cols and values differ in length")
+        if cols.device == rows.device and values.device == rows.device and \
+                self._push_gated(rows, (rows, cols.contiguous(), values.contiguous()), deterministic):
+            return True
         if rows.is_cuda and cols.device == rows.device and values.device == rows.device:
             ex, _, sr, sc, sv = self._begin_fused(rows, cols=cols.contiguous(), vals=values.contiguous())
             rr, rc, rv = (ex.forward(t) for t in (sr, sc, sv))

@@ -253,14 +253,21 @@ class PartialVector(_Shard):
     def __init__(self, partition: Partition, dtype="double", device: int = 0):
         super().__init__(partition, dtype, 0, device)
 
-    def update(self, keys, values, deterministic: bool = False, sync: bool = True, unordered: bool = False) -> bool:
+    def update(self, keys, values, deterministic: bool = False, sync: bool = True, unordered: bool = False,
+               gate=None) -> bool:
         """PartialVector.update (PartialVector.scala:35-43): data(globalToLocal(k)) += v.
-        ``unordered`` is a performance hint (GLINT_PUSH_UNORDERED): skip the order check, bin by slab."""
+        ``unordered`` is a performance hint (GLINT_PUSH_UNORDERED): skip the order check, bin by slab.
+        ``gate`` (device tensors only): a one-element int64 device tensor; the push applies nothing if
+        it is nonzero when the push runs (glint_vec_push_dev_gated)."""
         flags = _flags(deterministic, unordered)
         if _is_torch_cuda(keys):
             self._check_dev(keys.numel(), keys, values=values)
-            rc = self.lib.glint_vec_push_dev(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(), flags,
-                                             self._stream_of(keys))
+            if gate is not None:
+                rc = self.lib.glint_vec_push_dev_gated(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(),
+                                                       flags, gate.data_ptr(), self._stream_of(keys))
+            else:
+                rc = self.lib.glint_vec_push_dev(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(), flags,
+                                                 self._stream_of(keys))
             check(rc, self.handle)
             if sync:
                 self.sync(self._stream_of(keys))
@@ -322,13 +329,18 @@ class PartialMatrix(_Shard):
         self.rows = self.size
 
     def update(self, rows, cols, values, deterministic: bool = False, sync: bool = True,
-               unordered: bool = False) -> bool:
-        """PartialMatrix.update (PartialMatrix.scala:74-83)."""
+               unordered: bool = False, gate=None) -> bool:
+        """PartialMatrix.update (PartialMatrix.scala:74-83); ``gate`` as for PartialVector.update."""
         flags = _flags(deterministic, unordered)
         if _is_torch_cuda(rows):
             self._check_dev(rows.numel(), rows, cols=cols, values=values)
-            rc = self.lib.glint_mat_push_dev(self.handle, rows.data_ptr(), cols.data_ptr(), values.data_ptr(),
-                                             rows.numel(), flags, self._stream_of(rows))
+            if gate is not None:
+                rc = self.lib.glint_mat_push_dev_gated(self.handle, rows.data_ptr(), cols.data_ptr(),
+                                                       values.data_ptr(), rows.numel(), flags, gate.data_ptr(),
+                                                       self._stream_of(rows))
+            else:
+                rc = self.lib.glint_mat_push_dev(self.handle, rows.data_ptr(), cols.data_ptr(), values.data_ptr(),
+                                                 rows.numel(), flags, self._stream_of(rows))
             check(rc, self.handle)
             if sync:
                 self.sync(self._stream_of(rows))

@@ -130,6 +130,18 @@ int glint_mat_pull_dev(glint_shard_t shard, const int64_t* rows, const int32_t* 
 int glint_mat_pull_rows_dev(glint_shard_t shard, const int64_t* rows, void* out, int64_t n,
                             void* stream);
 
+/* glint_vec_push_dev / glint_mat_push_dev behind a device-side gate: the push is enqueued at once,
+ * and when it runs it applies NOTHING if the 64-bit device word *gate is nonzero (a route status word,
+ * glint_route_gather_dev's bad_dev: a batch with a key outside the partitioner is not applied, as
+ * AsyncBigVector.mapPartitions throws before any message is sent, AsyncBigVector.scala:96-98). The
+ * client reads the word after its one wait, so no host synchronisation separates the route from the
+ * push. The push takes the check + apply path (GLINT_PUSH_UNORDERED is ignored); deterministic pushes
+ * and unaligned arrays (keys not 16-B aligned, values not 2-element aligned) are GLINT_EINVAL. */
+int glint_vec_push_dev_gated(glint_shard_t shard, const int64_t* keys, const void* vals, int64_t n,
+                             int flags, const uint64_t* gate, void* stream);
+int glint_mat_push_dev_gated(glint_shard_t shard, const int64_t* rows, const int32_t* cols,
+                             const void* vals, int64_t n, int flags, const uint64_t* gate, void* stream);
+
 /* Waits for the shard's pending device work on `stream` and returns GLINT_EOUTOFRANGE if any
  * device-resident call since the last sync saw an out-of-range record (first_bad_record = its
  * index within the call that saw it, may be NULL). Clears the device error state. */

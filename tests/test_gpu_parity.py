@@ -229,6 +229,52 @@ def test_windowed_sweep_odd_record_once(gpu, monkeypatch, n, window):
             assert torch.equal(got, want), f"{dtype} n={n}"
 
 
+@pytest.mark.parametrize("pattern", ["dense", "zipf_binned", "small", "matrix"])
+def test_gated_push(gpu, pattern):
+    """glint_*_push_dev_gated: with the gate word set the push applies nothing and reports nothing;
+    with it clear the push is the plain device push; a cancelled push leaves no trace on the pushes
+    after it (the LaunchCtl slots alternate and each check clears the next one's cancel word)."""
+    import torch
+    d = torch.device("cuda", gpu)
+    rng = np.random.default_rng(17)
+    size = 1 << 22
+    if pattern == "matrix":
+        part = RangePartition(0, 0, 1 << 12)
+        sh = PartialMatrix(part, 512, "long", gpu)
+        r = torch.from_numpy(rng.integers(0, 1 << 12, 1 << 21).astype(np.int64)).to(d)
+        c = torch.from_numpy(rng.integers(0, 512, 1 << 21).astype(np.int32)).to(d)
+        v = torch.from_numpy(rng.integers(-9, 9, 1 << 21).astype(np.int64)).to(d)
+        args = (r, c, v)
+        flat = r * 512 + c.to(torch.int64)
+        ref = torch.zeros((1 << 12) * 512, dtype=torch.int64, device=d)
+    else:
+        part = RangePartition(0, 0, size)
+        sh = PartialVector(part, "long", gpu)
+        if pattern == "dense":
+            k = torch.arange(size, dtype=torch.int64, device=d)
+        elif pattern == "small":
+            k = torch.from_numpy(rng.integers(0, size, 1000).astype(np.int64)).to(d)
+        else:
+            k = torch.from_numpy(np.minimum(rng.zipf(1.1, 1 << 21) - 1, size - 1).astype(np.int64)).to(d)
+        v = torch.from_numpy(rng.integers(-9, 9, k.numel()).astype(np.int64)).to(d)
+        args = (k, v)
+        flat = k
+        ref = torch.zeros(size, dtype=torch.int64, device=d)
+    on = torch.ones(1, dtype=torch.int64, device=d)
+    off = torch.zeros(1, dtype=torch.int64, device=d)
+    with sh:
+        def state():
+            if pattern == "matrix":
+                return sh.getRows(torch.arange(1 << 12, dtype=torch.int64, device=d)).reshape(-1)
+            return sh.get(torch.arange(size, dtype=torch.int64, device=d))
+        for gate, applied in ((off, True), (on, False), (off, True), (on, False), (on, False), (None, True),
+                              (off, True)):
+            sh.update(*args, gate=gate)  # sync=True: a cancelled push reports no error either
+            if applied:
+                ref.index_add_(0, flat, args[-1])
+            assert torch.equal(state(), ref)
+
+
 def test_zipf_fixture_default_mode(gpu):
     z = np.load(GOLD / "zipf_push.npz")
     start, size = int(z["start"]), int(z["size"])

@@ -42,10 +42,12 @@
  * links, done once per client batch for the push and again for the pull, and timed on its own:
  *   groupby  the reference's algorithm restated: per GranularBigVector slice, one pass over its
  *            records appending each index to its partition's list (keys.indices.groupBy(partition));
- *   device   offloaded: the client's whole batch routed on the GPU by glint_route_dev (a stable
- *            counting sort by partition, one launch), then each partition's ordered index list is cut
- *            at the slice boundaries. Each client holds its device buffers, pinned read-back memory and
- *            its own stream from before the timed region. Both give the same messages, record for record.
+ *   device   offloaded: the client's whole batch (in pinned memory) routed on the GPU by
+ *            glint_route_gather_dev (a stable counting sort by partition, no synchronisation inside), the
+ *            order, counts and status word read back with the one wait, then each partition's ordered
+ *            index list is cut at the slice boundaries. Each client holds its device buffers, pinned
+ *            memory and its own stream from before the timed region. Both give the same messages, record
+ *            for record.
  *
  * Output: one JSON line.
  */
@@ -680,7 +682,8 @@ static int (*hip_memcpy_async)(void*, const void*, size_t, int, void*);
 static int (*hip_stream_create)(void**, unsigned);
 static int (*hip_stream_sync)(void*);
 static int (*hip_host_malloc)(void**, size_t, unsigned);
-static int (*route_dev)(const int64_t*, int64_t, int, int32_t, int64_t, int64_t*, int64_t*, int64_t*, void*);
+static int (*route_gather_dev)(const int64_t*, const int32_t*, const void*, int, int64_t, int, int32_t, int64_t,
+                               const int32_t*, int64_t*, int64_t*, int64_t*, int32_t*, void*, uint64_t*, void*);
 
 /* per partition: its record indices in record order (idx[p][0..cnt[p])) -> the link's messages, cut at
  * the GranularBigVector slice boundaries (every M records) */
@@ -702,19 +705,26 @@ static void cut_messages(link_arg* l, int64_t* idx, int64_t cnt) {
 
 /* A client's device context for the offloaded bucketing, set up before the timed region (a client
  * process holds its GPU buffers and stream for its lifetime): keys in, counts and order out, the order
- * read back into pinned host memory, all on the client's own stream. */
+ * read back into pinned host memory, all on the client's own stream. The client's batch itself lives
+ * in pinned memory (a JVM client would fill a direct buffer), so it crosses PCIe in one DMA with no
+ * staging copy; the route (glint_route_gather_dev) does not synchronise, so the whole offload is one
+ * wait: keys over, route, order + counts + status word back. */
 typedef struct {
-  void *dk, *dc, *dord, *stream;
+  void *dk, *dc, *dord, *dbad, *stream;
   int64_t* order; /* pinned */
-  int64_t* cnt;   /* pinned */
+  int64_t* cnt;   /* pinned: S counts, then the status word */
+  int64_t* keys;  /* pinned: the client's batch */
 } client_dev;
 
-static void client_dev_init(client_dev* d, int64_t n) {
+static void client_dev_init(client_dev* d, const int64_t* keys, int64_t n) {
   const size_t b = (size_t)(n > 0 ? n : 1) * 8;
-  if (hip_malloc(&d->dk, b) || hip_malloc(&d->dc, (size_t)S * 8) || hip_malloc(&d->dord, b)) die("hipMalloc");
+  if (hip_malloc(&d->dk, b) || hip_malloc(&d->dc, (size_t)S * 8 + 8) || hip_malloc(&d->dord, b)) die("hipMalloc");
+  d->dbad = (char*)d->dc + (size_t)S * 8;
   if (hip_stream_create(&d->stream, 1 /* hipStreamNonBlocking */)) die("hipStreamCreateWithFlags");
-  if (hip_host_malloc((void**)&d->order, b, 0) || hip_host_malloc((void**)&d->cnt, (size_t)S * 8, 0))
+  if (hip_host_malloc((void**)&d->order, b, 0) || hip_host_malloc((void**)&d->cnt, (size_t)S * 8 + 8, 0) ||
+      hip_host_malloc((void**)&d->keys, b, 0))
     die("hipHostMalloc");
+  memcpy(d->keys, keys, (size_t)n * 8);
 }
 
 /* Buckets client c's batch for its S links; returns the seconds it took. `store` receives the S
@@ -723,15 +733,15 @@ static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int
   const double t0 = now_s();
   int64_t* cnt = (int64_t*)calloc((size_t)S, 8);
   if (bucket_device && n > 0) {
-    /* offloaded: one stable route of the whole batch on the GPU (glint_route_dev), on the client's stream */
-    if (hip_memcpy_async(d->dk, keys, (size_t)n * 8, 1 /* hipMemcpyHostToDevice */, d->stream)) die("hipMemcpyAsync");
-    int64_t bad = -1;
-    if (route_dev((const int64_t*)d->dk, n, 0 /* GLINT_ROUTE_RANGE */, S, N, (int64_t*)d->dc, (int64_t*)d->dord, &bad,
-                  d->stream))
-      die("glint_route_dev");
+    /* offloaded: one stable route of the whole batch on the GPU, on the client's stream, one wait */
+    if (hip_memcpy_async(d->dk, d->keys, (size_t)n * 8, 1 /* hipMemcpyHostToDevice */, d->stream)) die("hipMemcpyAsync");
+    if (route_gather_dev((const int64_t*)d->dk, NULL, NULL, 0, n, 0 /* GLINT_ROUTE_RANGE */, S, N, NULL,
+                         (int64_t*)d->dc, (int64_t*)d->dord, NULL, NULL, NULL, (uint64_t*)d->dbad, d->stream))
+      die("glint_route_gather_dev");
     if (hip_memcpy_async(d->order, d->dord, (size_t)n * 8, 2 /* DeviceToHost */, d->stream) ||
-        hip_memcpy_async(d->cnt, d->dc, (size_t)S * 8, 2, d->stream) || hip_stream_sync(d->stream))
+        hip_memcpy_async(d->cnt, d->dc, (size_t)S * 8 + 8, 2, d->stream) || hip_stream_sync(d->stream))
       die("hipMemcpyAsync");
+    if (d->cnt[S] != 0) die("glint_route_gather_dev: key outside the partitioner");
     memcpy(cnt, d->cnt, (size_t)S * 8);
     const int64_t* order = d->order;
     int64_t o = 0;
@@ -928,10 +938,10 @@ int main(int argc, char** argv) {
     *(void**)&hip_stream_create = dlsym(hip_dl, "hipStreamCreateWithFlags");
     *(void**)&hip_stream_sync = dlsym(hip_dl, "hipStreamSynchronize");
     *(void**)&hip_host_malloc = dlsym(hip_dl, "hipHostMalloc");
-    *(void**)&route_dev = dlsym(dl, "glint_route_dev");
+    *(void**)&route_gather_dev = dlsym(dl, "glint_route_gather_dev");
     if (!hip_malloc || !hip_free || !hip_memcpy_async || !hip_stream_create || !hip_stream_sync || !hip_host_malloc ||
-        !route_dev)
-      die("dlsym hip*/glint_route_dev");
+        !route_gather_dev)
+      die("dlsym hip*/glint_route_gather_dev");
   }
 
   /* RangePartitioner.apply(S, N) (RangePartitioner.scala:62-84) and partition() (:27-43) */
@@ -1017,7 +1027,7 @@ int main(int argc, char** argv) {
   pthread_t* ct = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)C);
   client_arg* cargs = (client_arg*)calloc((size_t)C, sizeof(client_arg));
   if (bucket_device)
-    for (int c = 0; c < C; ++c) client_dev_init(&cargs[c].dev, cn[c]);
+    for (int c = 0; c < C; ++c) client_dev_init(&cargs[c].dev, ck[c], cn[c]);
   double t[3], bucket_s[2] = {0, 0}, bucket_max[2] = {0, 0};
   int64_t msgs[2] = {0, 0}, resends = 0;
   for (int mode = 0; mode < 2; ++mode) {
