@@ -75,6 +75,49 @@ struct BinGeom {
 __device__ __forceinline__ u32 bucket_of(u32 a, const BinGeom& g) { return a >> (kSlabBits + g.fb); }
 __device__ __forceinline__ u32 fine_of(u32 a, const BinGeom& g) { return (a >> kSlabBits) & (g.nf - 1); }
 
+// Skew-proof LDS counting: a Zipf tail's hot slab makes most lanes of a wave add to ONE LDS counter,
+// and same-address atomics serialise (a tile whose 2048 records hit one slab made 2048 of them). Up to
+// kPeel times per wave instruction, the digit of the first lane still unserved is broadcast; if at
+// least kPeelMin lanes share it, one lane adds the group's size and the group's ranks follow from a
+// popcount. The other lanes add one by one as before (uniform keys: nothing to peel, two ballots of
+// overhead). GLINT_BIN_MATCH=0 builds the plain per-record atomics (A/B).
+#ifndef GLINT_BIN_MATCH
+#define GLINT_BIN_MATCH 1
+#endif
+constexpr int kPeel = 1, kPeelMin = 8;
+// rank of this lane's record among its digit's records counted so far (cnt[d] advances); 0 if !valid.
+// Called by every lane of the wave (wave-uniform control flow).
+template <bool RANK>
+__device__ __forceinline__ u32 peel_add(u32* cnt, u32 d, bool valid) {
+  u32 r = 0;
+#if GLINT_BIN_MATCH
+  const int lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1ull;
+  u64 rem = __ballot(valid);
+  bool done = !valid;
+#pragma unroll
+  for (int it = 0; it < kPeel; ++it) {
+    if (!rem) break;
+    const int l = __ffsll((long long)rem) - 1;
+    const u32 dl = __shfl(d, l);
+    const u64 same = __ballot(!done && d == dl);
+    if (__popcll(same) < kPeelMin) break;
+    u32 base = 0;
+    if (lane == l) base = atomicAdd(&cnt[dl], (u32)__popcll(same));
+    if (RANK) base = __shfl(base, l);
+    if ((same >> lane) & 1ull) {
+      r = base + (u32)__popcll(same & below);
+      done = true;
+    }
+    rem &= ~same;
+  }
+  if (!done) r = RANK ? atomicAdd(&cnt[d], 1u) : (atomicAdd(&cnt[d], 1u), 0u);
+#else
+  if (valid) r = atomicAdd(&cnt[d], 1u);
+#endif
+  return r;
+}
+
 struct BinCtl {
   u32 m;       // records the partition emitted (after dedup)
   u32 tail;    // valid records in the tail
@@ -466,8 +509,7 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   const int tid = threadIdx.x;
   u32 rank[P];
 #pragma unroll
-  for (int j = 0; j < P; ++j)
-    if (valid & (1u << j)) rank[j] = atomicAdd(&dcnt[bucket_of(ad[j], g)], 1u);
+  for (int j = 0; j < P; ++j) rank[j] = peel_add<true>(dcnt, bucket_of(ad[j], g), (valid >> j) & 1u);
   __syncthreads();
   ph.mark(pb);
   const u32 total = block_scan<kATPB, 1>(
@@ -1049,7 +1091,7 @@ __global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, co
       }
 #pragma unroll
       for (int q = 0; q < kFCPer; ++q)
-        if (v0 + (u32)q * kFCTPB + (u32)tid < v1) atomicAdd(&fh[fine_of(a[q], g)], 1u);
+        peel_add<false>(fh, fine_of(a[q], g), v0 + (u32)q * kFCTPB + (u32)tid < v1);
     }
     __syncthreads();
     for (u32 f = tid; f < g.nf; f += kFCTPB) {
@@ -1178,8 +1220,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
       fetch(t0 + (TPB * kFPer));  // the next tile, in flight during this one's ranking, scan and stores
       ph.mark(25);
 #pragma unroll
-      for (int q = 0; q < kFPer; ++q)
-        if ((valid >> q) & 1u) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
+      for (int q = 0; q < kFPer; ++q) {
+        rank[q] = peel_add<true>(tcnt, fine_of(a[q], g), (valid >> q) & 1u);
+        __builtin_amdgcn_sched_barrier(0);  // one record at a time: interleaved, the peels spilled ~20 VGPRs
+      }
       __syncthreads();
       ph.mark(26);
       const u32 total = block_scan<TPB, 4>(
