@@ -118,6 +118,40 @@ __device__ __forceinline__ u32 peel_add(u32* cnt, u32 d, bool valid) {
   return r;
 }
 
+// The same peel for LDS sums: the lanes holding the hot element sum their values across the wave
+// (butterfly), and one lane adds the group's sum (a hot slab's records otherwise serialise on one
+// ds_add per record). Default mode only: the order of the additions is free there.
+template <typename A>
+__device__ __forceinline__ A wave_sum(A x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x = vadd(x, __shfl_xor(x, d));  // Int/Long wrap, as the JVM's +
+  return x;
+}
+template <typename A>
+__device__ __forceinline__ void peel_accum(A* acc, u32 e, A v, bool valid) {
+#if GLINT_BIN_MATCH
+  const int lane = threadIdx.x & 63;
+  u64 rem = __ballot(valid);
+  bool done = !valid;
+#pragma unroll
+  for (int it = 0; it < kPeel; ++it) {
+    if (!rem) break;
+    const int l = __ffsll((long long)rem) - 1;
+    const u32 el = __shfl(e, l);
+    const u64 same = __ballot(!done && e == el);
+    if (__popcll(same) < kPeelMin) break;
+    const bool in = (same >> lane) & 1ull;
+    const A x = wave_sum<A>(in ? v : A(0));
+    if (lane == l) lds_add(&acc[el], x);
+    done = done || in;
+    rem &= ~same;
+  }
+  if (!done) lds_add(&acc[e], v);
+#else
+  if (valid) lds_add(&acc[e], v);
+#endif
+}
+
 struct BinCtl {
   u32 m;       // records the partition emitted (after dedup)
   u32 tail;    // valid records in the tail
@@ -1378,10 +1412,10 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
       } else {
 #pragma unroll
         for (int q = 0; q < kCRB; ++q) {
-          if (ca[q] == kEmptySlot) continue;
+          const bool ok = ca[q] != kEmptySlot;
           const u32 e = ca[q] & (kSlab - 1);
-          lds_add(&acc[e], cv[q]);
-          touched[e] = 1;
+          peel_accum<A>(acc, e, cv[q], ok);
+          if (ok) touched[e] = 1;
         }
       }
       j0 += (u32)kCTPB * kCRB;
