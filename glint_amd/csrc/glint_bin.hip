@@ -56,8 +56,13 @@ constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments
 constexpr int kFPer = 8;               // records per thread per fine-partition tile (tile = TPB * kFPer;
                                        // bin_fpart runs at 256 or 512 threads, chosen per push)
 constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
-constexpr int kFCTPB = 512;            // bin_fcount's workgroup size: a whole item's addresses in flight
-constexpr int kFCPer = (int)kFItem / kFCTPB;  // at once, kFCPer per thread
+// bin_fcount, two shapes: a push with more items than the resident 256-thread workgroups walks each
+// item in 2048-record tiles (one tile in flight ahead); a small push (cfg5: ~640 items) takes one
+// 512-thread workgroup per item with the item's 16384 addresses in flight at once (the tile walk was 8
+// dependent round trips per item there: cfg5 0.435 -> 0.406 ms; cfg3's ~1500 items lost 3 % with it)
+constexpr int kFCTPB = 256;
+constexpr int kFCTPBWhole = 512;
+constexpr int kFCPer = (int)kFItem / kFCTPBWhole;
 #ifndef GLINT_APPLY_TPB
 #define GLINT_APPLY_TPB 256
 #endif
@@ -74,83 +79,6 @@ struct BinGeom {
 };
 __device__ __forceinline__ u32 bucket_of(u32 a, const BinGeom& g) { return a >> (kSlabBits + g.fb); }
 __device__ __forceinline__ u32 fine_of(u32 a, const BinGeom& g) { return (a >> kSlabBits) & (g.nf - 1); }
-
-// Skew-proof LDS counting: a Zipf tail's hot slab makes most lanes of a wave add to ONE LDS counter,
-// and same-address atomics serialise (a tile whose 2048 records hit one slab made 2048 of them). Up to
-// kPeel times per wave instruction, the digit of the first lane still unserved is broadcast; if at
-// least kPeelMin lanes share it, one lane adds the group's size and the group's ranks follow from a
-// popcount. The other lanes add one by one as before (uniform keys: nothing to peel, two ballots of
-// overhead). GLINT_BIN_MATCH=0 builds the plain per-record atomics (A/B).
-#ifndef GLINT_BIN_MATCH
-#define GLINT_BIN_MATCH 1
-#endif
-constexpr int kPeel = 1, kPeelMin = 8;
-// rank of this lane's record among its digit's records counted so far (cnt[d] advances); 0 if !valid.
-// Called by every lane of the wave (wave-uniform control flow).
-template <bool RANK>
-__device__ __forceinline__ u32 peel_add(u32* cnt, u32 d, bool valid) {
-  u32 r = 0;
-#if GLINT_BIN_MATCH
-  const int lane = threadIdx.x & 63;
-  const u64 below = (1ull << lane) - 1ull;
-  u64 rem = __ballot(valid);
-  bool done = !valid;
-#pragma unroll
-  for (int it = 0; it < kPeel; ++it) {
-    if (!rem) break;
-    const int l = __ffsll((long long)rem) - 1;
-    const u32 dl = __shfl(d, l);
-    const u64 same = __ballot(!done && d == dl);
-    if (__popcll(same) < kPeelMin) break;
-    u32 base = 0;
-    if (lane == l) base = atomicAdd(&cnt[dl], (u32)__popcll(same));
-    if (RANK) base = __shfl(base, l);
-    if ((same >> lane) & 1ull) {
-      r = base + (u32)__popcll(same & below);
-      done = true;
-    }
-    rem &= ~same;
-  }
-  if (!done) r = RANK ? atomicAdd(&cnt[d], 1u) : (atomicAdd(&cnt[d], 1u), 0u);
-#else
-  if (valid) r = atomicAdd(&cnt[d], 1u);
-#endif
-  return r;
-}
-
-// The same peel for LDS sums: the lanes holding the hot element sum their values across the wave
-// (butterfly), and one lane adds the group's sum (a hot slab's records otherwise serialise on one
-// ds_add per record). Default mode only: the order of the additions is free there.
-template <typename A>
-__device__ __forceinline__ A wave_sum(A x) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) x = vadd(x, __shfl_xor(x, d));  // Int/Long wrap, as the JVM's +
-  return x;
-}
-template <typename A>
-__device__ __forceinline__ void peel_accum(A* acc, u32 e, A v, bool valid) {
-#if GLINT_BIN_MATCH
-  const int lane = threadIdx.x & 63;
-  u64 rem = __ballot(valid);
-  bool done = !valid;
-#pragma unroll
-  for (int it = 0; it < kPeel; ++it) {
-    if (!rem) break;
-    const int l = __ffsll((long long)rem) - 1;
-    const u32 el = __shfl(e, l);
-    const u64 same = __ballot(!done && e == el);
-    if (__popcll(same) < kPeelMin) break;
-    const bool in = (same >> lane) & 1ull;
-    const A x = wave_sum<A>(in ? v : A(0));
-    if (lane == l) lds_add(&acc[el], x);
-    done = done || in;
-    rem &= ~same;
-  }
-  if (!done) lds_add(&acc[e], v);
-#else
-  if (valid) lds_add(&acc[e], v);
-#endif
-}
 
 struct BinCtl {
   u32 m;       // records the partition emitted (after dedup)
@@ -543,7 +471,8 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   const int tid = threadIdx.x;
   u32 rank[P];
 #pragma unroll
-  for (int j = 0; j < P; ++j) rank[j] = peel_add<true>(dcnt, bucket_of(ad[j], g), (valid >> j) & 1u);
+  for (int j = 0; j < P; ++j)
+    if (valid & (1u << j)) rank[j] = atomicAdd(&dcnt[bucket_of(ad[j], g)], 1u);
   __syncthreads();
   ph.mark(pb);
   const u32 total = block_scan<kATPB, 1>(
@@ -612,6 +541,8 @@ __device__ __forceinline__ u32 bucket_items(u32 t, u32 bcap, u32 bserial) {
   if (!bcap) return max(1u, (t + kFItem - 1) / kFItem);
   return t == 0 ? 0u : t <= bserial ? 1u : (t + bcap - 1) / bcap;
 }
+// Also the per-bucket bases bin_fpart needs, once per push instead of once per fine item: T[nb + b] =
+// the bucket's first output record (records of buckets < b), T[2 nb + b] = its first apply item slot.
 __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
                                            BinCtl* bc, u32 bcap, u32 bserial) {
   const u32 tot = block_scan<kATPB, 1>(
@@ -621,6 +552,11 @@ __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restri
         for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
       });
   if (threadIdx.x == 0) bc->nfitems = tot;
+  u32* const TB = const_cast<u32*>(T) + g.nb;
+  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; }, [&](u32 b, u32 excl) { TB[b] = excl; });
+  block_scan<kATPB, 1>(
+      g.nb, [&](u32 b) { return g.nf + (T[b] + kCItem - 1) / kCItem; },
+      [&](u32 b, u32 excl) { TB[g.nb + b] = excl; });
 }
 
 __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
@@ -1097,12 +1033,12 @@ __device__ __forceinline__ u32 load_segments(const BinGeom& g, u32 G, u32 b, con
   return M;
 }
 
-// per item: records per slab -> H[slab] (exact counts after dedup)
-__global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
-                                                           const BinCtl* bc, const u32* __restrict__ segoff,
-                                                           const u32* __restrict__ seglen,
-                                                           const u32* __restrict__ addr_in, u32* __restrict__ H,
-                                                           u32* __restrict__ IH) {
+// per item: records per slab -> H[slab] (exact counts after dedup). WHOLE: see kFCTPBWhole.
+template <bool WHOLE>
+__global__ __launch_bounds__(WHOLE ? kFCTPBWhole : kFCTPB) void bin_fcount_kernel(
+    BinGeom g, u32 G, const uint2* __restrict__ fitems, const BinCtl* bc, const u32* __restrict__ segoff,
+    const u32* __restrict__ seglen, const u32* __restrict__ addr_in, u32* __restrict__ H, u32* __restrict__ IH) {
+  constexpr int TPB = WHOLE ? kFCTPBWhole : kFCTPB;
   __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
   __shared__ u32 fh[kMaxDigit];
   const int tid = threadIdx.x;
@@ -1110,25 +1046,38 @@ __global__ __launch_bounds__(kFCTPB) void bin_fcount_kernel(BinGeom g, u32 G, co
   for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
     const uint2 d = fitems[it];
     const u32 b = d.x;
-    for (u32 f = tid; f < g.nf; f += kFCTPB) fh[f] = 0;
-    const u32 M = load_segments<kFCTPB>(g, G, b, segoff, seglen, segpre, segst);
+    for (u32 f = tid; f < g.nf; f += TPB) fh[f] = 0;
+    const u32 M = load_segments<TPB>(g, G, b, segoff, seglen, segpre, segst);
     const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
-    if (v1 > v0) {
-      // the whole item's addresses are loaded at once (one memory round trip per item; with 256-thread
-      // workgroups walking 2048-record tiles a small push's item was 8 dependent round trips)
-      u32 s = 0;
-      u32 a[kFCPer];
+    u32 s = 0;
+    if (WHOLE) {
+      if (v1 > v0) {
+        u32 a[kFCPer];
 #pragma unroll
-      for (int q = 0; q < kFCPer; ++q) {
-        const u32 v = v0 + (u32)q * kFCTPB + (u32)tid;
-        a[q] = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
+        for (int q = 0; q < kFCPer; ++q) {
+          const u32 v = v0 + (u32)q * TPB + (u32)tid;
+          a[q] = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
+        }
+#pragma unroll
+        for (int q = 0; q < kFCPer; ++q)
+          if (v0 + (u32)q * TPB + (u32)tid < v1) atomicAdd(&fh[fine_of(a[q], g)], 1u);
       }
+    } else {
+      u32 a[kFPer], avalid = 0;
+      if (v1 > v0) avalid = fetch_addr<TPB>(v0, v1, s, segpre, segst, addr_in, a);
+      for (u32 t0 = v0; t0 < v1; t0 += TPB * kFPer) {
+        u32 cur[kFPer];
+        const u32 cvalid = avalid;
 #pragma unroll
-      for (int q = 0; q < kFCPer; ++q)
-        peel_add<false>(fh, fine_of(a[q], g), v0 + (u32)q * kFCTPB + (u32)tid < v1);
+        for (int q = 0; q < kFPer; ++q) cur[q] = a[q];
+        avalid = fetch_addr<TPB>(t0 + TPB * kFPer, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
+#pragma unroll
+        for (int q = 0; q < kFPer; ++q)
+          if ((cvalid >> q) & 1u) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
+      }
     }
     __syncthreads();
-    for (u32 f = tid; f < g.nf; f += kFCTPB) {
+    for (u32 f = tid; f < g.nf; f += TPB) {
       const u32 c = fh[f];
       IH[(size_t)it * g.nf + f] = c;  // this item's own histogram: bin_fpart reserves from it
       if (c) atomicAdd(&H[b * g.nf + f], c);
@@ -1183,14 +1132,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
     const uint2 d = fitems[it];
     const u32 b = d.x;
     // where the bucket's records go (raw capacities: holes only at bucket ends) and its item slots
-    u32 ob = 0, ib = 0;
-    for (u32 x = tid; x < b; x += TPB) {
-      const u32 t = T[x];
-      ob += t;
-      ib += g.nf + (t + kCItem - 1) / kCItem;
-    }
-    ob = block_sum<TPB>(ob);
-    ib = block_sum<TPB>(ib);
+    const u32 ob = T[g.nb + b], ib = T[2 * g.nb + b];  // the bucket's bases (part_items)
     for (u32 f = tid; f < g.nf; f += TPB) tcnt[f] = 0;
     block_scan<TPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
     ph.mark(20);
@@ -1254,10 +1196,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
       fetch(t0 + (TPB * kFPer));  // the next tile, in flight during this one's ranking, scan and stores
       ph.mark(25);
 #pragma unroll
-      for (int q = 0; q < kFPer; ++q) {
-        rank[q] = peel_add<true>(tcnt, fine_of(a[q], g), (valid >> q) & 1u);
-        __builtin_amdgcn_sched_barrier(0);  // one record at a time: interleaved, the peels spilled ~20 VGPRs
-      }
+      for (int q = 0; q < kFPer; ++q)
+        if ((valid >> q) & 1u) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
       __syncthreads();
       ph.mark(26);
       const u32 total = block_scan<TPB, 4>(
@@ -1412,10 +1352,10 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
       } else {
 #pragma unroll
         for (int q = 0; q < kCRB; ++q) {
-          const bool ok = ca[q] != kEmptySlot;
+          if (ca[q] == kEmptySlot) continue;
           const u32 e = ca[q] & (kSlab - 1);
-          peel_accum<A>(acc, e, cv[q], ok);
-          if (ok) touched[e] = 1;
+          lds_add(&acc[e], cv[q]);
+          touched[e] = 1;
         }
       }
       j0 += (u32)kCTPB * kCRB;
@@ -1775,7 +1715,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
   const i64 max_fitems = (i64)g.nb + n / (bap ? (i64)kBCap : (i64)kFItem) + 1;
   // [BinCtl | T | H | cur2] zeroed per push; then R, segoff, seglen, item maps, the record buffers
-  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
+  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4 * 3), b_seg = pad256((size_t)G * g.nb * 4);  // T + bases
   const size_t b_H = pad256((size_t)g.nslab * 4);
   const size_t b_cd = pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8) +
                       pad256((size_t)max_fitems * g.nf * 4);  // + per-item slab histograms
@@ -1872,10 +1812,16 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     HIPCHK(hipGetLastError());
   }
   static EnvKnob fcount_knob("GLINT_FCOUNT_BPC");
-  static const int fcount_occ = resident_per_cu(bin_fcount_kernel, kFCTPB);
-  const int fcount_rpc = (int)fcount_knob.pos_or(fcount_occ);
-  const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
-  bin_fcount_kernel<<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
+  static const int fcount_occ = resident_per_cu(bin_fcount_kernel<false>, kFCTPB);
+  static const int fcount_whole_occ = resident_per_cu(bin_fcount_kernel<true>, kFCTPBWhole);
+  if (max_fitems <= (i64)s->cus * fcount_whole_occ) {  // every item gets its own workgroup at once
+    bin_fcount_kernel<true><<<(unsigned)max_fitems, kFCTPBWhole, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H,
+                                                                        IH);
+  } else {
+    const int fcount_rpc = (int)fcount_knob.pos_or(fcount_occ);
+    const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
+    bin_fcount_kernel<false><<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
+  }
   HIPCHK(hipGetLastError());
   const size_t fdyn = fpart_dyn_bytes(G, g.nf);
   // workgroup size: 512 threads (4096-record tiles, whole-line runs) unless the push has no more

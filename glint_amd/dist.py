@@ -344,7 +344,8 @@ class _Distributed:
         host reads the word after the one wait, so no synchronisation sits between them. Returns False
         when the call does not qualify (the general path then runs)."""
         if not (self.world == 1 and self.router.nparts == 1 and keys.is_cuda and not deterministic
-                and self._on_shard_device(keys) and hasattr(self.shards[0], "handle")):
+                and self._on_shard_device(keys) and hasattr(self.shards[0], "handle")
+                and getattr(N.load(), "glint_vec_push_dev_gated", None) is not None):  # (an older A/B library)
             return False
         esz = args[-1].element_size()
         if keys.data_ptr() % 16 or args[-1].data_ptr() % (2 * esz) or (len(args) == 3 and args[1].data_ptr() % 8):
