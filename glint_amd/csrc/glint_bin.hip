@@ -543,20 +543,52 @@ __device__ __forceinline__ u32 bucket_items(u32 t, u32 bcap, u32 bserial) {
 }
 // Also the per-bucket bases bin_fpart needs, once per push instead of once per fine item: T[nb + b] =
 // the bucket's first output record (records of buckets < b), T[2 nb + b] = its first apply item slot.
+// The three exclusive scans over the buckets (items, records, apply slots) in one pass: workgroup 0
+// does this before its own chunks, so it must stay short (three separate scans cost cfg5 ~3 %).
 __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
                                            BinCtl* bc, u32 bcap, u32 bserial) {
-  const u32 tot = block_scan<kATPB, 1>(
-      g.nb, [&](u32 b) { return bucket_items(T[b], bcap, bserial); },
-      [&](u32 b, u32 excl) {
-        const u32 J = bucket_items(T[b], bcap, bserial);
-        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
-      });
-  if (threadIdx.x == 0) bc->nfitems = tot;
+  __shared__ u32 wt3[3][kATPB / 64];
   u32* const TB = const_cast<u32*>(T) + g.nb;
-  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; }, [&](u32 b, u32 excl) { TB[b] = excl; });
-  block_scan<kATPB, 1>(
-      g.nb, [&](u32 b) { return g.nf + (T[b] + kCItem - 1) / kCItem; },
-      [&](u32 b, u32 excl) { TB[g.nb + b] = excl; });
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  u32 carry[3] = {0, 0, 0};
+  for (u32 base = 0; base < g.nb; base += kATPB) {
+    const u32 b = base + (u32)tid;
+    const u32 t = b < g.nb ? T[b] : 0u;
+    const u32 v[3] = {b < g.nb ? bucket_items(t, bcap, bserial) : 0u, t, b < g.nb ? g.nf + (t + kCItem - 1) / kCItem : 0u};
+    u32 incl[3] = {v[0], v[1], v[2]};
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const u32 y = __shfl_up(incl[k], d);
+        if (lane >= d) incl[k] += y;
+      }
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) wt3[k][wid] = incl[k];
+    }
+    __syncthreads();
+    u32 excl[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      u32 run = carry[k] + incl[k] - v[k], tot = 0;
+      for (int w = 0; w < kATPB / 64; ++w) {
+        const u32 x = wt3[k][w];
+        run += w < wid ? x : 0u;
+        tot += x;
+      }
+      excl[k] = run;
+      carry[k] += tot;
+    }
+    if (b < g.nb) {
+      for (u32 j = 0; j < v[0]; ++j) fitems[excl[0] + j] = make_uint2(b, j);
+      TB[b] = excl[1];           // the bucket's first output record
+      TB[g.nb + b] = excl[2];    // its first apply item slot
+    }
+    __syncthreads();
+  }
+  if (tid == 0) bc->nfitems = carry[0];
 }
 
 __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,

@@ -1,4 +1,5 @@
-"""Summarises an `abn` session of tools/gpu_run.sh: ms per step of each (library, pattern) over rounds.
+"""Summarises an `abn` session of tools/gpu_run.sh: ms per step of each (library, pattern) over rounds,
+and the push kernels' summed device time per step (steadier than the wall time across rounds).
 
     python tools/ab_summary.py gpurun_out/<TAG>
 """
@@ -15,6 +16,6 @@ for f in sorted(Path(sys.argv[1]).glob("ab_*.log")):
     if not m or not line:
         continue
     d = json.loads(line[-1])
-    rows[(m.group(2), m.group(1))].append((d["ms_per_step"], d.get("check")))
+    rows[(m.group(2), m.group(1))].append((d["ms_per_step"], d.get("check"), d["roofline"].get("kernel_ms")))
 for (pat, lib), v in sorted(rows.items()):
-    print(f"{pat:10s} {lib:12s} ms {[x[0] for x in v]} check {[x[1] for x in v]}")
+    print(f"{pat:10s} {lib:12s} ms {[x[0] for x in v]} kernel ms {[x[2] for x in v]} check {[x[1] for x in v]}")
