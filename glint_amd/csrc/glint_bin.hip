@@ -533,20 +533,15 @@ __device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks,
 
 // Workgroup 0 of bin_part: the fine-partition items -- bucket b gets max(1, ceil(T[b] / kFItem))
 // of them ({b, j}: its records [j * kFItem, (j + 1) * kFItem) in segment order).
-// With bcap > 0 the items are the bucket apply's (bin_bapply): a bucket of at most bserial records is
-// ONE item (its records in phases of bcap, plain read-modify-write: no other item touches its slabs),
-// a larger one ceil(T / bcap) items of one phase each (their slabs shared: device atomics); empty
-// buckets get none.
-__device__ __forceinline__ u32 bucket_items(u32 t, u32 bcap, u32 bserial) {
-  if (!bcap) return max(1u, (t + kFItem - 1) / kFItem);
-  return t == 0 ? 0u : t <= bserial ? 1u : (t + bcap - 1) / bcap;
-}
+// fine-partition items of a bucket of t records: ceil(t / kFItem), at least one (the bucket's first
+// item writes its apply items)
+__device__ __forceinline__ u32 bucket_items(u32 t) { return max(1u, (t + kFItem - 1) / kFItem); }
 // Also the per-bucket bases bin_fpart needs, once per push instead of once per fine item: T[nb + b] =
 // the bucket's first output record (records of buckets < b), T[2 nb + b] = its first apply item slot.
 // The three exclusive scans over the buckets (items, records, apply slots) in one pass: workgroup 0
 // does this before its own chunks, so it must stay short (three separate scans cost cfg5 ~3 %).
 __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
-                                           BinCtl* bc, u32 bcap, u32 bserial) {
+                                           BinCtl* bc) {
   __shared__ u32 wt3[3][kATPB / 64];
   u32* const TB = const_cast<u32*>(T) + g.nb;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -554,7 +549,7 @@ __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restri
   for (u32 base = 0; base < g.nb; base += kATPB) {
     const u32 b = base + (u32)tid;
     const u32 t = b < g.nb ? T[b] : 0u;
-    const u32 v[3] = {b < g.nb ? bucket_items(t, bcap, bserial) : 0u, t, b < g.nb ? g.nf + (t + kCItem - 1) / kCItem : 0u};
+    const u32 v[3] = {b < g.nb ? bucket_items(t) : 0u, t, b < g.nb ? g.nf + (t + kCItem - 1) / kCItem : 0u};
     u32 incl[3] = {v[0], v[1], v[2]};
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -740,8 +735,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
                                                          BinCtl* bc, const u32* __restrict__ T,
                                                          uint2* __restrict__ fitems,
                                                          const unsigned long long* __restrict__ hot_best,
-                                                         typename LdsAcc<V>::T* __restrict__ hot_partial,
-                                                         u32 bcap, u32 bserial) {
+                                                         typename LdsAcc<V>::T* __restrict__ hot_partial) {
   typedef typename LdsAcc<V>::T A;
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
   __shared__ u32 st_a[kAChunk];
@@ -761,7 +755,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
     }
   }
   PhaseClock ph(0);
-  if (w == 0) part_items(g, T, fitems, bc, bcap, bserial);
+  if (w == 0) part_items(g, T, fitems, bc);
   part_setup(g, w, nchunks, R, segoff, cur, dcnt);
   ph.mark(0);
   const i64 G = gridDim.x;
@@ -884,7 +878,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   }
   if (tid == 0) nused = 0;
   PhaseClock ph(8);
-  if (w == 0) part_items(g, T, fitems, bc, 0u, 0u);
+  if (w == 0) part_items(g, T, fitems, bc);
   part_setup(g, w, nchunks, R, segoff, cur, dcnt);
   ph.mark(8);
   const u64 below = (1ull << lane) - 1ull;
@@ -1455,172 +1449,6 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
   ph.flush(6);
 }
 
-// ---- bucket apply: the fine partition and the slab apply in one pass (small pushes) ------------------
-// When a push's coarse buckets are small enough to be held in registers (cfg5: 2^23 records into
-// 1024 buckets of 16 slabs, 8192 records on average), the fine partition (bin_fcount + bin_fpart) and
-// the slab apply need not move the records again: one workgroup takes a whole bucket, loads a phase
-// of up to kBCap of its records into registers (16 per thread), counts them per slab in LDS, and
-// then, slab by slab (only the slabs with records), sums that slab's records in LDS and writes the
-// touched elements back with one read-modify-write. The bucket's records are read once (12 B each),
-// never written again; the slab RMW is the same as bin_apply's. A bucket larger than bserial is cut
-// into items of one phase each, whose slabs are shared: those flush with device atomics (the hot
-// rows of a Zipf matrix; LDS summing has merged their duplicates first).
-constexpr int kBTPB = 512;
-constexpr int kBPer = 16;
-constexpr u32 kBCap = (u32)kBTPB * kBPer;  // records per phase
-constexpr u32 kBSerial = 4 * kBCap;        // a bucket up to this size is one item (phases in sequence)
-
-template <typename V>
-__global__ __launch_bounds__(kBTPB) void bin_bapply_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
-                                                           BinCtl* bc, const u32* __restrict__ T,
-                                                           const u32* __restrict__ segoff,
-                                                           const u32* __restrict__ seglen,
-                                                           const u32* __restrict__ addr_in,
-                                                           const typename LdsAcc<V>::T* __restrict__ val_in,
-                                                           i64 elems, V* __restrict__ data, u32 sparse_max,
-                                                           u64* hint) {
-  typedef typename Vec2<V>::T V2;
-  typedef typename LdsAcc<V>::T A;
-  __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
-  __shared__ A acc[kSlab];
-  __shared__ uint8_t touched[kSlab];
-  __shared__ uint16_t tlist[kSparseCap];
-  __shared__ u32 scnt[kMaxDigit];
-  __shared__ u32 ntl[2], s_next;  // list lengths, alternating per slab (the other is reset meanwhile)
-  const int tid = threadIdx.x, lane = tid & 63;
-  const u64 below = (1ull << lane) - 1ull;
-  if (blockIdx.x == 0 && tid == 0 && hint) {  // for the host's next binned push (as bin_fpart reports it)
-    __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(hint + 1, (u64)bc->cold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  for (int e = tid; e < kSlab; e += kBTPB) acc[e] = A(0);
-  for (int w = tid; w < kSlab / 16; w += kBTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
-  for (u32 f = tid; f < g.nf; f += kBTPB) scnt[f] = 0;
-  u32 par = 0;
-  if (tid < 2) ntl[tid] = 0;
-  if (tid == 0) s_next = atomicAdd(&bc->fnext, 1u);
-  __syncthreads();
-  const u32 nit = bc->nfitems;
-  for (u32 it = s_next; it < nit; it = s_next) {
-    __syncthreads();  // every thread has read s_next
-    if (tid == 0) s_next = atomicAdd(&bc->fnext, 1u);  // the next item, in flight meanwhile
-    const uint2 d = fitems[it];
-    const u32 b = d.x;
-    const u32 M = load_segments<kBTPB>(g, G, b, segoff, seglen, segpre, segst);
-    const bool exclusive = T[b] <= kBSerial;  // the bucket is this one item (as bucket_items decided)
-    const u32 v0 = exclusive ? 0u : d.y * kBCap, v1 = exclusive ? M : min(M, v0 + kBCap);
-    u32 s = 0;
-    for (u32 p0 = v0; p0 < v1; p0 += kBCap) {
-      // the phase's records into registers (clamped, branch-free; validity as a mask), counted per slab
-      u32 ad[kBPer];  // element addresses; ~0u past the phase's end (no slab matches it)
-      A va[kBPer];
-#pragma unroll
-      for (int q = 0; q < kBPer; ++q) {
-        const u32 v = p0 + (u32)q * kBTPB + (u32)tid;
-        const u32 r = seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst);
-        ad[q] = ld_in(addr_in + r);
-        va[q] = ld_in(val_in + r);
-      }
-#pragma unroll
-      for (int q = 0; q < kBPer; ++q) {
-        if (p0 + (u32)q * kBTPB + (u32)tid >= v1) ad[q] = ~0u;
-        else atomicAdd(&scnt[fine_of(ad[q], g)], 1u);
-      }
-      __syncthreads();
-#pragma unroll 1
-      for (u32 f = 0; f < g.nf; ++f) {  // workgroup-uniform: the slabs of the bucket with records
-        const u32 c = scnt[f];
-        if (c == 0) continue;
-        const bool sparse = c <= sparse_max;
-        const u32 slab = b * g.nf + f;
-        const i64 sbase_g = (i64)slab << kSlabBits;
-        V* const sbase = data + sbase_g;
-#pragma unroll
-        for (int q = 0; q < kBPer; ++q) {
-          u32 x = ad[q];
-          asm volatile("" : "+v"(x));  // per slab, not hoisted: 16 records' LDS addresses would cost ~100 VGPRs
-          const bool mine = (x >> kSlabBits) == slab;
-          const u32 e = x & (kSlab - 1);
-          bool first = false;
-          if (mine) {
-            lds_add(&acc[e], va[q]);
-            if (sparse) {
-              const u32 sh = 8u * (e & 3u);
-              first = ((atomicOr(reinterpret_cast<u32*>(touched) + (e >> 2), 1u << sh) >> sh) & 0xFFu) == 0u;
-            } else {
-              touched[e] = 1;
-            }
-          }
-          if (sparse) {  // first touches listed once each (one LDS counter add per wave)
-            const u64 bl = __ballot(first);
-            if (bl) {
-              u32 base = 0;
-              if (lane == 0) base = atomicAdd(&ntl[par], (u32)__popcll(bl));
-              base = __shfl(base, 0);
-              if (first) tlist[base + (u32)__popcll(bl & below)] = (uint16_t)e;
-            }
-          }
-        }
-        __syncthreads();
-        if (sparse) {
-          // the other parity's list was read by the previous slab's flush, before the barrier that
-          // ended it, and is appended to only after the barrier that ends this one
-          if (tid == 0) ntl[par ^ 1u] = 0;
-          const u32 L = ntl[par];
-          for (u32 i = tid; i < L; i += kBTPB) {
-            const u32 e = tlist[i];
-            if (sbase_g + e < elems) {
-              if (exclusive) sbase[e] = acc_add(sbase[e], acc[e]);
-              else gadd(sbase + e, (V)acc[e]);
-            }
-            acc[e] = A(0);
-            touched[e] = 0;
-          }
-          par ^= 1u;
-        } else if (exclusive) {  // one coalesced RMW of the touched pairs
-          constexpr int kPairs = kSlab / 2 / kBTPB;
-          V2 dd[kPairs];
-          u32 t[kPairs];
-#pragma unroll
-          for (int q = 0; q < kPairs; ++q) {
-            const int e0 = 2 * (tid + q * kBTPB);
-            t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
-            const bool vec = t[q] != 0u && sbase_g + e0 + 1 < elems;
-            dd[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
-            if (t[q]) *reinterpret_cast<uint16_t*>(touched + e0) = 0;
-          }
-#pragma unroll
-          for (int q = 0; q < kPairs; ++q) {
-            if (t[q] == 0u) continue;
-            const int e0 = 2 * (tid + q * kBTPB);
-            if (sbase_g + e0 + 1 < elems) {
-              V2 r = dd[q];
-              if (t[q] & 1u) r.x = acc_add((V)r.x, acc[e0]);
-              if (t[q] & 2u) r.y = acc_add((V)r.y, acc[e0 + 1]);
-              *reinterpret_cast<V2*>(sbase + e0) = r;
-            } else {  // the shard's last element, odd count
-              sbase[e0] = acc_add(sbase[e0], acc[e0]);
-            }
-            acc[e0] = A(0);
-            acc[e0 + 1] = A(0);
-          }
-        } else {
-          for (int e = tid; e < kSlab; e += kBTPB) {
-            if (touched[e]) {
-              if (sbase_g + e < elems) gadd(sbase + e, (V)acc[e]);
-              acc[e] = A(0);
-              touched[e] = 0;
-            }
-          }
-        }
-        __syncthreads();
-      }
-      for (u32 f = tid; f < g.nf; f += kBTPB) scnt[f] = 0;
-      __syncthreads();
-    }
-  }
-}
-
 // ---- host side ----------------------------------------------------------------------------------------
 // records per slab item from which bin_apply warms the whole slab into L2 (GLINT_BIN_PREFETCH_MIN;
 // 0xFFFFFFFF disables)
@@ -1672,38 +1500,12 @@ BinGeom bin_geometry(i64 elems) {
   return g;
 }
 
-// The bucket apply's geometry: as many coarse buckets as the partition pass takes (<= 1024), so that
-// each holds few slabs and, on average, at most one phase of records.
-BinGeom bapply_geometry(i64 elems) {
-  const i64 slabs = (elems + kSlab - 1) / kSlab;
-  u32 sb = 0;
-  while (((i64)1 << sb) < slabs) ++sb;
-  const u32 cb = std::min<u32>(sb, 10u);
-  BinGeom g;
-  g.fb = sb - cb;
-  g.nb = 1u << cb;
-  g.nf = 1u << g.fb;
-  g.nslab = g.nb * g.nf;
-  return g;
-}
-
-// Whether a binned push takes the bucket apply (GLINT_BIN_BAPPLY: 0 never, 1 always, unset = when the
-// average bucket fits one phase: n / nb <= kBCap, e.g. cfg5's 2^23 records into 1024 buckets).
-bool use_bapply(i64 n, i64 elems) {
-  static EnvKnob k("GLINT_BIN_BAPPLY");
-  const int mode = (int)k.get([](const char* e) -> long long { return (e && *e) ? atoi(e) : -1; });
-  (void)n;
-  (void)elems;
-  return mode > 0;  // off by default: measured slower than the three-pass pipeline
-}
-
 template <typename V, bool MAT>
 int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   if (n >= ((i64)1 << 32) - 2 * kAChunk || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
-  const bool bap = use_bapply(n, s->elems);
-  const BinGeom g = bap ? bapply_geometry(s->elems) : bin_geometry(s->elems);
+  const BinGeom g = bin_geometry(s->elems);
   // Front end, from what the last dedup push measured (the device reports m, the tail size and the
   // cold records of each push through host-mapped words, taken at the shard's last sync point, so the
   // choice does not depend on timing): chunk dedup when it kept < 80 % of the cold records it saw;
@@ -1734,7 +1536,6 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   });
   if (forced == 2 || forced == 0) front = forced;
   else if (forced == 1) front = hot_on ? 1 : 0;
-  if (bap) front = 0;  // the bucket apply takes the plain front end
   const bool dedup = front == 2;
   s->bin_last_front = front;
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
@@ -1745,7 +1546,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : plain_wpc)));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
-  const i64 max_fitems = (i64)g.nb + n / (bap ? (i64)kBCap : (i64)kFItem) + 1;
+  const i64 max_fitems = (i64)g.nb + n / kFItem + 1;
   // [BinCtl | T | H | cur2] zeroed per push; then R, segoff, seglen, item maps, the record buffers
   const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4 * 3), b_seg = pad256((size_t)G * g.nb * 4);  // T + bases
   const size_t b_H = pad256((size_t)g.nslab * 4);
@@ -1823,22 +1624,9 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
                                  : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
-                              val_a, a.err, bc, T, fitems, wbest, wpart, bap ? kBCap : 0u, kBSerial);
+                              val_a, a.err, bc, T, fitems, wbest, wpart);
   }
   HIPCHK(hipGetLastError());
-  if (bap) {  // fine partition + apply in one pass over the buckets
-    static std::atomic<int> bap_rpc{0};
-    int r = bap_rpc.load(std::memory_order_relaxed);
-    if (!r) {
-      r = resident_per_cu(bin_bapply_kernel<V>, kBTPB);
-      bap_rpc.store(r, std::memory_order_relaxed);
-    }
-    const unsigned gb = (unsigned)std::max<i64>(1, std::min<i64>(max_fitems, (i64)s->cus * r));
-    bin_bapply_kernel<V><<<gb, kBTPB, 0, st>>>(g, G, fitems, bc, T, segoff, seglen, addr_a, val_a, s->elems, a.data,
-                                               bin_sparse_max(), s->d_hint ? s->d_hint + 1 : nullptr);
-    HIPCHK(hipGetLastError());
-    return GLINT_OK;
-  }
   if (front == 1) {
     bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
     HIPCHK(hipGetLastError());

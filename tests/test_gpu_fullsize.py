@@ -87,16 +87,9 @@ def test_cfg3_full_size(gpu, cfg3, mode):
         np.testing.assert_array_equal(got, ref.data)
 
 
-@pytest.mark.parametrize("mode", ["long", "double", "double_det", "long_three_pass"])
-def test_cfg5_slice_full_size(gpu, cfg5, mode, monkeypatch):
-    """The cfg5 slice takes the bucket apply by itself (2^23 records into 1024 buckets); long_three_pass
-    forces the three-pass pipeline (bin_fcount + bin_fpart + bin_apply) on the same push."""
+@pytest.mark.parametrize("mode", ["long", "double", "double_det"])
+def test_cfg5_slice_full_size(gpu, cfg5, mode):
     import torch
-    from glint_amd import _native as N
-    if mode == "long_three_pass":
-        monkeypatch.setenv("GLINT_BIN_BAPPLY", "0")
-        N.reload_env()
-        mode = "long"
     dev = torch.device("cuda", gpu)
     rows, cols, rng = cfg5
     dtype = "long" if mode == "long" else "double"

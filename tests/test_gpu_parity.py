@@ -730,7 +730,6 @@ def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
     Float sums over duplicates are checked against the exact (float64) sum within 1e-6 of the sum
     of magnitudes per element -- the reference's sequential float order is one rounding of many."""
     monkeypatch.setenv("GLINT_BIN_FRONT", front)
-    monkeypatch.setenv("GLINT_BIN_BAPPLY", "0")  # the three-pass pipeline (the bucket apply takes the plain front)
     N.reload_env()
     rng = np.random.default_rng(zlib.crc32(f"fronts/{front}/{dtype}/{pattern}".encode()))
     start, size = 1 << 33, 2_000_003
@@ -782,7 +781,6 @@ def test_binned_fronts(gpu, monkeypatch, front, dtype, pattern):
 @pytest.mark.parametrize("front", ["dedup", "hot", "prep"])
 def test_binned_fronts_matrix(gpu, monkeypatch, front):
     monkeypatch.setenv("GLINT_BIN_FRONT", front)
-    monkeypatch.setenv("GLINT_BIN_BAPPLY", "0")
     N.reload_env()
     rng = np.random.default_rng(23)
     rows_n, cols_n = 30_011, 129  # pitch 130: row padding stays untouched
@@ -796,88 +794,6 @@ def test_binned_fronts_matrix(gpu, monkeypatch, front):
     with PartialMatrix(part, cols_n, "long", gpu) as sh:
         sh.update(r, c, v, unordered=True)
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
-
-
-@pytest.mark.parametrize("dtype", ["double", "float", "long", "int"])
-@pytest.mark.parametrize("pattern", ["zipf", "hot_slab", "uniform", "with_prefix", "one_key", "unique", "big_bucket"])
-def test_binned_bucket_apply(gpu, monkeypatch, dtype, pattern):
-    """The bucket apply (bin_bapply: fine partition + slab apply in one pass over 1024 coarse buckets)
-    against the oracle: buckets of one item (phases in sequence, plain read-modify-write), hot buckets
-    cut into items that flush with device atomics (zipf, hot_slab, one_key), buckets over several phases
-    (big_bucket), sparse and dense slabs, and the shard's odd last element. Int/Long bit-exact; Double
-    within 1e-6 (plus 1e-9 absolute for sums that cancel); Float per sum of magnitudes."""
-    monkeypatch.setenv("GLINT_BIN_BAPPLY", "1")
-    N.reload_env()
-    rng = np.random.default_rng(zlib.crc32(f"bapply/{dtype}/{pattern}".encode()))
-    start, size = 1 << 33, 9_000_007  # 2198 slabs: 1024 buckets of 4 slabs
-    part = RangePartition(2, start, start + size)
-    n = 1_500_000
-    if pattern == "zipf":
-        keys = rng.permutation(size)[np.minimum(rng.zipf(1.1, n) - 1, size - 1)]
-    elif pattern == "hot_slab":
-        keys = rng.permutation(np.concatenate([rng.integers(4096, 4096 + 300, n // 2), rng.integers(0, size, n - n // 2)]))
-    elif pattern == "uniform":
-        keys = rng.integers(0, size, n)
-    elif pattern == "with_prefix":
-        keys = np.concatenate([np.arange(0, size, 2), rng.permutation(size)[np.minimum(rng.zipf(1.3, n) - 1, size - 1)]])
-    elif pattern == "unique":
-        keys = rng.permutation(size)[:n]
-    elif pattern == "big_bucket":  # one bucket gets ~3 phases' worth (still one item), the rest uniform
-        keys = rng.permutation(np.concatenate([rng.integers(1 << 16, (1 << 16) + 3 * 4096, 24_000),
-                                               rng.integers(0, size, n - 24_000)]))
-    else:
-        keys = np.full(n, size - 1)
-    keys = keys.astype(np.int64) + start
-    if dtype in ("long", "int"):
-        vals = rand_vals(rng, dtype, keys.size) if dtype == "int" else rng.integers(-1 << 40, 1 << 40, keys.size)
-    else:
-        vals = rand_vals(rng, dtype, keys.size)
-    ref = oracle_vec(part, dtype)
-    with PartialVector(part, dtype, gpu) as sh:
-        lib = N.load()
-        lib.glint_prof_enable(sh.handle, 1)
-        for _ in range(2):
-            sh.update(keys, vals, unordered=(pattern != "with_prefix"))
-            assert ref.update(keys, vals) == -1
-        got = sh.to_numpy()
-        if dtype in ("long", "int") or (dtype == "float" and pattern == "unique"):
-            np.testing.assert_array_equal(got, ref.data)
-        elif dtype == "double":
-            np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9)
-        else:
-            exact = np.zeros(size)
-            mag = np.zeros(size)
-            np.add.at(exact, keys - start, 2 * vals.astype(np.float64))
-            np.add.at(mag, keys - start, 2 * np.abs(vals.astype(np.float64)))
-            assert np.all(np.abs(got.astype(np.float64) - exact) <= 1e-6 * mag + 1e-30)
-        bad = keys.copy()
-        bad[777] = start + size + 5
-        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
-            sh.update(bad, vals, unordered=True)
-        assert ei.value.record == 777
-
-
-@pytest.mark.parametrize("dtype", ["double", "long"])
-def test_binned_bucket_apply_matrix(gpu, monkeypatch, dtype):
-    """The bucket apply on a matrix with padded rows (pitch > cols: the padding stays untouched) and
-    Zipf rows (hot buckets split over items), against the oracle."""
-    monkeypatch.setenv("GLINT_BIN_BAPPLY", "1")
-    N.reload_env()
-    rng = np.random.default_rng(29)
-    rows_n, cols_n = 30_011, 129
-    part = RangePartition(0, 0, rows_n)
-    r = np.minimum(rng.zipf(1.05, 1_200_000) - 1, rows_n - 1).astype(np.int64)
-    c = rng.integers(0, cols_n, r.size).astype(np.int32)
-    v = rand_vals(rng, dtype, r.size) if dtype == "double" else rng.integers(-1000, 1000, r.size).astype(np.int64)
-    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE[dtype])
-    assert ref.update(r, c, v) == -1
-    with PartialMatrix(part, cols_n, dtype, gpu) as sh:
-        sh.update(r, c, v, unordered=True)
-        got = sh.to_numpy()
-    if dtype == "long":
-        np.testing.assert_array_equal(got, ref.data)
-    else:
-        np.testing.assert_allclose(got, ref.data, rtol=1e-6, atol=1e-9)
 
 
 def test_loopback_harness_gpu_backend(gpu):

@@ -85,7 +85,7 @@ for s in ${STAGES:-tests bench}; do
       ;;
     newtests)  # this round's new GPU tests first (fast feedback), then the config-shape tests
       step pytest_new 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-        -k "hot_chain or odd_record or scatter_rows or copy_segments or dist_exchange or bucket_apply or cfg5_slice or gated"
+        -k "hot_chain or odd_record or scatter_rows or copy_segments or dist_exchange or cfg5_slice or gated"
       step pytest_configs 1100 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread
       ;;
     pmccal)  # FETCH_SIZE / WRITE_SIZE per access shape against known byte counts (tools/microbench_pmc.hip)
@@ -103,10 +103,6 @@ for s in ${STAGES:-tests bench}; do
       for pat in ${PATTERNS:-matrix zipf exchange}; do
         step qb_$pat 300 python3 bench.py --no-cpu-baseline --no-north-star --pattern $pat
       done
-      ;;
-    bapstats)  # kernel stats of the cfg5 line with the bucket apply on and off
-      GLINT_BIN_BAPPLY=1 kstats matrix_bap1 300 --pattern matrix --steps 10 --warmup 2
-      GLINT_BIN_BAPPLY=0 kstats matrix_bap0 300 --pattern matrix --steps 10 --warmup 2
       ;;
     phases)  # phase clocks of the binned kernels (tools/bin_phases.py, a -DGLINT_BIN_PROF build)
       step bin_phases 300 python3 tools/bin_phases.py
