@@ -538,52 +538,15 @@ __device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks,
 __device__ __forceinline__ u32 bucket_items(u32 t) { return max(1u, (t + kFItem - 1) / kFItem); }
 // Also the per-bucket bases bin_fpart needs, once per push instead of once per fine item: T[nb + b] =
 // the bucket's first output record (records of buckets < b), T[2 nb + b] = its first apply item slot.
-// The three exclusive scans over the buckets (items, records, apply slots) in one pass: workgroup 0
-// does this before its own chunks, so it must stay short (three separate scans cost cfg5 ~3 %).
 __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
                                            BinCtl* bc) {
-  __shared__ u32 wt3[3][kATPB / 64];
-  u32* const TB = const_cast<u32*>(T) + g.nb;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  u32 carry[3] = {0, 0, 0};
-  for (u32 base = 0; base < g.nb; base += kATPB) {
-    const u32 b = base + (u32)tid;
-    const u32 t = b < g.nb ? T[b] : 0u;
-    const u32 v[3] = {b < g.nb ? bucket_items(t) : 0u, t, b < g.nb ? g.nf + (t + kCItem - 1) / kCItem : 0u};
-    u32 incl[3] = {v[0], v[1], v[2]};
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const u32 y = __shfl_up(incl[k], d);
-        if (lane >= d) incl[k] += y;
-      }
-    }
-    if (lane == 63) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) wt3[k][wid] = incl[k];
-    }
-    __syncthreads();
-    u32 excl[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      u32 run = carry[k] + incl[k] - v[k], tot = 0;
-      for (int w = 0; w < kATPB / 64; ++w) {
-        const u32 x = wt3[k][w];
-        run += w < wid ? x : 0u;
-        tot += x;
-      }
-      excl[k] = run;
-      carry[k] += tot;
-    }
-    if (b < g.nb) {
-      for (u32 j = 0; j < v[0]; ++j) fitems[excl[0] + j] = make_uint2(b, j);
-      TB[b] = excl[1];           // the bucket's first output record
-      TB[g.nb + b] = excl[2];    // its first apply item slot
-    }
-    __syncthreads();
-  }
-  if (tid == 0) bc->nfitems = carry[0];
+  const u32 tot = block_scan<kATPB, 1>(
+      g.nb, [&](u32 b) { return bucket_items(T[b]); },
+      [&](u32 b, u32 excl) {
+        const u32 J = bucket_items(T[b]);
+        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
+      });
+  if (threadIdx.x == 0) bc->nfitems = tot;
 }
 
 __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
@@ -1158,7 +1121,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART
     const uint2 d = fitems[it];
     const u32 b = d.x;
     // where the bucket's records go (raw capacities: holes only at bucket ends) and its item slots
-    const u32 ob = T[g.nb + b], ib = T[2 * g.nb + b];  // the bucket's bases (part_items)
+    u32 ob = 0, ib = 0;
+    for (u32 x = tid; x < b; x += TPB) {
+      const u32 t = T[x];
+      ob += t;
+      ib += g.nf + (t + kCItem - 1) / kCItem;
+    }
+    ob = block_sum<TPB>(ob);
+    ib = block_sum<TPB>(ib);
     for (u32 f = tid; f < g.nf; f += TPB) tcnt[f] = 0;
     block_scan<TPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
     ph.mark(20);
@@ -1548,7 +1518,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
   const i64 max_fitems = (i64)g.nb + n / kFItem + 1;
   // [BinCtl | T | H | cur2] zeroed per push; then R, segoff, seglen, item maps, the record buffers
-  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4 * 3), b_seg = pad256((size_t)G * g.nb * 4);  // T + bases
+  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
   const size_t b_H = pad256((size_t)g.nslab * 4);
   const size_t b_cd = pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8) +
                       pad256((size_t)max_fitems * g.nf * 4);  // + per-item slab histograms
