@@ -1206,6 +1206,23 @@ i64 host_first_bad(const glint_shard* s, const void* keys, const void* cols, i64
   const PartDesc& p = s->part;
   const char* kb = (const char*)keys;
   const char* cb = (const char*)cols;
+  if (p.kind == 0) {
+    // the common case (range layout): one branch-free pass the compiler vectorises -- (key - start)
+    // .toInt in [0, size) is one unsigned compare -- and a scalar search only when something failed
+    u32 any = 0;
+    const u32 size = (u32)p.size, ncols = (u32)p.cols;
+    for (i64 i = 0; i < n; ++i) {
+      int64_t k;
+      std::memcpy(&k, kb + 8 * i, 8);
+      any |= (u32)((u32)(int32_t)(k - p.start) >= size);
+      if (cb) {
+        int32_t c;
+        std::memcpy(&c, cb + 4 * i, 4);
+        any |= (u32)((u32)c >= ncols);
+      }
+    }
+    if (!any) return -1;
+  }
   for (i64 i = 0; i < n; ++i) {
     int64_t k;
     std::memcpy(&k, kb + 8 * i, 8);

@@ -71,6 +71,7 @@ for s in ${STAGES:-tests bench}; do
       ;;
     binned)
       for pat in ${PATTERNS:-zipf matrix exchange}; do kstats $pat 300 --pattern $pat --steps 10 --warmup 2; done
+      kstats exchange_mps8 300 --pattern exchange --parts-per-gpu 8 --steps 10 --warmup 2
       ;;
     pmc)
       for w in ${PMC:-dense_2p28 dense_2p30 zipf_2p28 matrix_2p17x512}; do
@@ -80,6 +81,7 @@ for s in ${STAGES:-tests bench}; do
           zipf_2p28) pmc $w --pattern zipf ;;
           matrix_2p17x512) pmc $w --pattern matrix ;;
           exchange_2p28) pmc $w --pattern exchange ;;
+          exchange_2p28_mps8) pmc $w --pattern exchange --parts-per-gpu 8 ;;
         esac
       done
       ;;
