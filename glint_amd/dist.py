@@ -27,6 +27,7 @@ the partition it hosts, which needs no exchange.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional
 
 import numpy as np
@@ -336,6 +337,43 @@ class _Distributed:
             if t.is_cuda and hasattr(sh, "sync"):
                 sh.sync(torch.cuda.current_stream(t.device).cuda_stream)
 
+    def _stream(self, j: int) -> "torch.cuda.Stream":
+        if not hasattr(self, "_streams"):
+            self._streams = {}
+        st = self._streams.get(j)
+        if st is None:
+            st = self._streams[j] = torch.cuda.Stream(self.device)
+        return st
+
+    def _run_local(self, ops) -> None:
+        """The local shards' calls of one push: ops = [(j, shard, first tensor, call)]. Several device
+        shards run concurrently, each on a stream of its own behind the caller's stream (the shards are
+        independent, so one push's short kernels -- counts, scans, tails -- overlap another's), and the
+        caller's stream waits for all of them; then one wait per shard (its errors)."""
+        concurrent = os.environ.get("GLINT_DIST_STREAMS", "1") != "0"  # 0: one stream (A/B)
+        if concurrent and len(ops) > 1 and all(self._on_shard_device(t) and hasattr(sh, "handle") for _, sh, t, _ in ops):
+            cur = torch.cuda.current_stream(self.device)
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            done = []
+            for j, sh, _, call in ops:
+                st = self._stream(j)
+                st.wait_event(ready)
+                with torch.cuda.stream(st):
+                    call()
+                ev = torch.cuda.Event()
+                ev.record(st)
+                cur.wait_event(ev)
+                done.append((sh, st))
+            for sh, st in done:
+                sh.sync(st.cuda_stream)
+            return
+        touched = []
+        for _, sh, t, call in ops:
+            call()
+            touched.append((sh, t))
+        self._sync(touched)
+
     def _push_gated(self, keys: torch.Tensor, args: tuple, deterministic: bool) -> bool:
         """A world of one with one partition: the batch is the shard's push as it is. The key check
         (the route's validation pass) and the push are enqueued back to back -- the push gated on the
@@ -431,14 +469,13 @@ class DistributedBigVector(_Distributed):
             order, ex = self._begin(keys)
             rk = ex.forward(keys.index_select(0, order))
             rv = ex.forward(values.index_select(0, order.to(values.device)))
-        touched = []
-        for _, sh, (k, v) in self._split(ex, rk, rv):
+        ops = []
+        for j, sh, (k, v) in self._split(ex, rk, rv):
             if k.numel():
                 # every local push is enqueued before the first wait (keys are validated by the route)
-                sh.update(self._to_shard(k), self._to_shard(v), deterministic=deterministic,
-                          **self._nosync(k))
-                touched.append((sh, k))
-        self._sync(touched)
+                ops.append((j, sh, k, lambda sh=sh, k=k, v=v: sh.update(
+                    self._to_shard(k), self._to_shard(v), deterministic=deterministic, **self._nosync(k))))
+        self._run_local(ops)
         ex.raise_if_bad(keys, self.router.nkeys)
         return True
 
@@ -479,13 +516,13 @@ class DistributedBigMatrix(_Distributed):
             rr = ex.forward(rows.index_select(0, order))
             rc = ex.forward(cols.index_select(0, order.to(cols.device)))
             rv = ex.forward(values.index_select(0, order.to(values.device)))
-        touched = []
-        for _, sh, (r, c, v) in self._split(ex, rr, rc, rv):
+        ops = []
+        for j, sh, (r, c, v) in self._split(ex, rr, rc, rv):
             if r.numel():
-                sh.update(self._to_shard(r), self._to_shard(c), self._to_shard(v), deterministic=deterministic,
-                          **self._nosync(r))
-                touched.append((sh, r))
-        self._sync(touched)
+                ops.append((j, sh, r, lambda sh=sh, r=r, c=c, v=v: sh.update(
+                    self._to_shard(r), self._to_shard(c), self._to_shard(v), deterministic=deterministic,
+                    **self._nosync(r))))
+        self._run_local(ops)
         ex.raise_if_bad(rows, self.router.nkeys)
         return True
 

@@ -109,6 +109,12 @@ for s in ${STAGES:-tests bench}; do
     phases)  # phase clocks of the binned kernels (tools/bin_phases.py, a -DGLINT_BIN_PROF build)
       step bin_phases 300 python3 tools/bin_phases.py
       ;;
+    mps8ab)  # the exchange line with 8 local partitions: local pushes on one stream / on a stream per shard
+      for r in 1 2; do
+        step mps8_seq_$r 300 env GLINT_DIST_STREAMS=0 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
+        step mps8_par_$r 300 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
+      done
+      ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
         -k "binned or fullsize or adaptive or cfg4 or exchange"
