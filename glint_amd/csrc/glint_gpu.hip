@@ -20,6 +20,7 @@
 #include <chrono>
 #include <cstring>
 #include <sched.h>
+#include <time.h>
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
@@ -1271,8 +1272,16 @@ StageLayout stage_layout(const glint_shard* s, i64 n) {
 // sched_yield between polls, so that a server with many more waiting threads than cores (one
 // thread per client connection) hands the CPU to the threads that have work instead of spinning
 // against them.
+// After a short spin the waiter yields; with GLINT_WAIT_SLEEP_US > 0 it sleeps that long per poll
+// instead, which leaves the cores to the threads with work when many waiters share few cores (the
+// loopback servers: hundreds of connection threads on a 16-core share).
+long long wait_sleep_us() {
+  static EnvKnob k("GLINT_WAIT_SLEEP_US");
+  return k.get([](const char* e) -> long long { return e ? atoll(e) : 0ll; });
+}
 bool poll_word(const u64* word, u64 ticket, double budget_us) {
   constexpr double kSpinUs = 4.0;
+  const long long sleep_us = wait_sleep_us();
   const auto t0 = std::chrono::steady_clock::now();
   for (u32 i = 0;; ++i) {
     if (__atomic_load_n(word, __ATOMIC_ACQUIRE) >= ticket) return true;
@@ -1280,7 +1289,12 @@ bool poll_word(const u64* word, u64 ticket, double budget_us) {
       const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       if (us > budget_us) return false;
       if (us > kSpinUs) {
-        sched_yield();
+        if (sleep_us > 0) {
+          const struct timespec ts = {0, (long)(sleep_us * 1000)};
+          nanosleep(&ts, nullptr);
+        } else {
+          sched_yield();
+        }
         continue;
       }
     }

@@ -115,6 +115,18 @@ for s in ${STAGES:-tests bench}; do
         step mps8_par_$r 300 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
       done
       ;;
+    lbsleep)  # the cfg4 loopback rows with the GPU servers' waits sleeping (GLINT_WAIT_SLEEP_US) or yielding
+      LB=tools/loopback/build/glint_loopback
+      G="--backend gpu --lib glint_amd/lib/libglint_gpu.so"
+      i=0
+      for args in "--clients 64 --servers 8 --keys 33554432" \
+                  "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
+        for r in 1 2; do
+          for us in 0 ${SLEEPS:-10 50}; do step lbs_${i}_${us}_$r 200 env GLINT_WAIT_SLEEP_US=$us $LB $G $args; done
+        done
+        i=$((i + 1))
+      done
+      ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
         -k "binned or fullsize or adaptive or cfg4 or exchange"
