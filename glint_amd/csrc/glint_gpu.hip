@@ -1272,16 +1272,25 @@ StageLayout stage_layout(const glint_shard* s, i64 n) {
 // sched_yield between polls, so that a server with many more waiting threads than cores (one
 // thread per client connection) hands the CPU to the threads that have work instead of spinning
 // against them.
-// After a short spin the waiter yields; with GLINT_WAIT_SLEEP_US > 0 it sleeps that long per poll
-// instead, which leaves the cores to the threads with work when many waiters share few cores (the
-// loopback servers: hundreds of connection threads on a 16-core share).
+// After a short spin a lone waiter yields (a message's round trip stays ~10 us: window-1 clients);
+// when more than kBusyWaiters threads of the process are waiting at once, each sleeps between polls
+// instead (GLINT_WAIT_SLEEP_US, default 50), leaving the cores to the threads that have work: the
+// loopback servers run hundreds of connection threads on a 16-core share, and yielding waiters there
+// cost the cfg4a / cfg4b pull rows 16 % / 10 % (profiles/r04/loopback_wait_sleep.txt).
+// GLINT_WAIT_SLEEP_US=0 always yields.
+std::atomic<int> g_waiters{0};
+constexpr int kBusyWaiters = 8;
 long long wait_sleep_us() {
   static EnvKnob k("GLINT_WAIT_SLEEP_US");
-  return k.get([](const char* e) -> long long { return e ? atoll(e) : 0ll; });
+  return k.get([](const char* e) -> long long { return e ? atoll(e) : 50ll; });
 }
 bool poll_word(const u64* word, u64 ticket, double budget_us) {
   constexpr double kSpinUs = 4.0;
   const long long sleep_us = wait_sleep_us();
+  struct Count {
+    Count() { g_waiters.fetch_add(1, std::memory_order_relaxed); }
+    ~Count() { g_waiters.fetch_sub(1, std::memory_order_relaxed); }
+  } count;
   const auto t0 = std::chrono::steady_clock::now();
   for (u32 i = 0;; ++i) {
     if (__atomic_load_n(word, __ATOMIC_ACQUIRE) >= ticket) return true;
@@ -1289,7 +1298,7 @@ bool poll_word(const u64* word, u64 ticket, double budget_us) {
       const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       if (us > budget_us) return false;
       if (us > kSpinUs) {
-        if (sleep_us > 0) {
+        if (sleep_us > 0 && g_waiters.load(std::memory_order_relaxed) > kBusyWaiters) {
           const struct timespec ts = {0, (long)(sleep_us * 1000)};
           nanosleep(&ts, nullptr);
         } else {

@@ -121,7 +121,7 @@ for s in ${STAGES:-tests bench}; do
       i=0
       for args in "--clients 64 --servers 8 --keys 33554432" \
                   "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
-        for r in 1 2; do
+        for r in $(seq ${ROUNDS:-2}); do
           for us in 0 ${SLEEPS:-10 50}; do step lbs_${i}_${us}_$r 200 env GLINT_WAIT_SLEEP_US=$us $LB $G $args; done
         done
         i=$((i + 1))
