@@ -62,6 +62,7 @@ SIGNATURES = {
     "glint_route_gather_dev": (_I, [_P, _P, _P, _I, _I64, _I, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "glint_scatter_rows_dev": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "glint_copy_segments_dev": (_I, [_P, _P, C.POINTER(_I64), _I, _P]),
+    "glint_send_matrix_dev": (_I, [_P, _P, _I32, _I32, _P, _P, _P]),
     "glint_prof_enable": (_I, [_P, _I]),
     "glint_prof_read": (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(_I64)]),
     "glint_prof_reset": (_I, [_P]),

@@ -9,9 +9,12 @@
 //   scatter_rows   dst[order[i]] = src[i], rows of row_bytes (8 B elements, 4 KiB matrix rows ...);
 //   copy_segments  a multi-range copy in one launch: a local partition's records that arrived from
 //                  several source ranks gathered into one contiguous buffer (and the inverse, its
-//                  answers put back into the response buffer's ranges).
-// Both are plain HBM streams: reads coalesced, writes coalesced per row (scatter_rows' element case
-// writes one 8-B word per record at a random position -- the caller's order is arbitrary).
+//                  answers put back into the response buffer's ranges);
+//   send_matrix    the (rank, local partition) count matrix a rank sends in the split exchange, from
+//                  the route's per-partition counts -- all zero when the batch had a bad key (the
+//                  rank still joins the collectives, sending nothing).
+// The copies are plain HBM streams: reads coalesced, writes coalesced per row (scatter_rows' element
+// case writes one 8-B word per record at a random position -- the caller's order is arbitrary).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
@@ -80,6 +83,17 @@ __global__ __launch_bounds__(kXT) void copy_segs(const W* __restrict__ src, W* _
   }
 }
 
+// send[cell[p]] = counts[p] (every other cell 0), or all zero when *bad != 0; one workgroup
+__global__ __launch_bounds__(kXT) void send_matrix(const i64* __restrict__ counts, const i64* __restrict__ cell,
+                                                   int nparts, int ncells, const unsigned long long* bad,
+                                                   i64* __restrict__ send) {
+  const bool ok = bad == nullptr || *bad == 0ull;
+  for (int c = threadIdx.x; c < ncells; c += kXT) send[c] = 0;
+  __syncthreads();
+  if (ok)
+    for (int p = threadIdx.x; p < nparts; p += kXT) send[cell[p]] = counts[p];
+}
+
 unsigned grid_of(i64 units, i64 per_block) {
   i64 g = (units + per_block - 1) / per_block;
   return (unsigned)std::max<i64>(1, std::min<i64>(g, 256 * 16));
@@ -118,10 +132,10 @@ extern "C" int glint_copy_segments_dev(const void* src, void* dst, const int64_t
   }
   if (al % 4) return GLINT_EINVAL;
   const int ub = al % 16 == 0 ? 16 : 4;
-  for (int k0 = 0; k0 < nseg; k0 += kMaxSeg) {
+  for (int k = 0; k < nseg;) {
     Segs s{};
     i64 tot = 0;
-    for (int k = k0; k < nseg && s.n < kMaxSeg; ++k) {
+    for (; k < nseg && s.n < kMaxSeg; ++k) {  // up to kMaxSeg nonempty segments per launch
       if (segs[3 * k + 2] == 0) continue;
       s.src[s.n] = segs[3 * k] / ub;
       s.dst[s.n] = segs[3 * k + 1] / ub;
@@ -138,4 +152,12 @@ extern "C" int glint_copy_segments_dev(const void* src, void* dst, const int64_t
     if (hipGetLastError() != hipSuccess) return GLINT_EDEVICE;
   }
   return GLINT_OK;
+}
+
+extern "C" int glint_send_matrix_dev(const int64_t* counts, const int64_t* cells, int32_t nparts, int32_t ncells,
+                                     const uint64_t* bad_dev, int64_t* send, void* stream) {
+  if (nparts < 0 || ncells <= 0 || !send || (nparts > 0 && (!counts || !cells))) return GLINT_EINVAL;
+  send_matrix<<<1, kXT, 0, (hipStream_t)stream>>>(counts, cells, nparts, ncells,
+                                                  (const unsigned long long*)bad_dev, send);
+  return hipGetLastError() == hipSuccess ? GLINT_OK : GLINT_EDEVICE;
 }

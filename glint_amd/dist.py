@@ -192,11 +192,18 @@ class _Exchange:
             recv_h = send_h
         else:
             _, cell = router._device_tables(counts.device)
-            send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
-            if bad_exc is None:
-                send[cell] = counts
-            if bad is not None:
-                send = torch.where(bad == 0, send, torch.zeros_like(send))
+            if counts.is_cuda:  # one launch: the counts into their cells, all zero after a bad key
+                send = torch.empty(W * maxp, dtype=torch.int64, device=counts.device)
+                n = 0 if bad_exc is not None else counts.numel()
+                check(N.load().glint_send_matrix_dev(counts.data_ptr(), cell.data_ptr(), n, W * maxp,
+                                                     None if bad is None else bad.data_ptr(), send.data_ptr(),
+                                                     torch.cuda.current_stream(counts.device).cuda_stream))
+            else:
+                send = torch.zeros(W * maxp, dtype=torch.int64, device=counts.device)
+                if bad_exc is None:
+                    send[cell] = counts
+                if bad is not None:
+                    send = torch.where(bad == 0, send, torch.zeros_like(send))
             recv = self._a2a(send)
             parts = [send, recv] + ([bad] if bad is not None else [])
             host = torch.cat(parts).cpu().numpy()  # the call's one host synchronisation

@@ -261,6 +261,12 @@ int glint_scatter_rows_dev(const void* src, const int64_t* order, int64_t n, int
  * gather a local partition's records that arrived from several source ranks into one buffer, and to
  * put its answers back into the response buffer's ranges. */
 int glint_copy_segments_dev(const void* src, void* dst, const int64_t* segs, int nseg, void* stream);
+/* The (rank, local partition) count matrix of a split exchange, from the route's per-partition counts:
+ * send[cells[p]] = counts[p] for p < nparts and every other of the ncells entries 0; all ncells
+ * entries 0 when the route's status word *bad_dev is nonzero (NULL: no status word) -- a rank with an
+ * out-of-range key sends nothing but still joins the collectives. Device arrays, one launch. */
+int glint_send_matrix_dev(const int64_t* counts, const int64_t* cells, int32_t nparts, int32_t ncells,
+                          const uint64_t* bad_dev, int64_t* send, void* stream);
 
 /* ---- kernel timing ------------------------------------------------------------------------- *
  * With profiling on, every kernel launch of the shard is bracketed by HIP events recorded on the
