@@ -255,3 +255,25 @@ def test_copy_segments_gathers_and_puts_ranges(gpu, row_elems, dtype):
         copy_ranges(out, back, [(b, a, c) for a, b, c in ranges])
         for a, _, c in ranges:
             assert torch.equal(back[a:a + c], src[a:a + c])
+
+
+def test_send_matrix_from_route_counts(gpu):
+    """glint_send_matrix_dev: the split exchange's (rank, local partition) count matrix from the route's
+    per-partition counts, and all zero when the route's status word reports a bad key."""
+    import torch
+    from glint_amd.dist import Router
+    from glint_amd.partitioning import RangePartitioner
+    d = torch.device("cuda", gpu)
+    lib = N.load()
+    router = Router(RangePartitioner.apply(7, 70_000), 3)  # 7 partitions over 3 ranks: maxp 3
+    _, cell = router._device_tables(d)
+    counts = torch.arange(11, 18, dtype=torch.int64, device=d)
+    for badv, want_zero in ((0, False), (~5 & 0xFFFFFFFFFFFFFFFF, True)):
+        bad = torch.tensor([badv - (1 << 64) if badv >= (1 << 63) else badv], dtype=torch.int64, device=d)
+        send = torch.full((3 * router.maxp,), -1, dtype=torch.int64, device=d)
+        assert lib.glint_send_matrix_dev(counts.data_ptr(), cell.data_ptr(), 7, 3 * router.maxp, bad.data_ptr(),
+                                         send.data_ptr(), torch.cuda.current_stream(d).cuda_stream) == N.GLINT_OK
+        want = torch.zeros(3 * router.maxp, dtype=torch.int64, device=d)
+        if not want_zero:
+            want[cell] = counts
+        assert torch.equal(send, want)

@@ -87,7 +87,7 @@ for s in ${STAGES:-tests bench}; do
       ;;
     newtests)  # this round's new GPU tests first (fast feedback), then the config-shape tests
       step pytest_new 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-        -k "hot_chain or odd_record or scatter_rows or copy_segments or dist_exchange or cfg5_slice or gated"
+        -k "hot_chain or odd_record or scatter_rows or copy_segments or send_matrix or dist_exchange or cfg5_slice or gated"
       step pytest_configs 1100 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread
       ;;
     pmccal)  # FETCH_SIZE / WRITE_SIZE per access shape against known byte counts (tools/microbench_pmc.hip)
