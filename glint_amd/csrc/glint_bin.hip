@@ -1265,7 +1265,8 @@ template <typename V>
 __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict__ addr,
                                                           const typename LdsAcc<V>::T* __restrict__ val,
                                                           const uint4* __restrict__ cdesc, const BinCtl* bc, i64 elems,
-                                                          V* __restrict__ data, u32 pre_min, u32 sparse_max) {
+                                                          V* __restrict__ data, u32 pre_min, u32 sparse_max,
+                                                          u32 list_max, bool line_wb) {
   typedef typename Vec2<V>::T V2;
   typedef typename LdsAcc<V>::T A;
   __shared__ A acc[kSlab];
@@ -1363,47 +1364,66 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
     __syncthreads();
     ph.mark(43);
     apply_fetch<A>(nd, addr, val, pa, pv);  // the next item's first batch: in flight during the RMW
+    bool sweep_wb = exclusive && !sparse;
     if (sparse) {
       // the other parity's list was read by the previous item, before the barrier that ended it,
       // and is appended to only after the barrier that ends this one
       if (tid == 0) ntl[par ^ 1u] = 0;
-      const u32 L = ntl[par];
-      for (u32 i = tid; i < L; i += kCTPB) {
-        const u32 e = tlist[i];
-        if (sbase_g + e < elems) sbase[e] = acc_add(sbase[e], acc[e]);
-        acc[e] = A(0);
-        touched[e] = 0;
+      const u32 L = ntl[par];  // block-uniform (read after the barrier)
+      if (L > list_max) {
+        sweep_wb = true;  // many distinct elements: most lines are touched, so whole-line write-back
+      } else {
+        for (u32 i = tid; i < L; i += kCTPB) {
+          const u32 e = tlist[i];
+          if (sbase_g + e < elems) sbase[e] = acc_add(sbase[e], acc[e]);
+          acc[e] = A(0);
+          touched[e] = 0;
+        }
       }
       par ^= 1u;
-    } else if (exclusive) {
-      // one coalesced RMW of the touched pairs; untouched lanes load the slab's first pair instead
-      // (one cached line), so all loads issue back to back without a branch
+    }
+    if (sweep_wb) {
+      // one coalesced RMW of the slab's touched 128-B lines: every pair of a line with a touched
+      // element is read and written back (the untouched ones unchanged -- the slab is this item's), so
+      // the stores are whole lines, not byte-masked pairs. Lanes of a line-less pair load the slab's
+      // first pair instead (one cached line), so all loads issue back to back without a branch.
+      // (GLINT_BIN_LINE_WB=0: the touched pairs only.)
+      constexpr int kPPL = 128 / (2 * (int)sizeof(V));  // pairs per line: 8 lanes (Double), 16 (Float)
+      const u64 gmask = (kPPL >= 64 ? ~0ull : ((1ull << kPPL) - 1ull)) << (lane & ~(kPPL - 1));
       V2 dd[kPairsPerThread];
       u32 t[kPairsPerThread];
+      bool wb[kPairsPerThread];
 #pragma unroll
       for (int q = 0; q < kPairsPerThread; ++q) {
         const int e0 = 2 * (tid + q * kCTPB);
         t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
-        const bool vec = t[q] != 0u && sbase_g + e0 + 1 < elems;
+        wb[q] = line_wb ? (__ballot(t[q] != 0u) & gmask) != 0ull : t[q] != 0u;  // wave-uniform loop
+      }
+#pragma unroll
+      for (int q = 0; q < kPairsPerThread; ++q) {
+        const int e0 = 2 * (tid + q * kCTPB);
+        const bool vec = wb[q] && sbase_g + e0 + 1 < elems;
         dd[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
         if (t[q]) *reinterpret_cast<uint16_t*>(touched + e0) = 0;
       }
 #pragma unroll
       for (int q = 0; q < kPairsPerThread; ++q) {
-        if (t[q] == 0u) continue;
+        if (!wb[q]) continue;
         const int e0 = 2 * (tid + q * kCTPB);
         if (sbase_g + e0 + 1 < elems) {
           V2 r = dd[q];
           if (t[q] & 1u) r.x = acc_add((V)r.x, acc[e0]);
           if (t[q] & 2u) r.y = acc_add((V)r.y, acc[e0 + 1]);
           *reinterpret_cast<V2*>(sbase + e0) = r;
-        } else {  // the shard's last element, odd count
+        } else if (t[q]) {  // the shard's last element, odd count
           sbase[e0] = acc_add(sbase[e0], acc[e0]);
         }
-        acc[e0] = A(0);
-        acc[e0 + 1] = A(0);
+        if (t[q]) {
+          acc[e0] = A(0);
+          acc[e0 + 1] = A(0);
+        }
       }
-    } else {
+    } else if (!exclusive) {
       for (int e = tid; e < kSlab; e += kCTPB) {
         if (touched[e]) {
           gadd(sbase + e, (V)acc[e]);
@@ -1434,6 +1454,21 @@ u32 bin_sparse_max() {
   return (u32)k.get([](const char* e) -> long long {
     return std::min<u32>(kSparseCap, e ? (u32)strtoul(e, nullptr, 10) : 1024u);
   });
+}
+
+// a sparse item whose list holds more distinct elements than this writes back by the line sweep
+// instead (GLINT_BIN_LIST_MAX): past a few hundred of a slab's 4096 elements most of its lines are
+// touched, and element stores would leave them byte-masked
+u32 bin_list_max() {
+  static EnvKnob k("GLINT_BIN_LIST_MAX");
+  return (u32)k.get([](const char* e) -> long long { return e ? (long long)strtoul(e, nullptr, 10) : 0xFFFFFFFFll; });
+}
+
+// bin_apply's swept items write back whole touched lines (GLINT_BIN_LINE_WB, default 1) or the
+// touched pairs only (0)
+bool bin_line_wb() {
+  static EnvKnob k("GLINT_BIN_LINE_WB");
+  return k.get([](const char* e) -> long long { return e ? atoll(e) : 1ll; }) != 0;
 }
 
 // resident blocks per CU of a kernel at its block size (occupancy query)
@@ -1641,7 +1676,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   static EnvKnob apply_knob("GLINT_BIN_APPLY_BPC");  // work-item blocks per CU (tuning knob)
   const int apply_bpc = (int)apply_knob.pos_or(64);
   bin_apply_kernel<V><<<(unsigned)std::min<i64>(nslots, (i64)s->cus * apply_bpc), kCTPB, 0, st>>>(
-      addr_b, val_b, cdesc, bc, s->elems, a.data, bin_prefetch_min(), bin_sparse_max());
+      addr_b, val_b, cdesc, bc, s->elems, a.data, bin_prefetch_min(), bin_sparse_max(), bin_list_max(), bin_line_wb());
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }

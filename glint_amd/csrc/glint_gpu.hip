@@ -766,6 +766,8 @@ int collect_errors(glint_shard* s, hipStream_t st, int64_t* first_bad) {
 
 int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   if (dtype < GLINT_I32 || dtype > GLINT_F64 || cols < 0) return GLINT_EINVAL;
+  static EnvKnob hprof_knob("GLINT_HOST_PROF");
+  s->hprof = hprof_knob.pos_or(0) != 0;
   if (s->part.size < 0) return GLINT_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
@@ -819,6 +821,17 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
 
 void free_shard(glint_shard* s) {
   if (!s) return;
+  if (s->hprof) {
+    const auto& p = s->hp;
+    fprintf(stderr,
+            "glint_host_prof {\"device\": %d, \"locks\": %llu, \"lock_wait_s\": %.6f, \"lock_hold_s\": %.6f, "
+            "\"launches\": %llu, \"launch_s\": %.6f, \"retire_waits\": %llu, \"retire_wait_s\": %.6f, "
+            "\"copy_s\": %.6f, \"tickets\": %llu}\n",
+            s->device, (unsigned long long)p.nlock.load(), 1e-9 * (double)p.lock_wait.load(),
+            1e-9 * (double)p.lock_hold.load(), (unsigned long long)p.nlaunch.load(), 1e-9 * (double)p.launch.load(),
+            (unsigned long long)p.nretire_wait.load(), 1e-9 * (double)p.retire_wait.load(),
+            1e-9 * (double)p.copy.load(), (unsigned long long)s->ticket_next);
+  }
   {
     DeviceGuard g(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
@@ -969,7 +982,7 @@ int glint_shard_destroy(glint_shard_t s) {
 
 int glint_shard_zero(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   int rc = ring_flush_locked(s);  // the restart comes after every message enqueued before it
   if (rc == GLINT_OK) rc = order_after_dev(s);
@@ -1013,14 +1026,14 @@ int glint_shard_last_error(glint_shard_t s, int64_t* first_bad) {
 
 int glint_prof_enable(glint_shard_t s, int on) {
   if (!s) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   s->prof = on != 0;
   return GLINT_OK;
 }
 
 int glint_prof_read(glint_shard_t s, int kernel_id, double* total_ms, int64_t* launches) {
   if (!s || kernel_id < 0 || kernel_id >= GLINT_K_COUNT) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   prof_drain(s);
   if (total_ms) *total_ms = s->prof_ms[kernel_id];
@@ -1030,7 +1043,7 @@ int glint_prof_read(glint_shard_t s, int kernel_id, double* total_ms, int64_t* l
 
 int glint_prof_reset(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   prof_drain(s);
   for (int k = 0; k < GLINT_K_COUNT; ++k) { s->prof_ms[k] = 0; s->prof_n[k] = 0; }
@@ -1039,7 +1052,7 @@ int glint_prof_reset(glint_shard_t s) {
 
 int glint_shard_sync(glint_shard_t s, void* stream, int64_t* first_bad) {
   if (!s) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(st));
@@ -1054,7 +1067,7 @@ int glint_shard_sync(glint_shard_t s, void* stream, int64_t* first_bad) {
 int glint_vec_push_dev(glint_shard_t s, const int64_t* keys, const void* vals, int64_t n, int flags, void* stream) {
   if (!s || n < 0) return GLINT_EINVAL;
   if (s->part.cols != 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)keys, nullptr, vals, n, flags, pick(s, stream));
@@ -1064,7 +1077,7 @@ int glint_mat_push_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
                        int flags, void* stream) {
   if (!s || n < 0) return GLINT_EINVAL;
   if (s->part.cols == 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
@@ -1074,7 +1087,7 @@ int glint_vec_push_dev_gated(glint_shard_t s, const int64_t* keys, const void* v
                              const uint64_t* gate, void* stream) {
   if (!s || n < 0 || !gate) return GLINT_EINVAL;
   if (s->part.cols != 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   struct Gate {
@@ -1089,7 +1102,7 @@ int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t
                              int flags, const uint64_t* gate, void* stream) {
   if (!s || n < 0 || !gate) return GLINT_EINVAL;
   if (s->part.cols == 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   struct Gate {
@@ -1103,7 +1116,7 @@ int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t
 int glint_vec_pull_dev(glint_shard_t s, const int64_t* keys, void* out, int64_t n, void* stream) {
   if (!s || n < 0) return GLINT_EINVAL;
   if (s->part.cols != 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, launch_vec_pull, s, (const i64*)keys, out, n, pick(s, stream));
@@ -1113,7 +1126,7 @@ int glint_mat_pull_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
                        void* stream) {
   if (!s || n < 0) return GLINT_EINVAL;
   if (s->part.cols == 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, launch_mat_pull, s, (const i64*)rows, cols, out, n, pick(s, stream));
@@ -1122,7 +1135,7 @@ int glint_mat_pull_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
 int glint_mat_pull_rows_dev(glint_shard_t s, const int64_t* rows, void* out, int64_t n, void* stream) {
   if (!s || n < 0) return GLINT_EINVAL;
   if (s->part.cols == 0) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   if (int rc = dev_order_after_host(s, (hipStream_t)stream)) return rc;
   GLINT_DISPATCH(s->dtype, launch_mat_pull_rows, s, (const i64*)rows, out, n, pick(s, stream));
@@ -1325,11 +1338,17 @@ int wait_done(glint_shard* s, u64 ticket) {
 // record here means the device and the host check disagree, a device fault.
 int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   if (!r.inflight) return GLINT_OK;
+  const u64 tw = s->hprof ? host_ns() : 0;
   if (r.sig) {
     const int rc = wait_done(s, r.ticket);
     if (rc) return rc;
   } else {
     HIPCHK(hipEventSynchronize(r.done));
+  }
+  const u64 tc = s->hprof ? host_ns() : 0;
+  if (tw) {
+    s->hp.retire_wait.fetch_add(tc - tw, std::memory_order_relaxed);
+    s->hp.nretire_wait.fetch_add(1, std::memory_order_relaxed);
   }
   r.inflight = false;
   const int err = __atomic_load_n(&r.herr->min_bad_enc, __ATOMIC_ACQUIRE) != 0 ? GLINT_EDEVICE : GLINT_OK;
@@ -1342,6 +1361,7 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
       std::memcpy(m.out, r.h + r.out_off + (size_t)m.off * s->vsize, (size_t)m.n * s->vsize);
     r.pull_batch = false;
   }
+  if (tc) s->hp.copy.fetch_add(host_ns() - tc, std::memory_order_relaxed);
   if (r.hcap > kSlotKeepBytes) {  // a large entry's slot: give the pinned memory back
     (void)hipHostFree(r.h);
     r.h = r.hd = nullptr;
@@ -1525,8 +1545,9 @@ inline bool batchable(const glint_shard* s, i64 n) { return n > 0 && n <= kBatch
 
 // Appends one message-sized push (sections: keys, cols for matrices, values; any alignment) to the
 // open batch, opening one if needed; *ticket = the message's own ticket.
-int ring_append_locked(glint_shard* s, i64 n, int flags, const void* k, const void* c, const void* v, u64* ticket) {
-  int rc = reject_if_bad(s, k, s->part.cols != 0 ? c : nullptr, n);
+int ring_append_locked(glint_shard* s, i64 n, int flags, const void* k, const void* c, const void* v, u64* ticket,
+                       bool checked = false) {
+  int rc = checked ? GLINT_OK : reject_if_bad(s, k, s->part.cols != 0 ? c : nullptr, n);
   if (rc) return rc;
   if (s->open_slot >= 0 &&
       (s->open_kind >= 0 || flags != s->open_flags || s->ring[s->open_slot].fill + n > kBatchMax)) {
@@ -1669,8 +1690,8 @@ int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind) {
 }
 
 int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys, const int32_t* cols, void* out,
-                            u64* ticket) {
-  int rc = reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
+                            u64* ticket, bool checked) {
+  int rc = checked ? GLINT_OK : reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
   if (rc) return rc;
   if (s->open_slot >= 0 && (s->open_kind != kind || s->ring[s->open_slot].fill + n > kBatchMax)) {
     rc = ring_flush_locked(s);
@@ -1743,9 +1764,9 @@ inline size_t pull_bytes(const glint_shard* s, int kind, i64 n) {
 // Copies a pull's keys (and cols) into a fresh slot and enqueues it. The slot's answer reaches `out`
 // when the slot retires.
 int pull_enqueue_locked(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols, void* out, int64_t n,
-                        u64* ticket) {
-  if (kind != 2 && batchable(s, n)) return ring_append_pull_locked(s, kind, n, keys, cols, out, ticket);
-  int rc = reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
+                        u64* ticket, bool checked = false) {
+  if (kind != 2 && batchable(s, n)) return ring_append_pull_locked(s, kind, n, keys, cols, out, ticket, checked);
+  int rc = checked ? GLINT_OK : reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
   if (rc) return rc;
   int slot = -1;
   const size_t ob = pull_bytes(s, kind, n);
@@ -1763,7 +1784,7 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
   if (n < 0 || (n > 0 && (!keys || !vals || (mat && !cols)))) return GLINT_EINVAL;
   if (mat != (s->part.cols != 0)) return GLINT_EINVAL;
   if (n == 0) return GLINT_OK;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   int rc = order_after_dev(s);
   if (rc) return rc;
@@ -1804,7 +1825,7 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   if (n < 0 || (n > 0 && (!keys || !out || (kind == 1 && !cols)))) return GLINT_EINVAL;
   if ((kind == 0) != (s->part.cols == 0)) return GLINT_EINVAL;
   if (n == 0) return GLINT_OK;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   int rc = ring_flush_locked(s);
   if (rc == GLINT_OK) rc = order_after_dev(s);
@@ -1905,7 +1926,7 @@ int glint_push_wire(glint_shard_t s, const uint8_t* payload, size_t len, int32_t
 
 int glint_stage_acquire(glint_shard_t s, int64_t n, void** keys, void** cols, void** vals, int* slot) {
   if (!s || !keys || !vals || !slot) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   int rc = ring_acquire_locked(s, n, slot);
   if (rc) return rc;
@@ -1919,7 +1940,7 @@ int glint_stage_acquire(glint_shard_t s, int64_t n, void** keys, void** cols, vo
 
 int glint_push_staged(glint_shard_t s, int slot, int64_t n, int flags, uint64_t* ticket) {
   if (!s) return GLINT_EINVAL;
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   return ring_push_locked(s, slot, n, flags, (u64*)ticket);
 }
@@ -1943,21 +1964,28 @@ int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, i
     // Checked on the host first, so a rejected message applies nothing, as every enqueued one; the
     // ticket is that of everything enqueued so far (complete on return).
     {
-      std::lock_guard<std::mutex> lk(s->mu);
+      ShardLock lk(s);
       const int rc = reject_if_bad(s, kp, mat ? kp + (size_t)n * 8 : nullptr, n);
       if (rc) return rc;
     }
     const int rc = host_push(s, mat, (const int64_t*)kp, (const int32_t*)(kp + (size_t)n * 8),
                              kp + (size_t)n * (8 + (mat ? 4 : 0)), n, flags);
-    std::lock_guard<std::mutex> lk(s->mu);
+    ShardLock lk(s);
     if (ticket) *ticket = s->ticket_next;
     return rc;
   }
-  std::lock_guard<std::mutex> lk(s->mu);
+  // the key check before the lock (it reads only the shard's fixed geometry), as in glint_pull_async
+  const bool small = batchable(s, n);
+  const i64 bad = small ? host_first_bad(s, kp, mat ? kp + (size_t)n * 8 : nullptr, n) : -1;
+  ShardLock lk(s);
   DeviceGuard g(s->device);
-  if (batchable(s, n))
+  if (bad >= 0) {
+    s->last_bad = bad;
+    return GLINT_EOUTOFRANGE;
+  }
+  if (small)
     return ring_append_locked(s, n, flags, kp, kp + (size_t)n * 8, kp + (size_t)n * (8 + (mat ? 4 : 0)),
-                              (u64*)ticket);
+                              (u64*)ticket, true);
   int slot = -1;
   int rc = ring_acquire_locked(s, n, &slot);
   if (rc) return rc;
@@ -1977,7 +2005,7 @@ int glint_shard_wait(glint_shard_t s, uint64_t ticket, int64_t* first_bad) {
   bool sig = false;
   hipEvent_t ev = nullptr;
   {
-    std::lock_guard<std::mutex> lk(s->mu);
+    ShardLock lk(s);
     DeviceGuard g(s->device);
     if (s->open_slot >= 0 && s->ring[s->open_slot].msgs.front().ticket <= ticket) {
       const int rc = ring_flush_locked(s);
@@ -1999,7 +2027,7 @@ int glint_shard_wait(glint_shard_t s, uint64_t ticket, int64_t* first_bad) {
     (void)hipEventSynchronize(ev);
     (void)hipGetLastError();
   }
-  std::lock_guard<std::mutex> lk(s->mu);
+  ShardLock lk(s);
   DeviceGuard g(s->device);
   return ring_wait_locked(s, (u64)ticket, (i64*)first_bad);
 }
@@ -2013,17 +2041,24 @@ int glint_pull_async(glint_shard_t s, int kind, const int64_t* keys, const int32
     // an answer too large for a ring slot (row pulls of wide matrices): answered now, through the
     // staged copies; the ticket is that of everything enqueued so far (complete on return)
     const int rc = host_pull(s, kind, keys, cols, out, n);
-    std::lock_guard<std::mutex> lk(s->mu);
+    ShardLock lk(s);
     *ticket = s->ticket_next;
     return rc;
   }
-  std::lock_guard<std::mutex> lk(s->mu);
+  // the key check reads only the shard's fixed geometry: done before the lock, so the threads
+  // enqueueing on one shard hold it only for the copy into the batch
+  const i64 bad = n > 0 ? host_first_bad(s, keys, kind == 1 ? cols : nullptr, n) : -1;
+  ShardLock lk(s);
   DeviceGuard g(s->device);
+  if (bad >= 0) {
+    s->last_bad = bad;
+    return GLINT_EOUTOFRANGE;
+  }
   if (n == 0) {  // nothing to enqueue: the ticket of everything so far
     *ticket = s->ticket_next;
     return GLINT_OK;
   }
-  return pull_enqueue_locked(s, kind, keys, cols, out, n, (u64*)ticket);
+  return pull_enqueue_locked(s, kind, keys, cols, out, n, (u64*)ticket, true);
 }
 
 // RequestSerializer.fromBinary for the pull messages + ResponseSerializer.toBinary of the answer

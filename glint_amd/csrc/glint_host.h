@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <mutex>
 #include <utility>
@@ -126,6 +127,15 @@ struct glint_shard {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[GLINT_K_COUNT];
   double prof_ms[GLINT_K_COUNT] = {0};
   int64_t prof_n[GLINT_K_COUNT] = {0};
+  // host-side time accounting (GLINT_HOST_PROF=1, read at create; printed to stderr at destroy as
+  // one "glint_host_prof {...}" line): what the message path's calls spend where
+  bool hprof = false;
+  struct HostProf {
+    std::atomic<u64> lock_wait{0}, lock_hold{0}, nlock{0};  // ns waiting for / holding mu
+    std::atomic<u64> launch{0}, nlaunch{0};                   // ns inside kernel launches
+    std::atomic<u64> retire_wait{0}, nretire_wait{0};         // ns waiting for an entry to retire
+    std::atomic<u64> copy{0};                                  // ns copying answers out of ring slots
+  } hp;
   std::mutex mu;
 };
 
@@ -157,6 +167,35 @@ struct EnvKnob {
 };
 
 namespace {
+
+inline u64 host_ns() {
+  return (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The shard's lock (one message at a time per shard, as the actor); with GLINT_HOST_PROF it also
+// accounts the time spent waiting for it and holding it.
+struct ShardLock {
+  glint_shard* s;
+  u64 t1 = 0;
+  explicit ShardLock(glint_shard* s_) : s(s_) {
+    if (!s->hprof) {
+      s->mu.lock();
+      return;
+    }
+    const u64 t0 = host_ns();
+    s->mu.lock();
+    t1 = host_ns();
+    s->hp.lock_wait.fetch_add(t1 - t0, std::memory_order_relaxed);
+    s->hp.nlock.fetch_add(1, std::memory_order_relaxed);
+  }
+  ~ShardLock() {
+    if (t1) s->hp.lock_hold.fetch_add(host_ns() - t1, std::memory_order_relaxed);
+    s->mu.unlock();
+  }
+  ShardLock(const ShardLock&) = delete;
+  ShardLock& operator=(const ShardLock&) = delete;
+};
 
 struct DeviceGuard {
   int prev = -1;
@@ -274,8 +313,13 @@ inline hipError_t launch_k(glint_shard* s, int id, void (*kernel)(KArgs...), uns
     (void)hipGetLastError();
     b = e = nullptr;
   }
+  const u64 t0 = s->hprof ? host_ns() : 0;
   hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, st, b, e, 0, static_cast<KArgs>(args)...);
   const hipError_t err = hipGetLastError();
+  if (t0) {
+    s->hp.launch.fetch_add(host_ns() - t0, std::memory_order_relaxed);
+    s->hp.nlaunch.fetch_add(1, std::memory_order_relaxed);
+  }
   if (b) s->prof_ev[id].emplace_back(b, e);
   return err;
 }

@@ -189,7 +189,9 @@ int glint_pull_wire(glint_shard_t shard, const uint8_t* payload, size_t len, uin
  * flags, and consecutive message-sized element pulls, are coalesced into one launch per batch (the
  * batch goes to the GPU when it is full or anything else needs the stream); every message keeps its
  * own ticket and its own errors. Tickets number pushes and pulls together. */
+#ifndef GLINT_RING_SLOTS
 #define GLINT_RING_SLOTS 16
+#endif
 #define GLINT_ZERO_COPY_MAX 4096
 
 /* A free slot for a push of n records, with the section pointers the caller fills: keys (i64 x n),

@@ -150,19 +150,21 @@ def test_jni_shim_compiles_and_links():
     ["--clients", "8", "--servers", "3", "--keys", "50000", "--pattern", "uniform", "--records", "20000"],
     ["--clients", "2", "--servers", "2", "--keys", "30000", "--window", "1"],                  # one in flight
 ])
-def test_loopback_concurrent_clients_cpu_backend(args):
+@pytest.mark.parametrize("server", ["threads", "actor"])
+def test_loopback_concurrent_clients_cpu_backend(args, server):
     """configs[3]'s shape over loopback TCP with the oracle's server loop: many clients, each with up
     to W messages in flight per server (GranularBigVector issues every chunk at once), messages of
-    different clients interleaving at the servers."""
+    different clients interleaving at the servers. `--server actor`: one thread per server takes the
+    messages of every connection from a mailbox, as the Akka actor does."""
     import json
     import subprocess
     from glint_amd.build import LOOPBACK_BIN, ORACLE_LIB, build_loopback
     build_loopback()
-    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "oracle", "--lib", str(ORACLE_LIB)] + args,
+    r = subprocess.run([str(LOOPBACK_BIN), "--backend", "oracle", "--lib", str(ORACLE_LIB), "--server", server] + args,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
-    assert d["check"] is True and d["resends"] == 0
+    assert d["check"] is True and d["resends"] == 0 and d["server"] == server
 
 
 @pytest.mark.parametrize("args", [[], ["--clients", "8", "--servers", "3", "--keys", "100003", "--pattern", "uniform",

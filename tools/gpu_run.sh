@@ -127,6 +127,34 @@ for s in ${STAGES:-tests bench}; do
         i=$((i + 1))
       done
       ;;
+    lbcpu)  # the cfg4 loopback rows with the process / server-call CPU time (--cpu-stats), both backends
+      LB=tools/loopback/build/glint_loopback
+      i=0
+      for args in "--clients 64 --servers 8 --keys 33554432" \
+                  "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
+        for r in $(seq ${ROUNDS:-2}); do
+          for lv in ${LBLIBS:-cur=glint_amd/lib/libglint_gpu.so}; do  # tag=path
+            step lbc_gpu_${lv%%=*}_${i}_$r 200 $LB --backend gpu --lib ${lv#*=} $args --cpu-stats
+          done
+          [ -z "$NO_ORACLE" ] && step lbc_oracle_${i}_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so $args --cpu-stats
+        done
+        i=$((i + 1))
+      done
+      cat $OUT/lbc_*.log | grep '^{' > $OUT/loopback_cpu.jsonl || true
+      ;;
+    lbactor)  # the cfg1 / cfg4 loopback rows with --server actor (one thread per server, as the Akka actor), both backends
+      LB=tools/loopback/build/glint_loopback
+      i=0
+      for args in "" "--clients 64 --servers 8 --keys 33554432" \
+                  "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
+        for r in $(seq ${ROUNDS:-2}); do
+          step lba_gpu_${i}_$r 200 $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so $args --server actor --cpu-stats
+          step lba_oracle_${i}_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so $args --server actor --cpu-stats
+        done
+        i=$((i + 1))
+      done
+      cat $OUT/lba_*.log | grep '^{' > $OUT/loopback_actor.jsonl || true
+      ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
         -k "binned or fullsize or adaptive or cfg4 or exchange"

@@ -65,6 +65,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/ioctl.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
@@ -237,6 +238,8 @@ typedef struct {
   uint8_t* receipt;   /* PushLogic.receipt, indexed by id */
   size_t rcap;
   int errors;
+  double cpu[8]; /* --cpu-stats: server thread CPU s in enqueue / update (push, pull), in waits (push,
+                    pull), wall s in waits (push, pull) and in enqueue / update (push, pull) */
 } server;
 
 static void receipt_set(server* s, int32_t id, uint8_t v) {
@@ -265,6 +268,20 @@ typedef struct {
   uint8_t* resp;   /* a pull's Response frame (filled by the wait) */
   size_t resp_len;
 } hold;
+
+/* --cpu-stats: the servers' thread CPU time around the backend calls (one clock read each side) */
+static int cpu_stats;
+static double tcpu(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+static double pcpu(void) { /* the whole process: user + system */
+  struct rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return (double)ru.ru_utime.tv_sec + 1e-6 * (double)ru.ru_utime.tv_usec + (double)ru.ru_stime.tv_sec +
+         1e-6 * (double)ru.ru_stime.tv_usec;
+}
 
 static int readable_now(int fd) {
   int avail = 0;
@@ -453,156 +470,340 @@ static void* conn_main_async(conn_arg* a) {
   return NULL;
 }
 
+/* One connection's server-side state: the replies owed, in request order, and the GPU work enqueued
+ * for it since its last settle. */
+typedef struct {
+  int fd;
+  obuf out;
+  uint8_t* resp; /* the oracle's response scratch */
+  size_t rcap;
+  int32_t* pending; /* ids of this connection's pushes enqueued on the GPU since the last settle */
+  size_t npend, pcap;
+  uint64_t last_ticket;
+  hold* holds; /* held replies, in reply order */
+  size_t nhold, hcap;
+  int enqueued; /* GPU work enqueued since the last settle */
+  double cs[8]; /* --cpu-stats, as server.cpu */
+  int wmode;    /* the kind (0 push, 1 pull) of the work a wait covers */
+  int dirty;    /* --server actor: owes replies (in the actor's settle list) */
+} cstate;
+
+/* PartialVector*.receive + PushLogic for one message of connection c; returns 1 on L_STOP */
+static int handle_msg(server* s, cstate* c, const uint8_t* buf, uint32_t len) {
+  const uint8_t t = buf[0];
+  int32_t id = 0;
+  if (len >= 5 && t >= L_GET_UID && t <= L_FORGET) memcpy(&id, buf + 1, 4);
+  const double c0 = cpu_stats ? tcpu() : 0.0, cw0 = cpu_stats ? now_s() : 0.0;
+  int cmode = -1;
+  if (t == W_PUSH_VEC_D || t == W_PUSH_VEC_L) {
+    int32_t mid = 0;
+    cmode = 0;
+    c->wmode = 0;
+    if (use_gpu) { /* enqueued: update runs on the GPU in arrival order; no reply */
+      uint64_t ticket = 0;
+      if (s->b.g_push_async(s->b.shard, buf, len, &mid, 0, &ticket) != 0) s->errors++;
+      if (c->npend == c->pcap) {
+        c->pcap = c->pcap ? 2 * c->pcap : 64;
+        c->pending = (int32_t*)realloc(c->pending, c->pcap * 4);
+      }
+      c->pending[c->npend++] = mid;
+      if (ticket > c->last_ticket) c->last_ticket = ticket;
+      c->enqueued = 1;
+    } else {
+      int32_t n;
+      memcpy(&n, buf + 1, 4);
+      memcpy(&mid, buf + 5, 4);
+      /* FastPrimitiveDeserializer.readArrayLong/readArray*: copy out of the frame into arrays */
+      int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
+      void* vals = malloc((size_t)n * 8 + 8);
+      memcpy(keys, buf + 9, (size_t)n * 8);
+      memcpy(vals, buf + 9 + (size_t)n * 8, (size_t)n * 8);
+      pthread_mutex_lock(&s->mu);
+      if (s->b.o_update(&s->b.opart, value_code(), s->b.data, s->b.size, keys, vals, n) >= 0) s->errors++;
+      receipt_set(s, mid, 1); /* updateFinished(id) */
+      pthread_mutex_unlock(&s->mu);
+      free(keys);
+      free(vals);
+    }
+  } else if (t == W_PULL_VECTOR) {
+    int32_t n;
+    cmode = 1;
+    c->wmode = 1;
+    memcpy(&n, buf + 1, 4);
+    const size_t need = 5 + (size_t)n * 8;
+    if (need > c->rcap) {
+      c->rcap = need;
+      c->resp = (uint8_t*)realloc(c->resp, c->rcap);
+    }
+    size_t olen = 0;
+    if (use_gpu) { /* enqueued after every push on the shard; its Response is held until the wait */
+      uint8_t* r = (uint8_t*)malloc(need);
+      uint64_t ticket = 0;
+      if (s->b.g_pull_async(s->b.shard, buf, len, r, need, &olen, &ticket) != 0) s->errors++;
+      if (ticket > c->last_ticket) c->last_ticket = ticket;
+      c->enqueued = 1;
+      if (c->nhold == c->hcap) {
+        c->hcap = c->hcap ? 2 * c->hcap : 64;
+        c->holds = (hold*)realloc(c->holds, c->hcap * sizeof(hold));
+      }
+      c->holds[c->nhold].end = c->out.len;
+      c->holds[c->nhold].ack_id = 0;
+      c->holds[c->nhold].resp = r;
+      c->holds[c->nhold].resp_len = olen;
+      ++c->nhold;
+    } else {
+      int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
+      memcpy(keys, buf + 5, (size_t)n * 8);
+      pthread_mutex_lock(&s->mu);
+      if (s->b.o_get(&s->b.opart, value_code(), s->b.data, s->b.size, keys, c->resp + 5, n) >= 0) s->errors++;
+      pthread_mutex_unlock(&s->mu);
+      free(keys);
+      c->resp[0] = dtype_long ? W_RESP_L : W_RESP_D;
+      memcpy(c->resp + 1, &n, 4);
+      olen = need;
+      ob_frame(&c->out, c->resp, (uint32_t)olen);
+    }
+  } else if (t == L_GET_UID) {
+    pthread_mutex_lock(&s->mu);
+    const int32_t u = ++s->uid; /* sender ! UniqueID(nextId()) */
+    pthread_mutex_unlock(&s->mu);
+    ob_logic(&c->out, L_UID, u);
+  } else if (t == L_ACK) {
+    int mine = 0;
+    for (size_t i = 0; i < c->npend && !mine; ++i) mine = c->pending[i] == id;
+    if (mine) { /* its push is still on the GPU: answered after the settle's wait */
+      if (c->nhold == c->hcap) {
+        c->hcap = c->hcap ? 2 * c->hcap : 64;
+        c->holds = (hold*)realloc(c->holds, c->hcap * sizeof(hold));
+      }
+      c->holds[c->nhold].end = c->out.len;
+      c->holds[c->nhold].ack_id = id;
+      c->holds[c->nhold].resp = NULL;
+      ++c->nhold;
+    } else {
+      pthread_mutex_lock(&s->mu);
+      ob_logic(&c->out, receipt_has(s, id) ? L_ACK : L_NACK, id);
+      pthread_mutex_unlock(&s->mu);
+    }
+  } else if (t == L_FORGET) {
+    pthread_mutex_lock(&s->mu);
+    if (receipt_has(s, id)) receipt_set(s, id, 0);
+    pthread_mutex_unlock(&s->mu);
+    ob_logic(&c->out, L_FORGET, id);
+  } else if (t == L_STOP) {
+    return 1;
+  } else {
+    s->errors++;
+  }
+  if (cpu_stats && cmode >= 0) {
+    c->cs[cmode] += tcpu() - c0;
+    c->cs[6 + cmode] += now_s() - cw0;
+  }
+  return 0;
+}
+
+/* After the wait that covered c's enqueued work (rc: its status): the pushes' receipts, then the held
+ * replies spliced into the reply stream at their places, then one send. */
+static void answer(server* s, cstate* c, int rc) {
+  if (c->enqueued) {
+    pthread_mutex_lock(&s->mu);
+    for (size_t i = 0; i < c->npend; ++i)
+      if (rc == 0) receipt_set(s, c->pending[i], 1); /* updateFinished(id) */
+    pthread_mutex_unlock(&s->mu);
+    if (rc != 0) s->errors++;
+    c->npend = 0;
+    c->enqueued = 0;
+    c->last_ticket = 0;
+  }
+  if (c->nhold) {
+    obuf merged = {0};
+    size_t from = 0;
+    pthread_mutex_lock(&s->mu);
+    for (size_t i = 0; i < c->nhold; ++i) {
+      ob_put(&merged, c->out.p + from, c->holds[i].end - from);
+      from = c->holds[i].end;
+      if (c->holds[i].resp) {
+        ob_frame(&merged, c->holds[i].resp, (uint32_t)c->holds[i].resp_len);
+        free(c->holds[i].resp);
+      } else {
+        ob_logic(&merged, receipt_has(s, c->holds[i].ack_id) ? L_ACK : L_NACK, c->holds[i].ack_id);
+      }
+    }
+    pthread_mutex_unlock(&s->mu);
+    ob_put(&merged, c->out.p + from, c->out.len - from);
+    free(c->out.p);
+    c->out = merged;
+    c->nhold = 0;
+  }
+  ob_flush(&c->out, c->fd);
+}
+
+/* the wait for everything a settle covers (ticket: the highest), timed for --cpu-stats */
+static int settle_wait(server* s, uint64_t ticket, double* cs, int wmode) {
+  const double w0 = cpu_stats ? tcpu() : 0.0, ww0 = cpu_stats ? now_s() : 0.0;
+  const int rc = s->b.g_wait(s->b.shard, ticket, NULL);
+  if (cpu_stats) {
+    cs[2 + wmode] += tcpu() - w0;
+    cs[4 + wmode] += now_s() - ww0;
+  }
+  return rc;
+}
+
+static void cstate_free(server* s, cstate* c) {
+  if (cpu_stats) {
+    pthread_mutex_lock(&s->mu);
+    for (int i = 0; i < 8; ++i) s->cpu[i] += c->cs[i];
+    pthread_mutex_unlock(&s->mu);
+  }
+  close(c->fd);
+  free(c->resp);
+  free(c->out.p);
+  free(c->pending);
+  free(c->holds);
+}
+
+/* --server threads (the default): each connection's thread runs the server loop for its messages
+ * (the actor's one-at-a-time update under the server's mutex), with one wait per drained burst */
 static void* conn_main(void* p) {
   conn_arg* a = (conn_arg*)p;
   if (use_gpu && replies_async) return conn_main_async(a);
   server* s = a->s;
-  const int fd = a->fd;
+  cstate c;
+  memset(&c, 0, sizeof(c));
+  c.fd = a->fd;
   uint8_t* buf = NULL;
   size_t cap = 0;
-  obuf out = {0};
-  uint8_t* resp = NULL;
-  size_t rcap = 0;
-  int32_t* pending = NULL; /* ids of this connection's pushes enqueued on the GPU since the last wait */
-  size_t npend = 0, pcap = 0;
-  uint64_t last_ticket = 0;
-  hold* holds = NULL;      /* held replies, in reply order */
-  size_t nhold = 0, hcap = 0;
-  int enqueued = 0;        /* GPU work enqueued since the last wait */
   for (;;) {
-    const uint32_t len = recv_frame(fd, &buf, &cap);
+    const uint32_t len = recv_frame(c.fd, &buf, &cap);
     if (len == 0) break;
-    const uint8_t t = buf[0];
-    int32_t id = 0;
-    if (len >= 5 && t >= L_GET_UID && t <= L_FORGET) memcpy(&id, buf + 1, 4);
-    if (t == W_PUSH_VEC_D || t == W_PUSH_VEC_L) {
-      int32_t mid = 0;
-      if (use_gpu) { /* enqueued: update runs on the GPU in arrival order; no reply */
-        uint64_t ticket = 0;
-        if (s->b.g_push_async(s->b.shard, buf, len, &mid, 0, &ticket) != 0) s->errors++;
-        if (npend == pcap) { pcap = pcap ? 2 * pcap : 64; pending = (int32_t*)realloc(pending, pcap * 4); }
-        pending[npend++] = mid;
-        last_ticket = ticket;
-        enqueued = 1;
-      } else {
-        int32_t n;
-        memcpy(&n, buf + 1, 4);
-        memcpy(&mid, buf + 5, 4);
-        /* FastPrimitiveDeserializer.readArrayLong/readArray*: copy out of the frame into arrays */
-        int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
-        void* vals = malloc((size_t)n * 8 + 8);
-        memcpy(keys, buf + 9, (size_t)n * 8);
-        memcpy(vals, buf + 9 + (size_t)n * 8, (size_t)n * 8);
-        pthread_mutex_lock(&s->mu);
-        if (s->b.o_update(&s->b.opart, value_code(), s->b.data, s->b.size, keys, vals, n) >= 0) s->errors++;
-        receipt_set(s, mid, 1); /* updateFinished(id) */
-        pthread_mutex_unlock(&s->mu);
-        free(keys);
-        free(vals);
-      }
-    } else if (t == W_PULL_VECTOR) {
-      int32_t n;
-      memcpy(&n, buf + 1, 4);
-      const size_t need = 5 + (size_t)n * 8;
-      if (need > rcap) { rcap = need; resp = (uint8_t*)realloc(resp, rcap); }
-      size_t olen = 0;
-      if (use_gpu) { /* enqueued after every push on the shard; its Response is held until the wait */
-        uint8_t* r = (uint8_t*)malloc(need);
-        uint64_t ticket = 0;
-        if (s->b.g_pull_async(s->b.shard, buf, len, r, need, &olen, &ticket) != 0) s->errors++;
-        if (ticket > last_ticket) last_ticket = ticket;
-        enqueued = 1;
-        if (nhold == hcap) { hcap = hcap ? 2 * hcap : 64; holds = (hold*)realloc(holds, hcap * sizeof(hold)); }
-        holds[nhold].end = out.len;
-        holds[nhold].ack_id = 0;
-        holds[nhold].resp = r;
-        holds[nhold].resp_len = olen;
-        ++nhold;
-      } else {
-        int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
-        memcpy(keys, buf + 5, (size_t)n * 8);
-        pthread_mutex_lock(&s->mu);
-        if (s->b.o_get(&s->b.opart, value_code(), s->b.data, s->b.size, keys, resp + 5, n) >= 0) s->errors++;
-        pthread_mutex_unlock(&s->mu);
-        free(keys);
-        resp[0] = dtype_long ? W_RESP_L : W_RESP_D;
-        memcpy(resp + 1, &n, 4);
-        olen = need;
-        ob_frame(&out, resp, (uint32_t)olen);
-      }
-    } else if (t == L_GET_UID) {
-      pthread_mutex_lock(&s->mu);
-      const int32_t u = ++s->uid; /* sender ! UniqueID(nextId()) */
-      pthread_mutex_unlock(&s->mu);
-      ob_logic(&out, L_UID, u);
-    } else if (t == L_ACK) {
-      int mine = 0;
-      for (size_t i = 0; i < npend && !mine; ++i) mine = pending[i] == id;
-      if (mine) { /* its push is still on the GPU: answered after the burst's wait */
-        if (nhold == hcap) { hcap = hcap ? 2 * hcap : 64; holds = (hold*)realloc(holds, hcap * sizeof(hold)); }
-        holds[nhold].end = out.len;
-        holds[nhold].ack_id = id;
-        holds[nhold].resp = NULL;
-        ++nhold;
-      } else {
-        pthread_mutex_lock(&s->mu);
-        ob_logic(&out, receipt_has(s, id) ? L_ACK : L_NACK, id);
-        pthread_mutex_unlock(&s->mu);
-      }
-    } else if (t == L_FORGET) {
-      pthread_mutex_lock(&s->mu);
-      if (receipt_has(s, id)) receipt_set(s, id, 0);
-      pthread_mutex_unlock(&s->mu);
-      ob_logic(&out, L_FORGET, id);
-    } else if (t == L_STOP) {
-      break;
-    } else {
-      s->errors++;
-    }
-    if (!readable_now(fd)) { /* the burst is drained: one wait for the enqueued work, then reply */
-      if (enqueued) {
-        const int rc = s->b.g_wait(s->b.shard, last_ticket, NULL);
-        pthread_mutex_lock(&s->mu);
-        for (size_t i = 0; i < npend; ++i)
-          if (rc == 0) receipt_set(s, pending[i], 1); /* updateFinished(id) */
-        pthread_mutex_unlock(&s->mu);
-        if (rc != 0) s->errors++;
-        npend = 0;
-        enqueued = 0;
-      }
-      if (nhold) { /* splice the held acks into the reply stream at their places */
-        obuf merged = {0};
-        size_t from = 0;
-        pthread_mutex_lock(&s->mu);
-        for (size_t i = 0; i < nhold; ++i) {
-          ob_put(&merged, out.p + from, holds[i].end - from);
-          from = holds[i].end;
-          if (holds[i].resp) {
-            ob_frame(&merged, holds[i].resp, (uint32_t)holds[i].resp_len);
-            free(holds[i].resp);
-          } else {
-            ob_logic(&merged, receipt_has(s, holds[i].ack_id) ? L_ACK : L_NACK, holds[i].ack_id);
-          }
-        }
-        pthread_mutex_unlock(&s->mu);
-        ob_put(&merged, out.p + from, out.len - from);
-        free(out.p);
-        out = merged;
-        nhold = 0;
-      }
-      ob_flush(&out, fd);
+    if (handle_msg(s, &c, buf, len)) break;
+    if (!readable_now(c.fd)) { /* the burst is drained: one wait for the enqueued work, then reply */
+      const int rc = c.enqueued ? settle_wait(s, c.last_ticket, c.cs, c.wmode) : 0;
+      answer(s, &c, rc);
     }
   }
-  ob_flush(&out, fd);
-  close(fd);
+  ob_flush(&c.out, c.fd);
+  cstate_free(s, &c);
   free(buf);
-  free(resp);
-  free(out.p);
-  free(pending);
-  free(holds);
   free(a);
   return NULL;
 }
+
+/* --server actor: the Akka model. Connection threads only receive frames into the server's mailbox;
+ * ONE thread per server (the PartialVector actor) takes them in arrival order and runs the update /
+ * get for each, enqueueing on the GPU without waiting. When the mailbox is empty it settles: one wait
+ * for the highest ticket it enqueued, then every connection's held replies (GpuShard.scala's
+ * FlushPulls, integration/scala). */
+typedef struct {
+  cstate* c; /* NULL: the sender's connection closed */
+  uint8_t* buf;
+  uint32_t len;
+} mitem;
+typedef struct {
+  server* s;
+  int nconn;
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  mitem* q;
+  size_t n, cap;
+  int closed; /* connections whose receive loop ended */
+} mailbox;
+
+static void mb_put(mailbox* m, mitem it) {
+  pthread_mutex_lock(&m->mu);
+  if (m->n == m->cap) {
+    m->cap = m->cap ? 2 * m->cap : 1024;
+    m->q = (mitem*)realloc(m->q, m->cap * sizeof(mitem));
+    if (!m->q) die("realloc");
+  }
+  m->q[m->n++] = it;
+  if (m->n == 1) pthread_cond_signal(&m->cv);
+  pthread_mutex_unlock(&m->mu);
+}
+
+typedef struct {
+  mailbox* m;
+  cstate* c;
+} aconn_arg;
+
+static void* aconn_main(void* p) { /* receive only: each frame (owned) into the mailbox */
+  aconn_arg* a = (aconn_arg*)p;
+  for (;;) {
+    uint8_t* buf = NULL;
+    size_t cap = 0;
+    const uint32_t len = recv_frame(a->c->fd, &buf, &cap);
+    if (len == 0) {
+      free(buf);
+      break;
+    }
+    const int stop = buf[0] == L_STOP;  /* read before the hand-off: the actor frees the frame */
+    mitem it = {a->c, buf, len};
+    mb_put(a->m, it);
+    if (stop) break;
+  }
+  mitem end = {NULL, NULL, 0};
+  mb_put(a->m, end);
+  free(a);
+  return NULL;
+}
+
+static void actor_loop(mailbox* m, cstate* conns) {
+  server* s = m->s;
+  cstate** dirty = (cstate**)malloc(sizeof(cstate*) * (size_t)m->nconn);
+  size_t ndirty = 0;
+  mitem* batch = NULL;
+  size_t bcap = 0;
+  int closed = 0;
+  double cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int wmode = 0;
+  while (closed < m->nconn) {
+    pthread_mutex_lock(&m->mu);
+    if (m->n == 0 && ndirty) { /* the mailbox is empty: settle before sleeping */
+      pthread_mutex_unlock(&m->mu);
+      uint64_t tmax = 0;
+      for (size_t i = 0; i < ndirty; ++i)
+        if (dirty[i]->last_ticket > tmax) tmax = dirty[i]->last_ticket;
+      const int rc = tmax ? settle_wait(s, tmax, cs, wmode) : 0;
+      for (size_t i = 0; i < ndirty; ++i) {
+        answer(s, dirty[i], rc);
+        dirty[i]->dirty = 0;
+      }
+      ndirty = 0;
+      continue;
+    }
+    while (m->n == 0) pthread_cond_wait(&m->cv, &m->mu);
+    mitem* q = m->q; /* swap the mailbox out: the receivers keep appending to the other array */
+    const size_t n = m->n, qcap = m->cap;
+    m->q = batch;
+    m->cap = bcap;
+    m->n = 0;
+    pthread_mutex_unlock(&m->mu);
+    batch = q;
+    bcap = qcap;
+    for (size_t i = 0; i < n; ++i) {
+      cstate* c = batch[i].c;
+      if (!c) {
+        ++closed;
+        continue;
+      }
+      if (batch[i].buf[0] != L_STOP) {
+        handle_msg(s, c, batch[i].buf, batch[i].len);
+        wmode = c->wmode;
+        if (!c->dirty) {
+          c->dirty = 1;
+          dirty[ndirty++] = c;
+        }
+      }
+      free(batch[i].buf);
+    }
+  }
+  for (size_t i = 0; i < ndirty; ++i) answer(s, dirty[i], 0);
+  for (int i = 0; i < 8; ++i) conns[0].cs[i] += cs[i];
+  free(dirty);
+  free(batch);
+}
+
+static int server_actor; /* --server actor */
 
 typedef struct {
   server* s;
@@ -612,6 +813,37 @@ typedef struct {
 static void* acceptor_main(void* p) {
   acceptor_arg* a = (acceptor_arg*)p;
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)a->nconn);
+  if (server_actor) { /* receivers per connection, this thread runs the server's actor */
+    mailbox m;
+    memset(&m, 0, sizeof(m));
+    m.s = a->s;
+    m.nconn = a->nconn;
+    pthread_mutex_init(&m.mu, NULL);
+    pthread_cond_init(&m.cv, NULL);
+    cstate* conns = (cstate*)calloc((size_t)a->nconn, sizeof(cstate));
+    for (int i = 0; i < a->nconn; ++i) {
+      int fd = accept(a->s->listen_fd, NULL, NULL);
+      if (fd < 0) die("accept");
+      tune_socket(fd);
+      conns[i].fd = fd;
+      aconn_arg* c = (aconn_arg*)malloc(sizeof(aconn_arg));
+      c->m = &m;
+      c->c = &conns[i];
+      pthread_create(&th[i], NULL, aconn_main, c);
+    }
+    actor_loop(&m, conns);
+    for (int i = 0; i < a->nconn; ++i) pthread_join(th[i], NULL);
+    for (int i = 0; i < a->nconn; ++i) {
+      ob_flush(&conns[i].out, conns[i].fd);
+      cstate_free(a->s, &conns[i]);
+    }
+    free(conns);
+    free(m.q);
+    pthread_mutex_destroy(&m.mu);
+    pthread_cond_destroy(&m.cv);
+    free(th);
+    return NULL;
+  }
   for (int i = 0; i < a->nconn; ++i) {
     int fd = accept(a->s->listen_fd, NULL, NULL);
     if (fd < 0) die("accept");
@@ -915,11 +1147,13 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--dtype") && i + 1 < argc) dtype_long = !strcmp(argv[++i], "long");
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) gpu_device = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--bucket") && i + 1 < argc) bucket_device = !strcmp(argv[++i], "device");
+    else if (!strcmp(argv[i], "--cpu-stats")) cpu_stats = 1;
+    else if (!strcmp(argv[i], "--server") && i + 1 < argc) server_actor = !strcmp(argv[++i], "actor");
     else if (!strcmp(argv[i], "--replies") && i + 1 < argc) replies_async = !strcmp(argv[++i], "async");
     else {
       fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--clients C] [--keys N] "
                       "[--pattern dense|uniform] [--records R] [--msg M] [--window W] [--dtype double|long] "
-                      "[--device D] [--bucket groupby|device] [--replies async|burst]\n", argv[0]);
+                      "[--device D] [--bucket groupby|device] [--replies async|burst] [--server threads|actor] [--cpu-stats]\n", argv[0]);
       return 2;
     }
   }
@@ -1028,10 +1262,11 @@ int main(int argc, char** argv) {
   client_arg* cargs = (client_arg*)calloc((size_t)C, sizeof(client_arg));
   if (bucket_device)
     for (int c = 0; c < C; ++c) client_dev_init(&cargs[c].dev, ck[c], cn[c]);
-  double t[3], bucket_s[2] = {0, 0}, bucket_max[2] = {0, 0};
+  double t[3], pc[3], bucket_s[2] = {0, 0}, bucket_max[2] = {0, 0};
   int64_t msgs[2] = {0, 0}, resends = 0;
   for (int mode = 0; mode < 2; ++mode) {
     t[mode] = now_s();
+    pc[mode] = pcpu();
     for (int c = 0; c < C; ++c) {
       for (int i = 0; i < S; ++i) {
         la[c * S + i].mode = mode;
@@ -1051,14 +1286,17 @@ int main(int argc, char** argv) {
     }
   }
   t[2] = now_s();
+  pc[2] = pcpu();
   for (int x = 0; x < L; ++x) {
     uint8_t stop[9] = {5, 0, 0, 0, L_STOP, 0, 0, 0, 0};
     write_all(la[x].fd, stop, 9);
   }
   int errors = 0;
+  double scpu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = 0; i < S; ++i) {
     pthread_join(at[i], NULL);
     errors += sv[i].errors;
+    for (int j = 0; j < 8; ++j) scpu[j] += sv[i].cpu[j];
     close(sv[i].listen_fd);
   }
   for (int x = 0; x < L; ++x) close(la[x].fd);
@@ -1093,12 +1331,15 @@ int main(int argc, char** argv) {
          "\"keys\": %lld, \"records\": %lld, \"max_records_per_message\": %d, \"window\": %d, "
          "\"push_messages\": %lld, \"pull_messages\": %lld, \"resends\": %lld, \"push_s\": %.6f, \"pull_s\": %.6f, "
          "\"push_records_per_s\": %.1f, \"pull_records_per_s\": %.1f, \"push_payload_MBps\": %.2f, "
-         "\"pull_payload_MBps\": %.2f, \"replies\": \"%s\", \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
-         "\"bucket_s_max\": [%.6f, %.6f], \"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
+         "\"pull_payload_MBps\": %.2f, \"server\": \"%s\", \"replies\": \"%s\", \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
+         "\"bucket_s_max\": [%.6f, %.6f], \"process_cpu_s\": [%.4f, %.4f], \"server_call_cpu_s\": [%.4f, %.4f], "
+         "\"server_wait_cpu_s\": [%.4f, %.4f], \"server_wait_wall_s\": [%.4f, %.4f], \"server_call_wall_s\": [%.4f, %.4f], "
+         "\"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
          kind, pattern, dtype_long ? "long" : "double", S, C, (long long)N, (long long)total, M, W,
          (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl, (double)total / tp, (double)total / tl,
          16.0 * (double)total / tp / 1e6, 16.0 * (double)total / tl / 1e6,
-         !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
+         server_actor ? "actor" : "threads", !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
+         pc[1] - pc[0], pc[2] - pc[1], scpu[0], scpu[1], scpu[2], scpu[3], scpu[4], scpu[5], scpu[6], scpu[7],
          dtype_long ? 0.0 : ((double*)cv[0])[0], (!dtype_long && cn[0] > 1) ? ((double*)cv[0])[1] : 0.0,
          (!dtype_long && cn[0] > 2) ? ((double*)cv[0])[2] : 0.0, ok ? "true" : "false");
   return ok ? 0 : 1;

@@ -2,6 +2,7 @@
 recompiled with extra -D defines, linked with the other objects of the current build.
 
     python tools/variant.py NAME -DGLINT_BIN_NT=1 [--src glint_bin]   # -> tools/build/libglint_gpu_NAME.so
+    python tools/variant.py NAME -DGLINT_RING_SLOTS=64 --all          # every source (layout-changing defines)
 
 Load it with GLINT_GPU_LIB=tools/build/libglint_gpu_NAME.so (the `ab` stage of tools/gpu_run.sh).
 """
@@ -21,11 +22,14 @@ def main():
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
     b.build_gpu_lib()
-    out = ROOT / "build" / "obj" / f"{src}_{name}.o"
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *defines]
-    subprocess.run([b._hipcc(), *flags, "-c", "-o", str(out), str(ROOT / "glint_amd" / "csrc" / f"{src}.hip")],
-                   check=True)
-    objs = [str(ROOT / "build" / "obj" / (s.stem + ".o")) for s in b.HIP_SOURCES if s.stem != src] + [str(out)]
+    srcs = [s.stem for s in b.HIP_SOURCES] if "--all" in sys.argv else [src]
+    objs = [str(ROOT / "build" / "obj" / (s.stem + ".o")) for s in b.HIP_SOURCES if s.stem not in srcs]
+    for sname in srcs:
+        out = ROOT / "build" / "obj" / f"{sname}_{name}.o"
+        subprocess.run([b._hipcc(), *flags, "-c", "-o", str(out), str(ROOT / "glint_amd" / "csrc" / f"{sname}.hip")],
+                       check=True)
+        objs.append(str(out))
     lib = ROOT / "tools" / "build" / f"libglint_gpu_{name}.so"
     lib.parent.mkdir(parents=True, exist_ok=True)
     subprocess.run([b._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(lib), *objs], check=True)
