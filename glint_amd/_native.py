@@ -14,7 +14,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "libglint_gpu.so"
 
 GLINT_I32, GLINT_I64, GLINT_F32, GLINT_F64 = 0, 1, 2, 3
 GLINT_OK, GLINT_EOUTOFRANGE, GLINT_EDEVICE, GLINT_EINVAL, GLINT_ENOMEM = 0, 1, 2, 3, 4
-GLINT_PUSH_DEFAULT, GLINT_PUSH_DETERMINISTIC, GLINT_PUSH_UNORDERED = 0, 1, 2
+GLINT_PUSH_DEFAULT, GLINT_PUSH_DETERMINISTIC, GLINT_PUSH_UNORDERED, GLINT_PUSH_VALIDATE = 0, 1, 2, 4
 GLINT_K_PUSH_APPLY, GLINT_K_PUSH_SCATTER, GLINT_K_VEC_PULL, GLINT_K_MAT_PULL, GLINT_K_MAT_PULL_ROWS = 0, 1, 2, 3, 4
 GLINT_K_PUSH_CHECK = 5
 GLINT_K_PUSH_BINNED = 6
@@ -70,6 +70,7 @@ SIGNATURES = {
     "glint_device_count": (_I, []),
     "glint_version": (_I, []),
     "glint_reload_env": (_I, []),
+    "glint_push_flags_supported": (_I, []),
 }
 
 _lib = None

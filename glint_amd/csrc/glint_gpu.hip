@@ -54,7 +54,7 @@ __device__ __forceinline__ bool rec_addr_t(const PartDesc& p, i64 key, int32_t c
 template <bool MAT, bool FULL, int KIND>
 __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const int32_t* __restrict__ cols, i64 n,
                                            const PartDesc& part, LaunchCtl* ctl, i64* __restrict__ desc,
-                                           u32 ntiles, u32 t, int lane) {
+                                           u32 ntiles, u32 t, int lane, bool validate) {
   typedef typename AddrT<MAT>::T A;
   const i64 pbase = (i64)t * (kTile / 2);
   K2 k[kPPT];
@@ -75,8 +75,12 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   const i64 kb = r_first > 0 ? keys[r_first - 1] : 0;  // the record before this tile
   const int32_t cb = (MAT && r_first > 0) ? cols[r_first - 1] : 0;
   // stop once a break before this tile is known (read after the loads are in flight)
+  // (a validating push reads every tile: its records are checked before anything is applied; a tile
+  // past a known break is only validated -- its order and descriptor no longer matter, and every such
+  // tile adding to brk_enc would serialise on that one word)
   const u32 brk = __builtin_amdgcn_readfirstlane(ld_relaxed(&ctl->brk_enc));
-  if (brk != 0u && ntiles - brk < t) return false;
+  const bool after = brk != 0u && ntiles - brk < t;
+  if (!validate && after) return false;
   A before = 0;
   if (r_first > 0) rec_addr_t<MAT, KIND>(part, kb, cb, before);
   bool mono = true, affine = true;
@@ -97,10 +101,12 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
     last = __shfl(a1, 63);
     const A off = (A)(r - r_first);
     affine = affine && (!h0 || (o0 && a0 == a_first + off)) && (!h1 || (o1 && a1 == a_first + off + 1));
+    if (validate && ((h0 && !o0) || (h1 && !o1)))  // rare: one atomic per lane with a rejected record
+      atomicMax(&ctl->bad, ~(u64)((h0 && !o0) ? r : r + 1));
   }
   const bool any_bad = __any(!mono);  // wave-wide votes, outside any lane-divergent branch
   const bool all_affine = __all(affine);
-  if (lane == 0) {
+  if (lane == 0 && !after) {
     if (any_bad) {
       atomicMax(&ctl->brk_enc, ntiles - t);
     } else {
@@ -121,20 +127,21 @@ __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict_
                                                           const int32_t* __restrict__ cols, i64 n,
                                                           PartDesc part, LaunchCtl* ctl, LaunchCtl* next,
                                                           i64* __restrict__ desc, u32 ntiles, u32 t_begin,
-                                                          u32 t_end) {
+                                                          u32 t_end, int validate) {
   const int lane = threadIdx.x & 63;
   if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // the next push's control words (no kernel of this push reads them)
     next->brk_enc = 0u;
     next->nonaffine = 0u;
     next->cancel = 0u;
+    next->bad = 0ull;
   }
   if (ctl->cancel) return;  // a cancelled gated push: brk_enc stays 0, so no tail either
   const u32 w0 = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
   const u32 nw = gridDim.x * (kTPB / 64);
   for (u32 t = t_begin + w0; t < t_end; t += nw) {
     const bool full = 2 * ((i64)t * (kTile / 2)) + kTile <= n;
-    const bool go = full ? check_tile<MAT, true, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane)
-                         : check_tile<MAT, false, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane);
+    const bool go = full ? check_tile<MAT, true, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane, validate != 0)
+                         : check_tile<MAT, false, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane, validate != 0);
     if (!go) return;
   }
 }
@@ -396,6 +403,20 @@ __global__ void push_gate_kernel(const u64* gate, LaunchCtl* ctl) {
   if (threadIdx.x == 0) ctl->cancel = *gate != 0ull ? 1u : 0u;
 }
 
+// A validating gated push (GLINT_PUSH_VALIDATE): push_check has checked every record; its verdict goes
+// to the caller's gate word, and a rejected batch is cancelled (no head: push_apply sees cancel; no
+// tail: the break is cleared) before anything is applied.
+__global__ void push_validate_gate_kernel(LaunchCtl* ctl, u64* gate) {
+  if (threadIdx.x == 0) {
+    const u64 b = ctl->bad;
+    *gate = b;
+    if (b != 0ull) {
+      ctl->cancel = 1u;
+      ctl->brk_enc = 0u;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // pulls
 // ------------------------------------------------------------------------------------------------
@@ -598,6 +619,11 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   // deterministic one, and host-pointer / wire pushes unless the caller said UNORDERED -- are one
   // launch of the order-preserving fold (glint_ordered.hip). Int/Long sums are exact in any order.
   const bool seq = det || (fp && (flags & kPushHostSequential) && !unordered);
+  // a gated push takes check + apply (+ its tail from the break): those kernels read the gate's
+  // verdict from the LaunchCtl (the ordered fold, the unordered hint and the one-launch small push
+  // have no such step)
+  const bool gated = s->gate != nullptr;
+  if (gated && (det || !vec_ok)) return GLINT_EINVAL;
   // a ring launch (one workgroup that signals its own completion) is always the ordered fold: for
   // Int/Long it is one more exact summation order
   if (a.sig.done || (seq && n <= kOrderedMax && s->elems < ((i64)1 << 32))) return push_ordered<V, MAT>(s, a, st);
@@ -618,10 +644,6 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
 
   const int bmode = binned_mode();
   const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
-  const bool gated = s->gate != nullptr;
-  // a gated push takes check + apply (+ its tail from the break): those kernels read the gate's
-  // verdict from the LaunchCtl (the unordered hint and the one-launch small push have no such step)
-  if (gated && (det || !vec_ok)) return GLINT_EINVAL;
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
   if (binned && unordered && !gated) return push_binned<V, MAT>(s, a, false, st);
@@ -640,7 +662,8 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
     static EnvKnob check_bpc("GLINT_CHECK_BPC");
-    if (gated) {
+    const bool validate = gated && (flags & GLINT_PUSH_VALIDATE) != 0;
+    if (gated && !validate) {
       push_gate_kernel<<<1, 64, 0, st>>>(s->gate, a.ctl);
       HIPCHK(hipGetLastError());
     }
@@ -648,9 +671,13 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     const unsigned gc =
         grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu<push_check_kernel<MAT, 0>>(2, &check_bpc));
     HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
-                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles)
+                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? 1 : 0)
                             : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
-                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles));
+                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? 1 : 0));
+    if (validate) {
+      push_validate_gate_kernel<<<1, 64, 0, st>>>(a.ctl, s->gate);
+      HIPCHK(hipGetLastError());
+    }
     s->ctl_par ^= 1;  // only once the check that zeroes the other slot is on the stream
   }
   {
@@ -918,6 +945,10 @@ int glint_reload_env(void) {
   return GLINT_OK;
 }
 
+int glint_push_flags_supported(void) {
+  return GLINT_PUSH_DETERMINISTIC | GLINT_PUSH_UNORDERED | GLINT_PUSH_VALIDATE;
+}
+
 int glint_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -1084,7 +1115,7 @@ int glint_mat_push_dev(glint_shard_t s, const int64_t* rows, const int32_t* cols
 }
 
 int glint_vec_push_dev_gated(glint_shard_t s, const int64_t* keys, const void* vals, int64_t n, int flags,
-                             const uint64_t* gate, void* stream) {
+                             uint64_t* gate, void* stream) {
   if (!s || n < 0 || !gate) return GLINT_EINVAL;
   if (s->part.cols != 0) return GLINT_EINVAL;
   ShardLock lk(s);
@@ -1094,12 +1125,16 @@ int glint_vec_push_dev_gated(glint_shard_t s, const int64_t* keys, const void* v
     glint_shard* s;
     ~Gate() { s->gate = nullptr; }
   } reset{s};
-  s->gate = (const u64*)gate;
+  s->gate = (u64*)gate;
+  if (n == 0 && (flags & GLINT_PUSH_VALIDATE)) {  // nothing to check: the verdict is "none rejected"
+    HIPCHK(hipMemsetAsync(gate, 0, sizeof(u64), pick(s, stream)));
+    return GLINT_OK;
+  }
   GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)keys, nullptr, vals, n, flags, pick(s, stream));
 }
 
 int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t* cols, const void* vals, int64_t n,
-                             int flags, const uint64_t* gate, void* stream) {
+                             int flags, uint64_t* gate, void* stream) {
   if (!s || n < 0 || !gate) return GLINT_EINVAL;
   if (s->part.cols == 0) return GLINT_EINVAL;
   ShardLock lk(s);
@@ -1109,7 +1144,11 @@ int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t
     glint_shard* s;
     ~Gate() { s->gate = nullptr; }
   } reset{s};
-  s->gate = (const u64*)gate;
+  s->gate = (u64*)gate;
+  if (n == 0 && (flags & GLINT_PUSH_VALIDATE)) {  // nothing to check: the verdict is "none rejected"
+    HIPCHK(hipMemsetAsync(gate, 0, sizeof(u64), pick(s, stream)));
+    return GLINT_OK;
+  }
   GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
 }
 

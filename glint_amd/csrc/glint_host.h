@@ -97,7 +97,7 @@ struct glint_shard {
   u64* h_done = nullptr;  // host-mapped: ticket of the last completed signalling launch
   u64* d_done = nullptr;
   MsgSig sig{};           // set only while a ring entry dispatches its one launch
-  const u64* gate = nullptr;  // set only while a gated device push launches (glint_*_push_dev_gated)
+  u64* gate = nullptr;  // set only while a gated device push launches (glint_*_push_dev_gated)
   int ring_next = 0;
   uint64_t ticket_next = 0;
   // tickets of ring entries whose launch failed after their tickets were handed out: a wait that

@@ -55,6 +55,7 @@ struct LaunchCtl {
   u32 nonaffine;  // some tile is not affine or does not continue its predecessor's affine run
   u32 cancel;     // a gated push whose gate word was set: it applies nothing (push_gate_kernel)
   u32 pad_;
+  u64 bad;        // a validating gated push: max of ~index over its out-of-range records (push_check)
 };
 
 // persistent error state, cleared by glint_shard_sync / host-pointer calls

@@ -386,8 +386,11 @@ class _Distributed:
         (the route's validation pass) and the push are enqueued back to back -- the push gated on the
         route's status word on the device (glint_*_push_dev_gated: a batch with an out-of-range key
         applies nothing, as mapPartitions throws before sending, AsyncBigVector.scala:96-98) -- and the
-        host reads the word after the one wait, so no synchronisation sits between them. Returns False
-        when the call does not qualify (the general path then runs)."""
+        host reads the word after the one wait, so no synchronisation sits between them. With a library
+        that has GLINT_PUSH_VALIDATE the push checks the keys itself (its order check reads them all)
+        and writes the word, so the route's pass over the keys is gone too (GLINT_GATE_ROUTE=1: the
+        route in front, for A/B). Returns False when the call does not qualify (the general path then
+        runs)."""
         if not (self.world == 1 and self.router.nparts == 1 and keys.is_cuda and not deterministic
                 and self._on_shard_device(keys) and hasattr(self.shards[0], "handle")
                 and getattr(N.load(), "glint_vec_push_dev_gated", None) is not None):  # (an older A/B library)
@@ -395,9 +398,16 @@ class _Distributed:
         esz = args[-1].element_size()
         if keys.data_ptr() % 16 or args[-1].data_ptr() % (2 * esz) or (len(args) == 3 and args[1].data_ptr() % 8):
             return False
-        _, _, _, _, _, bad = self.router.route(keys)
         sh = self.shards[0]
-        sh.update(*args, gate=bad, sync=False)
+        lib = N.load()
+        sup = getattr(lib, "glint_push_flags_supported", None)
+        if sup is not None and sup() & N.GLINT_PUSH_VALIDATE and os.environ.get("GLINT_GATE_ROUTE", "0") != "1":
+            # the push checks its own keys before applying any (GLINT_PUSH_VALIDATE): no route pass
+            bad = torch.empty(1, dtype=torch.int64, device=keys.device)
+            sh.update(*args, gate=bad, validate=True, sync=False)
+        else:
+            _, _, _, _, _, bad = self.router.route(keys)
+            sh.update(*args, gate=bad, sync=False)
         sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
         b = int(bad.cpu()[0])
         if b != 0:

@@ -254,12 +254,13 @@ class PartialVector(_Shard):
         super().__init__(partition, dtype, 0, device)
 
     def update(self, keys, values, deterministic: bool = False, sync: bool = True, unordered: bool = False,
-               gate=None) -> bool:
+               gate=None, validate: bool = False) -> bool:
         """PartialVector.update (PartialVector.scala:35-43): data(globalToLocal(k)) += v.
         ``unordered`` is a performance hint (GLINT_PUSH_UNORDERED): skip the order check, bin by slab.
         ``gate`` (device tensors only): a one-element int64 device tensor; the push applies nothing if
-        it is nonzero when the push runs (glint_vec_push_dev_gated)."""
-        flags = _flags(deterministic, unordered)
+        it is nonzero when the push runs (glint_vec_push_dev_gated). With ``validate`` the push writes
+        the gate itself (GLINT_PUSH_VALIDATE): 0, or ~(first out-of-range record), which cancels it."""
+        flags = _flags(deterministic, unordered) | (N.GLINT_PUSH_VALIDATE if validate else 0)
         if _is_torch_cuda(keys):
             self._check_dev(keys.numel(), keys, values=values)
             if gate is not None:
@@ -329,9 +330,10 @@ class PartialMatrix(_Shard):
         self.rows = self.size
 
     def update(self, rows, cols, values, deterministic: bool = False, sync: bool = True,
-               unordered: bool = False, gate=None) -> bool:
-        """PartialMatrix.update (PartialMatrix.scala:74-83); ``gate`` as for PartialVector.update."""
-        flags = _flags(deterministic, unordered)
+               unordered: bool = False, gate=None, validate: bool = False) -> bool:
+        """PartialMatrix.update (PartialMatrix.scala:74-83); ``gate`` and ``validate`` as for
+        PartialVector.update."""
+        flags = _flags(deterministic, unordered) | (N.GLINT_PUSH_VALIDATE if validate else 0)
         if _is_torch_cuda(rows):
             self._check_dev(rows.numel(), rows, cols=cols, values=values)
             if gate is not None:

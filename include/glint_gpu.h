@@ -62,7 +62,12 @@ enum glint_push_flags {
    * follow what earlier pushes measured on the device as of the shard's last sync point
    * (glint_shard_sync, or the end of a host-pointer call): a device-resident caller that never
    * syncs gets the no-history defaults. */
-  GLINT_PUSH_UNORDERED = 2
+  GLINT_PUSH_UNORDERED = 2,
+  /* glint_*_push_dev_gated only: the gate word is the push's OUTPUT. The push checks every record
+   * itself before applying any (its order check reads all keys), writes 0 or ~(index of the first
+   * out-of-range record) to *gate, and applies nothing when there is one -- the route's validation
+   * pass in front of a one-partition push, folded into the push. */
+  GLINT_PUSH_VALIDATE = 4
 };
 
 typedef struct glint_shard* glint_shard_t;
@@ -137,10 +142,11 @@ int glint_mat_pull_rows_dev(glint_shard_t shard, const int64_t* rows, void* out,
  * client reads the word after its one wait, so no host synchronisation separates the route from the
  * push. The push takes the check + apply path (GLINT_PUSH_UNORDERED is ignored); deterministic pushes
  * and unaligned arrays (keys not 16-B aligned, values not 2-element aligned) are GLINT_EINVAL. */
+/* With GLINT_PUSH_VALIDATE the push writes *gate itself (see the flag): no route in front. */
 int glint_vec_push_dev_gated(glint_shard_t shard, const int64_t* keys, const void* vals, int64_t n,
-                             int flags, const uint64_t* gate, void* stream);
+                             int flags, uint64_t* gate, void* stream);
 int glint_mat_push_dev_gated(glint_shard_t shard, const int64_t* rows, const int32_t* cols,
-                             const void* vals, int64_t n, int flags, const uint64_t* gate, void* stream);
+                             const void* vals, int64_t n, int flags, uint64_t* gate, void* stream);
 
 /* Waits for the shard's pending device work on `stream` and returns GLINT_EOUTOFRANGE if any
  * device-resident call since the last sync saw an out-of-range record (first_bad_record = its
@@ -298,6 +304,10 @@ int glint_version(void);
 /* The library reads its GLINT_* environment overrides (tuning and test knobs) once and caches them;
  * this makes the next call re-read them (tests that change the environment between calls). */
 int glint_reload_env(void);
+
+/* The glint_push_flags this library implements (a client built against a newer header checks
+ * before relying on a flag an older library would ignore, e.g. GLINT_PUSH_VALIDATE). */
+int glint_push_flags_supported(void);
 
 #ifdef __cplusplus
 }

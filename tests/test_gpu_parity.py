@@ -275,6 +275,71 @@ def test_gated_push(gpu, pattern):
             assert torch.equal(state(), ref)
 
 
+@pytest.mark.parametrize("pattern", ["dense", "zipf", "small", "matrix", "sorted_bad", "empty"])
+def test_validating_gated_push(gpu, pattern):
+    """GLINT_PUSH_VALIDATE: the gated push checks its own records and writes the verdict -- 0, or
+    ~(first out-of-range record) -- to the gate word; a batch with a bad record applies NOTHING (not
+    its dense head, not its tail), as mapPartitions throws before sending (AsyncBigVector.scala:96-98);
+    a clean batch is the plain device push. Pushes after a cancelled one are unaffected."""
+    import torch
+    d = torch.device("cuda", gpu)
+    rng = np.random.default_rng(23)
+    size = 1 << 22
+    if pattern == "matrix":
+        part = RangePartition(0, 0, 1 << 12)
+        sh = PartialMatrix(part, 512, "long", gpu)
+        r = torch.from_numpy(rng.integers(0, 1 << 12, 1 << 21).astype(np.int64)).to(d)
+        c = torch.from_numpy(rng.integers(0, 512, 1 << 21).astype(np.int32)).to(d)
+        v = torch.from_numpy(rng.integers(-9, 9, 1 << 21).astype(np.int64)).to(d)
+        good = (r, c, v)
+        c_bad = c.clone()
+        c_bad[777_777] = 512  # a column outside the matrix
+        c_bad[1_500_000] = -1
+        bad, first = (r, c_bad, v), 777_777
+        flat = r * 512 + c.to(torch.int64)
+        ref = torch.zeros((1 << 12) * 512, dtype=torch.int64, device=d)
+    else:
+        part = RangePartition(0, 0, size)
+        sh = PartialVector(part, "long", gpu)
+        if pattern in ("dense", "sorted_bad"):
+            k = torch.arange(size, dtype=torch.int64, device=d)
+        elif pattern == "small":
+            k = torch.from_numpy(rng.integers(0, size, 1000).astype(np.int64)).to(d)
+        elif pattern == "empty":
+            k = torch.empty(0, dtype=torch.int64, device=d)
+        else:
+            k = torch.from_numpy(np.minimum(rng.zipf(1.1, 1 << 21) - 1, size - 1).astype(np.int64)).to(d)
+        v = torch.from_numpy(rng.integers(-9, 9, k.numel()).astype(np.int64)).to(d)
+        good = (k, v)
+        kb = k.clone()
+        first = -1
+        if k.numel():
+            # sorted_bad: a dense increasing head, then the bad key (and a break after it)
+            first = k.numel() // 2 if pattern == "sorted_bad" else min(k.numel() - 1, 123_457)
+            kb[first] = size + 5
+            kb[-1] = -3 if k.numel() - 1 != first else kb[-1]
+        bad = (kb, v)
+        flat = k
+        ref = torch.zeros(size, dtype=torch.int64, device=d)
+    word = torch.full((1,), 12345, dtype=torch.int64, device=d)  # overwritten by every push
+    with sh:
+        def state():
+            if pattern == "matrix":
+                return sh.getRows(torch.arange(1 << 12, dtype=torch.int64, device=d)).reshape(-1)
+            return sh.get(torch.arange(size, dtype=torch.int64, device=d))
+        for batch, ok in ((good, True), (bad, False), (good, True), (bad, False), (bad, False), (good, True)):
+            if batch is bad and first < 0:
+                continue
+            sh.update(*batch, gate=word, validate=True)
+            w = int(word.cpu()[0])
+            if ok:
+                assert w == 0
+                ref.index_add_(0, flat, batch[-1])
+            else:
+                assert w != 0 and ~w == first, (w, first)
+            assert torch.equal(state(), ref)
+
+
 def test_zipf_fixture_default_mode(gpu):
     z = np.load(GOLD / "zipf_push.npz")
     start, size = int(z["start"]), int(z["size"])

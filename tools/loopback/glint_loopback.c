@@ -975,13 +975,16 @@ static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int
       die("hipMemcpyAsync");
     if (d->cnt[S] != 0) die("glint_route_gather_dev: key outside the partitioner");
     memcpy(cnt, d->cnt, (size_t)S * 8);
-    const int64_t* order = d->order;
+    /* each partition's ordered index list is read where it landed (the pinned order buffer, the
+     * client's for its lifetime): no copy */
     int64_t o = 0;
     for (int p = 0; p < S; ++p) {
-      store[p] = (int64_t*)malloc((size_t)(cnt[p] > 0 ? cnt[p] : 1) * 8);
-      memcpy(store[p], order + o, (size_t)cnt[p] * 8);
+      cut_messages(&links[p], d->order + o, cnt[p]);
+      store[p] = NULL;
       o += cnt[p];
     }
+    free(cnt);
+    return now_s() - t0;
   } else {
     /* the reference's groupBy, slice by slice: one pass per slice, each index appended to its
      * partition's list (lists grow as the groupBy's buffers do) */
