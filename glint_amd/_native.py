@@ -71,6 +71,8 @@ SIGNATURES = {
     "glint_version": (_I, []),
     "glint_reload_env": (_I, []),
     "glint_push_flags_supported": (_I, []),
+    "glint_host_alloc": (_I, [C.c_size_t, _P]),
+    "glint_host_free": (_I, [_P]),
 }
 
 _lib = None

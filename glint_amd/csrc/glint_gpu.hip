@@ -472,11 +472,17 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
 constexpr int kRingPullTPB = 1024;
 constexpr int kRingPullPer = 4;
 constexpr i64 kRingPullMax = (i64)kRingPullTPB * kRingPullPer;
+// With a destination table (a coalesced batch whose callers answer from glint_host_alloc buffers),
+// each record's answer goes to its own message's destination: the table (<= kPullDirectMax entries,
+// read over PCIe beside the keys) is staged in LDS and a record finds its message by binary search.
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __restrict__ keys,
                                                                 const int32_t* __restrict__ cols, i64 n,
                                                                 const V* __restrict__ data, PartDesc part,
-                                                                V* __restrict__ out, ErrState* err, MsgSig sig) {
+                                                                V* __restrict__ out, ErrState* err, MsgSig sig,
+                                                                const PullDst* __restrict__ tab, int nm) {
+  __shared__ u32 s_off[kPullDirectMax + 1];
+  __shared__ V* s_dst[kPullDirectMax];
   const i64 r0 = (i64)threadIdx.x * kRingPullPer;
   i64 k[kRingPullPer];
   int32_t c[kRingPullPer];
@@ -486,6 +492,13 @@ __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __re
     k[j] = keys[r];
     c[j] = MAT ? cols[r] : 0;
   }
+  if (tab) {  // launch-uniform
+    for (int i = threadIdx.x; i < nm; i += kRingPullTPB) {
+      s_off[i] = tab[i].off;
+      s_dst[i] = reinterpret_cast<V*>(tab[i].dst);
+    }
+    if (threadIdx.x == 0) s_off[nm] = (u32)n;
+  }
   V v[kRingPullPer];
 #pragma unroll
   for (int j = 0; j < kRingPullPer; ++j) {
@@ -494,9 +507,25 @@ __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __re
     v[j] = ok ? data[l] : V(0);
     if (!ok && r0 + j < n) record_error(err, r0 + j);
   }
+  if (tab) {
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kRingPullPer; ++j)
-    if (r0 + j < n) out[r0 + j] = v[j];
+    for (int j = 0; j < kRingPullPer; ++j) {
+      const i64 r = r0 + j;
+      if (r >= n) continue;
+      int lo = 0, hi = nm - 1;  // the last message starting at or before r
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((i64)s_off[mid] <= r) lo = mid;
+        else hi = mid - 1;
+      }
+      s_dst[lo][r - (i64)s_off[lo]] = v[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kRingPullPer; ++j)
+      if (r0 + j < n) out[r0 + j] = v[j];
+  }
   msg_signal(sig, err);
 }
 
@@ -706,7 +735,7 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   const MsgSig sig = s->sig;
   if (sig.done && n <= kRingPullMax) {
     HIPCHK(launch_k(s, GLINT_K_VEC_PULL, ring_pull_kernel<V, false>, 1u, kRingPullTPB, st, keys, (const int32_t*)nullptr,
-                    n, (const V*)s->data, s->part, (V*)out, err_of(s), sig));
+                    n, (const V*)s->data, s->part, (V*)out, err_of(s), sig, s->pull_tab, s->pull_nm));
     return GLINT_OK;
   }
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
@@ -736,7 +765,7 @@ int launch_mat_pull(glint_shard* s, const i64* rows, const int32_t* cols, void* 
   const MsgSig sig = s->sig;
   if (sig.done && n <= kRingPullMax) {
     HIPCHK(launch_k(s, GLINT_K_MAT_PULL, ring_pull_kernel<V, true>, 1u, kRingPullTPB, st, rows, cols, n,
-                    (const V*)s->data, s->part, (V*)out, err_of(s), sig));
+                    (const V*)s->data, s->part, (V*)out, err_of(s), sig, s->pull_tab, s->pull_nm));
     return GLINT_OK;
   }
   const unsigned g = sig.done ? 1u : grid_for(n, kTPB, (i64)s->cus * 8);
@@ -1397,7 +1426,7 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   }
   if (r.pull_batch) {
     for (const auto& m : r.msgs)
-      std::memcpy(m.out, r.h + r.out_off + (size_t)m.off * s->vsize, (size_t)m.n * s->vsize);
+      if (!m.dout) std::memcpy(m.out, r.h + r.out_off + (size_t)m.off * s->vsize, (size_t)m.n * s->vsize);
     r.pull_batch = false;
   }
   if (tc) s->hp.copy.fetch_add(host_ns() - tc, std::memory_order_relaxed);
@@ -1492,6 +1521,37 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
     return GLINT_OK;
   }
   return GLINT_ENOMEM;  // every slot handed out and not pushed
+}
+
+// ---- caller buffers the kernels can write (glint_host_alloc) -----------------------------------
+// Pinned, device-mapped host memory handed to a server for its response images: a coalesced pull
+// whose destination lies in one is answered by the kernel straight into it.
+struct HostRange {
+  char* h;
+  size_t n;
+  char* d;
+};
+std::mutex g_host_mu;
+std::vector<HostRange> g_host;  // sorted by h
+
+// p's device address if [p, p + bytes) lies in one glint_host_alloc buffer and p is aligned to
+// `align`, else nullptr
+void* host_dev_ptr(const void* p, size_t bytes, size_t align) {
+  if (!p || (uintptr_t)p % align) return nullptr;
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  if (g_host.empty()) return nullptr;
+  const char* c = (const char*)p;
+  auto it = std::upper_bound(g_host.begin(), g_host.end(), c,
+                             [](const char* x, const HostRange& r) { return x < r.h; });
+  if (it == g_host.begin()) return nullptr;
+  --it;
+  if (c + bytes > it->h + it->n) return nullptr;
+  return it->d + (c - it->h);
+}
+
+// a coalesced pull batch's destination table: behind the answer section of its slot
+inline size_t pull_tab_off(const glint_shard* s, const StageLayout& L) {
+  return L.kb + L.cb + pad256((size_t)GLINT_ZERO_COPY_MAX * s->vsize);  // (kBatchMax, below)
 }
 
 // whether an entry of n records is one signalling launch reading (and answering) in the mapped slot
@@ -1718,12 +1778,32 @@ int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind) {
   const i64 n = r.fill;
   r.out = nullptr;
   r.out_off = L.kb + L.cb;
+  // messages answering into glint_host_alloc buffers: the kernel writes there itself, through a
+  // destination table behind the answer section (the others keep their answer in the slot)
+  bool direct = false;
+  for (const auto& m : r.msgs) direct = direct || m.dout != nullptr;
+  if (direct && r.msgs.size() <= (size_t)kPullDirectMax) {
+    const size_t toff = pull_tab_off(s, L);
+    PullDst* tab = reinterpret_cast<PullDst*>(r.h + toff);
+    for (size_t i = 0; i < r.msgs.size(); ++i) {
+      const auto& m = r.msgs[i];
+      tab[i].off = (unsigned)m.off;
+      tab[i].n = (unsigned)m.n;
+      tab[i].dst = (unsigned long long)(uintptr_t)(m.dout ? (char*)m.dout : ans + (size_t)m.off * s->vsize);
+    }
+    s->pull_tab = reinterpret_cast<const PullDst*>(r.hd + toff);
+    s->pull_nm = (int)r.msgs.size();
+  } else {
+    for (auto& m : r.msgs) m.dout = nullptr;  // answered through the slot, copied out at retire
+  }
   const int rc = ring_dispatch(s, r, true, r.msgs.front().ticket, r.msgs.back().ticket, [&]() -> int {
     if (kind == 0) {
       GLINT_DISPATCH(s->dtype, launch_vec_pull, s, keys, ans, n, s->stream);
     }
     GLINT_DISPATCH(s->dtype, launch_mat_pull, s, keys, cols, ans, n, s->stream);
   });
+  s->pull_tab = nullptr;
+  s->pull_nm = 0;
   if (rc == GLINT_OK) r.pull_batch = true;
   return rc;
 }
@@ -1738,7 +1818,8 @@ int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys
   }
   if (s->open_slot < 0) {
     int slot = -1;
-    rc = ring_acquire_locked(s, kBatchMax, &slot, (size_t)kBatchMax * s->vsize);
+    // the answer section, then the destination table (pull_tab_off)
+    rc = ring_acquire_locked(s, kBatchMax, &slot, pad256((size_t)kBatchMax * s->vsize) + sizeof(PullDst) * kPullDirectMax);
     if (rc) return rc;
     s->open_slot = slot;
     s->open_kind = kind;
@@ -1751,6 +1832,7 @@ int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys
   const u64 t = ++s->ticket_next;
   glint_shard::RingSlot::Msg m{r.fill, n, t};
   m.out = out;
+  m.dout = host_dev_ptr(out, (size_t)n * s->vsize, s->vsize);
   r.msgs.push_back(m);
   r.fill += n;
   if (ticket) *ticket = t;
@@ -2144,6 +2226,39 @@ int glint_pull_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, u
                           size_t* out_len, uint64_t* ticket) {
   if (!ticket) return GLINT_EINVAL;
   return pull_wire(s, payload, len, response, cap, out_len, ticket);
+}
+
+int glint_host_alloc(size_t bytes, void** p) {
+  if (!p || bytes == 0) return GLINT_EINVAL;
+  *p = nullptr;
+  char* h = nullptr;
+  char* d = nullptr;
+  if (hipHostMalloc((void**)&h, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    if (h) (void)hipHostFree(h);
+    return GLINT_ENOMEM;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    const HostRange r{h, bytes, d};
+    g_host.insert(std::upper_bound(g_host.begin(), g_host.end(), r,
+                                   [](const HostRange& a, const HostRange& b) { return a.h < b.h; }),
+                  r);
+  }
+  *p = h;
+  return GLINT_OK;
+}
+
+int glint_host_free(void* p) {
+  if (!p) return GLINT_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = std::find_if(g_host.begin(), g_host.end(), [p](const HostRange& r) { return r.h == (char*)p; });
+    if (it == g_host.end()) return GLINT_EINVAL;
+    g_host.erase(it);
+  }
+  return hipHostFree(p) == hipSuccess ? GLINT_OK : GLINT_EDEVICE;
 }
 
 }  // extern "C"

@@ -84,6 +84,8 @@ struct glint_shard {
       int64_t off, n;
       uint64_t ticket;
       void* out = nullptr;  // a coalesced pull's destination (its answer sits at off in the slot)
+      void* dout = nullptr; // out's device address when out is glint_host_alloc memory: the kernel
+                            // writes the answer there itself (no copy out of the slot)
     };
     std::vector<Msg> msgs;      // the messages of this entry, for error attribution
     int64_t fill = 0;           // records appended to an open batch
@@ -97,6 +99,8 @@ struct glint_shard {
   u64* h_done = nullptr;  // host-mapped: ticket of the last completed signalling launch
   u64* d_done = nullptr;
   MsgSig sig{};           // set only while a ring entry dispatches its one launch
+  const PullDst* pull_tab = nullptr;  // set only while a pull batch with direct answers dispatches
+  int pull_nm = 0;
   u64* gate = nullptr;  // set only while a gated device push launches (glint_*_push_dev_gated)
   int ring_next = 0;
   uint64_t ticket_next = 0;

@@ -73,6 +73,15 @@ struct MsgSig {
   ErrState* herr;  // host-mapped: the error state after this launch
 };
 
+// A coalesced ring pull's answer destinations, one per message (the table sits in the slot, after
+// the answer section): records [off, off + n) of the batch are written to dst -- a glint_host_alloc
+// buffer the caller answers from, or the slot's own answer section.
+struct PullDst {
+  unsigned int off, n;
+  unsigned long long dst;  // device address
+};
+constexpr int kPullDirectMax = 256;  // messages per batch with a destination table, at most
+
 // Partition -> local index, for both partitioner kinds (kind is launch-uniform)
 struct PartDesc {
   int32_t kind;   // 0 range, 1 cyclic

@@ -72,6 +72,37 @@ def _host(x, dtype) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(x, dtype=dtype))
 
 
+class HostBuffer:
+    """Pinned, device-mapped host memory from glint_host_alloc: the buffers a server answers pulls
+    from. A message-sized pull whose ``out`` lies in one is answered by the kernel straight into it
+    (no copy out of the ring slot when it retires). ``array(dtype, count, offset)`` views a part of it
+    as a numpy array; free() (or leaving the ``with`` block) only once no pull into it is pending."""
+
+    def __init__(self, nbytes: int):
+        self.lib = N.load()
+        p = C.c_void_p()
+        check(self.lib.glint_host_alloc(int(nbytes), C.byref(p)))
+        self.ptr, self.nbytes = p.value, int(nbytes)
+
+    def array(self, dtype, count: int, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if offset < 0 or offset + count * dt.itemsize > self.nbytes:
+            raise ValueError("outside the buffer")
+        raw = (C.c_char * (count * dt.itemsize)).from_address(self.ptr + offset)
+        return np.frombuffer(raw, dtype=dt, count=count)
+
+    def free(self) -> None:
+        if self.ptr:
+            check(self.lib.glint_host_free(self.ptr))
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.free()
+
+
 class _Shard:
     def __init__(self, partition: Partition, dtype, cols: int = 0, device: int = 0):
         self.lib = N.load()

@@ -305,6 +305,14 @@ int glint_version(void);
  * this makes the next call re-read them (tests that change the environment between calls). */
 int glint_reload_env(void);
 
+/* Pinned, device-mapped host memory for the buffers a server answers from (the response images it
+ * sends). A message-sized pull (glint_pull_async, glint_pull_wire_async) whose answer destination
+ * lies in such a buffer and is aligned to the value size is answered by the kernel straight into
+ * it: no copy out of the ring slot when the entry retires. Free with glint_host_free (only once no
+ * pull into the buffer is pending). */
+int glint_host_alloc(size_t bytes, void** host_ptr);
+int glint_host_free(void* host_ptr);
+
 /* The glint_push_flags this library implements (a client built against a newer header checks
  * before relying on a flag an older library would ignore, e.g. GLINT_PUSH_VALIDATE). */
 int glint_push_flags_supported(void);

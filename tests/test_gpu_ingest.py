@@ -333,6 +333,69 @@ def test_coalesced_pulls_answer_each_message(gpu, dtype):
         np.testing.assert_array_equal(o1, base[q1])
 
 
+@pytest.mark.parametrize("dtype", ["double", "int"])
+def test_pulls_answer_straight_into_host_buffers(gpu, dtype):
+    """Answers whose destination is glint_host_alloc memory (HostBuffer) are written by the kernel
+    itself through the batch's destination table; in the same batch, messages answering into ordinary
+    memory or at a misaligned address still get theirs through the slot; a batch of more messages
+    than the table holds (kPullDirectMax) falls back to the copies; matrix element pulls likewise."""
+    from glint_amd.shard import HostBuffer
+    size = 20_000
+    rng = np.random.default_rng(93)
+    npd = np.dtype(np.float64 if dtype == "double" else np.int32)
+    with PartialVector(RangePartition(0, 0, size), dtype, gpu) as sh, HostBuffer(1 << 22) as hb:
+        base = _vals(rng, dtype, size)
+        sh.update(np.arange(size, dtype=np.int64), base)
+        for rnd in range(3):
+            outs, want, tickets, off = [], [], [], 0
+            for m in range(60):
+                n = int(rng.integers(1, 400))
+                q = rng.integers(0, size, n).astype(np.int64)
+                kind = m % 4
+                if kind == 3:  # ordinary numpy memory: through the slot
+                    out = np.empty(n, npd)
+                else:
+                    off = (off + 7) // 8 * 8
+                    if kind == 2 and npd.itemsize == 8:
+                        off += 4  # misaligned for 8-B values: through the slot
+                    out = hb.array(npd, n, off)
+                    off += n * npd.itemsize
+                t, got = sh.pull_async(q, out=out)
+                outs.append(got)
+                want.append(base[q])
+                tickets.append(t)
+            sh.wait(tickets[-1])
+            for w, g in zip(want, outs):
+                np.testing.assert_array_equal(g, w)
+        # more one-record messages in one batch than the destination table holds
+        outs, want = [], []
+        for m in range(300):
+            q = np.array([m * 7 % size], np.int64)
+            t, got = sh.pull_async(q, out=hb.array(npd, 1, 8 * m))
+            outs.append(got)
+            want.append(base[q])
+        sh.wait(t)
+        for w, g in zip(want, outs):
+            np.testing.assert_array_equal(g, w)
+    with PartialMatrix(RangePartition(0, 0, 300), 37, dtype, gpu) as mt, HostBuffer(1 << 20) as hb:
+        full = _vals(rng, dtype, 300 * 37).reshape(300, 37)
+        r = np.repeat(np.arange(300, dtype=np.int64), 37)
+        c = np.tile(np.arange(37, dtype=np.int32), 300)
+        mt.update(r, c, full.reshape(-1))
+        outs, want, off = [], [], 0
+        for m in range(20):
+            n = int(rng.integers(1, 500))
+            qr = rng.integers(0, 300, n).astype(np.int64)
+            qc = rng.integers(0, 37, n).astype(np.int32)
+            t, got = mt.pull_async(qr, qc, out=hb.array(npd, n, off))
+            off += (n * npd.itemsize + 7) // 8 * 8
+            outs.append(got)
+            want.append(full[qr, qc])
+        mt.wait(t)
+        for w, g in zip(want, outs):
+            np.testing.assert_array_equal(g, w)
+
+
 def test_wide_row_pull_answers_bypass_the_ring(gpu):
     """A row pull of a few rows of a very wide matrix (an answer > 16 MiB) is produced through the
     staged copies -- synchronous and async alike -- instead of growing a pinned ring slot to the

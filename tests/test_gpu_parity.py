@@ -880,20 +880,27 @@ def test_loopback_harness_gpu_backend(gpu):
      "--dtype", "long"],
     ["--clients", "16", "--servers", "4", "--keys", str(1 << 20), "--pattern", "uniform", "--records", "65536"],
 ])
-@pytest.mark.parametrize("replies", ["async", "burst"])
-def test_loopback_concurrent_clients_gpu_backend(gpu, args, replies):
+@pytest.mark.parametrize("server,replies,answers", [("threads", "async", "copy"), ("threads", "burst", "direct"),
+                                                    ("threads", "burst", "copy"), ("actor", "burst", "direct"),
+                                                    ("actor", "burst", "copy")])
+def test_loopback_concurrent_clients_gpu_backend(gpu, args, server, replies, answers):
     """configs[3]'s shape (64 concurrent loopback clients, 8 range-sharded servers -- here all on one
     GPU) with HBM shards: pushes enqueued through the pinned ring and acknowledged once applied, the
-    replies written by each connection's reply thread (async) or after one wait per drained burst;
-    Long sums bit-exact, dense ranges bit-exact."""
+    replies written by each connection's reply thread (async) or after one wait per drained burst, by
+    the connection's thread or by the server's one actor thread; pull answers written by the GPU
+    straight into pinned arenas (direct) or copied out of the ring (copy). Long sums bit-exact, dense
+    ranges bit-exact."""
     import json
     import subprocess
     from glint_amd.build import LIB, LOOPBACK_BIN
     r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--device", str(gpu),
-                        "--replies", replies] + args, capture_output=True, text=True, timeout=300)
+                        "--replies", replies, "--server", server, "--answers", answers] + args,
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
-    assert d["check"] is True and d["resends"] == 0 and d["replies"] == replies
+    assert d["check"] is True and d["resends"] == 0 and d["server"] == server and d["answers"] == answers
+    if server == "threads":
+        assert d["replies"] == replies
 
 
 def test_loopback_client_bucketing_offloaded(gpu):

@@ -148,7 +148,9 @@ for s in ${STAGES:-tests bench}; do
       for args in "" "--clients 64 --servers 8 --keys 33554432" \
                   "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
         for r in $(seq ${ROUNDS:-2}); do
-          step lba_gpu_${i}_$r 200 $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so $args --server actor --cpu-stats
+          for ans in ${ANSWERS:-direct}; do  # direct: answers written by the GPU into pinned arenas; copy: malloc'd
+            step lba_gpu_${ans}_${i}_$r 200 $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so $args --server actor --answers $ans --cpu-stats
+          done
           step lba_oracle_${i}_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so $args --server actor --cpu-stats
         done
         i=$((i + 1))

@@ -154,6 +154,13 @@ static void tune_socket(int fd) {
 /* ---- backends ----------------------------------------------------------------------------------- */
 static void* dl;
 static int use_gpu;
+/* --answers direct (the default when the library has glint_host_alloc): each connection answers
+ * pulls from a pinned, device-mapped arena, so the GPU writes the answers straight into the response
+ * images (no copy out of the ring slot); --answers copy: malloc'd response buffers */
+static int answers_direct = -1;
+static size_t arena_bytes; /* per connection: W responses of up to M records */
+static int (*g_host_alloc)(size_t, void**);
+static int (*g_host_free)(void*);
 static int gpu_device;
 static int dtype_long; /* 0: Double values, 1: Long values */
 
@@ -267,6 +274,7 @@ typedef struct {
   int32_t ack_id;  /* an AcknowledgeReceipt, or */
   uint8_t* resp;   /* a pull's Response frame (filled by the wait) */
   size_t resp_len;
+  int owned;       /* resp was malloc'd (else it lies in the connection's arena) */
 } hold;
 
 /* --cpu-stats: the servers' thread CPU time around the backend calls (one clock read each side) */
@@ -486,7 +494,14 @@ typedef struct {
   double cs[8]; /* --cpu-stats, as server.cpu */
   int wmode;    /* the kind (0 push, 1 pull) of the work a wait covers */
   int dirty;    /* --server actor: owes replies (in the actor's settle list) */
+  uint8_t* arena; /* --answers direct: the pinned response arena, reset after every settle */
+  size_t aused;
 } cstate;
+
+static void cstate_arena(cstate* c) {
+  if (use_gpu && answers_direct && arena_bytes && g_host_alloc((size_t)arena_bytes, (void**)&c->arena) != 0)
+    c->arena = NULL;
+}
 
 /* PartialVector*.receive + PushLogic for one message of connection c; returns 1 on L_STOP */
 static int handle_msg(server* s, cstate* c, const uint8_t* buf, uint32_t len) {
@@ -537,7 +552,17 @@ static int handle_msg(server* s, cstate* c, const uint8_t* buf, uint32_t len) {
     }
     size_t olen = 0;
     if (use_gpu) { /* enqueued after every push on the shard; its Response is held until the wait */
-      uint8_t* r = (uint8_t*)malloc(need);
+      /* the answer (r + 5) 8-aligned in the arena when it fits, else a malloc'd buffer */
+      size_t pos = c->aused + ((8 - ((uintptr_t)c->arena + c->aused + 5) % 8) % 8);
+      uint8_t* r;
+      int owned = 0;
+      if (c->arena && pos + need <= arena_bytes) {
+        r = c->arena + pos;
+        c->aused = pos + need;
+      } else {
+        r = (uint8_t*)malloc(need);
+        owned = 1;
+      }
       uint64_t ticket = 0;
       if (s->b.g_pull_async(s->b.shard, buf, len, r, need, &olen, &ticket) != 0) s->errors++;
       if (ticket > c->last_ticket) c->last_ticket = ticket;
@@ -550,6 +575,7 @@ static int handle_msg(server* s, cstate* c, const uint8_t* buf, uint32_t len) {
       c->holds[c->nhold].ack_id = 0;
       c->holds[c->nhold].resp = r;
       c->holds[c->nhold].resp_len = olen;
+      c->holds[c->nhold].owned = owned;
       ++c->nhold;
     } else {
       int64_t* keys = (int64_t*)malloc((size_t)n * 8 + 8);
@@ -624,7 +650,7 @@ static void answer(server* s, cstate* c, int rc) {
       from = c->holds[i].end;
       if (c->holds[i].resp) {
         ob_frame(&merged, c->holds[i].resp, (uint32_t)c->holds[i].resp_len);
-        free(c->holds[i].resp);
+        if (c->holds[i].owned) free(c->holds[i].resp);
       } else {
         ob_logic(&merged, receipt_has(s, c->holds[i].ack_id) ? L_ACK : L_NACK, c->holds[i].ack_id);
       }
@@ -634,6 +660,7 @@ static void answer(server* s, cstate* c, int rc) {
     free(c->out.p);
     c->out = merged;
     c->nhold = 0;
+    c->aused = 0; /* every answer in the arena has been sent */
   }
   ob_flush(&c->out, c->fd);
 }
@@ -656,6 +683,7 @@ static void cstate_free(server* s, cstate* c) {
     pthread_mutex_unlock(&s->mu);
   }
   close(c->fd);
+  if (c->arena) g_host_free(c->arena);
   free(c->resp);
   free(c->out.p);
   free(c->pending);
@@ -671,6 +699,7 @@ static void* conn_main(void* p) {
   cstate c;
   memset(&c, 0, sizeof(c));
   c.fd = a->fd;
+  cstate_arena(&c);
   uint8_t* buf = NULL;
   size_t cap = 0;
   for (;;) {
@@ -826,6 +855,7 @@ static void* acceptor_main(void* p) {
       if (fd < 0) die("accept");
       tune_socket(fd);
       conns[i].fd = fd;
+      cstate_arena(&conns[i]);
       aconn_arg* c = (aconn_arg*)malloc(sizeof(aconn_arg));
       c->m = &m;
       c->c = &conns[i];
@@ -1151,12 +1181,13 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) gpu_device = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--bucket") && i + 1 < argc) bucket_device = !strcmp(argv[++i], "device");
     else if (!strcmp(argv[i], "--cpu-stats")) cpu_stats = 1;
+    else if (!strcmp(argv[i], "--answers") && i + 1 < argc) answers_direct = !strcmp(argv[++i], "direct");
     else if (!strcmp(argv[i], "--server") && i + 1 < argc) server_actor = !strcmp(argv[++i], "actor");
     else if (!strcmp(argv[i], "--replies") && i + 1 < argc) replies_async = !strcmp(argv[++i], "async");
     else {
       fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--clients C] [--keys N] "
                       "[--pattern dense|uniform] [--records R] [--msg M] [--window W] [--dtype double|long] "
-                      "[--device D] [--bucket groupby|device] [--replies async|burst] [--server threads|actor] [--cpu-stats]\n", argv[0]);
+                      "[--device D] [--bucket groupby|device] [--replies async|burst] [--server threads|actor] [--answers direct|copy] [--cpu-stats]\n", argv[0]);
       return 2;
     }
   }
@@ -1164,6 +1195,15 @@ int main(int argc, char** argv) {
   if (!lib || S <= 0 || C <= 0 || N <= 0 || M <= 0 || W <= 0) { fprintf(stderr, "glint_loopback: bad arguments\n"); return 2; }
   if (uniform && R <= 0) R = N / C;
   backend_open(kind, lib);
+  if (use_gpu) {
+    *(void**)&g_host_alloc = dlsym(dl, "glint_host_alloc");
+    *(void**)&g_host_free = dlsym(dl, "glint_host_free");
+    if (answers_direct < 0) answers_direct = g_host_alloc && g_host_free;
+    if (answers_direct && (!g_host_alloc || !g_host_free)) die("dlsym glint_host_alloc");
+    arena_bytes = (size_t)W * ((size_t)M * 8 + 16);
+  } else {
+    answers_direct = 0;
+  }
   if (bucket_device) { /* the device route of libglint_gpu.so and the HIP runtime it runs on */
     if (!use_gpu) { fprintf(stderr, "glint_loopback: --bucket device needs --backend gpu\n"); return 2; }
     hip_dl = dlopen("libamdhip64.so", RTLD_NOW | RTLD_LOCAL);
@@ -1334,14 +1374,14 @@ int main(int argc, char** argv) {
          "\"keys\": %lld, \"records\": %lld, \"max_records_per_message\": %d, \"window\": %d, "
          "\"push_messages\": %lld, \"pull_messages\": %lld, \"resends\": %lld, \"push_s\": %.6f, \"pull_s\": %.6f, "
          "\"push_records_per_s\": %.1f, \"pull_records_per_s\": %.1f, \"push_payload_MBps\": %.2f, "
-         "\"pull_payload_MBps\": %.2f, \"server\": \"%s\", \"replies\": \"%s\", \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
+         "\"pull_payload_MBps\": %.2f, \"server\": \"%s\", \"answers\": \"%s\", \"replies\": \"%s\", \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
          "\"bucket_s_max\": [%.6f, %.6f], \"process_cpu_s\": [%.4f, %.4f], \"server_call_cpu_s\": [%.4f, %.4f], "
          "\"server_wait_cpu_s\": [%.4f, %.4f], \"server_wait_wall_s\": [%.4f, %.4f], \"server_call_wall_s\": [%.4f, %.4f], "
          "\"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
          kind, pattern, dtype_long ? "long" : "double", S, C, (long long)N, (long long)total, M, W,
          (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl, (double)total / tp, (double)total / tl,
          16.0 * (double)total / tp / 1e6, 16.0 * (double)total / tl / 1e6,
-         server_actor ? "actor" : "threads", !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
+         server_actor ? "actor" : "threads", answers_direct ? "direct" : "copy", !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
          pc[1] - pc[0], pc[2] - pc[1], scpu[0], scpu[1], scpu[2], scpu[3], scpu[4], scpu[5], scpu[6], scpu[7],
          dtype_long ? 0.0 : ((double*)cv[0])[0], (!dtype_long && cn[0] > 1) ? ((double*)cv[0])[1] : 0.0,
          (!dtype_long && cn[0] > 2) ? ((double*)cv[0])[2] : 0.0, ok ? "true" : "false");
