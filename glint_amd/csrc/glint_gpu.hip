@@ -465,16 +465,18 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
 }
 
 // A ring pull (one signalling workgroup, <= kRingPullMax records, keys read from the mapped slot
-// over PCIe): 1024 threads, four records each, every key load issued before any gather and every
-// gather before any store -- one PCIe round trip and one HBM round trip. The grid-stride kernels
-// above ran 8 dependent iterations per thread at 256 threads (their stores may alias the keys, so
-// the next iteration's loads could not move above them).
-constexpr int kRingPullTPB = 1024;
-constexpr int kRingPullPer = 4;
-constexpr i64 kRingPullMax = (i64)kRingPullTPB * kRingPullPer;
+// over PCIe): 1024 threads, up to sixteen records each (record j * 1024 + thread: every load
+// instruction of a wave reads 64 consecutive keys), every key load issued before any gather and every
+// gather before any store -- one PCIe round trip and one HBM round trip. A coalesced pull batch holds
+// up to kRingPullMax records (four times a push batch: one launch per ~16 Akka-sized pulls). The
+// grid-stride kernels above ran 8 dependent iterations per thread at 256 threads (their stores may
+// alias the keys, so the next iteration's loads could not move above them).
 // With a destination table (a coalesced batch whose callers answer from glint_host_alloc buffers),
 // each record's answer goes to its own message's destination: the table (<= kPullDirectMax entries,
 // read over PCIe beside the keys) is staged in LDS and a record finds its message by binary search.
+constexpr int kRingPullTPB = 1024;
+constexpr int kRingPullPer = 16;
+constexpr i64 kRingPullMax = (i64)kRingPullTPB * kRingPullPer;
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __restrict__ keys,
                                                                 const int32_t* __restrict__ cols, i64 n,
@@ -483,14 +485,18 @@ __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __re
                                                                 const PullDst* __restrict__ tab, int nm) {
   __shared__ u32 s_off[kPullDirectMax + 1];
   __shared__ V* s_dst[kPullDirectMax];
-  const i64 r0 = (i64)threadIdx.x * kRingPullPer;
+  // records per thread actually present (launch-uniform bound: no loads past the batch)
+  const int per = (int)min<i64>(kRingPullPer, (n + kRingPullTPB - 1) / kRingPullTPB);
   i64 k[kRingPullPer];
   int32_t c[kRingPullPer];
 #pragma unroll
   for (int j = 0; j < kRingPullPer; ++j) {  // clamped, branch-free: all loads in flight together
-    const i64 r = r0 + j < n ? r0 + j : n - 1;
-    k[j] = keys[r];
-    c[j] = MAT ? cols[r] : 0;
+    if (j < per) {
+      const i64 r0 = (i64)j * kRingPullTPB + threadIdx.x;
+      const i64 r = r0 < n ? r0 : n - 1;
+      k[j] = keys[r];
+      c[j] = MAT ? cols[r] : 0;
+    }
   }
   if (tab) {  // launch-uniform
     for (int i = threadIdx.x; i < nm; i += kRingPullTPB) {
@@ -502,17 +508,20 @@ __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __re
   V v[kRingPullPer];
 #pragma unroll
   for (int j = 0; j < kRingPullPer; ++j) {
-    i64 l;
-    const bool ok = rec_addr<MAT>(part, k[j], c[j], l);
-    v[j] = ok ? data[l] : V(0);
-    if (!ok && r0 + j < n) record_error(err, r0 + j);
+    if (j < per) {
+      const i64 r = (i64)j * kRingPullTPB + threadIdx.x;
+      i64 l;
+      const bool ok = rec_addr<MAT>(part, k[j], c[j], l);
+      v[j] = ok ? data[l] : V(0);
+      if (!ok && r < n) record_error(err, r);
+    }
   }
   if (tab) {
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kRingPullPer; ++j) {
-      const i64 r = r0 + j;
-      if (r >= n) continue;
+      const i64 r = (i64)j * kRingPullTPB + threadIdx.x;
+      if (j >= per || r >= n) continue;
       int lo = 0, hi = nm - 1;  // the last message starting at or before r
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -523,8 +532,10 @@ __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __re
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < kRingPullPer; ++j)
-      if (r0 + j < n) out[r0 + j] = v[j];
+    for (int j = 0; j < kRingPullPer; ++j) {
+      const i64 r = (i64)j * kRingPullTPB + threadIdx.x;
+      if (j < per && r < n) out[r] = v[j];
+    }
   }
   msg_signal(sig, err);
 }
@@ -1551,7 +1562,7 @@ void* host_dev_ptr(const void* p, size_t bytes, size_t align) {
 
 // a coalesced pull batch's destination table: behind the answer section of its slot
 inline size_t pull_tab_off(const glint_shard* s, const StageLayout& L) {
-  return L.kb + L.cb + pad256((size_t)GLINT_ZERO_COPY_MAX * s->vsize);  // (kBatchMax, below)
+  return L.kb + L.cb + pad256((size_t)kRingPullMax * s->vsize);  // (kPullBatch, below)
 }
 
 // whether an entry of n records is one signalling launch reading (and answering) in the mapped slot
@@ -1606,6 +1617,7 @@ int ring_dispatch(glint_shard* s, glint_shard::RingSlot& r, bool direct, u64 lo,
 // order -- each message applied after the one before it, the actor's own sequence -- so results
 // are those of one launch per message. Every message keeps its ticket; the launch signals the last.
 constexpr i64 kBatchMax = GLINT_ZERO_COPY_MAX;
+constexpr i64 kPullBatch = kRingPullMax;  // records per coalesced pull batch (messages <= kBatchMax each)
 
 int launch_push_entry(glint_shard* s, glint_shard::RingSlot& r, const char* base, const StageLayout& L, i64 n,
                       int flags, bool direct, u64 lo, u64 hi) {
@@ -1771,7 +1783,7 @@ int ring_pull_locked(glint_shard* s, int idx, int kind, i64 n, void* out, size_t
 // A coalesced pull batch: consecutive message-sized element pulls of one kind share one launch;
 // each answer is copied to its own destination when the batch retires.
 int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind) {
-  const StageLayout L = stage_layout(s, kBatchMax);
+  const StageLayout L = stage_layout(s, kPullBatch);
   const i64* keys = (const i64*)r.hd;
   const int32_t* cols = (const int32_t*)(r.hd + L.kb);
   char* ans = r.hd + L.kb + L.cb;
@@ -1812,21 +1824,21 @@ int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys
                             u64* ticket, bool checked) {
   int rc = checked ? GLINT_OK : reject_if_bad(s, keys, kind == 1 ? cols : nullptr, n);
   if (rc) return rc;
-  if (s->open_slot >= 0 && (s->open_kind != kind || s->ring[s->open_slot].fill + n > kBatchMax)) {
+  if (s->open_slot >= 0 && (s->open_kind != kind || s->ring[s->open_slot].fill + n > kPullBatch)) {
     rc = ring_flush_locked(s);
     if (rc) return rc;
   }
   if (s->open_slot < 0) {
     int slot = -1;
     // the answer section, then the destination table (pull_tab_off)
-    rc = ring_acquire_locked(s, kBatchMax, &slot, pad256((size_t)kBatchMax * s->vsize) + sizeof(PullDst) * kPullDirectMax);
+    rc = ring_acquire_locked(s, kPullBatch, &slot, pad256((size_t)kPullBatch * s->vsize) + sizeof(PullDst) * kPullDirectMax);
     if (rc) return rc;
     s->open_slot = slot;
     s->open_kind = kind;
     s->open_flags = 0;
   }
   glint_shard::RingSlot& r = s->ring[s->open_slot];
-  const StageLayout L = stage_layout(s, kBatchMax);
+  const StageLayout L = stage_layout(s, kPullBatch);
   std::memcpy(r.h + (size_t)r.fill * 8, keys, (size_t)n * 8);
   if (kind == 1) std::memcpy(r.h + L.kb + (size_t)r.fill * 4, cols, (size_t)n * 4);
   const u64 t = ++s->ticket_next;
@@ -1836,7 +1848,7 @@ int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys
   r.msgs.push_back(m);
   r.fill += n;
   if (ticket) *ticket = t;
-  if (r.fill == kBatchMax) return ring_flush_locked(s);
+  if (r.fill == kPullBatch) return ring_flush_locked(s);
   return GLINT_OK;
 }
 

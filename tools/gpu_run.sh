@@ -115,6 +115,13 @@ for s in ${STAGES:-tests bench}; do
         step mps8_par_$r 300 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
       done
       ;;
+    mps8lw)  # the exchange line with 8 local partitions: bin_apply's whole-line write-back on (1) / off (0)
+      for r in 1 2; do
+        for v in 1 0; do
+          step mps8lw_${v}_$r 300 env GLINT_BIN_LINE_WB=$v python3 bench.py --no-cpu-baseline --no-north-star --pattern exchange --parts-per-gpu 8
+        done
+      done
+      ;;
     lbsleep)  # the cfg4 loopback rows with the GPU servers' waits sleeping (GLINT_WAIT_SLEEP_US) or yielding
       LB=tools/loopback/build/glint_loopback
       G="--backend gpu --lib glint_amd/lib/libglint_gpu.so"
