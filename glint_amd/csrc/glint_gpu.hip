@@ -465,17 +465,17 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
 }
 
 // A ring pull (one signalling workgroup, <= kRingPullMax records, keys read from the mapped slot
-// over PCIe): 1024 threads, up to sixteen records each (record j * 1024 + thread: every load
+// over PCIe): 1024 threads, up to four records each (record j * 1024 + thread: every load
 // instruction of a wave reads 64 consecutive keys), every key load issued before any gather and every
-// gather before any store -- one PCIe round trip and one HBM round trip. A coalesced pull batch holds
-// up to kRingPullMax records (four times a push batch: one launch per ~16 Akka-sized pulls). The
-// grid-stride kernels above ran 8 dependent iterations per thread at 256 threads (their stores may
-// alias the keys, so the next iteration's loads could not move above them).
+// gather before any store -- one PCIe round trip and one HBM round trip. The grid-stride kernels
+// above ran 8 dependent iterations per thread at 256 threads (their stores may alias the keys, so the
+// next iteration's loads could not move above them). (Batches of 16 384 records, 16 per thread, were
+// tried in a build whose ring slots were re-pinned mid-traffic, and not re-measured.)
 // With a destination table (a coalesced batch whose callers answer from glint_host_alloc buffers),
 // each record's answer goes to its own message's destination: the table (<= kPullDirectMax entries,
 // read over PCIe beside the keys) is staged in LDS and a record finds its message by binary search.
 constexpr int kRingPullTPB = 1024;
-constexpr int kRingPullPer = 16;
+constexpr int kRingPullPer = 4;
 constexpr i64 kRingPullMax = (i64)kRingPullTPB * kRingPullPer;
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __restrict__ keys,
@@ -1496,7 +1496,10 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
       if (r.h) (void)hipHostFree(r.h);
       r.h = r.hd = nullptr;
       r.hcap = 0;
-      size_t cap = (size_t)1 << 16;
+      // at least a coalesced batch of either kind: a slot first sized for a push batch (keys + values,
+      // 64 KiB of Double) and later taken by a pull batch (keys + answers + destination table) would
+      // otherwise be freed and re-pinned in the middle of the traffic (cfg1 pulls 124 -> 62 M/s)
+      size_t cap = (size_t)1 << 17;
       while (cap < need) cap <<= 1;
       if (hipHostMalloc((void**)&r.h, cap, hipHostMallocMapped) != hipSuccess ||
           hipHostGetDevicePointer((void**)&r.hd, r.h, 0) != hipSuccess) {
@@ -1560,6 +1563,12 @@ void* host_dev_ptr(const void* p, size_t bytes, size_t align) {
   return it->d + (c - it->h);
 }
 
+// smallest answer (bytes) a pull writes straight into a glint_host_alloc buffer (GLINT_DIRECT_MIN_BYTES)
+size_t direct_min_bytes() {
+  static EnvKnob k("GLINT_DIRECT_MIN_BYTES");
+  return (size_t)k.get([](const char* e) -> long long { return e ? atoll(e) : 4096ll; });
+}
+
 // a coalesced pull batch's destination table: behind the answer section of its slot
 inline size_t pull_tab_off(const glint_shard* s, const StageLayout& L) {
   return L.kb + L.cb + pad256((size_t)kRingPullMax * s->vsize);  // (kPullBatch, below)
@@ -1617,7 +1626,7 @@ int ring_dispatch(glint_shard* s, glint_shard::RingSlot& r, bool direct, u64 lo,
 // order -- each message applied after the one before it, the actor's own sequence -- so results
 // are those of one launch per message. Every message keeps its ticket; the launch signals the last.
 constexpr i64 kBatchMax = GLINT_ZERO_COPY_MAX;
-constexpr i64 kPullBatch = kRingPullMax;  // records per coalesced pull batch (messages <= kBatchMax each)
+constexpr i64 kPullBatch = kRingPullMax;  // records per coalesced pull batch (= kBatchMax)
 
 int launch_push_entry(glint_shard* s, glint_shard::RingSlot& r, const char* base, const StageLayout& L, i64 n,
                       int flags, bool direct, u64 lo, u64 hi) {
@@ -1844,7 +1853,10 @@ int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys
   const u64 t = ++s->ticket_next;
   glint_shard::RingSlot::Msg m{r.fill, n, t};
   m.out = out;
-  m.dout = host_dev_ptr(out, (size_t)n * s->vsize, s->vsize);
+  // answered in place only from a page of answer on: each message's destination costs the kernel's
+  // stores a host-page translation, so small answers are cheaper copied out of the contiguous slot
+  // (cfg4b's ~125-record pulls ran at half the rate in place; cfg4a's 1000-record ones 1.4x faster)
+  m.dout = (size_t)n * s->vsize >= direct_min_bytes() ? host_dev_ptr(out, (size_t)n * s->vsize, s->vsize) : nullptr;
   r.msgs.push_back(m);
   r.fill += n;
   if (ticket) *ticket = t;

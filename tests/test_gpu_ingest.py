@@ -334,12 +334,17 @@ def test_coalesced_pulls_answer_each_message(gpu, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["double", "int"])
-def test_pulls_answer_straight_into_host_buffers(gpu, dtype):
+@pytest.mark.parametrize("min_bytes", ["0", None])
+def test_pulls_answer_straight_into_host_buffers(gpu, dtype, min_bytes, monkeypatch):
     """Answers whose destination is glint_host_alloc memory (HostBuffer) are written by the kernel
     itself through the batch's destination table; in the same batch, messages answering into ordinary
-    memory or at a misaligned address still get theirs through the slot; a batch of more messages
-    than the table holds (kPullDirectMax) falls back to the copies; matrix element pulls likewise."""
+    memory, at a misaligned address or below GLINT_DIRECT_MIN_BYTES (default one page; "0": every
+    message in place) still get theirs through the slot; a batch of more messages than the table holds
+    (kPullDirectMax) falls back to the copies; matrix element pulls likewise."""
     from glint_amd.shard import HostBuffer
+    if min_bytes is not None:
+        monkeypatch.setenv("GLINT_DIRECT_MIN_BYTES", min_bytes)
+    N.reload_env()
     size = 20_000
     rng = np.random.default_rng(93)
     npd = np.dtype(np.float64 if dtype == "double" else np.int32)
@@ -349,7 +354,7 @@ def test_pulls_answer_straight_into_host_buffers(gpu, dtype):
         for rnd in range(3):
             outs, want, tickets, off = [], [], [], 0
             for m in range(60):
-                n = int(rng.integers(1, 400))
+                n = int(rng.integers(1, 400 if min_bytes == "0" else 1500))
                 q = rng.integers(0, size, n).astype(np.int64)
                 kind = m % 4
                 if kind == 3:  # ordinary numpy memory: through the slot

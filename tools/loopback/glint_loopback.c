@@ -498,9 +498,13 @@ typedef struct {
   size_t aused;
 } cstate;
 
+/* connections whose server side is set up (arena allocated): the timed phases start only once all
+ * are, so no pinned allocation overlaps them */
+static int conns_ready;
 static void cstate_arena(cstate* c) {
   if (use_gpu && answers_direct && arena_bytes && g_host_alloc((size_t)arena_bytes, (void**)&c->arena) != 0)
     c->arena = NULL;
+  __atomic_add_fetch(&conns_ready, 1, __ATOMIC_RELEASE);
 }
 
 /* PartialVector*.receive + PushLogic for one message of connection c; returns 1 on L_STOP */
@@ -552,11 +556,13 @@ static int handle_msg(server* s, cstate* c, const uint8_t* buf, uint32_t len) {
     }
     size_t olen = 0;
     if (use_gpu) { /* enqueued after every push on the shard; its Response is held until the wait */
-      /* the answer (r + 5) 8-aligned in the arena when it fits, else a malloc'd buffer */
+      /* the answer (r + 5) 8-aligned in the arena when it fits and is answered in place (a page of
+       * answer or more, as the library decides: GLINT_DIRECT_MIN_BYTES), else a malloc'd buffer --
+       * smaller answers are copied out of the ring slot, and copied into ordinary memory faster */
       size_t pos = c->aused + ((8 - ((uintptr_t)c->arena + c->aused + 5) % 8) % 8);
       uint8_t* r;
       int owned = 0;
-      if (c->arena && pos + need <= arena_bytes) {
+      if (c->arena && (size_t)n * 8 >= 4096 && pos + need <= arena_bytes) {
         r = c->arena + pos;
         c->aused = pos + need;
       } else {
@@ -1305,6 +1311,8 @@ int main(int argc, char** argv) {
   client_arg* cargs = (client_arg*)calloc((size_t)C, sizeof(client_arg));
   if (bucket_device)
     for (int c = 0; c < C; ++c) client_dev_init(&cargs[c].dev, ck[c], cn[c]);
+  if (!(use_gpu && replies_async)) /* every connection's server side is set up (conn_main_async has no arena) */
+    while (__atomic_load_n(&conns_ready, __ATOMIC_ACQUIRE) < S * C) usleep(1000);
   double t[3], pc[3], bucket_s[2] = {0, 0}, bucket_max[2] = {0, 0};
   int64_t msgs[2] = {0, 0}, resends = 0;
   for (int mode = 0; mode < 2; ++mode) {
