@@ -475,7 +475,10 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
 // each record's answer goes to its own message's destination: the table (<= kPullDirectMax entries,
 // read over PCIe beside the keys) is staged in LDS and a record finds its message by binary search.
 constexpr int kRingPullTPB = 1024;
-constexpr int kRingPullPer = 4;
+#ifndef GLINT_RING_PULL_PER
+#define GLINT_RING_PULL_PER 4  // (a build-time experiment knob: records per thread of a ring pull)
+#endif
+constexpr int kRingPullPer = GLINT_RING_PULL_PER;
 constexpr i64 kRingPullMax = (i64)kRingPullTPB * kRingPullPer;
 template <typename V, bool MAT>
 __global__ __launch_bounds__(kRingPullTPB) void ring_pull_kernel(const i64* __restrict__ keys,
@@ -1467,6 +1470,13 @@ int ring_retire_through(glint_shard* s, u64 t) {
   }
 }
 
+// the pinned bytes a coalesced pull batch needs (keys, cols, answers, destination table): every
+// slot is pinned at least this large from the start
+inline size_t kPullSlotMin(const glint_shard* s) {
+  const StageLayout L = stage_layout(s, kRingPullMax);
+  return L.kb + L.cb + pad256((size_t)kRingPullMax * s->vsize) + sizeof(PullDst) * kPullDirectMax;
+}
+
 // Hands out a free slot sized for n records (and, for a pull, an answer of out_bytes behind the
 // key sections). Retires the slot's previous entry (and every older one) first.
 int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) {
@@ -1499,7 +1509,7 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
       // at least a coalesced batch of either kind: a slot first sized for a push batch (keys + values,
       // 64 KiB of Double) and later taken by a pull batch (keys + answers + destination table) would
       // otherwise be freed and re-pinned in the middle of the traffic (cfg1 pulls 124 -> 62 M/s)
-      size_t cap = (size_t)1 << 17;
+      size_t cap = std::max<size_t>((size_t)1 << 17, kPullSlotMin(s));
       while (cap < need) cap <<= 1;
       if (hipHostMalloc((void**)&r.h, cap, hipHostMallocMapped) != hipSuccess ||
           hipHostGetDevicePointer((void**)&r.hd, r.h, 0) != hipSuccess) {

@@ -908,12 +908,13 @@ def test_loopback_client_bucketing_offloaded(gpu):
     either as the reference's groupBy restated on the host or offloaded to the GPU (glint_route_dev,
     one stable route of the whole batch). Both send the same messages; with Long values the shards end
     bit-identical (each run's pulled values equal the exact sums), and each run reports its bucketing
-    time per client."""
+    time per client. `auto` routes a batch on the device while fewer than 4 clients are, else on the
+    host (the same messages either way)."""
     import json
     import subprocess
     from glint_amd.build import LIB, LOOPBACK_BIN
     out = {}
-    for mode in ("groupby", "device"):
+    for mode in ("groupby", "device", "auto"):
         r = subprocess.run([str(LOOPBACK_BIN), "--backend", "gpu", "--lib", str(LIB), "--device", str(gpu),
                             "--clients", "64", "--servers", "8", "--keys", str(1 << 22), "--pattern", "uniform",
                             "--records", "32768", "--dtype", "long", "--bucket", mode],
@@ -923,5 +924,7 @@ def test_loopback_client_bucketing_offloaded(gpu):
         assert d["check"] is True and d["resends"] == 0 and d["bucket"] == mode
         assert all(x > 0 for x in d["bucket_s_per_client"])
         out[mode] = d
-    assert out["groupby"]["push_messages"] == out["device"]["push_messages"]
-    assert out["groupby"]["pull_messages"] == out["device"]["pull_messages"]
+    for mode in ("device", "auto"):
+        assert out["groupby"]["push_messages"] == out[mode]["push_messages"]
+        assert out["groupby"]["pull_messages"] == out[mode]["pull_messages"]
+    assert out["device"]["device_batches"] == 2 * 64 and 0 < out["auto"]["device_batches"] <= 2 * 64

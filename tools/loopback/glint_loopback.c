@@ -942,7 +942,13 @@ typedef struct {
 } link_arg;
 
 /* ---- client bucketing (mapPartitions, AsyncBigVector.scala:96-98) ------------------------------------ */
-static int bucket_device;  /* --bucket device */
+static int bucket_device;  /* --bucket device (1) or auto (2) */
+/* --bucket auto: a batch is routed on the device while fewer than auto_max clients are (the one GPU
+ * and its PCIe link are shared by every client of the loopback; past a few concurrent routes each
+ * waits behind the others' transfers), else grouped on the host */
+static int auto_max = 4;
+static int dev_routes;     /* clients routing on the device right now */
+static int dev_batches;    /* batches routed on the device (--bucket auto reports it) */
 static void* hip_dl;
 static int (*hip_malloc)(void**, size_t);
 static int (*hip_free)(void*);
@@ -1000,7 +1006,12 @@ static void client_dev_init(client_dev* d, const int64_t* keys, int64_t n) {
 static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int64_t** store, client_dev* d) {
   const double t0 = now_s();
   int64_t* cnt = (int64_t*)calloc((size_t)S, 8);
-  if (bucket_device && n > 0) {
+  int on_dev = bucket_device == 1 && n > 0;
+  if (bucket_device == 2 && n > 0) {
+    if (__atomic_add_fetch(&dev_routes, 1, __ATOMIC_ACQ_REL) <= auto_max) on_dev = 1;
+    else __atomic_sub_fetch(&dev_routes, 1, __ATOMIC_ACQ_REL);
+  }
+  if (on_dev) {
     /* offloaded: one stable route of the whole batch on the GPU, on the client's stream, one wait */
     if (hip_memcpy_async(d->dk, d->keys, (size_t)n * 8, 1 /* hipMemcpyHostToDevice */, d->stream)) die("hipMemcpyAsync");
     if (route_gather_dev((const int64_t*)d->dk, NULL, NULL, 0, n, 0 /* GLINT_ROUTE_RANGE */, S, N, NULL,
@@ -1018,6 +1029,10 @@ static double bucket_client(link_arg* links, const int64_t* keys, int64_t n, int
       cut_messages(&links[p], d->order + o, cnt[p]);
       store[p] = NULL;
       o += cnt[p];
+    }
+    if (bucket_device == 2) {
+      __atomic_sub_fetch(&dev_routes, 1, __ATOMIC_ACQ_REL);
+      __atomic_add_fetch(&dev_batches, 1, __ATOMIC_ACQ_REL);
     }
     free(cnt);
     return now_s() - t0;
@@ -1185,7 +1200,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--pattern") && i + 1 < argc) pattern = argv[++i];
     else if (!strcmp(argv[i], "--dtype") && i + 1 < argc) dtype_long = !strcmp(argv[++i], "long");
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) gpu_device = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--bucket") && i + 1 < argc) bucket_device = !strcmp(argv[++i], "device");
+    else if (!strcmp(argv[i], "--bucket") && i + 1 < argc) {
+      ++i;
+      bucket_device = !strcmp(argv[i], "device") ? 1 : !strcmp(argv[i], "auto") ? 2 : 0;
+    } else if (!strcmp(argv[i], "--auto-max") && i + 1 < argc) auto_max = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--cpu-stats")) cpu_stats = 1;
     else if (!strcmp(argv[i], "--answers") && i + 1 < argc) answers_direct = !strcmp(argv[++i], "direct");
     else if (!strcmp(argv[i], "--server") && i + 1 < argc) server_actor = !strcmp(argv[++i], "actor");
@@ -1193,7 +1211,7 @@ int main(int argc, char** argv) {
     else {
       fprintf(stderr, "usage: %s --backend oracle|gpu --lib PATH [--servers S] [--clients C] [--keys N] "
                       "[--pattern dense|uniform] [--records R] [--msg M] [--window W] [--dtype double|long] "
-                      "[--device D] [--bucket groupby|device] [--replies async|burst] [--server threads|actor] [--answers direct|copy] [--cpu-stats]\n", argv[0]);
+                      "[--device D] [--bucket groupby|device|auto] [--auto-max K] [--replies async|burst] [--server threads|actor] [--answers direct|copy] [--cpu-stats]\n", argv[0]);
       return 2;
     }
   }
@@ -1383,14 +1401,14 @@ int main(int argc, char** argv) {
          "\"push_messages\": %lld, \"pull_messages\": %lld, \"resends\": %lld, \"push_s\": %.6f, \"pull_s\": %.6f, "
          "\"push_records_per_s\": %.1f, \"pull_records_per_s\": %.1f, \"push_payload_MBps\": %.2f, "
          "\"pull_payload_MBps\": %.2f, \"server\": \"%s\", \"answers\": \"%s\", \"replies\": \"%s\", \"bucket\": \"%s\", \"bucket_s_per_client\": [%.6f, %.6f], "
-         "\"bucket_s_max\": [%.6f, %.6f], \"process_cpu_s\": [%.4f, %.4f], \"server_call_cpu_s\": [%.4f, %.4f], "
+         "\"bucket_s_max\": [%.6f, %.6f], \"device_batches\": %d, \"process_cpu_s\": [%.4f, %.4f], \"server_call_cpu_s\": [%.4f, %.4f], "
          "\"server_wait_cpu_s\": [%.4f, %.4f], \"server_wait_wall_s\": [%.4f, %.4f], \"server_call_wall_s\": [%.4f, %.4f], "
          "\"first_values\": [%.17g, %.17g, %.17g], \"check\": %s}\n",
          kind, pattern, dtype_long ? "long" : "double", S, C, (long long)N, (long long)total, M, W,
          (long long)msgs[0], (long long)msgs[1], (long long)resends, tp, tl, (double)total / tp, (double)total / tl,
          16.0 * (double)total / tp / 1e6, 16.0 * (double)total / tl / 1e6,
-         server_actor ? "actor" : "threads", answers_direct ? "direct" : "copy", !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device ? "device" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
-         pc[1] - pc[0], pc[2] - pc[1], scpu[0], scpu[1], scpu[2], scpu[3], scpu[4], scpu[5], scpu[6], scpu[7],
+         server_actor ? "actor" : "threads", answers_direct ? "direct" : "copy", !use_gpu ? "inline" : replies_async ? "async" : "burst", bucket_device == 1 ? "device" : bucket_device == 2 ? "auto" : "groupby", bucket_s[0], bucket_s[1], bucket_max[0], bucket_max[1],
+         bucket_device == 1 ? 2 * C : dev_batches, pc[1] - pc[0], pc[2] - pc[1], scpu[0], scpu[1], scpu[2], scpu[3], scpu[4], scpu[5], scpu[6], scpu[7],
          dtype_long ? 0.0 : ((double*)cv[0])[0], (!dtype_long && cn[0] > 1) ? ((double*)cv[0])[1] : 0.0,
          (!dtype_long && cn[0] > 2) ? ((double*)cv[0])[2] : 0.0, ok ? "true" : "false");
   return ok ? 0 : 1;
