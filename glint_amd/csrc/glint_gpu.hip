@@ -469,8 +469,10 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
 // instruction of a wave reads 64 consecutive keys), every key load issued before any gather and every
 // gather before any store -- one PCIe round trip and one HBM round trip. The grid-stride kernels
 // above ran 8 dependent iterations per thread at 256 threads (their stores may alias the keys, so the
-// next iteration's loads could not move above them). (Batches of 16 384 records, 16 per thread, were
-// tried in a build whose ring slots were re-pinned mid-traffic, and not re-measured.)
+// next iteration's loads could not move above them). Batches of 16 384 records (16 per thread,
+// GLINT_RING_PULL_PER=16) were measured and not kept: the actor-model cfg4a pulls ran 695-759 M
+// records/s against 800-879 with 4 096 (profiles/r04/ab_ring_pull_per.txt): fewer launches, but one
+// workgroup reading 128 KB of keys over PCIe per launch, and the GPU waits for 16 messages.
 // With a destination table (a coalesced batch whose callers answer from glint_host_alloc buffers),
 // each record's answer goes to its own message's destination: the table (<= kPullDirectMax entries,
 // read over PCIe beside the keys) is staged in LDS and a record finds its message by binary search.
