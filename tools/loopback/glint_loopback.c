@@ -999,11 +999,12 @@ static void client_dev_init(client_dev* d, const int64_t* keys, int64_t n) {
       hip_host_malloc((void**)&d->keys, b, 0))
     die("hipHostMalloc");
   memcpy(d->keys, keys, (size_t)n * 8);
-  /* one route of one key on the new stream, before the timed region: the stream's first use (its
-   * hardware queue, the route's scratch) is paid here, as a client process pays it once */
+  /* one route of the batch on the new stream, before the timed region: the stream's first use (its
+   * hardware queue) and the route's scratch, sized by the batch, are paid here, as a client process
+   * pays them once for its batches */
   if (n > 0) {
-    if (hip_memcpy_async(d->dk, d->keys, 8, 1, d->stream) ||
-        route_gather_dev((const int64_t*)d->dk, NULL, NULL, 0, 1, 0, S, N, NULL, (int64_t*)d->dc, (int64_t*)d->dord,
+    if (hip_memcpy_async(d->dk, d->keys, (size_t)n * 8, 1, d->stream) ||
+        route_gather_dev((const int64_t*)d->dk, NULL, NULL, 0, n, 0, S, N, NULL, (int64_t*)d->dc, (int64_t*)d->dord,
                          NULL, NULL, NULL, (uint64_t*)d->dbad, d->stream) ||
         hip_memcpy_async(d->cnt, d->dc, (size_t)S * 8 + 8, 2, d->stream) || hip_stream_sync(d->stream))
       die("client warm-up route");
