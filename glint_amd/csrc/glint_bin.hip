@@ -1457,11 +1457,13 @@ u32 bin_sparse_max() {
 }
 
 // a sparse item whose list holds more distinct elements than this writes back by the line sweep
-// instead (GLINT_BIN_LIST_MAX): past a few hundred of a slab's 4096 elements most of its lines are
-// touched, and element stores would leave them byte-masked
+// instead (GLINT_BIN_LIST_MAX, default 768; 0xFFFFFFFF disables): at 768 of a slab's 4096 elements
+// ~95 % of its lines are touched, and element stores would leave them byte-masked. Same box, 3 rounds
+// (profiles/r04/ab_apply_writeback.txt): cfg4b exchange 2.91 -> 2.84-2.88 ms, cfg3 unchanged, cfg5
+// within its run-to-run spread (0.43-0.46 ms either way); lower thresholds (256, 512) slowed cfg5
 u32 bin_list_max() {
   static EnvKnob k("GLINT_BIN_LIST_MAX");
-  return (u32)k.get([](const char* e) -> long long { return e ? (long long)strtoul(e, nullptr, 10) : 0xFFFFFFFFll; });
+  return (u32)k.get([](const char* e) -> long long { return e ? (long long)strtoul(e, nullptr, 10) : 768ll; });
 }
 
 // bin_apply's swept items write back whole touched lines (GLINT_BIN_LINE_WB, default 1) or the

@@ -1474,7 +1474,7 @@ int ring_retire_through(glint_shard* s, u64 t) {
 
 // the pinned bytes a coalesced pull batch needs (keys, cols, answers, destination table): every
 // slot is pinned at least this large from the start
-inline size_t kPullSlotMin(const glint_shard* s) {
+inline size_t pull_slot_min(const glint_shard* s) {
   const StageLayout L = stage_layout(s, kRingPullMax);
   return L.kb + L.cb + pad256((size_t)kRingPullMax * s->vsize) + sizeof(PullDst) * kPullDirectMax;
 }
@@ -1511,7 +1511,7 @@ int ring_acquire_locked(glint_shard* s, i64 n, int* slot, size_t out_bytes = 0) 
       // at least a coalesced batch of either kind: a slot first sized for a push batch (keys + values,
       // 64 KiB of Double) and later taken by a pull batch (keys + answers + destination table) would
       // otherwise be freed and re-pinned in the middle of the traffic (cfg1 pulls 124 -> 62 M/s)
-      size_t cap = std::max<size_t>((size_t)1 << 17, kPullSlotMin(s));
+      size_t cap = std::max<size_t>((size_t)1 << 17, pull_slot_min(s));
       while (cap < need) cap <<= 1;
       if (hipHostMalloc((void**)&r.h, cap, hipHostMallocMapped) != hipSuccess ||
           hipHostGetDevicePointer((void**)&r.hd, r.h, 0) != hipSuccess) {
