@@ -307,8 +307,9 @@ int glint_reload_env(void);
 
 /* Pinned, device-mapped host memory for the buffers a server answers from (the response images it
  * sends). A message-sized pull (glint_pull_async, glint_pull_wire_async) whose answer destination
- * lies in such a buffer and is aligned to the value size is answered by the kernel straight into
- * it: no copy out of the ring slot when the entry retires. Free with glint_host_free (only once no
+ * lies in such a buffer, is aligned to the value size and is at least a page (GLINT_DIRECT_MIN_BYTES,
+ * default 4096) is answered by the kernel straight into it: no copy out of the ring slot when the
+ * entry retires. Free with glint_host_free (only once no
  * pull into the buffer is pending). */
 int glint_host_alloc(size_t bytes, void** host_ptr);
 int glint_host_free(void* host_ptr);
