@@ -971,6 +971,7 @@ uint8_t wire_response_type(int dtype) {
 
 // defined with the ring below: device-resident calls are ordered after the ring's entries
 int dev_order_after_host(glint_shard* s, hipStream_t st);
+void* host_dev_ptr(const void* p, size_t bytes, size_t align);  // glint_host_alloc buffers (below)
 int ring_flush_locked(glint_shard* s);
 int ring_retire_through(glint_shard* s, u64 t);
 
@@ -1170,9 +1171,12 @@ int glint_vec_push_dev_gated(glint_shard_t s, const int64_t* keys, const void* v
     glint_shard* s;
     ~Gate() { s->gate = nullptr; }
   } reset{s};
-  s->gate = (u64*)gate;
+  // a gate word in glint_host_alloc memory is read / written by the kernels through its device
+  // address, and the caller reads the verdict straight from host memory after its wait
+  u64* gd = (u64*)host_dev_ptr(gate, sizeof(u64), sizeof(u64));
+  s->gate = gd ? gd : (u64*)gate;
   if (n == 0 && (flags & GLINT_PUSH_VALIDATE)) {  // nothing to check: the verdict is "none rejected"
-    HIPCHK(hipMemsetAsync(gate, 0, sizeof(u64), pick(s, stream)));
+    HIPCHK(hipMemsetAsync(s->gate, 0, sizeof(u64), pick(s, stream)));
     return GLINT_OK;
   }
   GLINT_DISPATCH(s->dtype, push_vec_t, s, (const i64*)keys, nullptr, vals, n, flags, pick(s, stream));
@@ -1189,9 +1193,12 @@ int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t
     glint_shard* s;
     ~Gate() { s->gate = nullptr; }
   } reset{s};
-  s->gate = (u64*)gate;
+  // a gate word in glint_host_alloc memory is read / written by the kernels through its device
+  // address, and the caller reads the verdict straight from host memory after its wait
+  u64* gd = (u64*)host_dev_ptr(gate, sizeof(u64), sizeof(u64));
+  s->gate = gd ? gd : (u64*)gate;
   if (n == 0 && (flags & GLINT_PUSH_VALIDATE)) {  // nothing to check: the verdict is "none rejected"
-    HIPCHK(hipMemsetAsync(gate, 0, sizeof(u64), pick(s, stream)));
+    HIPCHK(hipMemsetAsync(s->gate, 0, sizeof(u64), pick(s, stream)));
     return GLINT_OK;
   }
   GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));

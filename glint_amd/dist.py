@@ -28,6 +28,7 @@ the partition it hosts, which needs no exchange.
 from __future__ import annotations
 
 import os
+import threading
 from typing import Callable, List, Optional
 
 import numpy as np
@@ -402,14 +403,29 @@ class _Distributed:
         lib = N.load()
         sup = getattr(lib, "glint_push_flags_supported", None)
         if sup is not None and sup() & N.GLINT_PUSH_VALIDATE and os.environ.get("GLINT_GATE_ROUTE", "0") != "1":
-            # the push checks its own keys before applying any (GLINT_PUSH_VALIDATE): no route pass
-            bad = torch.empty(1, dtype=torch.int64, device=keys.device)
-            sh.update(*args, gate=bad, validate=True, sync=False)
+            # the push checks its own keys before applying any (GLINT_PUSH_VALIDATE): no route pass.
+            # The verdict word lives in pinned host memory (a HostBuffer): read after the one wait,
+            # with no device-to-host copy (GLINT_GATE_HOST=0: a device word and a copy, for A/B)
+            if os.environ.get("GLINT_GATE_HOST", "1") != "0":
+                if getattr(self, "_gate_buf", None) is None:
+                    from .shard import HostBuffer
+                    self._gate_lock = threading.Lock()  # one word per model: one gated push at a time
+                    self._gate_buf = HostBuffer(64)
+                    self._gate_word = self._gate_buf.array(np.int64, 1)
+                with self._gate_lock:
+                    sh.update(*args, gate=self._gate_buf.ptr, validate=True, sync=False)
+                    sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
+                    b = int(self._gate_word[0])
+            else:
+                bad = torch.empty(1, dtype=torch.int64, device=keys.device)
+                sh.update(*args, gate=bad, validate=True, sync=False)
+                sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
+                b = int(bad.cpu()[0])
         else:
             _, _, _, _, _, bad = self.router.route(keys)
             sh.update(*args, gate=bad, sync=False)
-        sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
-        b = int(bad.cpu()[0])
+            sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
+            b = int(bad.cpu()[0])
         if b != 0:
             i = ~b
             raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.router.nkeys})")
@@ -461,6 +477,9 @@ class _Distributed:
     def destroy(self) -> bool:
         for sh in self.shards:
             sh.destroy()
+        if getattr(self, "_gate_buf", None) is not None:
+            self._gate_buf.free()
+            self._gate_buf = None
         return True
 
 

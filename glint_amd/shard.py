@@ -64,6 +64,11 @@ def _flags(deterministic: bool, unordered: bool) -> int:
     return (N.GLINT_PUSH_DETERMINISTIC if deterministic else 0) | (N.GLINT_PUSH_UNORDERED if unordered else 0)
 
 
+def _addr(x) -> int:
+    """A raw address (int) as it is, else the tensor's data pointer."""
+    return x if isinstance(x, int) else x.data_ptr()
+
+
 def _is_torch_cuda(x) -> bool:
     return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
 
@@ -288,15 +293,16 @@ class PartialVector(_Shard):
                gate=None, validate: bool = False) -> bool:
         """PartialVector.update (PartialVector.scala:35-43): data(globalToLocal(k)) += v.
         ``unordered`` is a performance hint (GLINT_PUSH_UNORDERED): skip the order check, bin by slab.
-        ``gate`` (device tensors only): a one-element int64 device tensor; the push applies nothing if
-        it is nonzero when the push runs (glint_vec_push_dev_gated). With ``validate`` the push writes
-        the gate itself (GLINT_PUSH_VALIDATE): 0, or ~(first out-of-range record), which cancels it."""
+        ``gate`` (device tensors only): a one-element int64 device tensor, or the address of a word in a
+        HostBuffer; the push applies nothing if it is nonzero when the push runs
+        (glint_vec_push_dev_gated). With ``validate`` the push writes the gate itself
+        (GLINT_PUSH_VALIDATE): 0, or ~(first out-of-range record), which cancels it."""
         flags = _flags(deterministic, unordered) | (N.GLINT_PUSH_VALIDATE if validate else 0)
         if _is_torch_cuda(keys):
             self._check_dev(keys.numel(), keys, values=values)
             if gate is not None:
                 rc = self.lib.glint_vec_push_dev_gated(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(),
-                                                       flags, gate.data_ptr(), self._stream_of(keys))
+                                                       flags, _addr(gate), self._stream_of(keys))
             else:
                 rc = self.lib.glint_vec_push_dev(self.handle, keys.data_ptr(), values.data_ptr(), keys.numel(), flags,
                                                  self._stream_of(keys))
@@ -369,7 +375,7 @@ class PartialMatrix(_Shard):
             self._check_dev(rows.numel(), rows, cols=cols, values=values)
             if gate is not None:
                 rc = self.lib.glint_mat_push_dev_gated(self.handle, rows.data_ptr(), cols.data_ptr(),
-                                                       values.data_ptr(), rows.numel(), flags, gate.data_ptr(),
+                                                       values.data_ptr(), rows.numel(), flags, _addr(gate),
                                                        self._stream_of(rows))
             else:
                 rc = self.lib.glint_mat_push_dev(self.handle, rows.data_ptr(), cols.data_ptr(), values.data_ptr(),

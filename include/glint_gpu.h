@@ -142,7 +142,9 @@ int glint_mat_pull_rows_dev(glint_shard_t shard, const int64_t* rows, void* out,
  * client reads the word after its one wait, so no host synchronisation separates the route from the
  * push. The push takes the check + apply path (GLINT_PUSH_UNORDERED is ignored); deterministic pushes
  * and unaligned arrays (keys not 16-B aligned, values not 2-element aligned) are GLINT_EINVAL. */
-/* With GLINT_PUSH_VALIDATE the push writes *gate itself (see the flag): no route in front. */
+/* With GLINT_PUSH_VALIDATE the push writes *gate itself (see the flag): no route in front. The gate
+ * word may be device memory or lie in a glint_host_alloc buffer (the caller then reads the verdict
+ * from host memory after its wait, with no copy). */
 int glint_vec_push_dev_gated(glint_shard_t shard, const int64_t* keys, const void* vals, int64_t n,
                              int flags, uint64_t* gate, void* stream);
 int glint_mat_push_dev_gated(glint_shard_t shard, const int64_t* rows, const int32_t* cols,

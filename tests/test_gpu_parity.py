@@ -276,7 +276,8 @@ def test_gated_push(gpu, pattern):
 
 
 @pytest.mark.parametrize("pattern", ["dense", "zipf", "small", "matrix", "sorted_bad", "empty"])
-def test_validating_gated_push(gpu, pattern):
+@pytest.mark.parametrize("word", ["device", "host"])
+def test_validating_gated_push(gpu, pattern, word):
     """GLINT_PUSH_VALIDATE: the gated push checks its own records and writes the verdict -- 0, or
     ~(first out-of-range record) -- to the gate word; a batch with a bad record applies NOTHING (not
     its dense head, not its tail), as mapPartitions throws before sending (AsyncBigVector.scala:96-98);
@@ -321,7 +322,16 @@ def test_validating_gated_push(gpu, pattern):
         bad = (kb, v)
         flat = k
         ref = torch.zeros(size, dtype=torch.int64, device=d)
-    word = torch.full((1,), 12345, dtype=torch.int64, device=d)  # overwritten by every push
+    from glint_amd.shard import HostBuffer
+    hb = HostBuffer(64) if word == "host" else None  # the verdict read from pinned host memory
+    if hb is not None:
+        hw = hb.array(np.int64, 1)
+        hw[0] = 12345
+    dw = torch.full((1,), 12345, dtype=torch.int64, device=d)  # overwritten by every push
+    gate = hb.ptr if hb is not None else dw
+
+    def verdict():
+        return int(hw[0]) if hb is not None else int(dw.cpu()[0])
     with sh:
         def state():
             if pattern == "matrix":
@@ -330,14 +340,16 @@ def test_validating_gated_push(gpu, pattern):
         for batch, ok in ((good, True), (bad, False), (good, True), (bad, False), (bad, False), (good, True)):
             if batch is bad and first < 0:
                 continue
-            sh.update(*batch, gate=word, validate=True)
-            w = int(word.cpu()[0])
+            sh.update(*batch, gate=gate, validate=True)
+            w = verdict()
             if ok:
                 assert w == 0
                 ref.index_add_(0, flat, batch[-1])
             else:
                 assert w != 0 and ~w == first, (w, first)
             assert torch.equal(state(), ref)
+    if hb is not None:
+        hb.free()
 
 
 def test_zipf_fixture_default_mode(gpu):
