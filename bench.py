@@ -5,18 +5,19 @@ One step = one push of a batch of (key, value) records that is already resident 
 rank's HBM shard: `glint_vec_push_dev` (include/glint_gpu.h), i.e. PartialVector.update
 (src/main/scala/glint/models/server/PartialVector.scala:35-43) on the GPU.
 
-Workload (default): BASELINE.json configs[1] -- 1 GPU, 2^28-key Double vector, dense contiguous
-push (keys[i] = start + i, values U[-1,1) from seed 42). With N GPUs (torchrun), the key space is
-RangePartitioner(N, N * 2^28) and every rank pushes its own dense range (cfg4a: clients own
+Workload (default): BASELINE.json north_star -- 1 GPU, 2^30-key Double vector, dense contiguous
+push scatter-add (keys[i] = start + i, values U[-1,1) from seed 42): the configuration its >= 70 %
+of HBM roofline target is quoted on. With N GPUs (torchrun), the key space is
+RangePartitioner(N, N * 2^30) and every rank pushes its own dense range (cfg4a: clients own
 contiguous key ranges, no exchange step) -- weak scaling, no collective in the timed region.
-The default 1-GPU run also measures the north-star size (2^30 keys, `north_star_2p30`).
+The default 1-GPU run also measures BASELINE.json configs[1] (2^28 keys, the extra key `cfg2_2p28`).
 
 Algorithmic bytes per record: 8 (key) + 8 (value) + 8 + 8 (shard read + write)
 = 32 B; value = all ranks' algorithmic bytes / max-over-ranks wall time of the K timed steps.
 The roofline figure uses the push kernels' own device time from HIP events carried on each launch
 on its stream (glint_prof_*); PMC HBM traffic comes from profiles/ when present.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--log2-keys 28]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log2-keys 30]
                     [--pattern dense|zipf|matrix|exchange|pull|rowpull] [--scaling weak|strong]
 
 --gpus N without torchrun starts N worker processes itself (one per GPU, before touching any GPU);
@@ -54,7 +55,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log2-keys", type=int, default=28, help="keys per GPU shard (cfg2: 28, north star: 30)")
+    ap.add_argument("--log2-keys", type=int, default=None,
+                    help="keys per GPU shard (default: 30 -- the north star -- for the weak-scaling dense push, "
+                         "28 for every other pattern: cfg2 / cfg3 / cfg4b's shard)")
     ap.add_argument("--pattern", choices=["dense", "zipf", "matrix", "exchange", "pull", "rowpull"], default="dense",
                     help="dense: cfg2/cfg4a push; zipf: cfg3 push; matrix: cfg5 push per GPU (2^17 x 512 Double "
                          "rows, 2^23 Zipf(1.0)-row x uniform-col triplets); exchange: cfg4b push through the "
@@ -64,7 +67,8 @@ def parse():
                     help="weak: 2^k keys per GPU (cfg4a); strong: one 2^k-key vector split over the GPUs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-north-star", action="store_true", help="skip the 2^30 leg of the default 1-GPU run")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the extra cfg2 (2^28) leg of the default 1-GPU run")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run shard check")
     ap.add_argument("--parts-per-gpu", type=int, default=1,
                     help="exchange only: range partitions hosted per GPU (modelsPerServer, Client.scala:63); "
@@ -317,6 +321,9 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             if strong:
                 workload = (f"strong scaling: one 2^{log2_keys}-key Double vector, RangePartitioner({world}, "
                             f"2^{log2_keys}); each rank pushes its own dense range")
+            elif world == 1 and log2_keys == 30:
+                workload = ("north star: dense contiguous-range push scatter-add, 2^30-key Double vector per GPU "
+                            "(BASELINE.json north_star's 1-GPU target configuration)")
             elif world == 1:
                 workload = f"cfg2: dense contiguous-range push, 2^{log2_keys}-key Double vector per GPU"
             else:
@@ -442,11 +449,11 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             a, order = torch.sort(addr)
             uq, counts = torch.unique_consecutive(a, return_counts=True)
             sums = segment_sums(v_all[order], counts) * reps
-            # the north star's 1e-6 relative, relative to each element's sum of magnitudes: the scale
-            # any summation order of a Double sum is accurate to (equal to the plain relative error
-            # where the terms do not cancel)
+            # 1e-9 of each element's sum of magnitudes: the scale any summation order of a Double sum
+            # is accurate to (~n eps sum |v|), far inside the north star's 1e-6 relative, while a lost
+            # or duplicated record cannot pass
             mags = segment_sums(v_all[order].abs(), counts) * reps
-            close = (got[uq] - sums).abs() <= 1e-6 * mags
+            close = (got[uq] - sums).abs() <= 1e-9 * mags
             ok = bool(close.all())
             if not ok:
                 bad = (~close).nonzero().reshape(-1)[:5]
@@ -461,8 +468,12 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
                 uniq, u_note = int(uq.numel()), ""
                 bytes_per_step = 16.0 * recv + 16.0 * uniq
             del a, order, uq, counts, sums, mags, addr, v_all, got
-        if not ok:
-            raise SystemExit(f"post-run shard check FAILED ({pat}, 2^{log2_keys})")
+    if check and world > 1:  # every rank's verdict: the line's check holds for all of them
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item() == 1.0)
+    if check and not ok:
+        raise SystemExit(f"post-run shard check FAILED ({pat}, 2^{log2_keys}, rank {rank})")
 
     total_bytes = bytes_per_step
     if world > 1:  # every rank's algorithmic bytes (exchange: its own recv and U)
@@ -565,19 +576,19 @@ def main():
     ctx = {"lib": N.load(), "dev": dev, "world": world, "rank": rank, "backend": backend}
     if args.parts_per_gpu > 1 and not exch:
         raise SystemExit("--parts-per-gpu applies to --pattern exchange")
-    line = run_line(ctx, args.pattern, args.log2_keys, args.scaling, args.steps, args.warmup, not args.no_check,
+    headline = args.log2_keys is None and args.pattern == "dense" and args.scaling == "weak"
+    log2_keys = args.log2_keys if args.log2_keys is not None else (30 if headline else 28)
+    line = run_line(ctx, args.pattern, log2_keys, args.scaling, args.steps, args.warmup, not args.no_check,
                     args.parts_per_gpu)
-    # the north star's own size (BASELINE.json north_star: >= 70 % of HBM roofline at 1 GPU over a
-    # 2^30-key Double vector) beside the driver's cfg2 line, with its own roofline and check
-    if (world == 1 and args.pattern == "dense" and args.scaling == "weak" and args.log2_keys == 28
-            and not args.no_north_star):
+    # BASELINE.json configs[1] (cfg2: 2^28 keys) beside the north-star line, with its own roofline and check
+    if world == 1 and headline and not args.no_north_star:
         torch.cuda.empty_cache()
-        ns = run_line(ctx, "dense", 30, "weak", 10, 2, not args.no_check)
-        line["north_star_2p30"] = {k: ns[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
-                                                      "pct_hbm_peak_per_gpu", "roofline", "check")}
-        line["north_star_2p30"]["workload"] = ns["config"]["workload"]
+        c2 = run_line(ctx, "dense", 28, "weak", args.steps, args.warmup, not args.no_check)
+        line["cfg2_2p28"] = {k: c2[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
+                                                "pct_hbm_peak_per_gpu", "roofline", "check")}
+        line["cfg2_2p28"]["workload"] = c2["config"]["workload"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.log2_keys, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(log2_keys, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1 or exch:

@@ -87,6 +87,7 @@ struct BinCtl {
   u32 nfitems; // fine-partition items (written by bin_part's workgroup 0)
   u32 fnext;   // bin_fpart's item queue: the next item to take
   u32 cold;    // valid records that were not hot (the dedup front end's input; m for the others)
+  u32 nunits;  // v2: apply units written by bin_plan (each bucket takes its range with one atomic)
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -281,17 +282,39 @@ __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const in
 constexpr int kCountAhead = GLINT_COUNT_AHEAD;  // bin_count: chunks in flight per workgroup
 // ---- bin_count ----------------------------------------------------------------------------------------
 // KIND: the partition layout (0 range, -1 read at run time), as push_check is specialised
+__device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
+// v2 (push_binned_v2): Roff[w][b] = where workgroup w's records of bucket b start inside the bucket (the
+// value its add to T[b] returned), so every bucket is one contiguous range of the partition buffer; and
+// with hot_best the push's hot elements are not counted (the hot front end sums them in LDS), so the
+// counts are exact and the buffer has no holes.
+constexpr int kWideSlots = 8192;  // the plain + hot front end's hot table (see bin_hot_select)
+__device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
 template <bool MAT, int KIND>
 __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                           i64 n, PartDesc part, const LaunchCtl* lctl, u32 ntiles,
                                                           int from_break, BinGeom g, u32* __restrict__ T,
-                                                          u32* __restrict__ R, BinCtl* bc) {
+                                                          u32* __restrict__ R, BinCtl* bc, u32* __restrict__ Roff,
+                                                          const unsigned long long* __restrict__ hot_best) {
   constexpr int kCopies = 4;  // histogram copies (wave % 4): fewer LDS atomics on one hot bucket
   __shared__ u32 h[kCopies * kMaxDigit];
+  __shared__ u32 htag[kWideSlots];
   const int tid = threadIdx.x;
   const u32 hc = (u32)((tid >> 6) % kCopies) * g.nb;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
+  if (hot_best)
+    for (int sl = tid; sl < kWideSlots; sl += kATPB) {
+      const unsigned long long x = hot_best[sl];
+      htag[sl] = x ? (u32)x : kEmptySlot;
+    }
   __syncthreads();
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
   const i64 G = gridDim.x;
@@ -324,8 +347,8 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       i64 ad;
-      bk[q] = (c0 + q * kATPB + tid < c1 && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad)) ? bucket_of((u32)ad, g)
-                                                                                             : kEmptySlot;
+      const bool ok = c0 + q * kATPB + tid < c1 && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad);
+      bk[q] = ok && !(hot_best && htag[wide_slot((u32)ad)] == (u32)ad) ? bucket_of((u32)ad, g) : kEmptySlot;
     }
     load(c + kCountAhead * G, r);  // kCountAhead chunks ahead, into the registers just consumed
 #pragma unroll
@@ -352,7 +375,8 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
 #pragma unroll
     for (int cpy = 0; cpy < kCopies; ++cpy) x += h[cpy * g.nb + b];
     R[blockIdx.x * g.nb + b] = x;
-    if (x) atomicAdd(&T[b], x);
+    const u32 o = x ? atomicAdd(&T[b], x) : 0u;
+    if (Roff) Roff[blockIdx.x * g.nb + b] = o;
   }
   const u32 tot = block_sum<kATPB>(nvalid);
   if (tid == 0 && tot) atomicAdd(&bc->tail, tot);
@@ -374,14 +398,6 @@ constexpr int kHotRuns = kHotSample / kHotRun;
 constexpr int kHotCount = 16384;    // sampler's LDS count table (load <= ~0.5: short probe chains)
 constexpr int kHotTPB = 1024;
 
-__device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
-  x ^= x >> 16;
-  x *= 0x85EBCA6Bu;
-  x ^= x >> 13;
-  x *= 0xC2B2AE35u;
-  x ^= x >> 16;
-  return x;
-}
 __device__ __forceinline__ u32 hot_slot(u32 a) { return hot_mix(a) & (kHotSlots - 1); }
 
 
@@ -520,8 +536,20 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
 
 // Workgroup w's bucket ranges: cur[b] = chunk_base(w) * kAChunk + exclusive scan of R[w][*], also
 // published bucket-major as segoff[b][w] for the fine partition.
+// v2 (Roff set): bucket b is the contiguous range [Bb[b], Bb[b] + T[b]) with Bb the exclusive scan of T
+// (written once, by workgroup 0); this workgroup's records of b start at Bb[b] + Roff[w][b].
 __device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks, const u32* __restrict__ R,
-                                           u32* __restrict__ segoff, u32* cur, u32* dcnt) {
+                                           u32* __restrict__ segoff, u32* cur, u32* dcnt, const u32* __restrict__ T,
+                                           const u32* __restrict__ Roff, u32* __restrict__ Bb) {
+  if (Roff) {
+    block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; },
+                         [&](u32 b, u32 excl) {
+                           cur[b] = excl + Roff[w * g.nb + b];
+                           dcnt[b] = 0;
+                           if (w == 0) Bb[b] = excl;
+                         });
+    return;
+  }
   const u32 base = chunk_base(w, gridDim.x, nchunks) * (u32)kAChunk;
   block_scan<kATPB, 1>(g.nb, [&](u32 b) { return R[w * g.nb + b]; },
                        [&](u32 b, u32 excl) {
@@ -535,24 +563,37 @@ __device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks,
 // of them ({b, j}: its records [j * kFItem, (j + 1) * kFItem) in segment order).
 // fine-partition items of a bucket of t records: ceil(t / kFItem), at least one (the bucket's first
 // item writes its apply items)
-__device__ __forceinline__ u32 bucket_items(u32 t) { return max(1u, (t + kFItem - 1) / kFItem); }
-// Also the per-bucket bases bin_fpart needs, once per push instead of once per fine item: T[nb + b] =
-// the bucket's first output record (records of buckets < b), T[2 nb + b] = its first apply item slot.
+__device__ __forceinline__ u32 bucket_items(u32 t, u32 item = kFItem) { return max(1u, (t + item - 1) / item); }
+// (v2: items of `item` records; Ib[b] = the bucket's first item)
 __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
-                                           BinCtl* bc) {
+                                           BinCtl* bc, u32 item, u32* __restrict__ Ib) {
   const u32 tot = block_scan<kATPB, 1>(
-      g.nb, [&](u32 b) { return bucket_items(T[b]); },
+      g.nb, [&](u32 b) { return bucket_items(T[b], item); },
       [&](u32 b, u32 excl) {
-        const u32 J = bucket_items(T[b]);
+        const u32 J = bucket_items(T[b], item);
         for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
+        if (Ib) Ib[b] = excl;
       });
   if (threadIdx.x == 0) bc->nfitems = tot;
 }
 
 __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
                                             u32* __restrict__ seglen, u32 emitted, BinCtl* bc) {
-  for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[b * gridDim.x + w] = cur[b] - segoff[b * gridDim.x + w];
+  if (segoff)
+    for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[b * gridDim.x + w] = cur[b] - segoff[b * gridDim.x + w];
   if (threadIdx.x == 0 && emitted) atomicAdd(&bc->m, emitted);
+}
+
+// v2, dedup front end: the chunk tables merged records, so this workgroup's bucket ranges end short of
+// what bin_count counted; the rest of each range is marked empty for bin_fsort.
+__device__ __forceinline__ void part_fill_holes(const BinGeom& g, u32 w, const u32* __restrict__ T,
+                                                const u32* __restrict__ R, const u32* __restrict__ Roff, const u32* cur,
+                                                u32* dcnt, u32* __restrict__ addr_out) {
+  __syncthreads();
+  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; },
+                       [&](u32 b, u32 excl) { dcnt[b] = excl + Roff[w * g.nb + b] + R[w * g.nb + b]; });
+  for (u32 b = 0; b < g.nb; ++b)
+    for (u32 p = cur[b] + threadIdx.x; p < dcnt[b]; p += kATPB) addr_out[p] = kEmptySlot;
 }
 
 // The plain + hot front end keeps a wider hot table (kWideSlots tags + sums fit the plain partition
@@ -561,11 +602,9 @@ __device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* 
 // slot by bin_hot_select; the partition workgroups' per-slot sums are stored (not added with atomics:
 // kWideSlots x G of them would cost more than the split saves) and bin_hot_reduce adds each hot
 // element's sum over the workgroups to the shard in workgroup order.
-constexpr int kWideSlots = 8192;
 constexpr int kWideHashBits = 20;           // global count table: 2^20 slots
 constexpr int kWideRunsPerWg = 8;           // sampled runs of kHotRun records per sampling workgroup
 constexpr int kWideSampleWgs = 256;         // 256 x 8 x 128 = 262 144 sampled records per push
-__device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
 
 // Each workgroup reads kWideRunsPerWg runs of kHotRun consecutive records (spread evenly over the
 // tail), counts them in LDS, then adds its (element, count) pairs to the global hash table.
@@ -698,7 +737,9 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
                                                          BinCtl* bc, const u32* __restrict__ T,
                                                          uint2* __restrict__ fitems,
                                                          const unsigned long long* __restrict__ hot_best,
-                                                         typename LdsAcc<V>::T* __restrict__ hot_partial) {
+                                                         typename LdsAcc<V>::T* __restrict__ hot_partial, u32 fitem,
+                                                         const u32* __restrict__ Roff, u32* __restrict__ Bb,
+                                                         u32* __restrict__ Ib) {
   typedef typename LdsAcc<V>::T A;
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
   __shared__ u32 st_a[kAChunk];
@@ -718,12 +759,13 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
     }
   }
   PhaseClock ph(0);
-  if (w == 0) part_items(g, T, fitems, bc);
-  part_setup(g, w, nchunks, R, segoff, cur, dcnt);
+  if (w == 0) part_items(g, T, fitems, bc, fitem, Ib);
+  part_setup(g, w, nchunks, R, segoff, cur, dcnt, T, Roff, Bb);
   ph.mark(0);
   const i64 G = gridDim.x;
-  const u32 wbase = chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
-  const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
+  // output window: v1 this workgroup's own range; v2 the whole buffer (bucket ranges; n * sizeof(A) < 2^32)
+  const u32 wbase = Roff ? 0u : chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
+  const u32 wlen = Roff ? (u32)(n - r0) : chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
   const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
   BadRecs bad;
   u32 emitted = 0;
@@ -814,7 +856,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, const u32* __restrict__ R,
     u32* __restrict__ segoff, u32* __restrict__ seglen, u32* __restrict__ addr_out,
     typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc, const u32* __restrict__ T,
-    uint2* __restrict__ fitems, const u32* __restrict__ hot_tags, V* __restrict__ data) {
+    uint2* __restrict__ fitems, const u32* __restrict__ hot_tags, V* __restrict__ data, u32 fitem,
+    const u32* __restrict__ Roff, u32* __restrict__ Bb, u32* __restrict__ Ib) {
   typedef typename LdsAcc<V>::T A;
   static_assert(kAChunk * (4 + sizeof(A)) <= kASlots * sizeof(A), "staging must fit the value table");
   __shared__ u32 hk[kASlots];
@@ -841,13 +884,13 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   }
   if (tid == 0) nused = 0;
   PhaseClock ph(8);
-  if (w == 0) part_items(g, T, fitems, bc);
-  part_setup(g, w, nchunks, R, segoff, cur, dcnt);
+  if (w == 0) part_items(g, T, fitems, bc, fitem, Ib);
+  part_setup(g, w, nchunks, R, segoff, cur, dcnt, T, Roff, Bb);
   ph.mark(8);
   const u64 below = (1ull << lane) - 1ull;
   const i64 G = gridDim.x;
-  const u32 wbase = chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
-  const u32 wlen = chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
+  const u32 wbase = Roff ? 0u : chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
+  const u32 wlen = Roff ? (u32)(n - r0) : chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
   const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
   BadRecs bad;
   u32 emitted = 0, ncold = 0;
@@ -969,6 +1012,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     }
   }
   part_finish(g, w, segoff, cur, seglen, emitted, bc);
+  if (Roff) part_fill_holes(g, w, T, R, Roff, cur, dcnt, addr_out);
   bad.report(err);
   {  // records that entered the hash table (valid, not hot): the host's measure of what chunk dedup merges
     const u32 tot = block_sum<kATPB>(ncold);
@@ -1439,6 +1483,516 @@ __global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict_
   ph.flush(6);
 }
 
+// ==== v2 fine stage: one sort pass per fine item, a plan per bucket, an apply that gathers runs =========
+// After the coarse partition (bucket b = the contiguous range [Bb[b], Bb[b] + T[b]) of the partition
+// buffer, no holes but the dedup front end's marked ones), bucket b is cut into fine items of kSItem
+// records in bucket order. bin_fsort loads one item with every load in flight, ranks its records by fine
+// digit (slab of the bucket) in LDS and writes them back IN PLACE of the item's range (other buffers),
+// sorted by slab, with the item's slab offsets off2[item][0..nf] -- no count pass, no global cursor,
+// contiguous reads and whole-wave stores. A slab's records are then one run per item of its bucket
+// (~32 records for uniform keys into 2^28). bin_plan (one workgroup per bucket) reads the bucket's off2
+// rows and cuts every slab's runs into apply units of <= kUnitCap records at item boundaries (a slab with
+// one unit is exclusive: plain read-modify-write; a hot slab's units flush with device atomics).
+// bin_apply2 sums a unit's runs in LDS and writes the slab back as bin_apply does.
+#ifndef GLINT_FSORT_TPB
+#define GLINT_FSORT_TPB 1024
+#endif
+#ifndef GLINT_FSORT_PER
+#define GLINT_FSORT_PER 16
+#endif
+constexpr int kSTPB = GLINT_FSORT_TPB;
+constexpr int kSPer = GLINT_FSORT_PER;
+constexpr u32 kSItem = (u32)kSTPB * kSPer;  // records per fine item (v2)
+static_assert(kSItem <= 32768, "u16 slab offsets and the u16 staging of one item");
+constexpr u32 kUnitExcl = 1u;  // apply unit descriptor {slab, runs, records, flags}: the slab's only unit
+constexpr u32 kSparseCap2 = 1024;  // bin_apply2's touched list (4 workgroups per CU fit in LDS)
+
+template <typename A>
+__global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, const BinCtl* bc,
+                                                          const u32* __restrict__ T, const u32* __restrict__ Bb,
+                                                          const u32* __restrict__ addr_in, const A* __restrict__ val_in,
+                                                          uint16_t* __restrict__ e_out, A* __restrict__ v_out,
+                                                          uint16_t* __restrict__ off2, u64* hint) {
+  constexpr u32 kStage = 65536;                      // bytes: the item's u16 offsets, then its values in rounds
+  constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
+  __shared__ u32 hist[kMaxDigit];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[kStage];
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0 && hint) {  // for the host's next binned push: how much did dedup keep?
+    __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hint + 1, (u64)bc->cold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const u32 it = blockIdx.x;
+  if (it >= bc->nfitems) return;  // the grid is the item count's upper bound
+  const uint2 d = fitems[it];
+  const u32 b = d.x;
+  const u32 s0 = Bb[b] + d.y * kSItem, s1 = Bb[b] + min(T[b], (d.y + 1) * kSItem);
+  const u32 nf1 = g.nf + 1;
+  uint16_t* const orow = off2 + (size_t)it * nf1;
+  for (u32 f = tid; f < g.nf; f += kSTPB) hist[f] = 0;
+  if (s1 == s0) {  // an empty bucket's one item
+    for (u32 f = tid; f < nf1; f += kSTPB) orow[f] = 0;
+    return;
+  }
+  u32 a[kSPer];
+  A v[kSPer];
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
+    const u32 i = s0 + q * kSTPB + tid;
+    const u32 ii = i < s1 ? i : s1 - 1;
+    a[q] = ld_in(addr_in + ii);
+    v[q] = ld_in(val_in + ii);
+    if (i >= s1) a[q] = kEmptySlot;
+  }
+  __syncthreads();
+  u32 p[kSPer];
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) p[q] = atomicAdd(&hist[fine_of(a[q], g)], 1u);
+  __syncthreads();
+  const u32 total = block_scan<kSTPB, 1>(
+      g.nf, [&](u32 f) { return hist[f]; },
+      [&](u32 f, u32 excl) {
+        hist[f] = excl;
+        orow[f] = (uint16_t)excl;
+      });
+  if (tid == 0) orow[g.nf] = (uint16_t)total;
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) p[q] += hist[fine_of(a[q], g)];
+  // the slab offsets (and the slab's low 4 bits: bin_apply2's groups of sparse slabs), staged as u16
+  // and stored as whole-wave runs
+  uint16_t* const ste = reinterpret_cast<uint16_t*>(stage);
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) ste[p[q]] = (uint16_t)((a[q] & (kSlab - 1)) | ((fine_of(a[q], g) & 15u) << kSlabBits));
+  __syncthreads();
+  for (u32 x = tid; x < total; x += kSTPB) e_out[s0 + x] = ste[x];
+  __syncthreads();
+  A* const stv = reinterpret_cast<A*>(stage);
+  for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
+#pragma unroll
+    for (int q = 0; q < kSPer; ++q)
+      if (a[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
+    __syncthreads();
+    const u32 r1 = min(total, r0 + kStageV);
+    for (u32 x = r0 + tid; x < r1; x += kSTPB) v_out[s0 + x] = stv[x - r0];
+    __syncthreads();
+  }
+}
+
+// One workgroup per bucket: every slab's runs (one per item of the bucket, from the bucket's off2 rows,
+// staged in LDS) cut into apply units of <= kUnitCap records and <= kRunMax runs (a run longer than
+// what is left of a unit is split). A unit is a descriptor {slab, runs, records, flags} and a
+// fixed-stride run table {start, records before it}, so bin_apply2 reads both in one round trip. A slab
+// with one unit is exclusive (plain read-modify-write); the units of a hot slab flush with device
+// atomics. Sparse neighbours are merged: an aligned group of 2..16 slabs whose records total at most
+// min(kGroupCap, 512 per slab) is ONE unit (one run per item covers all of them: fsort sorted the item
+// by slab), summed in an LDS hash table -- a sparse slab alone would hold a whole 32 KB accumulator for
+// a few hundred records and one element round trip. Each bucket takes its range of the dense unit list
+// with one atomic.
+constexpr int kPlanTPB = 1024;
+constexpr u32 kPlanLds = 65536;  // bytes of the bucket's off2 rows staged at once
+constexpr int kRunMax = 128;     // runs per apply unit at most
+#ifndef GLINT_UNIT_CAP
+#define GLINT_UNIT_CAP 4096
+#endif
+constexpr u32 kUnitCap = GLINT_UNIT_CAP;  // records per apply unit at most
+static_assert(kUnitCap <= 65535, "a unit's record prefix is staged as u16");
+#ifndef GLINT_GROUP_SLAB_AVG
+#define GLINT_GROUP_SLAB_AVG 512
+#endif
+constexpr u32 kGroupCap = 2048;      // records per grouped unit (= its LDS hash slots: never full)
+constexpr u32 kGroupSlabAvg = GLINT_GROUP_SLAB_AVG;  // ... and per slab of the group on average, at most
+constexpr u32 kGroupMax = 16;        // slabs per group (the record's u16 carries its slab's low 4 bits)
+static_assert(kSlabBits + 4 <= 16, "a slab offset and 4 slab bits in one u16");
+constexpr u32 kUnitGroup = 2u;       // unit flag: a group of sparse slabs (hash-table path)
+static_assert(kGroupCap <= kUnitCap && kGroupMax <= 64, "a group is one unit, inside one wave's lanes");
+__global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32* __restrict__ T, const u32* __restrict__ Bb,
+                                                            const u32* __restrict__ Ib, const uint16_t* __restrict__ off2,
+                                                            BinCtl* bc, uint4* __restrict__ units, uint2* __restrict__ runs,
+                                                            int group_on) {
+  __shared__ uint16_t rows[kPlanLds / 2];
+  __shared__ u32 nunit[kMaxDigit];
+  __shared__ u32 ubase;
+  static_assert(kMaxDigit == kPlanTPB, "one slab per thread");
+  const int tid = threadIdx.x;
+  const u32 b = blockIdx.x;
+  const u32 J = bucket_items(T[b], kSItem), I = Ib[b], nf1 = g.nf + 1, bb = Bb[b];
+  const u32 jt = kPlanLds / 2 / nf1;  // items per staged tile (>= 31 for nf <= 1024)
+  const u32 f = tid;                  // this thread's slab
+  auto stage = [&](u32 j0, u32 j1) {  // rows of items [j0, j1): every load of a round in flight together
+    const u32 nx = (j1 - j0) * nf1;
+    const uint16_t* src = off2 + (size_t)(I + j0) * nf1;
+    constexpr int U = 8;
+    for (u32 x0 = 0; x0 < nx; x0 += kPlanTPB * U) {
+      uint16_t t[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const u32 x = x0 + q * kPlanTPB + tid;
+        t[q] = src[x < nx ? x : nx - 1];
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const u32 x = x0 + q * kPlanTPB + tid;
+        if (x < nx) rows[x] = t[q];
+      }
+    }
+  };
+  // The units of slabs [f, f + span) (span 0: this slab belongs to a group another thread emits).
+  // emit = false counts them (and *tot = the records); emit = true writes them from unit `base` on.
+  auto walk = [&](bool emit, u32 base, u32 flags, u32 span, u32* tot) -> u32 {
+    u32 acc = 0, nr = 0, nu = 0, t = 0;
+    for (u32 j0 = 0; j0 < J; j0 += jt) {
+      const u32 j1 = min(J, j0 + jt);
+      if (!emit || J > jt) {  // block-uniform: the rows are staged once when they fit
+        __syncthreads();
+        stage(j0, j1);
+        __syncthreads();
+      }
+      if (f >= g.nf || span == 0) continue;
+      for (u32 j = j0; j < j1; ++j) {
+        const uint16_t* r = rows + (j - j0) * nf1 + f;
+        const u32 o0 = r[0];
+        u32 c = (u32)r[span] - o0;
+        u32 st = bb + j * kSItem + o0;
+        t += c;
+        while (c) {
+          const u32 take = min(c, kUnitCap - acc);
+          if (emit) runs[(size_t)(base + nu) * kRunMax + nr] = make_uint2(st, acc);
+          acc += take;
+          st += take;
+          c -= take;
+          ++nr;
+          if (acc == kUnitCap || nr == (u32)kRunMax) {
+            if (emit) units[base + nu] = make_uint4(b * g.nf + f, nr, acc, flags);
+            ++nu;
+            acc = 0;
+            nr = 0;
+          }
+        }
+      }
+    }
+    if (f < g.nf && span && acc) {
+      if (emit) units[base + nu] = make_uint4(b * g.nf + f, nr, acc, flags);
+      ++nu;
+    }
+    if (tot) *tot = t;
+    return nu;
+  };
+  u32 h = 0;
+  const u32 nu1 = walk(false, 0, 0, 1, &h);
+  // sparse neighbours: the largest aligned group (lanes f..f+gs-1 of one wave) within the caps
+  u32 span = 1;
+  if (group_on && J <= (u32)kRunMax) {
+    u32 s = f < g.nf ? h : 0u;
+    for (u32 gs = 2; gs <= kGroupMax && gs <= g.nf; gs <<= 1) {
+      s += __shfl_xor(s, (int)(gs >> 1));  // the sum over the aligned group of gs slabs
+      if (s > 0 && s <= min(kGroupCap, gs * kGroupSlabAvg)) span = gs;
+    }
+    if (span > 1 && (f & (span - 1))) span = 0;  // a member: its group's first slab emits it
+  }
+  // (a group's units: at most one, exclusive; a single slab's: the cut above)
+  const u32 nu = span > 1 ? 1u : span == 1 ? nu1 : 0u;  // a group (records > 0, <= kGroupCap): one unit
+  if (f < g.nf) nunit[f] = nu;
+  __syncthreads();
+  const u32 used = block_scan<kPlanTPB, 1>(g.nf, [&](u32 x) { return nunit[x]; },
+                                           [&](u32 x, u32 excl) { nunit[x] = excl; });
+  if (tid == 0) ubase = used ? atomicAdd(&bc->nunits, used) : 0u;
+  __syncthreads();
+  const u32 flags = span > 1 ? (kUnitExcl | kUnitGroup) : (nu == 1 ? kUnitExcl : 0u);
+  walk(true, ubase + (f < g.nf ? nunit[f] : 0u), flags, span, nullptr);
+}
+
+// Per apply unit: the records of its runs (record r lives in run i = the last one whose prefix is <= r:
+// a binary search over the unit's run table in LDS), kCRB2 per thread per batch. A slab unit sums them
+// in LDS and is written back as in bin_apply (exclusive: one coalesced RMW of the touched lines, or the
+// touched list of a sparse unit; shared: device atomics). A group unit (several sparse slabs) sums them
+// in an LDS hash table keyed by element (overlaying the slab accumulator) and read-modify-writes each
+// distinct element. Element write-backs issue all their loads before any store (a loop of dependent
+// load / store pairs would wait one round trip per element). Software-pipelined per workgroup: the
+// descriptor and run table of the unit two ahead load during this one, and the next unit's run table
+// and first record batch are issued before this unit's write-back.
+#ifndef GLINT_APPLY2_WAVES
+#define GLINT_APPLY2_WAVES 4  // bin_apply2's register budget: waves per SIMD (4 workgroups per CU fit in LDS)
+#endif
+#ifndef GLINT_APPLY2_WARM
+#define GLINT_APPLY2_WARM 2  // slab warm-up: 0 off, 1 one unit ahead, 2 at the unit's own start
+#endif
+#ifndef GLINT_CRB2
+#define GLINT_CRB2 8
+#endif
+constexpr int kCRB2 = GLINT_CRB2;  // records per thread per batch
+template <typename V>
+__global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APPLY2_WAVES))) void bin_apply2_kernel(
+    const uint16_t* __restrict__ e_in, const typename LdsAcc<V>::T* __restrict__ v_in, const uint4* __restrict__ units,
+    const uint2* __restrict__ runs, const BinCtl* bc, i64 elems, V* __restrict__ data, u32 pre_min, u32 sparse_max,
+    u32 list_max, bool line_wb, int xcd_map) {
+  typedef typename Vec2<V>::T V2;
+  typedef typename LdsAcc<V>::T A;
+  static_assert(kRunMax <= kCTPB, "one run per loading thread");
+  static_assert(kGroupCap * (4 + sizeof(A)) <= kSlab * sizeof(A), "the group table overlays the slab accumulator");
+  static_assert(kGroupCap * 2 <= kSlab, "the group's slot list overlays the touched flags");
+  __shared__ A acc[kSlab];
+  __shared__ uint8_t touched[kSlab];
+  __shared__ uint16_t tlist[kSparseCap2];
+  __shared__ u32 ntl[2];
+  __shared__ u32 rs[2][kRunMax];
+  __shared__ uint16_t rp[2][kRunMax + 1];
+  u32* const hk = reinterpret_cast<u32*>(acc);  // group units: element + 1 (0 = empty slot)
+  A* const hv = reinterpret_cast<A*>(reinterpret_cast<char*>(acc) + kGroupCap * 4);
+  uint16_t* const hused = reinterpret_cast<uint16_t*>(touched);  // the group's claimed slots, in order
+  constexpr int kPairsPerThread = kSlab / 2 / kCTPB;
+  constexpr int kListPer = (kGroupCap + kCTPB - 1) / kCTPB;  // element write-backs per thread at most
+  static_assert(kSparseCap2 <= kGroupCap, "the touched list fits the element write-back");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const u64 below = (1ull << lane) - 1ull;
+  for (int e = tid; e < kSlab; e += kCTPB) acc[e] = A(0);
+  for (int w = tid; w < kSlab / 16; w += kCTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
+  if (tid < 2) ntl[tid] = 0;
+  const u32 nunits = bc->nunits;
+  const u32 G = gridDim.x;
+  // this workgroup's i-th unit: blockIdx + i G, or (xcd_map) a contiguous eighth of the units per group
+  // of workgroups that dispatch to one XCD (blockIdx % 8), so the workgroups of an XCD take neighbouring
+  // slabs together and share in its L2 the lines where one item's runs for them meet
+  const u32 xk = blockIdx.x >> 3, xK = G >> 3, xC = (nunits + 7) >> 3, xbase = (blockIdx.x & 7u) * xC;
+  auto unit_of = [&](u32 i) -> u32 {
+    if (!xcd_map) return blockIdx.x + i * G;
+    const u32 k = xk + i * xK;
+    return k < xC ? xbase + k : 0xFFFFFFFFu;
+  };
+  const uint4 kNone = make_uint4(0u, 0u, 0u, 0u);
+  auto load_unit = [&](u32 uu, uint4& d, uint2& r) {
+    d = uu < nunits ? units[uu] : kNone;
+    r = make_uint2(0u, 0u);
+    if (uu < nunits && tid < kRunMax) r = runs[(size_t)uu * kRunMax + tid];
+  };
+  auto publish = [&](int slot, const uint4& d, const uint2& r) {  // the unit's run table into LDS
+    if ((u32)tid < d.y) {
+      rs[slot][tid] = r.x;
+      rp[slot][tid] = (uint16_t)r.y;
+    }
+    if (tid == 0) rp[slot][d.y] = (uint16_t)d.z;  // (d.y == 0 only for a missing unit: count 0)
+  };
+  auto fetch = [&](int slot, const uint4& d, u32 r0, u32 (&ca)[kCRB2], A (&cv)[kCRB2]) {
+    const u32 cnt = d.z, nr = d.y;
+#pragma unroll
+    for (int q = 0; q < kCRB2; ++q) {  // clamped, branch-free loads
+      const u32 r = r0 + q * kCTPB + tid;
+      ca[q] = kEmptySlot;
+      cv[q] = A(0);
+      if (cnt) {
+        const u32 rr = r < cnt ? r : cnt - 1;
+        u32 lo = 0, hi = nr - 1;  // the last run starting at or before rr
+        while (lo < hi) {
+          const u32 mid = (lo + hi + 1) >> 1;
+          if ((u32)rp[slot][mid] <= rr) lo = mid;
+          else hi = mid - 1;
+        }
+        const u32 idx = rs[slot][lo] + (rr - (u32)rp[slot][lo]);
+        ca[q] = ld_in(e_in + idx);
+        cv[q] = ld_in(v_in + idx);
+        if (r >= cnt) ca[q] = kEmptySlot;
+      }
+    }
+  };
+  auto warm_slab = [&](const uint4& d) -> u32 {  // most of the slab's lines will be touched: into L2 now
+    u32 w = 0;
+    if ((d.w & (kUnitExcl | kUnitGroup)) == kUnitExcl && d.z >= pre_min) {
+      constexpr int kLines = kSlab * (int)sizeof(V) / 128;
+      constexpr int kPerLine = 128 / (int)sizeof(V);
+      const i64 sb = (i64)d.x << kSlabBits;
+      for (int l = tid; l < kLines; l += kCTPB)
+        if (sb + (i64)l * kPerLine < elems) w ^= *reinterpret_cast<const u32*>(data + sb + (i64)l * kPerLine);
+    }
+    return w;
+  };
+  // a wave's claimed list entries: one LDS atomic per wave for all its lanes' new entries
+  auto list_append = [&](bool first, u32 val, u32 par_, uint16_t* list) {
+    const u64 bl = __ballot(first);
+    if (bl) {
+      u32 base = 0;
+      if (lane == 0) base = atomicAdd(&ntl[par_], (u32)__popcll(bl));
+      base = __shfl(base, 0);
+      if (first) list[base + (u32)__popcll(bl & below)] = (uint16_t)val;
+    }
+  };
+  // prologue: unit u published, its first batch in flight; unit u + G loaded
+  uint4 dcur, dnext;
+  uint2 rcur, rnext;
+  u32 i = 0, u = unit_of(0);
+  load_unit(u, dcur, rcur);
+  load_unit(unit_of(1), dnext, rnext);
+  publish(0, dcur, rcur);
+  __syncthreads();
+  u32 pa[kCRB2];
+  A pv[kCRB2];
+  fetch(0, dcur, 0u, pa, pv);
+  u32 warm = GLINT_APPLY2_WARM == 1 ? warm_slab(dcur) : 0u;
+  int cs = 0;  // LDS table slot of unit u
+  u32 par = 0;
+  for (; u < nunits; u = unit_of(++i)) {
+    const uint4 d = dcur;
+    const u32 slab = d.x, cnt = d.z;
+    const bool group = (d.w & kUnitGroup) != 0;
+    const bool exclusive = (d.w & kUnitExcl) != 0;
+    const i64 sbase_g = (i64)slab << kSlabBits;
+    V* const sbase = data + sbase_g;
+    const bool sparse = !group && exclusive && cnt <= sparse_max;
+    if (GLINT_APPLY2_WARM == 2) warm = warm_slab(d);
+    u32 ca[kCRB2];
+    A cv[kCRB2];
+#pragma unroll
+    for (int q = 0; q < kCRB2; ++q) {
+      ca[q] = pa[q];
+      cv[q] = pv[q];
+    }
+    for (u32 r0 = 0;;) {  // the first batch came with the prefetch
+      if (group) {
+#pragma unroll
+        for (int q = 0; q < kCRB2; ++q) {
+          bool first = false;
+          u32 h = 0;
+          if (ca[q] != kEmptySlot) {
+            const u32 ad = (((slab & ~(kGroupMax - 1)) | (ca[q] >> kSlabBits)) << kSlabBits) | (ca[q] & (kSlab - 1));
+            const u32 key = ad + 1u;
+            h = (ad * 0x9E3779B1u) >> (32 - 11);
+            static_assert(kGroupCap == 2048, "11-bit slot hash");
+            for (;;) {  // <= kGroupCap distinct keys in kGroupCap slots: an insert always finds one
+              const u32 prev = atomicCAS(&hk[h], 0u, key);
+              if (prev == 0u) { first = true; break; }
+              if (prev == key) break;
+              h = (h + 1) & (kGroupCap - 1);
+            }
+            lds_add(&hv[h], cv[q]);
+          }
+          list_append(first, h, par, hused);
+        }
+      } else if (sparse) {
+#pragma unroll
+        for (int q = 0; q < kCRB2; ++q) {
+          bool first = false;
+          u32 e = 0;
+          if (ca[q] != kEmptySlot) {
+            e = ca[q] & (kSlab - 1);
+            lds_add(&acc[e], cv[q]);
+            const u32 sh = 8u * (e & 3u);
+            first = ((atomicOr(reinterpret_cast<u32*>(touched) + (e >> 2), 1u << sh) >> sh) & 0xFFu) == 0u;
+          }
+          list_append(first, e, par, tlist);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kCRB2; ++q) {
+          if (ca[q] == kEmptySlot) continue;
+          const u32 e = ca[q] & (kSlab - 1);
+          lds_add(&acc[e], cv[q]);
+          touched[e] = 1;
+        }
+      }
+      r0 += (u32)kCTPB * kCRB2;
+      if (r0 >= cnt) break;
+      fetch(cs, d, r0, ca, cv);
+    }
+    asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
+    // the next unit's run table into the other slot; the one after it starts loading
+    publish(cs ^ 1, dnext, rnext);
+    dcur = dnext;
+    load_unit(unit_of(i + 2), dnext, rnext);
+    __syncthreads();
+    if (tid == 0) ntl[par ^ 1u] = 0;  // the next list unit's count (the last one read it before a barrier)
+    // the next unit's first batch (and warm-up): in flight during this unit's write-back
+    fetch(cs ^ 1, dcur, 0u, pa, pv);
+    if (GLINT_APPLY2_WARM == 1) warm = warm_slab(dcur);
+    bool sweep_wb = exclusive && !sparse && !group;
+    if (group || sparse) {
+      const u32 L = ntl[par];  // block-uniform (read after the barrier)
+      par ^= 1u;
+      if (sparse && L > list_max) {
+        sweep_wb = true;  // many distinct elements: whole-line write-back
+      } else {
+        // element read-modify-writes: every load issued before any store
+        u32 ad[kListPer];
+        V old[kListPer];
+#pragma unroll
+        for (int k = 0; k < kListPer; ++k) {
+          const u32 x = tid + k * kCTPB;
+          ad[k] = 0xFFFFFFFFu;
+          if (x < L) {
+            const u32 s2 = group ? hused[x] : tlist[x];
+            ad[k] = group ? hk[s2] - 1u : (u32)(sbase_g + s2);
+            if ((i64)ad[k] < elems) old[k] = data[ad[k]];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kListPer; ++k) {
+          if (ad[k] == 0xFFFFFFFFu) continue;
+          const u32 x = tid + k * kCTPB;
+          const u32 s2 = group ? hused[x] : tlist[x];
+          if (group) {
+            if ((i64)ad[k] < elems) data[ad[k]] = acc_add(old[k], hv[s2]);
+            hk[s2] = 0u;
+            hv[s2] = A(0);
+            hused[x] = 0;
+          } else {
+            if ((i64)ad[k] < elems) data[ad[k]] = acc_add(old[k], acc[s2]);
+            acc[s2] = A(0);
+            touched[s2] = 0;
+          }
+        }
+      }
+    }
+    if (sweep_wb) {  // as bin_apply: whole touched lines, read and written back
+      constexpr int kPPL = 128 / (2 * (int)sizeof(V));
+      const u64 gmask = (kPPL >= 64 ? ~0ull : ((1ull << kPPL) - 1ull)) << (lane & ~(kPPL - 1));
+      V2 dd[kPairsPerThread];
+      u32 t[kPairsPerThread];
+      bool wb[kPairsPerThread];
+#pragma unroll
+      for (int q = 0; q < kPairsPerThread; ++q) {
+        const int e0 = 2 * (tid + q * kCTPB);
+        t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
+        wb[q] = line_wb ? (__ballot(t[q] != 0u) & gmask) != 0ull : t[q] != 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < kPairsPerThread; ++q) {
+        const int e0 = 2 * (tid + q * kCTPB);
+        const bool vec = wb[q] && sbase_g + e0 + 1 < elems;
+        dd[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
+        if (t[q]) *reinterpret_cast<uint16_t*>(touched + e0) = 0;
+      }
+#pragma unroll
+      for (int q = 0; q < kPairsPerThread; ++q) {
+        if (!wb[q]) continue;
+        const int e0 = 2 * (tid + q * kCTPB);
+        if (sbase_g + e0 + 1 < elems) {
+          V2 r = dd[q];
+          if (t[q] & 1u) r.x = acc_add((V)r.x, acc[e0]);
+          if (t[q] & 2u) r.y = acc_add((V)r.y, acc[e0 + 1]);
+          *reinterpret_cast<V2*>(sbase + e0) = r;
+        } else if (t[q]) {
+          sbase[e0] = acc_add(sbase[e0], acc[e0]);
+        }
+        if (t[q]) {
+          acc[e0] = A(0);
+          acc[e0 + 1] = A(0);
+        }
+      }
+    } else if (!exclusive) {
+      for (int e = tid; e < kSlab; e += kCTPB) {
+        if (touched[e]) {
+          gadd(sbase + e, (V)acc[e]);
+          acc[e] = A(0);
+          touched[e] = 0;
+        }
+      }
+    }
+    __syncthreads();
+    cs ^= 1;
+  }
+  asm volatile("" ::"v"(warm));
+}
+
 // ---- host side ----------------------------------------------------------------------------------------
 // records per slab item from which bin_apply warms the whole slab into L2 (GLINT_BIN_PREFETCH_MIN;
 // 0xFFFFFFFF disables)
@@ -1507,6 +2061,130 @@ BinGeom bin_geometry(i64 elems) {
   return g;
 }
 
+// The v2 binned push (front: 0 plain, 1 plain + hot split, 2 chunk dedup; see push_binned).
+template <typename V, bool MAT>
+int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, int front, bool hot_on) {
+  typedef typename LdsAcc<V>::T A;
+  const i64 n = a.n;
+  const BinGeom g = bin_geometry(s->elems);
+  const bool dedup = front == 2;
+  const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
+  static EnvKnob wpc_knob("GLINT_PART_WPC");
+  const int plain_wpc = (int)wpc_knob.pos_or(kPartWgPerCuPlain);
+  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : plain_wpc)));
+  if (G > (u32)kMaxSegs) return GLINT_EINVAL;
+  const i64 max_fitems = (i64)g.nb + n / kSItem + 1;
+  // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
+  // floor(H / cap) + floor(runs / kRunMax) + 1 per non-empty slab
+  const i64 max_units = (i64)g.nslab + n / kUnitCap + std::min<i64>(n, max_fitems * g.nf) / kRunMax + 1;
+  // [BinCtl | T] zeroed per push; then R, Roff, Bb, Ib, the fine items, off2, the apply units, the hot
+  // tables and the record buffers (coarse: u32 address + A value; fine: u16 slab offset + A value)
+  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
+  const size_t b_nb = pad256((size_t)g.nb * 4);
+  const size_t b_fit = pad256((size_t)max_fitems * 8), b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 2);
+  const size_t b_units = pad256((size_t)max_units * 16) + pad256((size_t)max_units * kRunMax * 8);
+  const size_t b_hot = pad256((size_t)kHotSlots * 4);
+  const size_t b_wk = front == 1 ? pad256(((size_t)4 << kWideHashBits)) : 0;
+  const size_t b_wbest = front == 1 ? pad256((size_t)kWideSlots * 8) : 0;
+  const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
+  const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(A)), b_e = pad256((size_t)n * 2);
+  const size_t b_zero = b_ctl + b_T;
+  const size_t need = b_zero + 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + 2 * b_wk + b_wbest + b_wpart +
+                      b_a + 2 * b_v + b_e;
+  int rc = grow(&s->d_bin, &s->bin_bytes, need);
+  if (rc) return rc;
+  char* p = (char*)s->d_bin;
+  BinCtl* bc = (BinCtl*)p;
+  u32* T = (u32*)(p + b_ctl);
+  p += b_zero;
+  u32* R = (u32*)p;
+  u32* Roff = (u32*)(p + b_seg);
+  p += 2 * b_seg;
+  u32* Bb = (u32*)p;
+  u32* Ib = (u32*)(p + b_nb);
+  p += 2 * b_nb;
+  uint2* fitems = (uint2*)p;
+  p += b_fit;
+  uint16_t* off2 = (uint16_t*)p;
+  p += b_off2;
+  uint4* units = (uint4*)p;
+  uint2* runs = (uint2*)(p + pad256((size_t)max_units * 16));
+  p += b_units;
+  u32* hot_tags = (u32*)p;
+  p += b_hot;
+  u32* wkey = (u32*)p;
+  u32* wcnt = (u32*)(p + b_wk);
+  unsigned long long* wbest = (unsigned long long*)(p + 2 * b_wk);
+  A* wpart = (A*)(p + 2 * b_wk + b_wbest);
+  p += 2 * b_wk + b_wbest + b_wpart;
+  u32* addr_a = (u32*)p;
+  A* val_a = (A*)(p + b_a);
+  A* val_b = (A*)(p + b_a + b_v);
+  uint16_t* e_b = (uint16_t*)(p + b_a + 2 * b_v);
+
+  ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
+  HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
+  const int fb = from_break ? 1 : 0;
+  if (front == 1) {  // the wide hot table: sample, count, pick
+    static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");
+    const u32 wide_min = (u32)wide_knob.pos_or(3);
+    HIPCHK(hipMemsetAsync(wkey, 0xFF, b_wk, st));
+    HIPCHK(hipMemsetAsync(wcnt, 0, b_wk + b_wbest, st));
+    bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
+                                                                wcnt);
+    HIPCHK(hipGetLastError());
+    bin_hot_select_kernel<<<(1u << kWideHashBits) / 256u, 256, 0, st>>>(wkey, wcnt, wide_min, wbest);
+    HIPCHK(hipGetLastError());
+  }
+  if (dedup && hot_on) {
+    static EnvKnob hmin_knob("GLINT_BIN_HOT_MIN");
+    const u32 hot_min = (u32)hmin_knob.pos_or(2);
+    bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, hot_min, hot_tags);
+    HIPCHK(hipGetLastError());
+  }
+  const unsigned long long* count_hot = front == 1 ? wbest : nullptr;  // the hot records are not partitioned
+  if (a.part.kind == 0)
+    bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
+                                                  count_hot);
+  else
+    bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
+                                                   count_hot);
+  HIPCHK(hipGetLastError());
+  if (dedup) {
+    auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
+                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data, kSItem, Roff, Bb, Ib);
+  } else {
+    auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
+                                 : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
+                              val_a, a.err, bc, T, fitems, wbest, wpart, kSItem, Roff, Bb, Ib);
+  }
+  HIPCHK(hipGetLastError());
+  if (front == 1) {
+    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
+    HIPCHK(hipGetLastError());
+  }
+  bin_fsort_kernel<A><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b, off2,
+                                                              s->d_hint ? s->d_hint + 1 : nullptr);
+  HIPCHK(hipGetLastError());
+  static EnvKnob group_knob("GLINT_BIN_GROUP");  // 0: no groups of sparse slabs (A/B)
+  const int group_on = (int)group_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; });
+  bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on);
+  HIPCHK(hipGetLastError());
+  // a persistent grid of the resident workgroups: each pipelines its units two deep
+  static const int apply2_occ = resident_per_cu(bin_apply2_kernel<V>, kCTPB);
+  static EnvKnob apply2_knob("GLINT_BIN_APPLY2_BPC");
+  static EnvKnob xcd_knob("GLINT_BIN_XCD");  // XCD-grouped unit order (see bin_apply2_kernel); 2 = off
+  const int apply2_bpc = (int)apply2_knob.pos_or(apply2_occ);
+  const unsigned apply2_grid = (unsigned)std::min<i64>(max_units, (i64)s->cus * apply2_bpc);
+  bin_apply2_kernel<V><<<apply2_grid, kCTPB, 0, st>>>(
+      e_b, val_b, units, runs, bc, s->elems, a.data, bin_prefetch_min(), std::min<u32>(bin_sparse_max(), kSparseCap2),
+      bin_list_max(), bin_line_wb(), apply2_grid % 8 == 0 && xcd_knob.pos_or(1) == 1 ? 1 : 0);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
 template <typename V, bool MAT>
 int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
   typedef typename LdsAcc<V>::T A;
@@ -1545,6 +2223,11 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   else if (forced == 1) front = hot_on ? 1 : 0;
   const bool dedup = front == 2;
   s->bin_last_front = front;
+  // the v2 fine stage (bin_fsort / bin_plan / bin_apply2) unless GLINT_BIN_V1=1; its coarse partition
+  // addresses the whole buffer through one 32-bit buffer window
+  static EnvKnob v1_knob("GLINT_BIN_V1");
+  const bool v1 = v1_knob.get([](const char* e) -> long long { return e && atoi(e) != 0; }) != 0;
+  if (!v1 && (u64)n * sizeof(A) < ((u64)1 << 32)) return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on);
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
@@ -1619,19 +2302,22 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     HIPCHK(hipGetLastError());
   }
   if (a.part.kind == 0)
-    bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
+    bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, nullptr,
+                                                  nullptr);
   else
-    bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc);
+    bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, nullptr,
+                                                   nullptr);
   HIPCHK(hipGetLastError());
   if (dedup) {
     auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
-                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data);
+                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data, kFItem, nullptr,
+                              nullptr, nullptr);
   } else {
     auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
                                  : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
-                              val_a, a.err, bc, T, fitems, wbest, wpart);
+                              val_a, a.err, bc, T, fitems, wbest, wpart, kFItem, nullptr, nullptr, nullptr);
   }
   HIPCHK(hipGetLastError());
   if (front == 1) {

@@ -83,6 +83,16 @@ __device__ __forceinline__ bool rec_addr(const PartDesc& p, i64 key, int32_t col
 }
 
 
+// The 64-bit key itself lies in the partition's key range (no Int wrap): what RangePartitioner.partition
+// checks (key < 0 || key >= size, RangePartitioner.scala:30) before the shard's (key - start).toInt
+// (RangePartition.scala:33) could alias a key 2^32 away onto element key - start - 2^32. A validating
+// push (GLINT_PUSH_VALIDATE) stands in for that check, so it tests the raw key too.
+template <int KIND = -1>
+__device__ __forceinline__ bool key_in_part(const PartDesc& p, i64 key) {
+  if (KIND == 0 || (KIND < 0 && p.kind == 0)) return key >= p.start && key - p.start < (i64)p.size;
+  return key >= (i64)p.cidx && (key - (i64)p.cidx) / (i64)p.cparts < (i64)p.size;
+}
+
 __device__ __forceinline__ void lds_add(double* p, double v) { unsafeAtomicAdd(p, v); }
 __device__ __forceinline__ void lds_add(float* p, float v) { unsafeAtomicAdd(p, v); }
 __device__ __forceinline__ void lds_add(long long* p, long long v) { atomicAdd((u64*)p, (u64)v); }

@@ -101,8 +101,11 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
     last = __shfl(a1, 63);
     const A off = (A)(r - r_first);
     affine = affine && (!h0 || (o0 && a0 == a_first + off)) && (!h1 || (o1 && a1 == a_first + off + 1));
-    if (validate && ((h0 && !o0) || (h1 && !o1)))  // rare: one atomic per lane with a rejected record
-      atomicMax(&ctl->bad, ~(u64)((h0 && !o0) ? r : r + 1));
+    if (validate) {  // the raw keys too (no Int wrap); rare: one atomic per lane with a rejected record
+      const bool b0 = h0 && (!o0 || !key_in_part<KIND>(part, k[j].x));
+      const bool b1 = h1 && (!o1 || !key_in_part<KIND>(part, k[j].y));
+      if (b0 || b1) atomicMax(&ctl->bad, ~(u64)(b0 ? r : r + 1));
+    }
   }
   const bool any_bad = __any(!mono);  // wave-wide votes, outside any lane-divergent branch
   const bool all_affine = __all(affine);
@@ -971,7 +974,7 @@ uint8_t wire_response_type(int dtype) {
 
 // defined with the ring below: device-resident calls are ordered after the ring's entries
 int dev_order_after_host(glint_shard* s, hipStream_t st);
-void* host_dev_ptr(const void* p, size_t bytes, size_t align);  // glint_host_alloc buffers (below)
+void* host_dev_ptr(const void* p, size_t bytes, size_t align, HostHold* hold = nullptr);  // glint_host_alloc buffers (below)
 int ring_flush_locked(glint_shard* s);
 int ring_retire_through(glint_shard* s, u64 t);
 
@@ -1386,7 +1389,7 @@ std::atomic<int> g_waiters{0};
 constexpr int kBusyWaiters = 8;
 long long wait_sleep_us() {
   static EnvKnob k("GLINT_WAIT_SLEEP_US");
-  return k.get([](const char* e) -> long long { return e ? atoll(e) : 50ll; });
+  return k.get([](const char* e) -> long long { return e ? std::max(0ll, atoll(e)) : 50ll; });
 }
 bool poll_word(const u64* word, u64 ticket, double budget_us) {
   constexpr double kSpinUs = 4.0;
@@ -1403,7 +1406,7 @@ bool poll_word(const u64* word, u64 ticket, double budget_us) {
       if (us > budget_us) return false;
       if (us > kSpinUs) {
         if (sleep_us > 0 && g_waiters.load(std::memory_order_relaxed) > kBusyWaiters) {
-          const struct timespec ts = {0, (long)(sleep_us * 1000)};
+          const struct timespec ts = {(time_t)(sleep_us / 1000000), (long)(sleep_us % 1000000) * 1000};  // tv_nsec < 1e9
           nanosleep(&ts, nullptr);
         } else {
           sched_yield();
@@ -1450,6 +1453,7 @@ int ring_retire(glint_shard* s, glint_shard::RingSlot& r) {
   if (r.pull_batch) {
     for (const auto& m : r.msgs)
       if (!m.dout) std::memcpy(m.out, r.h + r.out_off + (size_t)m.off * s->vsize, (size_t)m.n * s->vsize);
+    for (auto& m : r.msgs) m.hold.reset();  // the kernel's writes into caller buffers are complete
     r.pull_batch = false;
   }
   if (tc) s->hp.copy.fetch_add(host_ns() - tc, std::memory_order_relaxed);
@@ -1563,13 +1567,14 @@ struct HostRange {
   char* h;
   size_t n;
   char* d;
+  std::shared_ptr<std::atomic<long>> pending;  // kernel writes enqueued into it and not yet retired
 };
 std::mutex g_host_mu;
 std::vector<HostRange> g_host;  // sorted by h
 
 // p's device address if [p, p + bytes) lies in one glint_host_alloc buffer and p is aligned to
-// `align`, else nullptr
-void* host_dev_ptr(const void* p, size_t bytes, size_t align) {
+// `align`, else nullptr; with `hold`, the buffer is held (glint_host_free refuses it) until *hold resets
+void* host_dev_ptr(const void* p, size_t bytes, size_t align, HostHold* hold) {
   if (!p || (uintptr_t)p % align) return nullptr;
   std::lock_guard<std::mutex> lk(g_host_mu);
   if (g_host.empty()) return nullptr;
@@ -1579,6 +1584,7 @@ void* host_dev_ptr(const void* p, size_t bytes, size_t align) {
   if (it == g_host.begin()) return nullptr;
   --it;
   if (c + bytes > it->h + it->n) return nullptr;
+  if (hold) *hold = HostHold(it->pending);
   return it->d + (c - it->h);
 }
 
@@ -1834,7 +1840,10 @@ int launch_pull_batch(glint_shard* s, glint_shard::RingSlot& r, int kind) {
     s->pull_tab = reinterpret_cast<const PullDst*>(r.hd + toff);
     s->pull_nm = (int)r.msgs.size();
   } else {
-    for (auto& m : r.msgs) m.dout = nullptr;  // answered through the slot, copied out at retire
+    for (auto& m : r.msgs) {  // answered through the slot, copied out at retire
+      m.dout = nullptr;
+      m.hold.reset();
+    }
   }
   const int rc = ring_dispatch(s, r, true, r.msgs.front().ticket, r.msgs.back().ticket, [&]() -> int {
     if (kind == 0) {
@@ -1875,7 +1884,8 @@ int ring_append_pull_locked(glint_shard* s, int kind, i64 n, const int64_t* keys
   // answered in place only from a page of answer on: each message's destination costs the kernel's
   // stores a host-page translation, so small answers are cheaper copied out of the contiguous slot
   // (cfg4b's ~125-record pulls ran at half the rate in place; cfg4a's 1000-record ones 1.4x faster)
-  m.dout = (size_t)n * s->vsize >= direct_min_bytes() ? host_dev_ptr(out, (size_t)n * s->vsize, s->vsize) : nullptr;
+  m.dout = (size_t)n * s->vsize >= direct_min_bytes() ? host_dev_ptr(out, (size_t)n * s->vsize, s->vsize, &m.hold)
+                                                       : nullptr;
   r.msgs.push_back(m);
   r.fill += n;
   if (ticket) *ticket = t;
@@ -2284,7 +2294,7 @@ int glint_host_alloc(size_t bytes, void** p) {
   }
   {
     std::lock_guard<std::mutex> lk(g_host_mu);
-    const HostRange r{h, bytes, d};
+    const HostRange r{h, bytes, d, std::make_shared<std::atomic<long>>(0)};
     g_host.insert(std::upper_bound(g_host.begin(), g_host.end(), r,
                                    [](const HostRange& a, const HostRange& b) { return a.h < b.h; }),
                   r);
@@ -2299,6 +2309,8 @@ int glint_host_free(void* p) {
     std::lock_guard<std::mutex> lk(g_host_mu);
     auto it = std::find_if(g_host.begin(), g_host.end(), [p](const HostRange& r) { return r.h == (char*)p; });
     if (it == g_host.end()) return GLINT_EINVAL;
+    // a pull enqueued to answer into it has not retired: its kernel would write into freed memory
+    if (it->pending->load(std::memory_order_acquire) != 0) return GLINT_EINVAL;
     g_host.erase(it);
   }
   return hipHostFree(p) == hipSuccess ? GLINT_OK : GLINT_EDEVICE;

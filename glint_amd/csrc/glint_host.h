@@ -10,11 +10,47 @@
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <utility>
 #include <vector>
 
 using namespace glint;
+
+// One pending kernel write into a glint_host_alloc buffer (a pull answering in place): the buffer's
+// pending count is held from enqueue until the entry retires, and glint_host_free refuses the buffer
+// while it is non-zero.
+struct HostHold {
+  std::shared_ptr<std::atomic<long>> c;
+  HostHold() = default;
+  explicit HostHold(std::shared_ptr<std::atomic<long>> p) : c(std::move(p)) {
+    if (c) c->fetch_add(1, std::memory_order_acq_rel);
+  }
+  HostHold(const HostHold& o) : c(o.c) {
+    if (c) c->fetch_add(1, std::memory_order_acq_rel);
+  }
+  HostHold(HostHold&& o) noexcept : c(std::move(o.c)) {}
+  HostHold& operator=(const HostHold& o) {
+    if (this != &o) {
+      reset();
+      c = o.c;
+      if (c) c->fetch_add(1, std::memory_order_acq_rel);
+    }
+    return *this;
+  }
+  HostHold& operator=(HostHold&& o) noexcept {
+    if (this != &o) {
+      reset();
+      c = std::move(o.c);
+    }
+    return *this;
+  }
+  ~HostHold() { reset(); }
+  void reset() {
+    if (c) c->fetch_sub(1, std::memory_order_acq_rel);
+    c.reset();
+  }
+};
 
 struct glint_shard {
   int device = 0;
@@ -86,6 +122,7 @@ struct glint_shard {
       void* out = nullptr;  // a coalesced pull's destination (its answer sits at off in the slot)
       void* dout = nullptr; // out's device address when out is glint_host_alloc memory: the kernel
                             // writes the answer there itself (no copy out of the slot)
+      HostHold hold;        // dout's buffer stays allocated until the entry retires
     };
     std::vector<Msg> msgs;      // the messages of this entry, for error attribution
     int64_t fill = 0;           // records appended to an open batch

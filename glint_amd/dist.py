@@ -37,7 +37,7 @@ import torch.distributed as dist
 
 from . import _native as N
 from .client import bucket
-from .errors import IndexOutOfBoundsException, ModelCreationException
+from .errors import ArrayIndexOutOfBoundsException, IndexOutOfBoundsException, ModelCreationException
 from .partitioning import CyclicPartitioner, RangePartitioner
 from .shard import PartialMatrix, PartialVector, check, resolve_dtype
 
@@ -428,7 +428,13 @@ class _Distributed:
             b = int(bad.cpu()[0])
         if b != 0:
             i = ~b
-            raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.router.nkeys})")
+            k = int(keys[i])
+            if len(args) == 3 and 0 <= k < self.router.nkeys:
+                # the row is in range, so the column failed: what the general path's shard reports
+                # (PartialMatrix.update indexes data(row)(col), PartialMatrix.scala:77-79)
+                raise ArrayIndexOutOfBoundsException(
+                    f"record {i}: column {int(args[1][i])} outside [0, {self.cols})", i)
+            raise IndexOutOfBoundsException(f"key {k} (record {i}) outside [0, {self.router.nkeys})")
         return True
 
     def _answer(self, ex: _Exchange, order, bufs: tuple, caller: torch.Tensor, tail: tuple, get):

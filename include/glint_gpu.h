@@ -311,8 +311,8 @@ int glint_reload_env(void);
  * sends). A message-sized pull (glint_pull_async, glint_pull_wire_async) whose answer destination
  * lies in such a buffer, is aligned to the value size and is at least a page (GLINT_DIRECT_MIN_BYTES,
  * default 4096) is answered by the kernel straight into it: no copy out of the ring slot when the
- * entry retires. Free with glint_host_free (only once no
- * pull into the buffer is pending). */
+ * entry retires. Free with glint_host_free: it returns GLINT_EINVAL (and frees nothing) while a pull
+ * enqueued to answer into the buffer has not retired (glint_shard_wait for its ticket first). */
 int glint_host_alloc(size_t bytes, void** host_ptr);
 int glint_host_free(void* host_ptr);
 

@@ -244,6 +244,12 @@ class GpuPartialMatrixDouble(partition: Partition, cols: Int) extends PartialMat
   def getRowsFlat(rows: Array[Long]): Array[Double] = {
     val out = new Array[Double](rows.length * cols); GpuShard.matPullRowsD(shard, rows, out); out
   }
+  // PartialMatrix.getRows (PartialMatrix.scala:37-46) reads data(row), which lives in HBM here: the
+  // rows come back flat in one pull and are cut into cols-long arrays (MatrixBenchmark.scala:73,99)
+  override def getRows(rows: Array[Long]): Array[Array[Double]] = {
+    val flat = getRowsFlat(rows)
+    Array.tabulate(rows.length)(i => java.util.Arrays.copyOfRange(flat, i * cols, (i + 1) * cols))
+  }
   override def receive: Receive = {
     case pull: PullMatrix =>
       val to = sender(); val out = new Array[Double](pull.rows.length)
@@ -271,6 +277,12 @@ class GpuPartialMatrixFloat(partition: Partition, cols: Int) extends PartialMatr
   }
   def getRowsFlat(rows: Array[Long]): Array[Float] = {
     val out = new Array[Float](rows.length * cols); GpuShard.matPullRowsF(shard, rows, out); out
+  }
+  // PartialMatrix.getRows (PartialMatrix.scala:37-46) reads data(row), which lives in HBM here: the
+  // rows come back flat in one pull and are cut into cols-long arrays (MatrixBenchmark.scala:73,99)
+  override def getRows(rows: Array[Long]): Array[Array[Float]] = {
+    val flat = getRowsFlat(rows)
+    Array.tabulate(rows.length)(i => java.util.Arrays.copyOfRange(flat, i * cols, (i + 1) * cols))
   }
   override def receive: Receive = {
     case pull: PullMatrix =>
@@ -300,6 +312,12 @@ class GpuPartialMatrixLong(partition: Partition, cols: Int) extends PartialMatri
   def getRowsFlat(rows: Array[Long]): Array[Long] = {
     val out = new Array[Long](rows.length * cols); GpuShard.matPullRowsL(shard, rows, out); out
   }
+  // PartialMatrix.getRows (PartialMatrix.scala:37-46) reads data(row), which lives in HBM here: the
+  // rows come back flat in one pull and are cut into cols-long arrays (MatrixBenchmark.scala:73,99)
+  override def getRows(rows: Array[Long]): Array[Array[Long]] = {
+    val flat = getRowsFlat(rows)
+    Array.tabulate(rows.length)(i => java.util.Arrays.copyOfRange(flat, i * cols, (i + 1) * cols))
+  }
   override def receive: Receive = {
     case pull: PullMatrix =>
       val to = sender(); val out = new Array[Long](pull.rows.length)
@@ -327,6 +345,12 @@ class GpuPartialMatrixInt(partition: Partition, cols: Int) extends PartialMatrix
   }
   def getRowsFlat(rows: Array[Long]): Array[Int] = {
     val out = new Array[Int](rows.length * cols); GpuShard.matPullRowsI(shard, rows, out); out
+  }
+  // PartialMatrix.getRows (PartialMatrix.scala:37-46) reads data(row), which lives in HBM here: the
+  // rows come back flat in one pull and are cut into cols-long arrays (MatrixBenchmark.scala:73,99)
+  override def getRows(rows: Array[Long]): Array[Array[Int]] = {
+    val flat = getRowsFlat(rows)
+    Array.tabulate(rows.length)(i => java.util.Arrays.copyOfRange(flat, i * cols, (i + 1) * cols))
   }
   override def receive: Receive = {
     case pull: PullMatrix =>

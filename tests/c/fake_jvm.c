@@ -5,7 +5,9 @@
  * receive, PartialVectorDouble.scala:17-23) and applies nothing, while earlier pushes' awaits and a
  * pull stay clean; an out-of-partition pull throws the same way; pipelined pulls (pullAsync, then
  * pullFinish after the burst) see the pushes enqueued before them; zero (the Akka restart) -> push again;
- * argument errors (value type, short arrays); a matrix shard's element and row pulls; destroy.
+ * argument errors (value type, short arrays); a matrix shard's element and row pulls; destroy; and
+ * MatrixBenchmark's update -> get -> getRows sequence on a range and a cyclic Double matrix, getRows
+ * restated from the Scala override (a flat row pull cut into cols-long rows).
  * Exit status 0 and "ok" on stdout when every check passes. */
 #include <math.h>
 #include <stdio.h>
@@ -75,6 +77,10 @@ void NAT(matPullRowsI)(JNIEnv*, jclass, jlong, jlongArray, jintArray);
 jlong NAT(pullAsync)(JNIEnv*, jclass, jlong, jint, jlongArray, jintArray);
 void NAT(pullFinishD)(JNIEnv*, jclass, jlong, jdoubleArray);
 void NAT(pullFinishI)(JNIEnv*, jclass, jlong, jintArray);
+jlong NAT(createCyclic)(JNIEnv*, jclass, jint, jint, jint, jint, jlong, jint);
+jlong NAT(matPushD)(JNIEnv*, jclass, jlong, jlongArray, jintArray, jdoubleArray, jint);
+void NAT(matPullD)(JNIEnv*, jclass, jlong, jlongArray, jintArray, jdoubleArray);
+void NAT(matPullRowsD)(JNIEnv*, jclass, jlong, jlongArray, jdoubleArray);
 
 static int failures = 0;
 #define CHECK(cond, what)                                            \
@@ -85,6 +91,55 @@ static int took(const char* cls) {
   const int hit = strncmp(pending, cls, strlen(cls)) == 0;
   pending[0] = 0;
   return hit;
+}
+
+/* GpuPartialMatrixDouble.getRows (integration/scala/GpuShard.scala): getRowsFlat -- one flat row pull
+ * (matPullRowsD) -- cut into cols-long rows, each its own array, as PartialMatrix.getRows returns
+ * Array[Array[Double]] (PartialMatrix.scala:37-46) */
+static Arr** get_rows(jlong h, Arr* rows, int cols) {
+  Arr* flat = arr(rows->len * cols, 8);
+  NAT(matPullRowsD)(env, NULL, h, rows, flat);
+  Arr** out = (Arr**)calloc((size_t)rows->len, sizeof(Arr*));
+  for (jsize i = 0; i < rows->len; ++i) {
+    out[i] = arr(cols, 8);
+    memcpy(out[i]->data, flat->data + (size_t)i * cols * 8, (size_t)cols * 8);
+  }
+  return out;
+}
+
+/* MatrixBenchmark.scala:24-47,54-101 on one shard: update, then get, then getRows, for its range
+ * (RangePartition(1, 10000, 20000)) and cyclic (CyclicPartition(3, 10, 100000)) PartialMatrixDouble of
+ * 300 cols, `size` records row x + 10000 (range) / 10 x + 3 (cyclic), col x % 300, value 0.25 x + 1 */
+static void matrix_benchmark(int dev, int cyclic, int size) {
+  const int cols = 300;
+  const jlong h = cyclic ? NAT(createCyclic)(env, NULL, dev, 3, 3, 10, (jlong)(10000 - 1) * 10 + 3 + 1, cols)
+                         : NAT(createRange)(env, NULL, dev, 3, 10000, 20000, cols);
+  CHECK(h != 0 && !pending[0], "MatrixBenchmark shard");
+  Arr* r = arr(size, 8);
+  Arr* c = arr(size, 4);
+  Arr* v = arr(size, 8);
+  for (int x = 0; x < size; ++x) {
+    ((jlong*)r->data)[x] = cyclic ? 10L * x + 3 : (jlong)x + 10000;
+    ((jint*)c->data)[x] = x % cols;
+    ((jdouble*)v->data)[x] = 0.25 * x + 1.0;
+  }
+  NAT(await)(env, NULL, h, NAT(matPushD)(env, NULL, h, r, c, v, 0));  /* update */
+  CHECK(!pending[0], "MatrixBenchmark update");
+  Arr* o = arr(size, 8);
+  NAT(matPullD)(env, NULL, h, r, c, o);  /* get */
+  CHECK(!pending[0] && !memcmp(o->data, v->data, (size_t)size * 8), "MatrixBenchmark get");
+  Arr** rows = get_rows(h, r, cols);  /* getRows: row x holds 0.25 x + 1 at col x % 300, zeros elsewhere */
+  int ok = !pending[0];
+  for (int x = 0; x < size && ok; ++x)
+    for (int j = 0; j < cols; ++j)
+      ok &= ((jdouble*)rows[x]->data)[j] == (j == x % cols ? 0.25 * x + 1.0 : 0.0);
+  CHECK(ok, cyclic ? "MatrixBenchmark getRows (cyclic)" : "MatrixBenchmark getRows (range)");
+  /* a row outside the partition: getRows throws as data(row) would (ArrayIndexOutOfBoundsException) */
+  Arr* bad = arr(1, 8);
+  ((jlong*)bad->data)[0] = cyclic ? 100003 : 20000;
+  free(get_rows(h, bad, cols));
+  CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "getRows of a row outside the partition");
+  NAT(destroy)(env, NULL, h);
 }
 
 int main(int argc, char** argv) {
@@ -208,6 +263,10 @@ int main(int argc, char** argv) {
   NAT(matPushI)(env, NULL, m, r, cs, mv, 0);
   CHECK(took("java/lang/ArrayIndexOutOfBoundsException"), "short cols");
   NAT(destroy)(env, NULL, m);
+  for (int size = 4000; size <= 10000; size += 2000) {  /* Gen.range("size")(4000, 10000, 2000) */
+    matrix_benchmark(dev, 0, size);
+    matrix_benchmark(dev, 1, size);
+  }
   if (failures) return 1;
   printf("ok\n");
   return 0;

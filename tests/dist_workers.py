@@ -17,7 +17,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from glint_amd.errors import IndexOutOfBoundsException  # noqa: E402
+from glint_amd.errors import ArrayIndexOutOfBoundsException, IndexOutOfBoundsException  # noqa: E402
 from glint_amd.partitioning import CyclicPartitioner, RangePartition, RangePartitioner  # noqa: E402
 from glint_amd.shard import resolve_dtype  # noqa: E402
 from oracle import oracle as O  # noqa: E402
@@ -36,7 +36,9 @@ class OracleShard:
         self.o = O.OracleVector(part, self.code) if kind == "vector" else O.OracleMatrix(part, cols, self.code)
 
     def update(self, *args, deterministic=False):
-        assert self.o.update(*[a.cpu().numpy() for a in args]) == -1
+        bad = self.o.update(*[a.cpu().numpy() for a in args])
+        if bad != -1:  # as the HBM shard reports it (glint_amd/shard.py)
+            raise ArrayIndexOutOfBoundsException(f"record {bad} is outside the partition", bad)
 
     def get(self, *args):
         out, bad = self.o.get(*[a.cpu().numpy() for a in args])
@@ -117,6 +119,16 @@ def _vector_case(nkeys, mps, partitioner, dtype, n=3000):
             pass
         got2 = vec.pull(torch.from_numpy(q).to(dev)).cpu().numpy()
         np.testing.assert_array_equal(got2, want)
+        # keys 2^32 away from an in-range key: (key - start).toInt would alias them onto elements, but
+        # RangePartitioner.partition rejects them (RangePartitioner.scala:30), on every path
+        for wrap in ([nkeys + 2**32], [-(2**32) + 1], [1, nkeys - 1 + 2**32]):
+            kw = np.array(wrap, dtype=np.int64)
+            try:
+                vec.push(torch.from_numpy(kw).to(dev), torch.from_numpy(np.ones(kw.size, np_dtype)).to(dev))
+                raise AssertionError(f"wrapped key {wrap} accepted")
+            except IndexOutOfBoundsException:
+                pass
+        np.testing.assert_array_equal(vec.pull(torch.from_numpy(q).to(dev)).cpu().numpy(), want)
         # only rank 0's batch is bad: it raises after the collectives, the other ranks' pushes land
         k1 = np.array([3], np.int64) if rank else np.array([1, nkeys + 5], np.int64)
         try:
@@ -166,6 +178,26 @@ def _matrix_case(nrows, ncols, mps, dtype="double", n=2500):
         np.testing.assert_array_equal(got, ref.get(qr, qc)[0])
         rows_got = mat.pull(torch.from_numpy(qr[:50]).to(dev)).cpu().numpy()
         np.testing.assert_array_equal(rows_got, ref.get_rows(qr[:50])[0])
+        # rows 2^32 away from an in-range row are rejected as keys; at world 1 (one rank hosts every
+        # shard) a bad column is the shard's ArrayIndexOutOfBoundsException on every path
+        one = torch.ones(2, dtype=mat.dtype, device=dev)
+        for wrap in ([nrows + 2**32, 0], [-(2**32) + 1, 0]):
+            try:
+                mat.push(torch.tensor(wrap, dtype=torch.int64, device=dev),
+                         torch.zeros(2, dtype=torch.int32, device=dev), one)
+                raise AssertionError(f"wrapped row {wrap} accepted")
+            except IndexOutOfBoundsException:
+                pass
+        if world == 1:
+            for badc in (ncols, -1):
+                try:
+                    mat.push(torch.tensor([1], dtype=torch.int64, device=dev),
+                             torch.tensor([badc], dtype=torch.int32, device=dev), one[:1])
+                    raise AssertionError("bad column accepted")
+                except ArrayIndexOutOfBoundsException as e:
+                    assert e.record == 0, e.record
+        np.testing.assert_array_equal(mat.pull(torch.from_numpy(qr).to(dev), torch.from_numpy(qc).to(dev)).cpu().numpy(),
+                                      ref.get(qr, qc)[0])
         mat.destroy()
     return body
 
@@ -181,13 +213,13 @@ CASES = {
 
 
 def _check_close(got, ref, mag, what):
-    """Default-mode Double sums of repeated keys are summed in no particular order. The bound is the
-    north star's 1e-6 relative, taken relative to each element's sum of magnitudes (sum |v|) -- the
-    scale every ordering of a floating-point sum is accurate to; it equals the plain relative error
-    wherever the terms do not cancel, and demands exact zeros where nothing was pushed."""
+    """Default-mode Double sums of repeated keys are summed in no particular order. The bound is 1e-9
+    of each element's sum of magnitudes (sum |v|) -- the scale every ordering of a floating-point sum
+    is accurate to (n terms: ~n eps sum |v|) and far inside the north star's 1e-6 relative, while a
+    lost or duplicated record cannot pass; it demands exact zeros where nothing was pushed."""
     err = (got - ref).abs()
-    bad = err > 1e-6 * mag
-    assert not bool(bad.any()), f"{what}: {int(bad.sum())} elements off by more than 1e-6 of sum |v|"
+    bad = err > 1e-9 * mag
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} elements off by more than 1e-9 of sum |v|"
 
 
 def run_cfg4(rank, world, port, backend, nbatch, log2_batch, dtype="long"):

@@ -117,15 +117,16 @@ def _bench(args, **env):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("pattern", ["dense", "exchange"])
-def test_bench_self_launches_ranks(gpu, pattern):
+@pytest.mark.parametrize("args", [["--pattern", "dense"], ["--pattern", "dense", "--scaling", "strong"],
+                                  ["--pattern", "exchange"]])
+def test_bench_self_launches_ranks(gpu, args):
     """`python bench.py --gpus 2` with no launcher: two rank processes (here both on this GPU over
-    gloo -- the rehearsal hooks), one JSON line with n_gpus 2."""
-    d = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--log2-keys", "22", "--pattern", pattern,
-                "--no-cpu-baseline"], GLINT_BENCH_DEVICE=str(gpu), GLINT_BENCH_BACKEND="gloo")
-    assert d["n_gpus"] == 2 and d["value"] > 0
-    if pattern == "dense":
-        assert d["check"] is True
+    gloo -- the rehearsal hooks), one JSON line with n_gpus 2 whose check is every rank's (the ranks
+    agree on it with an all-reduce before rank 0 prints): what an 8-GPU SCALE run executes, at N = 2."""
+    d = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--log2-keys", "22", "--no-cpu-baseline"] + args,
+               GLINT_BENCH_DEVICE=str(gpu), GLINT_BENCH_BACKEND="gloo")
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["check"] is True
+    assert d["scaling"] == ("strong" if "strong" in args else "weak")
 
 
 @pytest.mark.parametrize("args", [["--pattern", "pull"], ["--pattern", "rowpull"],
@@ -133,6 +134,14 @@ def test_bench_self_launches_ranks(gpu, pattern):
 def test_bench_patterns(gpu, args):
     d = _bench(args + ["--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
     assert d["check"] is True and d["value"] > 0 and d["roofline"]["achieved"] > 0
+
+
+def test_bench_default_line_is_the_north_star(gpu):
+    """With no --log2-keys the driver's line is BASELINE.json north_star's configuration (a 2^30-key
+    Double vector, dense push at 1 GPU), with cfg2 (2^28) as the extra key; both are checked."""
+    d = _bench(["--steps", "2", "--warmup", "1", "--no-cpu-baseline"])
+    assert "2^30" in d["config"]["workload"] and d["config"]["keys_per_gpu"] == 1 << 30 and d["check"] is True
+    assert d["cfg2_2p28"]["check"] is True and "2^28" in d["cfg2_2p28"]["workload"]
 
 
 @pytest.mark.parametrize("n", [1, 7, 100_001, 1 << 20])

@@ -333,6 +333,26 @@ def test_coalesced_pulls_answer_each_message(gpu, dtype):
         np.testing.assert_array_equal(o1, base[q1])
 
 
+def test_host_free_refuses_a_buffer_with_pending_pulls(gpu):
+    """glint_host_free of a buffer that an enqueued, not yet retired pull answers into would let the
+    kernel write into freed pinned memory: it returns GLINT_EINVAL and frees nothing; once the pull's
+    ticket has been waited for, the buffer frees normally."""
+    from glint_amd.shard import HostBuffer
+    lib = N.load()
+    size = 10_000
+    with PartialVector(RangePartition(0, 0, size), "double", gpu) as sh:
+        base = np.arange(size, dtype=np.float64) * 0.5
+        sh.update(np.arange(size, dtype=np.int64), base)
+        hb = HostBuffer(1 << 16)
+        q = np.arange(0, 2 * 1024, 2, dtype=np.int64)  # 1024 doubles: a page of answer, in place
+        t, got = sh.pull_async(q, out=hb.array(np.float64, q.size))
+        assert lib.glint_host_free(hb.ptr) == N.GLINT_EINVAL
+        sh.wait(t)
+        np.testing.assert_array_equal(got, base[q])
+        assert lib.glint_host_free(hb.ptr) == N.GLINT_OK
+        hb.ptr = None
+
+
 @pytest.mark.parametrize("dtype", ["double", "int"])
 @pytest.mark.parametrize("min_bytes", ["0", None])
 def test_pulls_answer_straight_into_host_buffers(gpu, dtype, min_bytes, monkeypatch):

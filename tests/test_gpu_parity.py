@@ -275,7 +275,7 @@ def test_gated_push(gpu, pattern):
             assert torch.equal(state(), ref)
 
 
-@pytest.mark.parametrize("pattern", ["dense", "zipf", "small", "matrix", "sorted_bad", "empty"])
+@pytest.mark.parametrize("pattern", ["dense", "zipf", "small", "matrix", "sorted_bad", "empty", "wrap"])
 @pytest.mark.parametrize("word", ["device", "host"])
 def test_validating_gated_push(gpu, pattern, word):
     """GLINT_PUSH_VALIDATE: the gated push checks its own records and writes the verdict -- 0, or
@@ -302,7 +302,7 @@ def test_validating_gated_push(gpu, pattern, word):
     else:
         part = RangePartition(0, 0, size)
         sh = PartialVector(part, "long", gpu)
-        if pattern in ("dense", "sorted_bad"):
+        if pattern in ("dense", "sorted_bad", "wrap"):
             k = torch.arange(size, dtype=torch.int64, device=d)
         elif pattern == "small":
             k = torch.from_numpy(rng.integers(0, size, 1000).astype(np.int64)).to(d)
@@ -317,8 +317,12 @@ def test_validating_gated_push(gpu, pattern, word):
         if k.numel():
             # sorted_bad: a dense increasing head, then the bad key (and a break after it)
             first = k.numel() // 2 if pattern == "sorted_bad" else min(k.numel() - 1, 123_457)
-            kb[first] = size + 5
-            kb[-1] = -3 if k.numel() - 1 != first else kb[-1]
+            if pattern == "wrap":  # 2^32 away from in-range keys: (key - start).toInt aliases them
+                kb[first] = first + 2**32
+                kb[-1] = -(2**32) + 1
+            else:
+                kb[first] = size + 5
+                kb[-1] = -3 if k.numel() - 1 != first else kb[-1]
         bad = (kb, v)
         flat = k
         ref = torch.zeros(size, dtype=torch.int64, device=d)

@@ -19,7 +19,7 @@
 #   ring      tools/ring_probe.py: pipelined message-sized wire pushes, timed and with kernel stats
 #   loopback  tools/loopback/build/glint_loopback, HBM shards vs the oracle's CPU loop (cfg1, cfg4 shapes)
 set -o pipefail
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
@@ -66,7 +66,7 @@ for s in ${STAGES:-tests bench}; do
       step bench_exchange_mps8 300 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
       ;;
     prof2p30)
-      kstats dense_2p28 300
+      kstats dense_2p28 300 --log2-keys 28
       kstats dense_2p30 400 --log2-keys 30 --steps 10
       ;;
     binned)
@@ -76,7 +76,7 @@ for s in ${STAGES:-tests bench}; do
     pmc)
       for w in ${PMC:-dense_2p28 dense_2p30 zipf_2p28 matrix_2p17x512}; do
         case $w in
-          dense_2p28) pmc $w ;;
+          dense_2p28) pmc $w --log2-keys 28 ;;
           dense_2p30) pmc $w --log2-keys 30 ;;
           zipf_2p28) pmc $w --pattern zipf ;;
           matrix_2p17x512) pmc $w --pattern matrix ;;
