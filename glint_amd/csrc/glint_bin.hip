@@ -40,7 +40,10 @@ constexpr int kMaxDigit = 1024;        // coarse buckets and fine slabs per buck
 #define GLINT_PART_TPB 1024
 #endif
 constexpr int kATPB = GLINT_PART_TPB;  // partition workgroup size (build-time knob: 1024 or 512)
-constexpr int kAPer = 4;               // records per thread per chunk
+#ifndef GLINT_PART_PER
+#define GLINT_PART_PER 4
+#endif
+constexpr int kAPer = GLINT_PART_PER;  // records per thread per chunk (build-time knob)
 constexpr int kAChunk = kATPB * kAPer; // records per partition chunk (and dedup table fill)
 constexpr int kASlots = 2 * kAChunk;   // dedup hash slots (load <= 0.5)
 constexpr int kASlotBits = kASlots == 8192 ? 13 : kASlots == 4096 ? 12 : 11;
@@ -1534,6 +1537,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
     for (u32 f = tid; f < nf1; f += kSTPB) orow[f] = 0;
     return;
   }
+  PhaseClock ph(32);
   u32 a[kSPer];
   A v[kSPer];
 #pragma unroll
@@ -1545,11 +1549,13 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
     if (i >= s1) a[q] = kEmptySlot;
   }
   __syncthreads();
+  ph.mark(32);
   u32 p[kSPer];
 #pragma unroll
   for (int q = 0; q < kSPer; ++q)
     if (a[q] != kEmptySlot) p[q] = atomicAdd(&hist[fine_of(a[q], g)], 1u);
   __syncthreads();
+  ph.mark(33);
   const u32 total = block_scan<kSTPB, 1>(
       g.nf, [&](u32 f) { return hist[f]; },
       [&](u32 f, u32 excl) {
@@ -1557,6 +1563,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
         orow[f] = (uint16_t)excl;
       });
   if (tid == 0) orow[g.nf] = (uint16_t)total;
+  ph.mark(34);
 #pragma unroll
   for (int q = 0; q < kSPer; ++q)
     if (a[q] != kEmptySlot) p[q] += hist[fine_of(a[q], g)];
@@ -1569,6 +1576,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
   __syncthreads();
   for (u32 x = tid; x < total; x += kSTPB) e_out[s0 + x] = ste[x];
   __syncthreads();
+  ph.mark(35);
   A* const stv = reinterpret_cast<A*>(stage);
   for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
 #pragma unroll
@@ -1579,6 +1587,8 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
     for (u32 x = r0 + tid; x < r1; x += kSTPB) v_out[s0 + x] = stv[x - r0];
     __syncthreads();
   }
+  ph.mark(36);
+  ph.flush(5);
 }
 
 // One workgroup per bucket: every slab's runs (one per item of the bucket, from the bucket's off2 rows,
@@ -1680,8 +1690,10 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
     if (tot) *tot = t;
     return nu;
   };
+  PhaseClock ph(48);
   u32 h = 0;
   const u32 nu1 = walk(false, 0, 0, 1, &h);
+  ph.mark(48);
   // sparse neighbours: the largest aligned group (lanes f..f+gs-1 of one wave) within the caps
   u32 span = 1;
   if (group_on && J <= (u32)kRunMax) {
@@ -1698,10 +1710,15 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
   __syncthreads();
   const u32 used = block_scan<kPlanTPB, 1>(g.nf, [&](u32 x) { return nunit[x]; },
                                            [&](u32 x, u32 excl) { nunit[x] = excl; });
+  ph.mark(49);
   if (tid == 0) ubase = used ? atomicAdd(&bc->nunits, used) : 0u;
   __syncthreads();
+  ph.mark(50);
   const u32 flags = span > 1 ? (kUnitExcl | kUnitGroup) : (nu == 1 ? kUnitExcl : 0u);
   walk(true, ubase + (f < g.nf ? nunit[f] : 0u), flags, span, nullptr);
+  __syncthreads();
+  ph.mark(51);
+  ph.flush(4);
 }
 
 // Per apply unit: the records of its runs (record r lives in run i = the last one whose prefix is <= r:
@@ -1717,17 +1734,17 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
 #define GLINT_APPLY2_WAVES 4  // bin_apply2's register budget: waves per SIMD (4 workgroups per CU fit in LDS)
 #endif
 #ifndef GLINT_APPLY2_WARM
-#define GLINT_APPLY2_WARM 2  // slab warm-up: 0 off, 1 one unit ahead, 2 at the unit's own start
+#define GLINT_APPLY2_WARM 0  // slab warm-up: 0 off, 1 one unit ahead, 2 at the unit's own start
 #endif
 #ifndef GLINT_CRB2
-#define GLINT_CRB2 8
+#define GLINT_CRB2 4  // (8: 18 spilled VGPRs; A/B profiles/r05: cfg5 0.383 vs 0.403 ms, cfg3 1.130 vs 1.136, cfg4b 2.508 vs 2.501)
 #endif
 constexpr int kCRB2 = GLINT_CRB2;  // records per thread per batch
 template <typename V>
 __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APPLY2_WAVES))) void bin_apply2_kernel(
     const uint16_t* __restrict__ e_in, const typename LdsAcc<V>::T* __restrict__ v_in, const uint4* __restrict__ units,
     const uint2* __restrict__ runs, const BinCtl* bc, i64 elems, V* __restrict__ data, u32 pre_min, u32 sparse_max,
-    u32 list_max, bool line_wb, int xcd_map) {
+    u32 list_max, bool line_wb, int xcd_map, u32 nf) {
   typedef typename Vec2<V>::T V2;
   typedef typename LdsAcc<V>::T A;
   static_assert(kRunMax <= kCTPB, "one run per loading thread");
@@ -1744,6 +1761,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
   uint16_t* const hused = reinterpret_cast<uint16_t*>(touched);  // the group's claimed slots, in order
   constexpr int kPairsPerThread = kSlab / 2 / kCTPB;
   constexpr int kListPer = (kGroupCap + kCTPB - 1) / kCTPB;  // element write-backs per thread at most
+  constexpr int kListPass = 4;                                // ... in passes of this many
   static_assert(kSparseCap2 <= kGroupCap, "the touched list fits the element write-back");
   const int tid = threadIdx.x, lane = tid & 63;
   const u64 below = (1ull << lane) - 1ull;
@@ -1774,27 +1792,40 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
     }
     if (tid == 0) rp[slot][d.y] = (uint16_t)d.z;  // (d.y == 0 only for a missing unit: count 0)
   };
-  auto fetch = [&](int slot, const uint4& d, u32 r0, u32 (&ca)[kCRB2], A (&cv)[kCRB2]) {
+  // a batch's records: record rr lives in run lo = the last one whose prefix is <= rr, found by a
+  // fixed-step search (kRunMax = 2^7: seven steps, the kCRB2 searches in lockstep -- a data-dependent
+  // loop ran them one after another, ~40 % of the workgroup's clocks); runs past nr are never chosen
+  // (the prefix array holds the unit's count at nr, and rr < count)
+  static_assert((kRunMax & (kRunMax - 1)) == 0, "fixed-step search over a power of two");
+  // returns which of the thread's kCRB2 records are valid as a mask: selecting on the loaded registers
+  // would make the compiler wait for the loads right there (and the prefetch would not overlap anything)
+  auto fetch = [&](int slot, const uint4& d, u32 r0, u32 (&ca)[kCRB2], A (&cv)[kCRB2]) -> u32 {
     const u32 cnt = d.z, nr = d.y;
+    if (cnt == 0) return 0u;  // block-uniform: a missing unit
+    u32 rr[kCRB2], lo[kCRB2];
 #pragma unroll
-    for (int q = 0; q < kCRB2; ++q) {  // clamped, branch-free loads
+    for (int q = 0; q < kCRB2; ++q) {
       const u32 r = r0 + q * kCTPB + tid;
-      ca[q] = kEmptySlot;
-      cv[q] = A(0);
-      if (cnt) {
-        const u32 rr = r < cnt ? r : cnt - 1;
-        u32 lo = 0, hi = nr - 1;  // the last run starting at or before rr
-        while (lo < hi) {
-          const u32 mid = (lo + hi + 1) >> 1;
-          if ((u32)rp[slot][mid] <= rr) lo = mid;
-          else hi = mid - 1;
-        }
-        const u32 idx = rs[slot][lo] + (rr - (u32)rp[slot][lo]);
-        ca[q] = ld_in(e_in + idx);
-        cv[q] = ld_in(v_in + idx);
-        if (r >= cnt) ca[q] = kEmptySlot;
+      rr[q] = r < cnt ? r : cnt - 1;  // clamped, branch-free loads
+      lo[q] = 0;
+    }
+#pragma unroll
+    for (u32 step = kRunMax / 2; step > 0; step >>= 1) {
+#pragma unroll
+      for (int q = 0; q < kCRB2; ++q) {
+        const u32 m = lo[q] + step;
+        if (m < nr && (u32)rp[slot][m] <= rr[q]) lo[q] = m;
       }
     }
+    u32 valid = 0;
+#pragma unroll
+    for (int q = 0; q < kCRB2; ++q) {
+      const u32 idx = rs[slot][lo[q]] + (rr[q] - (u32)rp[slot][lo[q]]);
+      ca[q] = ld_in(e_in + idx);
+      cv[q] = ld_in(v_in + idx);
+      valid |= (r0 + q * kCTPB + tid < cnt ? 1u : 0u) << q;
+    }
+    return valid;
   };
   auto warm_slab = [&](const uint4& d) -> u32 {  // most of the slab's lines will be touched: into L2 now
     u32 w = 0;
@@ -1827,10 +1858,11 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
   __syncthreads();
   u32 pa[kCRB2];
   A pv[kCRB2];
-  fetch(0, dcur, 0u, pa, pv);
+  u32 pvalid = fetch(0, dcur, 0u, pa, pv);
   u32 warm = GLINT_APPLY2_WARM == 1 ? warm_slab(dcur) : 0u;
   int cs = 0;  // LDS table slot of unit u
   u32 par = 0;
+  PhaseClock ph(56);
   for (; u < nunits; u = unit_of(++i)) {
     const uint4 d = dcur;
     const u32 slab = d.x, cnt = d.z;
@@ -1842,6 +1874,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
     if (GLINT_APPLY2_WARM == 2) warm = warm_slab(d);
     u32 ca[kCRB2];
     A cv[kCRB2];
+    u32 valid = pvalid;
 #pragma unroll
     for (int q = 0; q < kCRB2; ++q) {
       ca[q] = pa[q];
@@ -1853,8 +1886,11 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
         for (int q = 0; q < kCRB2; ++q) {
           bool first = false;
           u32 h = 0;
-          if (ca[q] != kEmptySlot) {
-            const u32 ad = (((slab & ~(kGroupMax - 1)) | (ca[q] >> kSlabBits)) << kSlabBits) | (ca[q] & (kSlab - 1));
+          if ((valid >> q) & 1u) {
+            // the record's slab: the group's first slab + the difference of their fine digits' low 4 bits
+            // (a group of <= 16 aligned slabs lies in one 16-aligned block of its bucket's fine digits)
+            const u32 ad = ((slab + (ca[q] >> kSlabBits) - ((slab & (nf - 1)) & (kGroupMax - 1))) << kSlabBits) |
+                           (ca[q] & (kSlab - 1));
             const u32 key = ad + 1u;
             h = (ad * 0x9E3779B1u) >> (32 - 11);
             static_assert(kGroupCap == 2048, "11-bit slot hash");
@@ -1873,7 +1909,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
         for (int q = 0; q < kCRB2; ++q) {
           bool first = false;
           u32 e = 0;
-          if (ca[q] != kEmptySlot) {
+          if ((valid >> q) & 1u) {
             e = ca[q] & (kSlab - 1);
             lds_add(&acc[e], cv[q]);
             const u32 sh = 8u * (e & 3u);
@@ -1884,7 +1920,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
       } else {
 #pragma unroll
         for (int q = 0; q < kCRB2; ++q) {
-          if (ca[q] == kEmptySlot) continue;
+          if (!((valid >> q) & 1u)) continue;
           const u32 e = ca[q] & (kSlab - 1);
           lds_add(&acc[e], cv[q]);
           touched[e] = 1;
@@ -1892,18 +1928,21 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
       }
       r0 += (u32)kCTPB * kCRB2;
       if (r0 >= cnt) break;
-      fetch(cs, d, r0, ca, cv);
+      valid = fetch(cs, d, r0, ca, cv);
     }
     asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
+    ph.mark(56);
     // the next unit's run table into the other slot; the one after it starts loading
     publish(cs ^ 1, dnext, rnext);
     dcur = dnext;
     load_unit(unit_of(i + 2), dnext, rnext);
     __syncthreads();
+    ph.mark(57);
     if (tid == 0) ntl[par ^ 1u] = 0;  // the next list unit's count (the last one read it before a barrier)
     // the next unit's first batch (and warm-up): in flight during this unit's write-back
-    fetch(cs ^ 1, dcur, 0u, pa, pv);
+    pvalid = fetch(cs ^ 1, dcur, 0u, pa, pv);
     if (GLINT_APPLY2_WARM == 1) warm = warm_slab(dcur);
+    ph.mark(58);
     bool sweep_wb = exclusive && !sparse && !group;
     if (group || sparse) {
       const u32 L = ntl[par];  // block-uniform (read after the barrier)
@@ -1911,12 +1950,15 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
       if (sparse && L > list_max) {
         sweep_wb = true;  // many distinct elements: whole-line write-back
       } else {
-        // element read-modify-writes: every load issued before any store
-        u32 ad[kListPer];
-        V old[kListPer];
+        // element read-modify-writes: every load of a pass (kListPass per thread, 1024 elements)
+        // issued before any store
+        for (int k0 = 0; k0 < kListPer; k0 += kListPass) {
+          if ((u32)(k0 * kCTPB) >= L) break;  // block-uniform
+        u32 ad[kListPass];
+        V old[kListPass];
 #pragma unroll
-        for (int k = 0; k < kListPer; ++k) {
-          const u32 x = tid + k * kCTPB;
+        for (int k = 0; k < kListPass; ++k) {
+          const u32 x = tid + (k0 + k) * kCTPB;
           ad[k] = 0xFFFFFFFFu;
           if (x < L) {
             const u32 s2 = group ? hused[x] : tlist[x];
@@ -1925,9 +1967,9 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
           }
         }
 #pragma unroll
-        for (int k = 0; k < kListPer; ++k) {
+        for (int k = 0; k < kListPass; ++k) {
           if (ad[k] == 0xFFFFFFFFu) continue;
-          const u32 x = tid + k * kCTPB;
+          const u32 x = tid + (k0 + k) * kCTPB;
           const u32 s2 = group ? hused[x] : tlist[x];
           if (group) {
             if ((i64)ad[k] < elems) data[ad[k]] = acc_add(old[k], hv[s2]);
@@ -1939,6 +1981,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
             acc[s2] = A(0);
             touched[s2] = 0;
           }
+        }
         }
       }
     }
@@ -1987,10 +2030,13 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
         }
       }
     }
+    ph.mark(59);
     __syncthreads();
+    ph.mark(60);
     cs ^= 1;
   }
   asm volatile("" ::"v"(warm));
+  ph.flush(5);
 }
 
 // ---- host side ----------------------------------------------------------------------------------------
@@ -2070,8 +2116,11 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const bool dedup = front == 2;
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
   static EnvKnob wpc_knob("GLINT_PART_WPC");
+  // partition workgroups per CU: what fits at once (the hot front end's LDS table allows fewer)
+  static const int hot_occ = resident_per_cu(bin_part_kernel<V, MAT, true, 0>, kATPB);
   const int plain_wpc = (int)wpc_knob.pos_or(kPartWgPerCuPlain);
-  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : plain_wpc)));
+  const int wpc = dedup ? kPartWgPerCuDedup : front == 1 ? std::min(plain_wpc, hot_occ) : plain_wpc;
+  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * wpc));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const i64 max_fitems = (i64)g.nb + n / kSItem + 1;
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
@@ -2180,7 +2229,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const unsigned apply2_grid = (unsigned)std::min<i64>(max_units, (i64)s->cus * apply2_bpc);
   bin_apply2_kernel<V><<<apply2_grid, kCTPB, 0, st>>>(
       e_b, val_b, units, runs, bc, s->elems, a.data, bin_prefetch_min(), std::min<u32>(bin_sparse_max(), kSparseCap2),
-      bin_list_max(), bin_line_wb(), apply2_grid % 8 == 0 && xcd_knob.pos_or(1) == 1 ? 1 : 0);
+      bin_list_max(), bin_line_wb(), apply2_grid % 8 == 0 && xcd_knob.pos_or(1) == 1 ? 1 : 0, g.nf);
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }

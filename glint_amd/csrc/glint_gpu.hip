@@ -632,6 +632,16 @@ int binned_mode() {
   });
 }
 constexpr i64 kBinMin = (i64)1 << 20;  // records: below this the LDS-hash scatter wins
+// ... and below this many records per 4096-element slab of the shard (GLINT_BIN_DENSITY): the binned
+// pipeline's passes cost about the same whatever the density, the atomic scatter's time grows with
+// the records. Measured crossover (tools/tail_ab.py, profiles/r05/tail_ab.jsonl, uniform keys into a
+// 2^28-element shard): scatter 0.55 / 1.02 / 1.98 / 3.83 ms against binned 0.88 / 1.27 / 1.99 / 2.24 ms
+// at 128 / 256 / 512 / 1024 records per slab; 8 shards pushed on 8 concurrent streams at 128 per slab
+// (the cfg4 key space's local pushes) 3.70 against 4.69 ms
+i64 bin_density() {
+  static EnvKnob k("GLINT_BIN_DENSITY");
+  return k.get([](const char* e) -> long long { return e ? std::max(0ll, atoll(e)) : 512ll; });
+}
 // records: up to this many, a (non-deterministic) push is the single scatter launch.
 // GLINT_SMALL_PUSH overrides it (0 = always check + apply).
 i64 small_push_max() {
@@ -692,8 +702,10 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
 
   const int bmode = binned_mode();
   const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
+  const i64 slabs = (s->elems + 4095) / 4096;
   const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
-                      (unordered || (n >= kBinMin && (bmode == 1 || last_tail >= kBinMin)));
+                      (unordered || (n >= kBinMin && (bmode == 1 || (last_tail >= kBinMin &&
+                                                                     last_tail >= bin_density() * slabs))));
   if (binned && unordered && !gated) return push_binned<V, MAT>(s, a, false, st);
   // Small pushes (an Akka message is ~1000 records, GranularBigVectorSpec.scala:21) are one launch:
   // the scatter handles every record, instead of check + apply + scatter. Launch latency is the

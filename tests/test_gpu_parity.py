@@ -723,6 +723,45 @@ def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
         assert cnt.value == 0
 
 
+def test_binned_switch_density_floor(gpu, monkeypatch):
+    """The adaptive switch bins a large unordered tail only from GLINT_BIN_DENSITY (default 512)
+    records per 4096-element slab of the shard on: below it the atomic scatter is faster at every
+    size measured (tools/tail_ab.py). 2^20 records into a 2^24-element shard (256 per slab) stay on the
+    scatter; 2^22 (1024 per slab) are binned; with the floor at 0 the sparse push is binned too."""
+    import ctypes as C
+    lib = N.load()
+    size = 1 << 24
+    part = RangePartition(0, 0, size)
+    rng = np.random.default_rng(41)
+    monkeypatch.delenv("GLINT_BINNED", raising=False)
+    monkeypatch.delenv("GLINT_BIN_DENSITY", raising=False)
+    N.reload_env()
+
+    def binned(sh):
+        ms, cnt = C.c_double(), C.c_int64()
+        lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
+        return cnt.value
+    ref = np.zeros(size, np.int64)
+    with PartialVector(part, "long", gpu) as sh:
+        lib.glint_prof_enable(sh.handle, 1)
+        # (the switch decides from the previous push's tail: binned pushes counted cumulatively)
+        for lg, want in ((20, 0), (20, 0), (22, 0), (22, 1), (20, 2), (20, 2)):
+            k = rng.integers(0, size, 1 << lg).astype(np.int64)
+            v = rng.integers(-9, 9, k.size).astype(np.int64)
+            sh.update(k, v)  # a host call ends at a sync point: its tail is the next push's history
+            np.add.at(ref, k, v)
+            assert binned(sh) == want, (lg, want)
+        np.testing.assert_array_equal(sh.to_numpy(), ref)
+    monkeypatch.setenv("GLINT_BIN_DENSITY", "0")
+    N.reload_env()
+    with PartialVector(part, "long", gpu) as sh:
+        lib.glint_prof_enable(sh.handle, 1)
+        k = rng.integers(0, size, 1 << 20).astype(np.int64)
+        for _ in range(2):
+            sh.update(k, np.ones(k.size, np.int64))
+        assert binned(sh) == 1
+
+
 def test_adaptive_switch_decides_at_sync_points(gpu, monkeypatch):
     """The binned/scatter choice of a device-resident push comes from the previous pushes' tails as
     of the shard's last sync point, never from a word the device may or may not have written yet:

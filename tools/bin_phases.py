@@ -23,6 +23,9 @@ PHASES = {
     "bin_fpart": (20, ["T/H scans", "item descs", "segments", "sync", "reserve", "fetch issue",
                        "rank+sync", "scan", "stage+sync", "store+sync", "clear+sync"]),
     "bin_apply": (40, ["desc/warm", "clear+sync", "records", "sync", "rmw", "sync"]),
+    "bin_fsort (v2)": (32, ["load+sync", "rank+sync", "scan", "stage e+store", "values"]),
+    "bin_plan (v2)": (48, ["stage+walk", "groups+scan", "atomic+sync", "emit+sync"]),
+    "bin_apply2 (v2)": (56, ["records", "publish+sync", "prefetch issue", "write-back", "sync"]),
 }
 
 

@@ -101,6 +101,10 @@ for s in ${STAGES:-tests bench}; do
       python3 tools/pmc_calibrate.py $OUT/pmccal_known.log $OUT/pmccal_FETCH_SIZE.csv $OUT/pmccal_WRITE_SIZE.csv \
         $OUT/pmc_calibration.json >&2
       ;;
+    tailab)  # the unordered tail: atomic scatter vs binned by density, one stream and 8 (tools/tail_ab.py)
+      step tail_ab 600 python3 tools/tail_ab.py --reps ${REPS:-10}
+      grep '^{' $OUT/tail_ab.log > $OUT/tail_ab.jsonl || true
+      ;;
     quickbench)  # the binned lines only, no CPU baseline
       for pat in ${PATTERNS:-matrix zipf exchange}; do
         step qb_$pat 300 python3 bench.py --no-cpu-baseline --no-north-star --pattern $pat
