@@ -83,12 +83,13 @@ def pmc_traffic(workload_tag: str):
     PMC counters cannot be read inside the timed run itself, so the source file is named."""
     files = sorted(glob.glob(str(ROOT / "profiles" / "*" / f"pmc_{workload_tag}.json")))
     if not files:
-        return None, None
+        return None, None, None
     try:
         d = json.loads(Path(files[-1]).read_text())
-        return d.get("hbm_bytes_per_launch"), "replayed from " + str(Path(files[-1]).relative_to(ROOT))
+        return (d.get("hbm_bytes_per_launch"), "replayed from " + str(Path(files[-1]).relative_to(ROOT)),
+                d.get("records_per_push"))
     except Exception:
-        return None, None
+        return None, None, None
 
 
 def sparse_floor(workload_tag: str, ms_per_step: float):
@@ -96,15 +97,21 @@ def sparse_floor(workload_tag: str, ms_per_step: float):
     tools/microbench_sparse measurement (profiles/<round>/micro_sparse_floor.json): the time to stream
     the records once plus read-modify-write each distinct element once in ascending order, as if
     partitioning were free. frac = floor / ms_per_step; None for lines without one."""
-    case = {"zipf_2p28": "cfg3", "exchange_2p28": "cfg4b", "matrix_2p17x512": "cfg5"}.get(workload_tag)
-    files = sorted(glob.glob(str(ROOT / "profiles" / "*" / "micro_sparse_floor.json")))
+    # (case, shard pushes per step): the 8-partition line's step is eight shard pushes, each floored alone
+    case, per_step = {"zipf_2p28": ("cfg3", 1), "exchange_2p28": ("cfg4b", 1), "matrix_2p17x512": ("cfg5", 1),
+                      "exchange_2p28_mps8": ("cfg4_mps8_shard", 8)}.get(workload_tag, (None, 1))
+    files = [f for f in sorted(glob.glob(str(ROOT / "profiles" / "*" / "micro_sparse_floor.json")))
+             if case and f'"{case}"' in Path(f).read_text()]
     if not case or not files:
         return None
     try:
         for d in json.loads(Path(files[-1]).read_text())["cases"]:
             if d.get("case") == case:
-                return {"floor_ms": d["floor_ms"], "frac": round(d["floor_ms"] / ms_per_step, 4),
-                        "read_ms": d["read_ms"], "rmw_sorted_ms": d["rmw_sorted_ms"],
+                floor = d["floor_ms"] * per_step
+                return {"floor_ms": round(floor, 4), "frac": round(floor / ms_per_step, 4),
+                        "read_ms": round(d["read_ms"] * per_step, 4),
+                        "rmw_sorted_ms": round(d["rmw_sorted_ms"] * per_step, 4),
+                        "shard_pushes_per_step": per_step,
                         "source": "replayed from " + str(Path(files[-1]).relative_to(ROOT))}
     except Exception:
         return None
@@ -506,7 +513,14 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     if overlap:  # the local shards' pushes run on concurrent streams: their summed device time exceeds the
         kern_ms = dt / steps * 1e3  # step, so the roofline is taken over the step's wall time instead
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(tag)
+    traffic, traffic_src, traffic_recs = pmc_traffic(tag)
+    if traffic is not None and traffic_recs and push:
+        # the summary is per profiled shard push: scaled to the records this step's pushes take (the
+        # 8-partition exchange line's step is eight shard pushes of ~2^23 records each)
+        step_recs = recv if exch else nrec
+        if abs(step_recs / traffic_recs - 1.0) > 0.01:
+            traffic = traffic * step_recs / traffic_recs
+            traffic_src += f" (x {step_recs / traffic_recs:.3f}: {step_recs} records per step / {traffic_recs} per push)"
     line = {
         "metric": metric,
         "value": round(value, 2),

@@ -300,12 +300,19 @@ __device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
 // counts are exact and the buffer has no holes.
 constexpr int kWideSlots = 8192;  // the plain + hot front end's hot table (see bin_hot_select)
 __device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
-template <bool MAT, int KIND>
+// VALIDATE (a validating gated push, GLINT_PUSH_VALIDATE, whose tail is binned): the count also checks
+// every tail record -- the key itself in the partition's key range, as key_in_part -- and records the
+// first rejected one in the push's LaunchCtl (vctl->bad), as push_check does for the records before the
+// break; the push's verdict and cancel come after this kernel (push_validate_gate_binned_kernel), so the
+// keys are read once instead of by push_check and here.
+template <bool MAT, int KIND, bool VALIDATE = false>
 __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                           i64 n, PartDesc part, const LaunchCtl* lctl, u32 ntiles,
                                                           int from_break, BinGeom g, u32* __restrict__ T,
                                                           u32* __restrict__ R, BinCtl* bc, u32* __restrict__ Roff,
-                                                          const unsigned long long* __restrict__ hot_best) {
+                                                          const unsigned long long* __restrict__ hot_best,
+                                                          BinCtl* next_bc, u32* __restrict__ next_T,
+                                                          LaunchCtl* vctl = nullptr) {
   constexpr int kCopies = 4;  // histogram copies (wave % 4): fewer LDS atomics on one hot bucket
   __shared__ u32 h[kCopies * kMaxDigit];
   __shared__ u32 htag[kWideSlots];
@@ -313,6 +320,10 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   const u32 hc = (u32)((tid >> 6) % kCopies) * g.nb;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
+  if (next_bc && blockIdx.x == 0) {  // v2: the next push's header (the previous push used it; it is done)
+    for (u32 b = tid; b < g.nb; b += kATPB) next_T[b] = 0;
+    if (tid < (int)(sizeof(BinCtl) / 4)) reinterpret_cast<u32*>(next_bc)[tid] = 0;
+  }
   if (hot_best)
     for (int sl = tid; sl < kWideSlots; sl += kATPB) {
       const unsigned long long x = hot_best[sl];
@@ -326,9 +337,10 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   // partition grid is one 1024-thread workgroup per CU). Every step issues its loads unconditionally
   // (chunk index clamped; a step past the end counts nothing), so the compiler can wait for one
   // chunk's loads while the next chunk's stay in flight: with conditional loads it waited vmcnt(0).
+  BadRecs bad;
   auto load = [&](i64 c, RecRegs<double, MAT>& r) {
     const i64 cc = min(c, nchunks - 1);
-    if constexpr (KIND == 0) {
+    if constexpr (KIND == 0 && !VALIDATE) {
       // the range layout reads only the key's low word ((key - start).toInt): loading the whole key
       // left its high half dead, the compiler reused that register while the load was in flight and
       // had to wait for it (vmcnt(0)), so only one chunk was ever in flight
@@ -350,7 +362,12 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       i64 ad;
-      const bool ok = c0 + q * kATPB + tid < c1 && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad);
+      const bool in = c0 + q * kATPB + tid < c1;
+      bool ok = in && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad);
+      if constexpr (VALIDATE) {
+        ok = ok && key_in_part<KIND>(part, r.k[q]);
+        if (in && !ok) bad.add(c0 + q * kATPB + tid);
+      }
       bk[q] = ok && !(hot_best && htag[wide_slot((u32)ad)] == (u32)ad) ? bucket_of((u32)ad, g) : kEmptySlot;
     }
     load(c + kCountAhead * G, r);  // kCountAhead chunks ahead, into the registers just consumed
@@ -383,6 +400,28 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   }
   const u32 tot = block_sum<kATPB>(nvalid);
   if (tid == 0 && tot) atomicAdd(&bc->tail, tot);
+  if (VALIDATE && bad.count) atomicMax(&vctl->bad, ~(u64)bad.first);  // rare: one atomic per thread
+}
+
+// The verdict of a validating gated push whose tail is binned (after bin_count validated the tail and
+// push_check the records before the break): 0 or ~(first rejected record) to the caller's gate word; a
+// rejected batch is cancelled before anything is applied -- no head (push_apply sees cancel), no tail
+// (the break is cleared, so every binned kernel sees an empty tail, and the counts already taken are
+// zeroed, so no fine item reads the partition buffer).
+__global__ __launch_bounds__(256) void push_validate_gate_binned_kernel(LaunchCtl* ctl, u64* gate, BinCtl* bc,
+                                                                        u32* __restrict__ T, u32 nb) {
+  const u64 b = ctl->bad;
+  if (b == 0ull) {
+    if (threadIdx.x == 0) *gate = 0ull;
+    return;
+  }
+  for (u32 x = threadIdx.x; x < nb; x += 256) T[x] = 0;
+  if (threadIdx.x == 0) {
+    *gate = b;
+    ctl->cancel = 1u;
+    ctl->brk_enc = 0u;
+    bc->tail = 0u;
+  }
 }
 
 // ---- hot elements ----------------------------------------------------------------------------------
@@ -669,10 +708,12 @@ __global__ __launch_bounds__(256) void bin_hot_sample_kernel(const i64* __restri
 
 // Every counted element with >= min_count samples competes for its wide slot; the most sampled wins
 // (best[slot] = count << 32 | element; zeroed per push). The partition kernel reads the tags from it.
-__global__ __launch_bounds__(256) void bin_hot_select_kernel(const u32* __restrict__ gkey, const u32* __restrict__ gcnt,
+__global__ __launch_bounds__(256) void bin_hot_select_kernel(u32* __restrict__ gkey, u32* __restrict__ gcnt,
                                                              u32 min_count, unsigned long long* __restrict__ best) {
   const u32 i = blockIdx.x * 256u + threadIdx.x;
   const u32 a = gkey[i], c = gcnt[i];
+  gkey[i] = kEmptySlot;  // the table's last reader empties it for the next push (no memset)
+  gcnt[i] = 0;
   if (a != kEmptySlot && c >= min_count) atomicMax(&best[wide_slot(a)], ((unsigned long long)c << 32) | a);
 }
 
@@ -683,7 +724,7 @@ __global__ __launch_bounds__(256) void bin_hot_select_kernel(const u32* __restri
 // group sums are added in group order -- the result is the same on every run.
 constexpr int kRedSlots = 64, kRedTPB = 1024, kRedGroups = kRedTPB / kRedSlots;
 template <typename V>
-__global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned long long* __restrict__ best, u32 G,
+__global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(unsigned long long* __restrict__ best, u32 G,
                                                                  const typename LdsAcc<V>::T* __restrict__ partial,
                                                                  V* __restrict__ data) {
   typedef typename LdsAcc<V>::T A;
@@ -714,6 +755,7 @@ __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned 
   if (grp != 0) return;
   const unsigned long long b = best[sl];
   if (!b) return;
+  best[sl] = 0ull;  // the picks' last reader empties them for the next push (no memset)
   A tot = hot_zero<A>();
   bool seen = false;
   for (int q = 0; q < kRedGroups; ++q) {
@@ -2108,8 +2150,25 @@ BinGeom bin_geometry(i64 elems) {
 }
 
 // The v2 binned push (front: 0 plain, 1 plain + hot split, 2 chunk dedup; see push_binned).
+bool bin_v1() {
+  static EnvKnob v1_knob("GLINT_BIN_V1");
+  return v1_knob.get([](const char* e) -> long long { return e && atoi(e) != 0; }) != 0;
+}
+
+bool push_binned_fusable(const glint_shard* s, i64 n, size_t asize) {
+  return !bin_v1() && (u64)n * asize < ((u64)1 << 32) && n < ((i64)1 << 32) - 2 * kAChunk &&
+         s->elems < ((i64)1 << 32) - 1;
+}
+
+int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32 nb, hipStream_t st) {
+  push_validate_gate_binned_kernel<<<1, 256, 0, st>>>(ctl, gate, (BinCtl*)bc, T, nb);
+  HIPCHK(hipGetLastError());
+  return GLINT_OK;
+}
+
 template <typename V, bool MAT>
-int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, int front, bool hot_on) {
+int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, int front, bool hot_on,
+                   const BinHook* hook) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   const BinGeom g = bin_geometry(s->elems);
@@ -2126,26 +2185,46 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
   // floor(H / cap) + floor(runs / kRunMax) + 1 per non-empty slab
   const i64 max_units = (i64)g.nslab + n / kUnitCap + std::min<i64>(n, max_fitems * g.nf) / kRunMax + 1;
-  // [BinCtl | T] zeroed per push; then R, Roff, Bb, Ib, the fine items, off2, the apply units, the hot
-  // tables and the record buffers (coarse: u32 address + A value; fine: u16 slab offset + A value)
-  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
+  // R, Roff, Bb, Ib, the fine items, off2, the apply units, the dedup front end's hot tags and the
+  // record buffers (coarse: u32 address + A value; fine: u16 slab offset + A value). The [BinCtl | T]
+  // headers and the hot front end's tables live in buffers of their own (stable addresses: emptied by
+  // the kernels of the push before, not by memsets)
+  const size_t b_seg = pad256((size_t)G * g.nb * 4);
   const size_t b_nb = pad256((size_t)g.nb * 4);
   const size_t b_fit = pad256((size_t)max_fitems * 8), b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 2);
   const size_t b_units = pad256((size_t)max_units * 16) + pad256((size_t)max_units * kRunMax * 8);
   const size_t b_hot = pad256((size_t)kHotSlots * 4);
-  const size_t b_wk = front == 1 ? pad256(((size_t)4 << kWideHashBits)) : 0;
-  const size_t b_wbest = front == 1 ? pad256((size_t)kWideSlots * 8) : 0;
   const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
   const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(A)), b_e = pad256((size_t)n * 2);
-  const size_t b_zero = b_ctl + b_T;
-  const size_t need = b_zero + 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + 2 * b_wk + b_wbest + b_wpart +
-                      b_a + 2 * b_v + b_e;
+  const size_t need = 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + b_wpart + b_a + 2 * b_v + b_e;
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
+  constexpr size_t kHdr = 8192;  // one [BinCtl (256 B) | T (<= kMaxDigit u32)] header
+  static_assert(256 + 4 * kMaxDigit <= kHdr && sizeof(BinCtl) <= 256, "header slot");
+  if (!s->d_binctl) {
+    if (hipMalloc(&s->d_binctl, 2 * kHdr) != hipSuccess) {
+      (void)hipGetLastError();
+      s->d_binctl = nullptr;
+      return GLINT_ENOMEM;
+    }
+    HIPCHK(hipMemsetAsync(s->d_binctl, 0, 2 * kHdr, st));
+    s->bin_par = 0;
+  }
+  const size_t b_wk = ((size_t)4 << kWideHashBits), b_wbest = (size_t)kWideSlots * 8;
+  if (front == 1 && !s->d_hot) {  // keys empty, counts and picks zero; their readers keep them so
+    if (hipMalloc(&s->d_hot, 2 * b_wk + b_wbest) != hipSuccess) {
+      (void)hipGetLastError();
+      s->d_hot = nullptr;
+      return GLINT_ENOMEM;
+    }
+    HIPCHK(hipMemsetAsync(s->d_hot, 0xFF, b_wk, st));
+    HIPCHK(hipMemsetAsync((char*)s->d_hot + b_wk, 0, b_wk + b_wbest, st));
+  }
+  char* const hdr = (char*)s->d_binctl + (size_t)s->bin_par * kHdr;
+  char* const nhdr = (char*)s->d_binctl + (size_t)(s->bin_par ^ 1) * kHdr;
+  BinCtl* bc = (BinCtl*)hdr;
+  u32* T = (u32*)(hdr + 256);
   char* p = (char*)s->d_bin;
-  BinCtl* bc = (BinCtl*)p;
-  u32* T = (u32*)(p + b_ctl);
-  p += b_zero;
   u32* R = (u32*)p;
   u32* Roff = (u32*)(p + b_seg);
   p += 2 * b_seg;
@@ -2161,24 +2240,21 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   p += b_units;
   u32* hot_tags = (u32*)p;
   p += b_hot;
-  u32* wkey = (u32*)p;
-  u32* wcnt = (u32*)(p + b_wk);
-  unsigned long long* wbest = (unsigned long long*)(p + 2 * b_wk);
-  A* wpart = (A*)(p + 2 * b_wk + b_wbest);
-  p += 2 * b_wk + b_wbest + b_wpart;
+  u32* wkey = front == 1 ? (u32*)s->d_hot : nullptr;
+  u32* wcnt = front == 1 ? (u32*)((char*)s->d_hot + b_wk) : nullptr;
+  unsigned long long* wbest = front == 1 ? (unsigned long long*)((char*)s->d_hot + 2 * b_wk) : nullptr;
+  A* wpart = (A*)p;
+  p += b_wpart;
   u32* addr_a = (u32*)p;
   A* val_a = (A*)(p + b_a);
   A* val_b = (A*)(p + b_a + b_v);
   uint16_t* e_b = (uint16_t*)(p + b_a + 2 * b_v);
 
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
-  HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
   const int fb = from_break ? 1 : 0;
-  if (front == 1) {  // the wide hot table: sample, count, pick
+  if (front == 1) {  // the wide hot table: sample, count, pick (the table and picks start empty)
     static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");
     const u32 wide_min = (u32)wide_knob.pos_or(3);
-    HIPCHK(hipMemsetAsync(wkey, 0xFF, b_wk, st));
-    HIPCHK(hipMemsetAsync(wcnt, 0, b_wk + b_wbest, st));
     bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
                                                                 wcnt);
     HIPCHK(hipGetLastError());
@@ -2192,13 +2268,25 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
     HIPCHK(hipGetLastError());
   }
   const unsigned long long* count_hot = front == 1 ? wbest : nullptr;  // the hot records are not partitioned
-  if (a.part.kind == 0)
+  BinCtl* const nbc = (BinCtl*)nhdr;
+  u32* const nT = (u32*)(nhdr + 256);
+  if (hook) {  // a validating gated push: the count validates the tail records
+    auto kern = a.part.kind == 0 ? bin_count_kernel<MAT, 0, true> : bin_count_kernel<MAT, -1, true>;
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff, count_hot, nbc, nT,
+                              a.ctl);
+  } else if (a.part.kind == 0) {
     bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
-                                                  count_hot);
-  else
+                                                  count_hot, nbc, nT);
+  } else {
     bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
-                                                   count_hot);
+                                                   count_hot, nbc, nT);
+  }
   HIPCHK(hipGetLastError());
+  s->bin_par ^= 1;  // this push's header is [hdr]; bin_count zeroed the other one for the next push
+  if (hook) {  // the verdict (and a rejected batch's cancel) and the head's apply, before any partition
+    rc = (*hook)(bc, T, g.nb);
+    if (rc) return rc;
+  }
   if (dedup) {
     auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
@@ -2235,7 +2323,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
 }
 
 template <typename V, bool MAT>
-int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st) {
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   if (n >= ((i64)1 << 32) - 2 * kAChunk || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
@@ -2274,9 +2362,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   s->bin_last_front = front;
   // the v2 fine stage (bin_fsort / bin_plan / bin_apply2) unless GLINT_BIN_V1=1; its coarse partition
   // addresses the whole buffer through one 32-bit buffer window
-  static EnvKnob v1_knob("GLINT_BIN_V1");
-  const bool v1 = v1_knob.get([](const char* e) -> long long { return e && atoi(e) != 0; }) != 0;
-  if (!v1 && (u64)n * sizeof(A) < ((u64)1 << 32)) return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on);
+  if (hook || push_binned_fusable(s, n, sizeof(A))) return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on, hook);
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
@@ -2352,10 +2438,10 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   }
   if (a.part.kind == 0)
     bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, nullptr,
-                                                  nullptr);
+                                                  nullptr, nullptr, nullptr);
   else
     bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, nullptr,
-                                                   nullptr);
+                                                   nullptr, nullptr, nullptr);
   HIPCHK(hipGetLastError());
   if (dedup) {
     auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
@@ -2418,7 +2504,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   return GLINT_OK;
 }
 
-#define GLINT_INST(V, MAT) template int push_binned<V, MAT>(glint_shard*, const PushArgs<V>&, bool, hipStream_t);
+#define GLINT_INST(V, MAT) \
+  template int push_binned<V, MAT>(glint_shard*, const PushArgs<V>&, bool, hipStream_t, const BinHook*);
 GLINT_INST(int, false)
 GLINT_INST(int, true)
 GLINT_INST(long long, false)

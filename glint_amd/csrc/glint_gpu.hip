@@ -54,7 +54,7 @@ __device__ __forceinline__ bool rec_addr_t(const PartDesc& p, i64 key, int32_t c
 template <bool MAT, bool FULL, int KIND>
 __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const int32_t* __restrict__ cols, i64 n,
                                            const PartDesc& part, LaunchCtl* ctl, i64* __restrict__ desc,
-                                           u32 ntiles, u32 t, int lane, bool validate) {
+                                           u32 ntiles, u32 t, int lane, bool validate, bool read_all) {
   typedef typename AddrT<MAT>::T A;
   const i64 pbase = (i64)t * (kTile / 2);
   K2 k[kPPT];
@@ -80,7 +80,7 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   // tile adding to brk_enc would serialise on that one word)
   const u32 brk = __builtin_amdgcn_readfirstlane(ld_relaxed(&ctl->brk_enc));
   const bool after = brk != 0u && ntiles - brk < t;
-  if (!validate && after) return false;
+  if (!read_all && after) return false;
   A before = 0;
   if (r_first > 0) rec_addr_t<MAT, KIND>(part, kb, cb, before);
   bool mono = true, affine = true;
@@ -125,6 +125,9 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
 
 // One launch covers the wave tiles [t_begin, t_end) (a push is checked in windows of tiles, see
 // sweep_window_tiles); the first window's launch also zeroes the next push's control words.
+// validate: 0 none; 1 every record of the push (every tile is read); 2 the records of the tiles it
+// reads, which stop after the break as for an ordinary push (a binned tail is validated by its count
+// pass, bin_count_kernel<..., VALIDATE>)
 template <bool MAT, int KIND>
 __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict__ keys,
                                                           const int32_t* __restrict__ cols, i64 n,
@@ -143,8 +146,10 @@ __global__ __launch_bounds__(kTPB) void push_check_kernel(const i64* __restrict_
   const u32 nw = gridDim.x * (kTPB / 64);
   for (u32 t = t_begin + w0; t < t_end; t += nw) {
     const bool full = 2 * ((i64)t * (kTile / 2)) + kTile <= n;
-    const bool go = full ? check_tile<MAT, true, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane, validate != 0)
-                         : check_tile<MAT, false, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane, validate != 0);
+    const bool go = full ? check_tile<MAT, true, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane, validate != 0,
+                                                       validate == 1)
+                         : check_tile<MAT, false, KIND>(keys, cols, n, part, ctl, desc, ntiles, t, lane, validate != 0,
+                                                        validate == 1);
     if (!go) return;
   }
 }
@@ -719,10 +724,13 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     return GLINT_OK;
   }
   const u64 win = std::min<u64>(sweep_window_tiles(), a.ntiles);
+  const bool validate = gated && (flags & GLINT_PUSH_VALIDATE) != 0;
+  // a validating push whose tail is binned reads its keys once: push_check validates the records up to
+  // the break, the tail's count pass the rest, and the verdict comes after that count (BinHook)
+  const bool fuse = validate && binned && !det && push_binned_fusable(s, n, sizeof(typename LdsAcc<V>::T));
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
     static EnvKnob check_bpc("GLINT_CHECK_BPC");
-    const bool validate = gated && (flags & GLINT_PUSH_VALIDATE) != 0;
     if (gated && !validate) {
       push_gate_kernel<<<1, 64, 0, st>>>(s->gate, a.ctl);
       HIPCHK(hipGetLastError());
@@ -731,16 +739,16 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     const unsigned gc =
         grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu<push_check_kernel<MAT, 0>>(2, &check_bpc));
     HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
-                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? 1 : 0)
+                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? (fuse ? 2 : 1) : 0)
                             : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
-                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? 1 : 0));
-    if (validate) {
+                                       a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? (fuse ? 2 : 1) : 0));
+    if (validate && !fuse) {
       push_validate_gate_kernel<<<1, 64, 0, st>>>(a.ctl, s->gate);
       HIPCHK(hipGetLastError());
     }
     s->ctl_par ^= 1;  // only once the check that zeroes the other slot is on the stream
   }
-  {
+  auto apply_head = [&]() -> int {  // the records before the break (every record of an ordered push)
     static EnvKnob apply_bpc("GLINT_APPLY_BPC");
     const i64 bpc = blocks_per_cu<push_apply_kernel<V, MAT>>(2, &apply_bpc);
     for (u64 t0 = 0; t0 < a.ntiles; t0 += win) {
@@ -749,7 +757,17 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
       a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * sweep_blocks_per_cu()));
       HIPCHK(launch_k(s, GLINT_K_PUSH_APPLY, push_apply_kernel<V, MAT>, ga, kTPB, st, a, (const i64*)desc, (u32)t0, t1));
     }
+    return GLINT_OK;
+  };
+  if (fuse) {  // verdict, cancel and the head, behind the tail's validating count
+    const BinHook hook = [&](void* bc, u32* T, u32 nb) -> int {
+      const int rc2 = launch_validate_gate_binned(a.ctl, s->gate, bc, T, nb, st);
+      return rc2 ? rc2 : apply_head();
+    };
+    return push_binned<V, MAT>(s, a, true, st, &hook);
   }
+  rc = apply_head();
+  if (rc) return rc;
   if (det) return push_det_tail<V, MAT>(s, a, true, st);
   if (binned) return push_binned<V, MAT>(s, a, true, st);
   const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
@@ -936,6 +954,8 @@ void free_shard(glint_shard* s) {
     for (auto& e : s->det_ev)
       if (e) (void)hipEventDestroy(e);
     if (s->d_bin) (void)hipFree(s->d_bin);
+    if (s->d_binctl) (void)hipFree(s->d_binctl);
+    if (s->d_hot) (void)hipFree(s->d_hot);
     if (s->h_hint) (void)hipHostFree(s->h_hint);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->h_err) (void)hipHostFree(s->h_err);

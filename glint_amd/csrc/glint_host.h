@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <cstdlib>
 #include <memory>
 #include <mutex>
@@ -78,6 +79,13 @@ struct glint_shard {
   hipStream_t det_stream = nullptr;
   hipEvent_t det_ev[2] = {nullptr, nullptr};
   void* d_bin = nullptr;  // binned-push scratch
+  // v2 binned push: two [BinCtl | T] headers, used by alternate pushes; each push's bin_count zeroes
+  // the other one for the next push (no memset per push). Zeroed once when allocated.
+  void* d_binctl = nullptr;
+  int bin_par = 0;
+  // the hot front end's global sample table and picks, emptied by their last reader (bin_hot_select,
+  // bin_hot_reduce) for the next push instead of by memsets; initialised once when allocated
+  void* d_hot = nullptr;
   size_t bin_bytes = 0;
   // binned front end (glint_bin.hip push_binned): 0 plain, 1 plain + hot-element split, 2 chunk dedup
   // (+ hot split). What the last dedup push measured decides: chunk_ratio = records it kept of the cold
@@ -435,8 +443,16 @@ namespace glint {
 // and MAT in {false, true}
 template <typename V, bool MAT>
 int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
+// Work a caller slots into a binned push right after its count pass, given the push's [BinCtl | T]
+// header (the validating gated push: its verdict, cancel and head apply; see push_binned_v2)
+typedef std::function<int(void* bc, u32* T, u32 nb)> BinHook;
 template <typename V, bool MAT>
-int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st);
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook = nullptr);
+// whether a push of n records (LDS partial sums of asize bytes) takes the v2 binned pipeline, whose
+// count pass can validate the tail (BinHook)
+bool push_binned_fusable(const glint_shard* s, i64 n, size_t asize);
+// the verdict of a validating gated push whose tail is binned (glint_bin.hip)
+int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32 nb, hipStream_t st);
 // one-launch order-preserving push (glint_ordered.hip): n <= kOrderedMax, elems < 2^32
 template <typename V, bool MAT>
 int push_ordered(glint_shard* s, const PushArgs<V>& a, hipStream_t st);

@@ -275,13 +275,17 @@ def test_gated_push(gpu, pattern):
             assert torch.equal(state(), ref)
 
 
-@pytest.mark.parametrize("pattern", ["dense", "zipf", "small", "matrix", "sorted_bad", "empty", "wrap"])
+@pytest.mark.parametrize("pattern", ["dense", "zipf", "small", "matrix", "sorted_bad", "empty", "wrap", "zipf_wrap",
+                                     "head_bad"])
 @pytest.mark.parametrize("word", ["device", "host"])
 def test_validating_gated_push(gpu, pattern, word):
     """GLINT_PUSH_VALIDATE: the gated push checks its own records and writes the verdict -- 0, or
     ~(first out-of-range record) -- to the gate word; a batch with a bad record applies NOTHING (not
     its dense head, not its tail), as mapPartitions throws before sending (AsyncBigVector.scala:96-98);
-    a clean batch is the plain device push. Pushes after a cancelled one are unaffected."""
+    a clean batch is the plain device push. Pushes after a cancelled one are unaffected. Once the
+    pushes' unordered tails are large (zipf*, head_bad), the tail is binned and the check is split: the
+    count pass validates the tail and push_check the sorted head before it (zipf_wrap: keys 2^32 away
+    from in-range ones in the tail; head_bad: the bad key inside a 2^20-record sorted head)."""
     import torch
     d = torch.device("cuda", gpu)
     rng = np.random.default_rng(23)
@@ -308,6 +312,9 @@ def test_validating_gated_push(gpu, pattern, word):
             k = torch.from_numpy(rng.integers(0, size, 1000).astype(np.int64)).to(d)
         elif pattern == "empty":
             k = torch.empty(0, dtype=torch.int64, device=d)
+        elif pattern == "head_bad":
+            tail = np.minimum(rng.zipf(1.1, 1 << 20) - 1, size - 1)
+            k = torch.from_numpy(np.concatenate([np.arange(1 << 20), tail]).astype(np.int64)).to(d)
         else:
             k = torch.from_numpy(np.minimum(rng.zipf(1.1, 1 << 21) - 1, size - 1).astype(np.int64)).to(d)
         v = torch.from_numpy(rng.integers(-9, 9, k.numel()).astype(np.int64)).to(d)
@@ -317,8 +324,12 @@ def test_validating_gated_push(gpu, pattern, word):
         if k.numel():
             # sorted_bad: a dense increasing head, then the bad key (and a break after it)
             first = k.numel() // 2 if pattern == "sorted_bad" else min(k.numel() - 1, 123_457)
-            if pattern == "wrap":  # 2^32 away from in-range keys: (key - start).toInt aliases them
-                kb[first] = first + 2**32
+            if pattern == "head_bad":
+                first = 1000
+                kb[first] = -5  # inside the sorted head
+                kb[-1] = size + 9  # and one in the tail
+            elif pattern in ("wrap", "zipf_wrap"):  # 2^32 away from in-range keys: (key - start).toInt aliases them
+                kb[first] = int(k[first]) + 2**32
                 kb[-1] = -(2**32) + 1
             else:
                 kb[first] = size + 5

@@ -10,7 +10,8 @@
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/microbench_sparse tools/microbench_sparse.hip
 // Run:   tools/microbench_sparse   (cfg3: 2^26 records, 7.78 M distinct of 2^28; cfg4b: 2^26 / 59.2 M
-//        of 2^28; cfg5: 2^23 / 3.54 M of 2^26 -- U from the bench lines' post-run checks)
+//        of 2^28; cfg5: 2^23 / 3.54 M of 2^26 -- U from the bench lines' post-run checks; cfg4_mps8_shard:
+//        one of the eight 2^23-record shard pushes of the cfg4 key space on one GPU, 8.26 M of 2^28)
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
@@ -121,5 +122,8 @@ int main() {
   run_case("cfg3", 28, 1ll << 26, 7780619, prop.multiProcessorCount);
   run_case("cfg4b", 28, 1ll << 26, 59236000, prop.multiProcessorCount);
   run_case("cfg5", 26, 1ll << 23, 3540048, prop.multiProcessorCount);
+  // one of the 8 shard pushes of the cfg4 key space on one GPU (bench --pattern exchange
+  // --parts-per-gpu 8): 2^23 uniform records into a 2^28-element shard, U = 2^28 (1 - e^-(1/32))
+  run_case("cfg4_mps8_shard", 28, 1ll << 23, 8259000, prop.multiProcessorCount);
   return 0;
 }

@@ -38,6 +38,11 @@ SHAPES = {
     "bin_fpart": (["ld4", "ld8"], ["*st4runs", "*st8runs"]),
     "bin_apply": (["ld4", "ld8", "rmw16"], ["rmw16"]),
     "bin_hot": (["ld8"], ["st8"]),
+    # v2 fine stage: the item sort reads its item contiguously and writes it back (u16 offsets, values)
+    # as whole-wave runs; the apply gathers ~16-32-record runs per item and read-modify-writes lines
+    "bin_fsort": (["ld4", "ld8"], ["st8"]),
+    "bin_plan": (["ld4"], ["st8"]),
+    "bin_apply2": (["*ld4", "*ld8", "rmw16"], ["rmw16"]),
 }
 
 
