@@ -91,6 +91,7 @@ struct BinCtl {
   u32 fnext;   // bin_fpart's item queue: the next item to take
   u32 cold;    // valid records that were not hot (the dedup front end's input; m for the others)
   u32 nunits;  // v2: apply units written by bin_plan (each bucket takes its range with one atomic)
+  u32 disorder;  // v2, a whole-push bin (no push_check): some wave saw two adjacent records out of order
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -243,8 +244,11 @@ __device__ __forceinline__ u32 block_sum(u32 x) {
   return t;
 }
 
+// from_break: 0 the whole push; 1 from push_check's break; 2 the whole push unless its gate cancelled it
+// (a validating whole-push bin: the kernels after its verdict see an empty tail, as a cancelled break)
 __device__ __forceinline__ i64 tail_start(const LaunchCtl* lctl, u32 ntiles, int from_break, i64 n) {
   if (!from_break) return 0;
+  if (from_break == 2) return lctl->cancel ? n : 0;
   const u32 brk = lctl->brk_enc;  // written by push_check; ordered by the kernel boundary
   return brk == 0u ? n : (i64)(ntiles - brk) * kTile;
 }
@@ -312,7 +316,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
                                                           u32* __restrict__ R, BinCtl* bc, u32* __restrict__ Roff,
                                                           const unsigned long long* __restrict__ hot_best,
                                                           BinCtl* next_bc, u32* __restrict__ next_T,
-                                                          LaunchCtl* vctl = nullptr) {
+                                                          LaunchCtl* vctl = nullptr, LaunchCtl* next_ctl = nullptr) {
   constexpr int kCopies = 4;  // histogram copies (wave % 4): fewer LDS atomics on one hot bucket
   __shared__ u32 h[kCopies * kMaxDigit];
   __shared__ u32 htag[kWideSlots];
@@ -321,8 +325,17 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
   if (next_bc && blockIdx.x == 0) {  // v2: the next push's header (the previous push used it; it is done)
-    for (u32 b = tid; b < g.nb; b += kATPB) next_T[b] = 0;
+    for (u32 b = tid; b < g.nb; b += kATPB) {
+      next_T[b] = 0;
+      next_T[kMaxDigit + b] = 0;  // the fused plan's per-bucket item counters (push_binned_v2's header)
+    }
     if (tid < (int)(sizeof(BinCtl) / 4)) reinterpret_cast<u32*>(next_bc)[tid] = 0;
+    if (next_ctl && tid == 0) {  // a whole-push bin runs no push_check: the next push's control words, as it zeroes them
+      next_ctl->brk_enc = 0u;
+      next_ctl->nonaffine = 0u;
+      next_ctl->cancel = 0u;
+      next_ctl->bad = 0ull;
+    }
   }
   if (hot_best)
     for (int sl = tid; sl < kWideSlots; sl += kATPB) {
@@ -333,6 +346,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
   const i64 G = gridDim.x;
   u32 nvalid = 0;
+  bool dis = false;  // (a whole-push bin) two adjacent records of one wave out of order
   // keys (and cols) only: load_recs reads no values here. Two chunks in flight per workgroup (the
   // partition grid is one 1024-thread workgroup per CU). Every step issues its loads unconditionally
   // (chunk index clamped; a step past the end counts nothing), so the compiler can wait for one
@@ -369,6 +383,12 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
         if (in && !ok) bad.add(c0 + q * kATPB + tid);
       }
       bk[q] = ok && !(hot_best && htag[wide_slot((u32)ad)] == (u32)ad) ? bucket_of((u32)ad, g) : kEmptySlot;
+      if (next_ctl && q == 0) {  // a wave's records are consecutive: are they strictly increasing? (one
+        // record per thread per chunk is sample enough: an unordered push shows it in every wave, a sorted
+        // one nowhere; a record before this one is in the push whenever this one is)
+        const u32 a32 = ok ? (u32)ad : 0xFFFFFFFFu, prev = __shfl_up(a32, 1);
+        dis = dis || (in && (!ok || ((threadIdx.x & 63) && prev >= a32)));
+      }
     }
     load(c + kCountAhead * G, r);  // kCountAhead chunks ahead, into the registers just consumed
 #pragma unroll
@@ -400,6 +420,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   }
   const u32 tot = block_sum<kATPB>(nvalid);
   if (tid == 0 && tot) atomicAdd(&bc->tail, tot);
+  if (next_ctl && __syncthreads_or(dis) && tid == 0) atomicOr(&bc->disorder, 1u);
   if (VALIDATE && bad.count) atomicMax(&vctl->bad, ~(u64)bad.first);  // rare: one atomic per thread
 }
 
@@ -1552,87 +1573,6 @@ static_assert(kSItem <= 32768, "u16 slab offsets and the u16 staging of one item
 constexpr u32 kUnitExcl = 1u;  // apply unit descriptor {slab, runs, records, flags}: the slab's only unit
 constexpr u32 kSparseCap2 = 1024;  // bin_apply2's touched list (4 workgroups per CU fit in LDS)
 
-template <typename A>
-__global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, const BinCtl* bc,
-                                                          const u32* __restrict__ T, const u32* __restrict__ Bb,
-                                                          const u32* __restrict__ addr_in, const A* __restrict__ val_in,
-                                                          uint16_t* __restrict__ e_out, A* __restrict__ v_out,
-                                                          uint16_t* __restrict__ off2, u64* hint) {
-  constexpr u32 kStage = 65536;                      // bytes: the item's u16 offsets, then its values in rounds
-  constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
-  __shared__ u32 hist[kMaxDigit];
-  __shared__ __attribute__((aligned(16))) unsigned char stage[kStage];
-  const int tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0 && hint) {  // for the host's next binned push: how much did dedup keep?
-    __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(hint + 1, (u64)bc->cold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  const u32 it = blockIdx.x;
-  if (it >= bc->nfitems) return;  // the grid is the item count's upper bound
-  const uint2 d = fitems[it];
-  const u32 b = d.x;
-  const u32 s0 = Bb[b] + d.y * kSItem, s1 = Bb[b] + min(T[b], (d.y + 1) * kSItem);
-  const u32 nf1 = g.nf + 1;
-  uint16_t* const orow = off2 + (size_t)it * nf1;
-  for (u32 f = tid; f < g.nf; f += kSTPB) hist[f] = 0;
-  if (s1 == s0) {  // an empty bucket's one item
-    for (u32 f = tid; f < nf1; f += kSTPB) orow[f] = 0;
-    return;
-  }
-  PhaseClock ph(32);
-  u32 a[kSPer];
-  A v[kSPer];
-#pragma unroll
-  for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
-    const u32 i = s0 + q * kSTPB + tid;
-    const u32 ii = i < s1 ? i : s1 - 1;
-    a[q] = ld_in(addr_in + ii);
-    v[q] = ld_in(val_in + ii);
-    if (i >= s1) a[q] = kEmptySlot;
-  }
-  __syncthreads();
-  ph.mark(32);
-  u32 p[kSPer];
-#pragma unroll
-  for (int q = 0; q < kSPer; ++q)
-    if (a[q] != kEmptySlot) p[q] = atomicAdd(&hist[fine_of(a[q], g)], 1u);
-  __syncthreads();
-  ph.mark(33);
-  const u32 total = block_scan<kSTPB, 1>(
-      g.nf, [&](u32 f) { return hist[f]; },
-      [&](u32 f, u32 excl) {
-        hist[f] = excl;
-        orow[f] = (uint16_t)excl;
-      });
-  if (tid == 0) orow[g.nf] = (uint16_t)total;
-  ph.mark(34);
-#pragma unroll
-  for (int q = 0; q < kSPer; ++q)
-    if (a[q] != kEmptySlot) p[q] += hist[fine_of(a[q], g)];
-  // the slab offsets (and the slab's low 4 bits: bin_apply2's groups of sparse slabs), staged as u16
-  // and stored as whole-wave runs
-  uint16_t* const ste = reinterpret_cast<uint16_t*>(stage);
-#pragma unroll
-  for (int q = 0; q < kSPer; ++q)
-    if (a[q] != kEmptySlot) ste[p[q]] = (uint16_t)((a[q] & (kSlab - 1)) | ((fine_of(a[q], g) & 15u) << kSlabBits));
-  __syncthreads();
-  for (u32 x = tid; x < total; x += kSTPB) e_out[s0 + x] = ste[x];
-  __syncthreads();
-  ph.mark(35);
-  A* const stv = reinterpret_cast<A*>(stage);
-  for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
-#pragma unroll
-    for (int q = 0; q < kSPer; ++q)
-      if (a[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
-    __syncthreads();
-    const u32 r1 = min(total, r0 + kStageV);
-    for (u32 x = r0 + tid; x < r1; x += kSTPB) v_out[s0 + x] = stv[x - r0];
-    __syncthreads();
-  }
-  ph.mark(36);
-  ph.flush(5);
-}
-
 // One workgroup per bucket: every slab's runs (one per item of the bucket, from the bucket's off2 rows,
 // staged in LDS) cut into apply units of <= kUnitCap records and <= kRunMax runs (a run longer than
 // what is left of a unit is split). A unit is a descriptor {slab, runs, records, flags} and a
@@ -1645,6 +1585,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
 // with one atomic.
 constexpr int kPlanTPB = 1024;
 constexpr u32 kPlanLds = 65536;  // bytes of the bucket's off2 rows staged at once
+constexpr u32 kPlanPTab = 16640; // u32 run prefixes (items x (slabs + 1)) of the wave emit
 constexpr int kRunMax = 128;     // runs per apply unit at most
 #ifndef GLINT_UNIT_CAP
 #define GLINT_UNIT_CAP 4096
@@ -1660,29 +1601,45 @@ constexpr u32 kGroupMax = 16;        // slabs per group (the record's u16 carrie
 static_assert(kSlabBits + 4 <= 16, "a slab offset and 4 slab bits in one u16");
 constexpr u32 kUnitGroup = 2u;       // unit flag: a group of sparse slabs (hash-table path)
 static_assert(kGroupCap <= kUnitCap && kGroupMax <= 64, "a group is one unit, inside one wave's lanes");
-__global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32* __restrict__ T, const u32* __restrict__ Bb,
-                                                            const u32* __restrict__ Ib, const uint16_t* __restrict__ off2,
-                                                            BinCtl* bc, uint4* __restrict__ units, uint2* __restrict__ runs,
-                                                            int group_on) {
-  __shared__ uint16_t rows[kPlanLds / 2];
-  __shared__ u32 nunit[kMaxDigit];
-  __shared__ u32 ubase;
+struct PlanLds {
+  uint16_t rows[kPlanLds / 2];
+  u32 ptab[kPlanPTab];  // (wave emit) records of the slab (group) before each item's run
+  u32 nunit[kMaxDigit];
+  u32 utot[kMaxDigit];
+  uint8_t spanv[kMaxDigit];
+  u32 ubase;
+};
+// The plan of bucket b by one workgroup of kPlanTPB threads. SC1: the bucket's off2 rows were written by
+// other workgroups of this launch (bin_fsort's fused plan, the last item of the bucket plans it), so
+// they are read with sc1 loads, as they were stored (the hand-off of the MI355X guide's sc1 table: each
+// storing workgroup waits for its stores, then adds to the bucket's counter; the last adder reads).
+template <bool SC1>
+__device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* __restrict__ T, const u32* __restrict__ Bb,
+                                            const u32* __restrict__ Ib, const u32* off2, BinCtl* bc,
+                                            uint4* __restrict__ units, uint2* __restrict__ runs, int group_on,
+                                            PlanLds& L) {
   static_assert(kMaxDigit == kPlanTPB, "one slab per thread");
+  uint16_t* const rows = L.rows;
+  u32* const ptab = L.ptab;
+  u32* const nunit = L.nunit;
+  u32* const utot = L.utot;
+  uint8_t* const spanv = L.spanv;
+  u32& ubase = L.ubase;
   const int tid = threadIdx.x;
-  const u32 b = blockIdx.x;
   const u32 J = bucket_items(T[b], kSItem), I = Ib[b], nf1 = g.nf + 1, bb = Bb[b];
   const u32 jt = kPlanLds / 2 / nf1;  // items per staged tile (>= 31 for nf <= 1024)
   const u32 f = tid;                  // this thread's slab
   auto stage = [&](u32 j0, u32 j1) {  // rows of items [j0, j1): every load of a round in flight together
     const u32 nx = (j1 - j0) * nf1;
-    const uint16_t* src = off2 + (size_t)(I + j0) * nf1;
+    const u32* src = off2 + (size_t)(I + j0) * nf1;
     constexpr int U = 8;
     for (u32 x0 = 0; x0 < nx; x0 += kPlanTPB * U) {
       uint16_t t[U];
 #pragma unroll
       for (int q = 0; q < U; ++q) {
         const u32 x = x0 + q * kPlanTPB + tid;
-        t[q] = src[x < nx ? x : nx - 1];
+        const u32* ps = src + (x < nx ? x : nx - 1);
+        t[q] = (uint16_t)(SC1 ? __hip_atomic_load(ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *ps);
       }
 #pragma unroll
       for (int q = 0; q < U; ++q) {
@@ -1733,8 +1690,30 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
     return nu;
   };
   PhaseClock ph(48);
-  u32 h = 0;
-  const u32 nu1 = walk(false, 0, 0, 1, &h);
+  // A bucket of at most 64 items whose rows fit in LDS at once (every shape measured) is planned with
+  // its rows staged once: a thread per slab sums its runs and notes each run's prefix (ptab), so a
+  // slab's units are ceil(records / kUnitCap) (a unit never reaches kRunMax runs with <= 64 items); the
+  // units are then written by lanes of one wave per slab (2 or 4 slabs per wave for <= 32 / 16 items),
+  // a lane per item, so the run-table stores are contiguous (the per-thread walk stored one 8-byte run
+  // per lane into 64 different run tables per instruction). Larger buckets take the walk.
+  const u32 ps = g.nf + 1;  // ptab row stride: +1 so the lanes of one slab's column hit different banks
+  const bool wave_emit = J <= 64u && J <= jt && J * ps <= kPlanPTab;  // block-uniform
+  u32 h = 0, nu1 = 0;
+  if (wave_emit) {
+    stage(0, J);
+    __syncthreads();
+    if (f < g.nf) {
+      const uint16_t* r = rows + f;
+#pragma unroll 8
+      for (u32 j = 0; j < J; ++j) {
+        ptab[j * ps + f] = h;
+        h += (u32)r[j * nf1 + 1] - (u32)r[j * nf1];
+      }
+    }
+    nu1 = (h + kUnitCap - 1) / kUnitCap;
+  } else {
+    nu1 = walk(false, 0, 0, 1, &h);
+  }
   ph.mark(48);
   // sparse neighbours: the largest aligned group (lanes f..f+gs-1 of one wave) within the caps
   u32 span = 1;
@@ -1748,7 +1727,20 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
   }
   // (a group's units: at most one, exclusive; a single slab's: the cut above)
   const u32 nu = span > 1 ? 1u : span == 1 ? nu1 : 0u;  // a group (records > 0, <= kGroupCap): one unit
-  if (f < g.nf) nunit[f] = nu;
+  u32 tot_f = h;
+  if (wave_emit && span > 1 && f < g.nf) {  // a group's leader: its column over the group's slabs
+    const uint16_t* r = rows + f;
+    tot_f = 0;
+    for (u32 j = 0; j < J; ++j) {
+      ptab[j * ps + f] = tot_f;
+      tot_f += (u32)r[j * nf1 + span] - (u32)r[j * nf1];
+    }
+  }
+  if (f < g.nf) {
+    nunit[f] = nu;
+    spanv[f] = (uint8_t)span;
+    utot[f] = tot_f;
+  }
   __syncthreads();
   const u32 used = block_scan<kPlanTPB, 1>(g.nf, [&](u32 x) { return nunit[x]; },
                                            [&](u32 x, u32 excl) { nunit[x] = excl; });
@@ -1756,11 +1748,166 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
   if (tid == 0) ubase = used ? atomicAdd(&bc->nunits, used) : 0u;
   __syncthreads();
   ph.mark(50);
-  const u32 flags = span > 1 ? (kUnitExcl | kUnitGroup) : (nu == 1 ? kUnitExcl : 0u);
-  walk(true, ubase + (f < g.nf ? nunit[f] : 0u), flags, span, nullptr);
+  if (wave_emit) {
+    const u32 lane = (u32)tid & 63u;
+    const u32 spw = J <= 16u ? 4u : J <= 32u ? 2u : 1u;  // slabs per wave pass, 64 / spw lanes each
+    const u32 lpw = 64u / spw, sub = lane / lpw, j = lane % lpw;
+    const u64 gmask = lpw == 64u ? ~0ull : ((1ull << lpw) - 1ull) << (sub * lpw);
+    const u64 below = (1ull << lane) - 1ull;
+    for (u32 f0 = (u32)(tid >> 6) * spw; f0 < g.nf; f0 += (kPlanTPB / 64) * spw) {
+      const u32 ff = f0 + sub;
+      u32 sp = 0, base = 0, tot = 0;
+      if (ff < g.nf) {
+        sp = spanv[ff];
+        base = ubase + nunit[ff];
+        tot = utot[ff];
+      }
+      const bool on = sp != 0u && j < J;
+      u32 c = 0, st = 0, P = 0;
+      if (on) {  // this item's run of the slab (or of the group's slabs: fsort sorted the item by slab)
+        const uint16_t* r = rows + j * nf1 + ff;
+        const u32 o0 = r[0];
+        c = (u32)r[sp] - o0;
+        st = bb + j * kSItem + o0;
+        P = ptab[j * ps + ff];
+      }
+      const u32 nus = sp == 0u ? 0u : sp > 1u ? 1u : (tot + kUnitCap - 1) / kUnitCap;
+      const u32 fl = sp > 1u ? (kUnitExcl | kUnitGroup) : (nus == 1u ? kUnitExcl : 0u);
+      for (u32 u = 0; __ballot(u < nus); ++u) {  // unit u: records [u * cap, min(tot, (u + 1) * cap)) of the slab
+        const u32 lo = u * kUnitCap, hi = min(tot, lo + kUnitCap);
+        const bool in = on && u < nus && c > 0u && P < hi && P + c > lo;
+        const u64 m = __ballot(in) & gmask;
+        if (in) {
+          const u32 from = max(P, lo);
+          runs[(size_t)(base + u) * kRunMax + (u32)__popcll(m & below)] = make_uint2(st + (from - P), from - lo);
+        }
+        if (j == 0u && u < nus) units[base + u] = make_uint4(b * g.nf + ff, (u32)__popcll(m), hi - lo, fl);
+      }
+    }
+  } else {
+    const u32 flags = span > 1 ? (kUnitExcl | kUnitGroup) : (nu == 1 ? kUnitExcl : 0u);
+    walk(true, ubase + (f < g.nf ? nunit[f] : 0u), flags, span, nullptr);
+  }
   __syncthreads();
   ph.mark(51);
   ph.flush(4);
+}
+
+__global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32* __restrict__ T, const u32* __restrict__ Bb,
+                                                            const u32* __restrict__ Ib, const u32* __restrict__ off2,
+                                                            BinCtl* bc, uint4* __restrict__ units, uint2* __restrict__ runs,
+                                                            int group_on) {
+  __shared__ PlanLds L;
+  plan_bucket<false>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L);
+}
+
+// FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
+// (plan_bucket<true>), so no plan launch follows and the buckets' plans overlap the other items' sorts.
+constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
+template <typename A, bool FUSED>
+__global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
+                                                          const u32* __restrict__ T, const u32* __restrict__ Bb,
+                                                          const u32* __restrict__ addr_in, const A* __restrict__ val_in,
+                                                          uint16_t* __restrict__ e_out, A* __restrict__ v_out,
+                                                          u32* __restrict__ off2, u64* hint, u64* whole_hint,
+                                                          u32 whole_n, const u32* __restrict__ Ib, u32* done,
+                                                          uint4* __restrict__ units, uint2* __restrict__ runs,
+                                                          int group_on) {
+  constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
+  constexpr size_t kSortLds = 4 * kMaxDigit + kStage;
+  constexpr size_t kLds = FUSED && sizeof(PlanLds) > kSortLds ? sizeof(PlanLds) : kSortLds;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
+  __shared__ u32 last_flag;
+  u32* const hist = reinterpret_cast<u32*>(smem);
+  unsigned char* const stage = smem + 4 * kMaxDigit;
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0 && hint) {  // for the host's next binned push: how much did dedup keep?
+    __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hint + 1, (u64)bc->cold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (whole_hint) {  // a whole-push bin, in push_apply's words: an unordered push has its tail from record
+      const bool dis = bc->disorder != 0u;  // 0 on (so the next push bins whole again); an ordered one none
+      __hip_atomic_store(whole_hint, dis ? (u64)whole_n : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(whole_hint + 3, dis ? 0ull : ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const u32 it = blockIdx.x;
+  if (it >= bc->nfitems) return;  // the grid is the item count's upper bound
+  const uint2 d = fitems[it];
+  const u32 b = d.x;
+  const u32 s0 = Bb[b] + d.y * kSItem, s1 = Bb[b] + min(T[b], (d.y + 1) * kSItem);
+  const u32 nf1 = g.nf + 1;
+  u32* const orow = off2 + (size_t)it * nf1;
+  auto put_row = [&](u32 f, u32 x) {  // (fused: sc1 stores, read by the bucket's planner with sc1 loads)
+    if (FUSED) __hip_atomic_store(orow + f, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else orow[f] = x;
+  };
+  auto finish = [&]() {  // fused: count this item in; the bucket's last one plans it
+    if (!FUSED) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its stores done
+    __syncthreads();
+    if (tid == 0) last_flag = atomicAdd(&done[b], 1u) + 1u == bucket_items(T[b], kSItem);
+    __syncthreads();
+    if (last_flag) plan_bucket<true>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, *reinterpret_cast<PlanLds*>(smem));
+  };
+  for (u32 f = tid; f < g.nf; f += kSTPB) hist[f] = 0;
+  if (s1 == s0) {  // an empty bucket's one item
+    for (u32 f = tid; f < nf1; f += kSTPB) put_row(f, 0u);
+    finish();
+    return;
+  }
+  PhaseClock ph(32);
+  u32 a[kSPer];
+  A v[kSPer];
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
+    const u32 i = s0 + q * kSTPB + tid;
+    const u32 ii = i < s1 ? i : s1 - 1;
+    a[q] = ld_in(addr_in + ii);
+    v[q] = ld_in(val_in + ii);
+    if (i >= s1) a[q] = kEmptySlot;
+  }
+  __syncthreads();
+  ph.mark(32);
+  u32 p[kSPer];
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) p[q] = atomicAdd(&hist[fine_of(a[q], g)], 1u);
+  __syncthreads();
+  ph.mark(33);
+  const u32 total = block_scan<kSTPB, 1>(
+      g.nf, [&](u32 f) { return hist[f]; },
+      [&](u32 f, u32 excl) {
+        hist[f] = excl;
+        put_row(f, excl);
+      });
+  if (tid == 0) put_row(g.nf, total);
+  ph.mark(34);
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) p[q] += hist[fine_of(a[q], g)];
+  // the slab offsets (and the slab's low 4 bits: bin_apply2's groups of sparse slabs), staged as u16
+  // and stored as whole-wave runs
+  uint16_t* const ste = reinterpret_cast<uint16_t*>(stage);
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) ste[p[q]] = (uint16_t)((a[q] & (kSlab - 1)) | ((fine_of(a[q], g) & 15u) << kSlabBits));
+  __syncthreads();
+  for (u32 x = tid; x < total; x += kSTPB) e_out[s0 + x] = ste[x];
+  __syncthreads();
+  ph.mark(35);
+  A* const stv = reinterpret_cast<A*>(stage);
+  for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
+#pragma unroll
+    for (int q = 0; q < kSPer; ++q)
+      if (a[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
+    __syncthreads();
+    const u32 r1 = min(total, r0 + kStageV);
+    for (u32 x = r0 + tid; x < r1; x += kSTPB) v_out[s0 + x] = stv[x - r0];
+    __syncthreads();
+  }
+  ph.mark(36);
+  ph.flush(5);
+  finish();
 }
 
 // Per apply unit: the records of its runs (record r lives in run i = the last one whose prefix is <= r:
@@ -2168,7 +2315,7 @@ int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32
 
 template <typename V, bool MAT>
 int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, int front, bool hot_on,
-                   const BinHook* hook) {
+                   const BinHook* hook, LaunchCtl* whole_next) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   const BinGeom g = bin_geometry(s->elems);
@@ -2191,7 +2338,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   // the kernels of the push before, not by memsets)
   const size_t b_seg = pad256((size_t)G * g.nb * 4);
   const size_t b_nb = pad256((size_t)g.nb * 4);
-  const size_t b_fit = pad256((size_t)max_fitems * 8), b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 2);
+  const size_t b_fit = pad256((size_t)max_fitems * 8), b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 4);
   const size_t b_units = pad256((size_t)max_units * 16) + pad256((size_t)max_units * kRunMax * 8);
   const size_t b_hot = pad256((size_t)kHotSlots * 4);
   const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
@@ -2199,8 +2346,8 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const size_t need = 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + b_wpart + b_a + 2 * b_v + b_e;
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
-  constexpr size_t kHdr = 8192;  // one [BinCtl (256 B) | T (<= kMaxDigit u32)] header
-  static_assert(256 + 4 * kMaxDigit <= kHdr && sizeof(BinCtl) <= 256, "header slot");
+  constexpr size_t kHdr = 12288;  // one [BinCtl (256 B) | T (<= kMaxDigit u32) | done (<= kMaxDigit u32)] header
+  static_assert(256 + 8 * kMaxDigit <= kHdr && sizeof(BinCtl) <= 256, "header slot");
   if (!s->d_binctl) {
     if (hipMalloc(&s->d_binctl, 2 * kHdr) != hipSuccess) {
       (void)hipGetLastError();
@@ -2224,6 +2371,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   char* const nhdr = (char*)s->d_binctl + (size_t)(s->bin_par ^ 1) * kHdr;
   BinCtl* bc = (BinCtl*)hdr;
   u32* T = (u32*)(hdr + 256);
+  u32* done = T + kMaxDigit;  // the fused plan: items of each bucket sorted so far
   char* p = (char*)s->d_bin;
   u32* R = (u32*)p;
   u32* Roff = (u32*)(p + b_seg);
@@ -2233,7 +2381,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   p += 2 * b_nb;
   uint2* fitems = (uint2*)p;
   p += b_fit;
-  uint16_t* off2 = (uint16_t*)p;
+  u32* off2 = (u32*)p;
   p += b_off2;
   uint4* units = (uint4*)p;
   uint2* runs = (uint2*)(p + pad256((size_t)max_units * 16));
@@ -2251,7 +2399,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   uint16_t* e_b = (uint16_t*)(p + b_a + 2 * b_v);
 
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
-  const int fb = from_break ? 1 : 0;
+  const int fb = from_break ? 1 : (hook && whole_next ? 2 : 0);
   if (front == 1) {  // the wide hot table: sample, count, pick (the table and picks start empty)
     static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");
     const u32 wide_min = (u32)wide_knob.pos_or(3);
@@ -2273,13 +2421,13 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   if (hook) {  // a validating gated push: the count validates the tail records
     auto kern = a.part.kind == 0 ? bin_count_kernel<MAT, 0, true> : bin_count_kernel<MAT, -1, true>;
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff, count_hot, nbc, nT,
-                              a.ctl);
+                              a.ctl, whole_next);
   } else if (a.part.kind == 0) {
     bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
-                                                  count_hot, nbc, nT);
+                                                  count_hot, nbc, nT, nullptr, whole_next);
   } else {
     bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
-                                                   count_hot, nbc, nT);
+                                                   count_hot, nbc, nT, nullptr, whole_next);
   }
   HIPCHK(hipGetLastError());
   s->bin_par ^= 1;  // this push's header is [hdr]; bin_count zeroed the other one for the next push
@@ -2302,13 +2450,30 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
     bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
     HIPCHK(hipGetLastError());
   }
-  bin_fsort_kernel<A><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b, off2,
-                                                              s->d_hint ? s->d_hint + 1 : nullptr);
-  HIPCHK(hipGetLastError());
   static EnvKnob group_knob("GLINT_BIN_GROUP");  // 0: no groups of sparse slabs (A/B)
   const int group_on = (int)group_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; });
-  bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on);
-  HIPCHK(hipGetLastError());
+  static EnvKnob fused_knob("GLINT_BIN_FUSED_PLAN");  // 0: the plan as a launch of its own (A/B)
+  // (fused: a push of at most 4 items per CU -- cfg5's 641 -- where the plan launch and its tail are a
+  // real share of the push; with many items per CU every item's wait for its stores before counting
+  // itself in costs more: cfg3 1.067 -> 1.078, cfg4b 2.375 -> 2.44 ms, cfg5 0.347 -> 0.335,
+  // profiles/r05/ab_fused_plan.txt. GLINT_BIN_FUSED_PLAN=0 / 1 forces it off / on)
+  const long long fz = fused_knob.get([](const char* e) -> long long { return e ? atoi(e) : -1; });
+  const bool fused = fz == 1 || (fz < 0 && max_fitems <= (i64)4 * s->cus);
+  u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
+  u64* const whint = whole_next ? s->d_hint : nullptr;
+  if (fused) {
+    bin_fsort_kernel<A, true><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
+                                                                      off2, bhint, whint, (u32)n, Ib, done, units, runs,
+                                                                      group_on);
+    HIPCHK(hipGetLastError());
+  } else {
+    bin_fsort_kernel<A, false><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
+                                                                       off2, bhint, whint, (u32)n, Ib, done, units, runs,
+                                                                       group_on);
+    HIPCHK(hipGetLastError());
+    bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on);
+    HIPCHK(hipGetLastError());
+  }
   // a persistent grid of the resident workgroups: each pipelines its units two deep
   static const int apply2_occ = resident_per_cu(bin_apply2_kernel<V>, kCTPB);
   static EnvKnob apply2_knob("GLINT_BIN_APPLY2_BPC");
@@ -2323,7 +2488,8 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
 }
 
 template <typename V, bool MAT>
-int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook) {
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook,
+                LaunchCtl* whole_next) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   if (n >= ((i64)1 << 32) - 2 * kAChunk || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
@@ -2362,7 +2528,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   s->bin_last_front = front;
   // the v2 fine stage (bin_fsort / bin_plan / bin_apply2) unless GLINT_BIN_V1=1; its coarse partition
   // addresses the whole buffer through one 32-bit buffer window
-  if (hook || push_binned_fusable(s, n, sizeof(A))) return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on, hook);
+  if (hook || whole_next || push_binned_fusable(s, n, sizeof(A)))
+    return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on, hook, whole_next);
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
@@ -2505,7 +2672,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
 }
 
 #define GLINT_INST(V, MAT) \
-  template int push_binned<V, MAT>(glint_shard*, const PushArgs<V>&, bool, hipStream_t, const BinHook*);
+  template int push_binned<V, MAT>(glint_shard*, const PushArgs<V>&, bool, hipStream_t, const BinHook*, LaunchCtl*);
 GLINT_INST(int, false)
 GLINT_INST(int, true)
 GLINT_INST(long long, false)

@@ -110,8 +110,8 @@ __device__ __forceinline__ bool check_tile(const i64* __restrict__ keys, const i
   const bool any_bad = __any(!mono);  // wave-wide votes, outside any lane-divergent branch
   const bool all_affine = __all(affine);
   if (lane == 0 && !after) {
-    if (any_bad) {
-      atomicMax(&ctl->brk_enc, ntiles - t);
+    if (any_bad) {  // (an earlier break already recorded: no atomic -- every wave of an unordered push gets here)
+      if (ld_relaxed(&ctl->brk_enc) < ntiles - t) atomicMax(&ctl->brk_enc, ntiles - t);
     } else {
       desc[t] = all_affine ? (i64)a_first : kNotAffine;
       // the push is ONE affine run iff every tile is affine and continues its predecessor; only a
@@ -306,9 +306,12 @@ __global__ __launch_bounds__(kTPB) void push_apply_kernel(PushArgs<V> a, const i
                                                           u32 t_end) {
   if (a.ctl->cancel) return;  // a gated push whose gate was set applies nothing (and leaves the hint)
   const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
-  if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0 && a.hint)  // for the host's next push: how unordered was this one?
+  if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0 && a.hint) {  // for the host's next push: how unordered was this one?
     __hip_atomic_store(a.hint, brk == 0u ? 0ull : (u64)(a.n - (i64)(a.ntiles - brk) * kTile), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.hint + 3, brk == 0u ? (u64)a.n : (u64)(a.ntiles - brk) * kTile, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);  // ... and where its tail started
+  }
   if (brk == 0u && a.ctl->nonaffine == 0u) {
     const i64 delta = desc[0];  // tile 0 starts the run at record 0
     const i64 p0 = (i64)t_begin * (kTile / 2), p1 = min((i64)t_end * (kTile / 2), a.n >> 1);
@@ -349,8 +352,14 @@ constexpr u64 kEmpty = ~0ull;
 // force_all: every record (unaligned caller pointers, no push_check ran); otherwise the records
 // from the first non-increasing tile push_check found (none when the push was increasing).
 template <typename V, bool MAT>
+// force_all: 0 the records from push_check's break; 1 every record; 2 every record of a whole-push
+// scatter, which also writes the hint words as push_apply would for a push that broke in its first tile
 __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int force_all) {
   i64 r0 = 0;
+  if (force_all == 2 && blockIdx.x == 0 && threadIdx.x == 0 && a.hint) {
+    __hip_atomic_store(a.hint, (u64)a.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.hint + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (!force_all) {
     const u32 brk = a.ctl->brk_enc;  // written by push_check; ordered by the kernel boundary
     if (brk == 0u) return;
@@ -712,19 +721,46 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
                       (unordered || (n >= kBinMin && (bmode == 1 || (last_tail >= kBinMin &&
                                                                      last_tail >= bin_density() * slabs))));
   if (binned && unordered && !gated) return push_binned<V, MAT>(s, a, false, st);
+  const bool validate = gated && (flags & GLINT_PUSH_VALIDATE) != 0;
+  // Whole-push bin: when the last push (as of the last sync point) broke order in its first tile, the
+  // binned pipeline takes this one from record 0 with no push_check (the unordered push's check found
+  // only that, at one contended atomic per wave tile) and no head. Sums are the same in any order (this
+  // is not a deterministic push); bin_count validates every record of a validating push, zeroes the
+  // next push's LaunchCtl slot as push_check does, and notes whether two adjacent records were ever out
+  // of order, so an ordered push is followed by the checked path again. GLINT_BIN_WHOLE=0: always check.
+  static EnvKnob whole_knob("GLINT_BIN_WHOLE");
+  const bool whole = binned && (!gated || validate) && s->hint_tail > 0 && s->hint_head == 0 &&
+                     whole_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; }) != 0 &&
+                     push_binned_fusable(s, n, sizeof(typename LdsAcc<V>::T));
+  if (whole) {
+    LaunchCtl* const next = slots + (s->ctl_par ^ 1);
+    const BinHook hook = [&](void* bc, u32* T, u32 nb) -> int {
+      return launch_validate_gate_binned(a.ctl, s->gate, bc, T, nb, st);
+    };
+    rc = push_binned<V, MAT>(s, a, false, st, validate ? &hook : nullptr, next);
+    if (rc == GLINT_OK) s->ctl_par ^= 1;  // bin_count zeroed the other slot
+    return rc;
+  }
   // Small pushes (an Akka message is ~1000 records, GranularBigVectorSpec.scala:21) are one launch:
   // the scatter handles every record, instead of check + apply + scatter. Launch latency is the
   // whole cost at this size, so two fewer launches is the win; results are those of the scatter
   // path (bit-exact for unique keys and for Int/Long, unordered sums otherwise).
   const bool small = !det && !gated && n <= small_push_max();
-  if (!vec_ok || small) {  // unaligned caller pointers or a small push: the scatter for everything
+  // Whole-push scatter: the sparse counterpart of the whole-push bin. When the last checked push broke
+  // order in its first tile and this one stays below the binned density, the scatter takes every record
+  // from 0 with no push_check / push_apply in front (they found only that). Its hint words say so (the
+  // push's size, a tail from record 0) without looking, so every 8th such push is checked again (its
+  // push_apply writes the measured words: an ordered push returns the shard to the checked path).
+  const bool whole_scatter = !binned && !det && !gated && vec_ok && !small && s->hint_tail > 0 &&
+                             s->hint_head == 0 && (s->whole_probe++ & 7u) != 7u &&
+                             whole_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; }) != 0;
+  if (!vec_ok || small || whole_scatter) {  // unaligned caller pointers or a small push: the scatter for everything
     if (det) return push_det_tail<V, MAT>(s, a, false, st);
     const unsigned g2 = grid_for(n, kScatterChunk, (i64)s->cus * 2);
-    HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, 1));
+    HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, whole_scatter ? 2 : 1));
     return GLINT_OK;
   }
   const u64 win = std::min<u64>(sweep_window_tiles(), a.ntiles);
-  const bool validate = gated && (flags & GLINT_PUSH_VALIDATE) != 0;
   // a validating push whose tail is binned reads its keys once: push_check validates the records up to
   // the break, the tail's count pass the rest, and the verdict comes after that count (BinHook)
   const bool fuse = validate && binned && !det && push_binned_fusable(s, n, sizeof(typename LdsAcc<V>::T));
@@ -907,6 +943,7 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
     s->h_hint[0] = 0;  // unordered-tail size of the last push (push_apply)
     s->h_hint[1] = 0;  // (m << 32 | tail) of the last binned push (bin_fpart)
     s->h_hint[2] = 0;  // cold records of the last binned push (bin_fpart)
+    s->h_hint[3] = 0;  // where the last push's unordered tail started (push_apply; bin_fsort for a whole-push bin)
     if (hipHostGetDevicePointer((void**)&s->d_hint, s->h_hint, 0) != hipSuccess) s->d_hint = nullptr;
   } else {
     s->h_hint = nullptr;

@@ -164,6 +164,8 @@ struct glint_shard {
   u64 hint_tail = 0;  // h_hint[0]
   u64 hint_bin = 0;   // h_hint[1]
   u64 hint_bin_cold = 0;  // h_hint[2]
+  u64 hint_head = 0;  // h_hint[3]: where the last push's unordered tail started (records before it were ordered)
+  u32 whole_probe = 0;  // whole-push scatters so far (every 8th is checked: launch_push)
   int hint_bin_front = -1;  // the front end of the binned push that wrote hint_bin (-1: none yet)
   i64 last_bad = -1;
   // ordering of host-pointer calls (private stream) after device-resident calls (caller's stream):
@@ -396,6 +398,7 @@ inline void latch_hints(glint_shard* s) {
   s->hint_tail = __atomic_load_n(s->h_hint, __ATOMIC_ACQUIRE);
   s->hint_bin = __atomic_load_n(s->h_hint + 1, __ATOMIC_ACQUIRE);
   s->hint_bin_cold = __atomic_load_n(s->h_hint + 2, __ATOMIC_ACQUIRE);
+  s->hint_head = __atomic_load_n(s->h_hint + 3, __ATOMIC_ACQUIRE);
   s->hint_bin_front = s->bin_last_front;  // the stream has drained: the hint is the last binned push's
 }
 
@@ -447,7 +450,10 @@ int push_det_tail(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStre
 // header (the validating gated push: its verdict, cancel and head apply; see push_binned_v2)
 typedef std::function<int(void* bc, u32* T, u32 nb)> BinHook;
 template <typename V, bool MAT>
-int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook = nullptr);
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook = nullptr,
+                LaunchCtl* whole_next = nullptr);
+// whole_next: a whole-push bin (from_break false, no push_check ran): bin_count zeroes this LaunchCtl slot
+// for the next push as push_check would, and reports through the hint words whether the push was ordered.
 // whether a push of n records (LDS partial sums of asize bytes) takes the v2 binned pipeline, whose
 // count pass can validate the tail (BinHook)
 bool push_binned_fusable(const glint_shard* s, i64 n, size_t asize);

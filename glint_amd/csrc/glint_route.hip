@@ -23,6 +23,8 @@
 #include <memory>
 #include <mutex>
 #include <utility>
+#include <type_traits>
+#include <cstdlib>
 #include "../../include/glint_gpu.h"
 
 namespace {
@@ -42,18 +44,35 @@ struct RangeDesc {
   int32_t q;      // smallPartitionSize
   int32_t nparts;
   int32_t cyclic; // GLINT_ROUTE_CYCLIC
+  int32_t fastdiv;  // nkeys <= 2^52: the quotients below by a double reciprocal and one correction
+  double inv_q, inv_large, inv_p;  // 1 / smallPartitionSize, 1 / largePartitionSize, 1 / nparts
 };
+
+// floor(x / dv) for 0 <= x < 2^52 and 0 < dv < 2^31, from inv = 1.0 / dv: the estimate is within one of
+// the quotient (both roundings are relative 2^-53), and one step each way fixes it. (An i64 division
+// is a ~100-instruction sequence: per record it bound route_hist and route_scatter.)
+__device__ __forceinline__ i64 div_fast(i64 x, i64 dv, double inv) {
+  i64 o = (i64)((double)x * inv);
+  const i64 r = x - o * dv;
+  o += r < 0 ? -1 : (r >= dv ? 1 : 0);
+  return o;
+}
 
 // RangePartitioner.partition (RangePartitioner.scala:27-43) or CyclicPartitioner.partition
 // (CyclicPartitioner.scala:19-22); -1 where the reference throws
 __device__ __forceinline__ int32_t owner_of(const RangeDesc& d, i64 key) {
   if (key < 0 || key >= d.nkeys) return -1;
-  if (d.cyclic) return (int32_t)(key % d.nparts);
+  if (d.cyclic) return (int32_t)(d.fastdiv ? key - div_fast(key, d.nparts, d.inv_p) * d.nparts : key % d.nparts);
   // largePartitionSize is an Int (smallPartitionSize + 1, :18): it wraps to Int.MinValue when
   // small partitions hold 2^31-1 keys, as on the JVM. .toInt of the index; a partitioner whose Int
   // sizes overflowed yields an index outside the partition array (ArrayIndexOutOfBoundsException
   // in the reference) -> rejected like a bad key
   const i64 large = (int32_t)((uint32_t)d.q + 1u);
+  if (d.fastdiv) {  // (large > 0 here: fastdiv is off when the Int sum wrapped)
+    const int32_t o = (int32_t)(uint32_t)(u64)(key < d.small_keys ? div_fast(key, d.q, d.inv_q)
+                                                                   : (i64)d.n_small + div_fast(key - d.small_keys, large, d.inv_large));
+    return o >= 0 && o < d.nparts ? o : -1;
+  }
   const int32_t o = (int32_t)(uint32_t)(u64)(key < d.small_keys ? key / d.q : (i64)d.n_small + (key - d.small_keys) / large);
   return o >= 0 && o < d.nparts ? o : -1;
 }
@@ -79,24 +98,35 @@ __device__ __forceinline__ int32_t slot_of_key(const RangeDesc& d, const int32_t
 }
 
 // The block's chunk is `rounds` x 256 consecutive records; owners outside [0, nparts) count as bad.
+// (LDS: nparts counters, launch-sized, so small routes fit many blocks per CU; the chunk's keys are
+// loaded kMinRounds at a time, all in flight together, before any is used)
 __global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, i64 n, RangeDesc d,
                                                   const int32_t* __restrict__ slot_of, int nbits, int rounds,
                                                   u32* __restrict__ hist, i64 nblocks, u64* __restrict__ bad) {
-  __shared__ u32 h[kMaxParts];
+  extern __shared__ u32 h[];
   const int lane = threadIdx.x & 63;
   for (int p = threadIdx.x; p < d.nparts; p += kRT) h[p] = 0;
   __syncthreads();
   const i64 base = (i64)blockIdx.x * rounds * kRT;
-  for (int r = 0; r < rounds; ++r) {
-    const i64 i = base + (i64)r * kRT + threadIdx.x;
-    int32_t o = d.nparts;  // sentinel: past the end
-    if (i < n) {
-      o = slot_of_key(d, slot_of, keys[i]);
-      if (o < 0) { atomicMax(bad, ~(u64)i); o = d.nparts; }
+  for (int r0 = 0; r0 < rounds; r0 += kMinRounds) {
+    i64 k[kMinRounds];
+#pragma unroll
+    for (int r = 0; r < kMinRounds; ++r) {  // clamped, unconditional: every load in flight at once
+      const i64 i = base + (i64)(r0 + r) * kRT + threadIdx.x;
+      k[r] = keys[i < n ? i : n - 1];
     }
-    const u64 m = match_owner(o, nbits);
-    // the group's lowest lane adds the group size: one LDS atomic per distinct owner per wave
-    if (o < d.nparts && (m & ((1ull << lane) - 1)) == 0) atomicAdd(&h[o], (u32)__popcll(m));
+#pragma unroll
+    for (int r = 0; r < kMinRounds; ++r) {
+      const i64 i = base + (i64)(r0 + r) * kRT + threadIdx.x;
+      int32_t o = d.nparts;  // sentinel: past the end
+      if (r0 + r < rounds && i < n) {
+        o = slot_of_key(d, slot_of, k[r]);
+        if (o < 0) { atomicMax(bad, ~(u64)i); o = d.nparts; }
+      }
+      const u64 m = match_owner(o, nbits);
+      // the group's lowest lane adds the group size: one LDS atomic per distinct owner per wave
+      if (o < d.nparts && (m & ((1ull << lane) - 1)) == 0) atomicAdd(&h[o], (u32)__popcll(m));
+    }
   }
   __syncthreads();
   for (int p = threadIdx.x; p < d.nparts; p += kRT) hist[(i64)p * nblocks + blockIdx.x] = h[p];  // partition-major
@@ -117,7 +147,7 @@ struct RouteOut {
 __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ keys, i64 n, RangeDesc d,
                                                      const int32_t* __restrict__ slot_of, int nbits, int rounds,
                                                      const u32* __restrict__ offs, i64 nblocks, RouteOut out) {
-  __shared__ u32 cnt[kMaxParts];  // records of each owner this block has placed so far
+  extern __shared__ u32 cnt[];    // records of each owner this block has placed so far (nparts, launch-sized)
   __shared__ u32 grp_base[kRT];   // per group leader: the group's first slot within its owner
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int p = threadIdx.x; p < d.nparts; p += kRT) cnt[p] = 0;
@@ -156,6 +186,116 @@ __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ key
     }
     __syncthreads();  // grp_base is rewritten next round
   }
+}
+
+// route_scatter for nparts <= 64 (the exchange's shapes: P = world x partitions per rank): a block's
+// 4096 records (16 rounds of 256, rounds == kMinRounds) are sorted by owner in LDS, stably, and each
+// owner's run is written out contiguously -- the per-lane stores of route_scatter left one 8-64-byte
+// segment per owner per wave instruction, and its wave-ordered claims took 5 barriers per round.
+// Per (round, wave) each owner group's size goes into a table [owner][round x 4 + wave]; one exclusive
+// scan of the table in that (owner-major) order gives every group its first position in the block's
+// sorted order, so a record's position is its group's plus its rank in the group -- the order of
+// (round, wave, lane) = the caller's order. The records then go through one LDS staging buffer per
+// output (keys, values, cols, record indices).
+constexpr int kSmallParts = 64;
+constexpr int kSChunk = kMinRounds * kRT;  // 4096
+__global__ __launch_bounds__(kRT) void route_scatter_small(const i64* __restrict__ keys, i64 n, RangeDesc d,
+                                                           const int32_t* __restrict__ slot_of, int nbits,
+                                                           const u32* __restrict__ offs, i64 nblocks, RouteOut out) {
+  constexpr int R = kMinRounds, RW = R * (kRT / 64);  // (round, wave) groups per owner: 64
+  static_assert(RW == 64, "one table row of 64 per owner");
+  __shared__ u32 wc[kSmallParts * RW];
+  __shared__ __attribute__((aligned(16))) u64 stage[kSChunk];
+  __shared__ uint8_t ob[kSChunk];        // owner of each sorted position
+  __shared__ u32 goff[kSmallParts + 1];  // per owner: its first output slot minus its first sorted position
+  __shared__ u32 wt[kRT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const i64 base = (i64)blockIdx.x * kSChunk;
+  const int np = d.nparts;
+  i64 k[R];
+  u64 v[R];
+  int32_t c[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {  // every load of the chunk in flight at once (clamped, unconditional)
+    const i64 i = base + (i64)r * kRT + tid;
+    const i64 ic = i < n ? i : n - 1;
+    k[r] = keys[ic];
+    v[r] = 0;
+    c[r] = 0;
+    if (out.vals)  // (launch-uniform)
+      v[r] = out.vsize == 8 ? reinterpret_cast<const u64*>(out.in_vals)[ic] : (u64)reinterpret_cast<const u32*>(out.in_vals)[ic];
+    if (out.cols) c[r] = out.in_cols[ic];
+  }
+  for (int e = tid; e < np * RW; e += kRT) wc[e] = 0;
+  __syncthreads();
+  int32_t o[R];
+  u32 rk[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const i64 i = base + (i64)r * kRT + tid;
+    o[r] = np;  // sentinel: past the end, or a bad key (route_hist reported it)
+    if (i < n) {
+      const int32_t x = slot_of_key(d, slot_of, k[r]);
+      if (x >= 0) o[r] = x;
+    }
+    const u64 m = match_owner(o[r], nbits);
+    const u64 below = m & ((1ull << lane) - 1);
+    rk[r] = (u32)__popcll(below);
+    if (o[r] < np && below == 0) wc[o[r] * RW + r * (kRT / 64) + wid] = (u32)__popcll(m);
+  }
+  __syncthreads();
+  // exclusive scan of the np x 64 table, owner-major: 16 entries per thread
+  const int E = np * RW, per = (E + kRT - 1) / kRT, e0 = tid * per;
+  u32 sum = 0;
+  for (int j = 0; j < per; ++j) sum += e0 + j < E ? wc[e0 + j] : 0u;
+  u32 incl = sum;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const u32 y = __shfl_up(incl, dd);
+    if (lane >= dd) incl += y;
+  }
+  if (lane == 63) wt[wid] = incl;
+  __syncthreads();
+  u32 run = incl - sum;
+  for (int w = 0; w < wid; ++w) run += wt[w];
+  for (int j = 0; j < per; ++j) {
+    if (e0 + j < E) {
+      const u32 x = wc[e0 + j];
+      wc[e0 + j] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  u32 total = 0;
+  for (int w = 0; w < kRT / 64; ++w) total += wt[w];
+  if (tid < np) goff[tid] = offs[(i64)tid * nblocks + blockIdx.x] - wc[tid * RW];
+  u32 pos[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    pos[r] = o[r] < np ? wc[o[r] * RW + r * (kRT / 64) + wid] + rk[r] : 0u;
+    if (o[r] < np) ob[pos[r]] = (uint8_t)o[r];
+  }
+  __syncthreads();
+  // one output at a time: the chunk's records into their sorted positions, then each owner's run
+  // written out as it lies (consecutive threads, consecutive slots)
+  auto emit = [&](auto val, auto* dst) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (o[r] < np) stage[pos[r]] = (u64)val(r);
+    __syncthreads();
+    for (u32 x = tid; x < total; x += kRT) {
+      typedef typename std::remove_pointer<decltype(dst)>::type T;
+      dst[goff[ob[x]] + x] = (T)stage[x];
+    }
+    __syncthreads();
+  };
+  if (out.keys) emit([&](int r) { return (u64)k[r]; }, out.keys);
+  if (out.vals) {
+    if (out.vsize == 8) emit([&](int r) { return v[r]; }, reinterpret_cast<u64*>(out.vals));
+    else emit([&](int r) { return v[r]; }, reinterpret_cast<u32*>(out.vals));
+  }
+  if (out.cols) emit([&](int r) { return (u64)(u32)c[r]; }, out.cols);
+  if (out.order) emit([&](int r) { return (u64)(base + (i64)r * kRT + tid); }, out.order);
 }
 
 // ---- the (partition, block) offsets -------------------------------------------------------------
@@ -373,6 +513,13 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   d.nkeys = nkeys;
   d.nparts = nparts;
   d.cyclic = kind == GLINT_ROUTE_CYCLIC;
+  {
+    const i64 large = (int32_t)((uint32_t)d.q + 1u);
+    d.fastdiv = nkeys <= ((i64)1 << 52) && (d.cyclic || (d.q > 0 && large > 0)) ? 1 : 0;
+    d.inv_q = d.q > 0 ? 1.0 / (double)d.q : 0.0;
+    d.inv_large = large > 0 ? 1.0 / (double)large : 0.0;
+    d.inv_p = 1.0 / (double)nparts;
+  }
   // chunk per block grows with nparts so the (partition x block) histogram stays <= n/4 entries
   const int rounds = std::max<int>(kMinRounds, (4 * nparts + kRT - 1) / kRT);
   const i64 chunk = (i64)rounds * kRT;
@@ -412,13 +559,22 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   if (n == 0) {
     if (hipMemsetAsync(counts, 0, (size_t)nparts * 8, st) != hipSuccess) return GLINT_EDEVICE;
   } else {
-    route_hist<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, hist, nblocks, bad_dev);
+    route_hist<<<(unsigned)nblocks, kRT, (size_t)nparts * 4, st>>>(keys, n, d, slot_of, nbits, rounds, hist, nblocks,
+                                                                 bad_dev);
     route_row_sums<<<(unsigned)nparts, kST, 0, st>>>(hist, nblocks, tot, counts);
     // no output requested (a single partition: the batch is its own send buffer): counts and the
     // status word only
     if (out.order || out.keys || out.cols || out.vals) {
       route_row_scan<<<(unsigned)nparts, kST, 0, st>>>(hist, nblocks, tot, offs);
-      route_scatter<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, rounds, offs, nblocks, out);
+      static const bool small_off = [] {
+        const char* e = getenv("GLINT_ROUTE_SMALL");  // 0: the general scatter at every size (A/B)
+        return e && atoi(e) == 0;
+      }();
+      if (nparts <= kSmallParts && rounds == kMinRounds && !small_off)
+        route_scatter_small<<<(unsigned)nblocks, kRT, 0, st>>>(keys, n, d, slot_of, nbits, offs, nblocks, out);
+      else
+        route_scatter<<<(unsigned)nblocks, kRT, (size_t)nparts * 4, st>>>(keys, n, d, slot_of, nbits, rounds, offs,
+                                                                           nblocks, out);
     }
   }
   if (hipGetLastError() != hipSuccess) return GLINT_EDEVICE;

@@ -773,6 +773,52 @@ def test_binned_switch_density_floor(gpu, monkeypatch):
         assert binned(sh) == 1
 
 
+@pytest.mark.parametrize("whole", ["1", "0"])
+def test_whole_push_bin(gpu, monkeypatch, whole):
+    """Once a push broke order in its first tile, the next binned push takes every record from 0 with
+    no push_check (a whole-push bin); one whose records all arrive in order sends the push after it
+    back to the checked path (its ordered sweep). GLINT_BIN_WHOLE=0 checks every push. Sums exact
+    (Long) whichever path each push took."""
+    import ctypes as C
+    lib = N.load()
+    size = 1 << 22
+    part = RangePartition(0, 0, size)
+    rng = np.random.default_rng(43)
+    monkeypatch.delenv("GLINT_BINNED", raising=False)
+    monkeypatch.delenv("GLINT_BIN_DENSITY", raising=False)
+    monkeypatch.setenv("GLINT_BIN_WHOLE", whole)
+    N.reload_env()
+
+    def count(sh, k):
+        ms, cnt = C.c_double(), C.c_int64()
+        lib.glint_prof_read(sh.handle, k, C.byref(ms), C.byref(cnt))
+        return cnt.value
+    ref = np.zeros(size, np.int64)
+    # (pattern, push_check launches and binned pushes so far)
+    if whole == "1":
+        seq = (("rand", 1, 0), ("rand", 1, 1), ("rand", 1, 2), ("dense", 1, 3), ("dense", 2, 3), ("rand", 3, 3),
+               ("rand", 3, 4))
+    else:
+        seq = (("rand", 1, 0), ("rand", 2, 1), ("rand", 3, 2), ("dense", 4, 3), ("dense", 5, 3), ("rand", 6, 3),
+               ("rand", 7, 4))
+    with PartialVector(part, "long", gpu) as sh:
+        lib.glint_prof_enable(sh.handle, 1)
+        for pat, checks, bins in seq:
+            k = rng.integers(0, size, 1 << 21).astype(np.int64) if pat == "rand" else np.arange(size, dtype=np.int64)
+            v = rng.integers(-9, 9, k.size).astype(np.int64)
+            sh.update(k, v)
+            np.add.at(ref, k, v)
+            assert (count(sh, N.GLINT_K_PUSH_CHECK), count(sh, N.GLINT_K_PUSH_BINNED)) == (checks, bins), pat
+            np.testing.assert_array_equal(sh.to_numpy(), ref)
+        bad = rng.integers(0, size, 1 << 21).astype(np.int64)
+        bad[4321] = size + 3  # an out-of-range record in a whole-push bin is reported
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.update(bad, np.ones(bad.size, np.int64))
+        assert ei.value.record == 4321
+    monkeypatch.delenv("GLINT_BIN_WHOLE", raising=False)
+    N.reload_env()
+
+
 def test_adaptive_switch_decides_at_sync_points(gpu, monkeypatch):
     """The binned/scatter choice of a device-resident push comes from the previous pushes' tails as
     of the shard's last sync point, never from a word the device may or may not have written yet:
