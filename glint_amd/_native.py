@@ -48,6 +48,7 @@ SIGNATURES = {
     "glint_mat_pull_dev": (_I, [_P, _P, _P, _P, _I64, _P]),
     "glint_mat_pull_rows_dev": (_I, [_P, _P, _P, _I64, _P]),
     "glint_shard_sync": (_I, [_P, _P, C.POINTER(_I64)]),
+    "glint_shards_sync": (_I, [_P, _P, _I, C.POINTER(_I), C.POINTER(_I64)]),
     "glint_shard_data": (_I, [_P, C.POINTER(_P)]),
     "glint_shard_pitch": (_I, [_P, C.POINTER(_I64)]),
     "glint_push_wire": (_I, [_P, _P, _SZ, C.POINTER(_I32), _I]),

@@ -745,9 +745,11 @@ __global__ __launch_bounds__(256) void bin_hot_select_kernel(u32* __restrict__ g
 // group sums are added in group order -- the result is the same on every run.
 constexpr int kRedSlots = 64, kRedTPB = 1024, kRedGroups = kRedTPB / kRedSlots;
 template <typename V>
+// clear: empty the picks after reading them (v1: every push samples; v2 keeps them for the next pushes
+// and clears the table itself before it samples again)
 __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(unsigned long long* __restrict__ best, u32 G,
                                                                  const typename LdsAcc<V>::T* __restrict__ partial,
-                                                                 V* __restrict__ data) {
+                                                                 V* __restrict__ data, int clear) {
   typedef typename LdsAcc<V>::T A;
   __shared__ A gs[kRedGroups][kRedSlots];
   __shared__ u32 gany[kRedGroups][kRedSlots];
@@ -776,7 +778,7 @@ __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(unsigned long l
   if (grp != 0) return;
   const unsigned long long b = best[sl];
   if (!b) return;
-  best[sl] = 0ull;  // the picks' last reader empties them for the next push (no memset)
+  if (clear) best[sl] = 0ull;  // the picks' last reader empties them for the next push (no memset)
   A tot = hot_zero<A>();
   bool seen = false;
   for (int q = 0; q < kRedGroups; ++q) {
@@ -2315,7 +2317,7 @@ int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32
 
 template <typename V, bool MAT>
 int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, int front, bool hot_on,
-                   const BinHook* hook, LaunchCtl* whole_next) {
+                   const BinHook* hook, LaunchCtl* whole_next, bool hot_refresh) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   const BinGeom g = bin_geometry(s->elems);
@@ -2400,9 +2402,10 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
 
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   const int fb = from_break ? 1 : (hook && whole_next ? 2 : 0);
-  if (front == 1) {  // the wide hot table: sample, count, pick (the table and picks start empty)
+  if (front == 1 && hot_refresh) {  // the wide hot table: sample, count, pick (the count table starts empty)
     static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");
     const u32 wide_min = (u32)wide_knob.pos_or(3);
+    HIPCHK(hipMemsetAsync(wbest, 0, b_wbest, st));  // the picks of the pushes before (kept for reuse)
     bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
                                                                 wcnt);
     HIPCHK(hipGetLastError());
@@ -2447,11 +2450,15 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   }
   HIPCHK(hipGetLastError());
   if (front == 1) {
-    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
+    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, 0);
     HIPCHK(hipGetLastError());
   }
-  static EnvKnob group_knob("GLINT_BIN_GROUP");  // 0: no groups of sparse slabs (A/B)
-  const int group_on = (int)group_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; });
+  // Groups of sparse slabs for vector shards; a matrix shard's sparse slabs stay units of their own: its
+  // records cluster in a slab's few hot rows, and grouping cost cfg5 0.309 -> 0.337 ms while it takes
+  // cfg3 1.077 -> 1.038 (profiles/r05/ab_group_unitcap.txt). GLINT_BIN_GROUP=0 / 1 forces it.
+  static EnvKnob group_knob("GLINT_BIN_GROUP");
+  const long long gk = group_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : -1; });
+  const int group_on = gk < 0 ? (MAT ? 0 : 1) : (int)gk;
   static EnvKnob fused_knob("GLINT_BIN_FUSED_PLAN");  // 0: the plan as a launch of its own (A/B)
   // (fused: a push of at most 4 items per CU -- cfg5's 641 -- where the plan launch and its tail are a
   // real share of the push; with many items per CU every item's wait for its stores before counting
@@ -2525,11 +2532,22 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   if (forced == 2 || forced == 0) front = forced;
   else if (forced == 1) front = hot_on ? 1 : 0;
   const bool dedup = front == 2;
+  // The wide hot table (front 1) is sampled every GLINT_BIN_HOT_EVERY-th push (default 8) and kept in
+  // between: a push's hot set only decides how much work leaves the partition path (any set gives the
+  // same sums), and a Zipf-like stream keeps its hot elements from push to push. A shard coming from
+  // another front end samples at once.
+  static EnvKnob hot_every_knob("GLINT_BIN_HOT_EVERY");
+  const u32 hot_every = (u32)hot_every_knob.pos_or(8);
+  bool hot_refresh = true;
+  if (front == 1) {
+    hot_refresh = s->bin_last_front != 1 || s->hot_age == 0 || s->hot_age >= hot_every;
+    s->hot_age = hot_refresh ? 1u : s->hot_age + 1u;
+  }
   s->bin_last_front = front;
   // the v2 fine stage (bin_fsort / bin_plan / bin_apply2) unless GLINT_BIN_V1=1; its coarse partition
   // addresses the whole buffer through one 32-bit buffer window
   if (hook || whole_next || push_binned_fusable(s, n, sizeof(A)))
-    return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on, hook, whole_next);
+    return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on, hook, whole_next, hot_refresh);
   // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
   // on the same grid so that its per-workgroup counts are the partition's capacities
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
@@ -2623,7 +2641,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   }
   HIPCHK(hipGetLastError());
   if (front == 1) {
-    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
+    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, 1);
     HIPCHK(hipGetLastError());
   }
   static EnvKnob fcount_knob("GLINT_FCOUNT_BPC");

@@ -890,21 +890,6 @@ int push_mat_t(glint_shard* s, const i64* k, const int32_t* c, const void* v, i6
   return launch_push<V, true>(s, k, c, v, n, f, st);
 }
 
-// read and clear the device-resident calls' error state (caller has synchronised the stream)
-int collect_errors(glint_shard* s, hipStream_t st, int64_t* first_bad) {
-  ErrState h{};
-  HIPCHK(hipMemcpyAsync(&h, s->d_err, sizeof(h), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (h.min_bad_enc != 0) {
-    HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), st));
-    HIPCHK(hipStreamSynchronize(st));
-    s->last_bad = (i64)~h.min_bad_enc;
-    if (first_bad) *first_bad = s->last_bad;
-    return GLINT_EOUTOFRANGE;
-  }
-  return GLINT_OK;
-}
-
 int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   if (dtype < GLINT_I32 || dtype > GLINT_F64 || cols < 0) return GLINT_EINVAL;
   static EnvKnob hprof_knob("GLINT_HOST_PROF");
@@ -1199,17 +1184,72 @@ int glint_prof_reset(glint_shard_t s) {
   return GLINT_OK;
 }
 
+int glint_shards_sync(glint_shard_t* shards, void** streams, int n, int* rcs, int64_t* first_bad) {
+  if (n < 0 || (n > 0 && (!shards || !streams || !rcs))) return GLINT_EINVAL;
+  std::vector<glint_shard*> order(shards, shards + n);
+  std::sort(order.begin(), order.end());
+  if (n > 0 && (!order[0] || std::adjacent_find(order.begin(), order.end()) != order.end())) return GLINT_EINVAL;
+  struct Locks {  // every shard's lock, taken in address order, for the whole call
+    std::vector<glint_shard*>& v;
+    size_t k = 0;
+    ~Locks() {
+      for (size_t i = 0; i < k; ++i) v[i]->mu.unlock();
+    }
+  } locks{order};
+  for (; locks.k < order.size(); ++locks.k) lock_spin(order[locks.k]->mu);
+  std::vector<ErrState> local((size_t)n);
+  std::vector<ErrState*> h((size_t)n);
+  for (int i = 0; i < n; ++i) {  // the error states ride behind each stream's work
+    glint_shard* s = shards[i];
+    DeviceGuard g(s->device);
+    h[i] = s->h_err ? s->h_err : &local[i];
+    rcs[i] = hipMemcpyAsync(h[i], s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, (hipStream_t)streams[i]) ==
+                     hipSuccess ? GLINT_OK : GLINT_EDEVICE;
+  }
+  int rc = GLINT_OK;
+  for (int i = 0; i < n; ++i) {
+    glint_shard* s = shards[i];
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)streams[i];
+    if (rcs[i] == GLINT_OK && hipStreamSynchronize(st) != hipSuccess) rcs[i] = GLINT_EDEVICE;
+    if (rcs[i] == GLINT_OK) {
+      if (st == s->last_dev_stream) {
+        s->dev_dirty = false;
+        latch_hints(s);
+      }
+      if (h[i]->min_bad_enc != 0) {
+        s->last_bad = (i64)~h[i]->min_bad_enc;
+        if (first_bad) first_bad[i] = s->last_bad;
+        rcs[i] = hipMemsetAsync(s->d_err, 0, sizeof(ErrState), st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess
+                     ? GLINT_EOUTOFRANGE : GLINT_EDEVICE;
+      }
+    }
+    if (rcs[i] != GLINT_OK) (void)hipGetLastError();
+    if (rc == GLINT_OK) rc = rcs[i];
+  }
+  return rc;
+}
+
 int glint_shard_sync(glint_shard_t s, void* stream, int64_t* first_bad) {
   if (!s) return GLINT_EINVAL;
   ShardLock lk(s);
   DeviceGuard g(s->device);
   hipStream_t st = (hipStream_t)stream;
+  // the error state rides back behind the stream's work (pinned, async): one synchronisation
+  ErrState local{};
+  ErrState* h = s->h_err ? s->h_err : &local;
+  HIPCHK(hipMemcpyAsync(h, s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (st == s->last_dev_stream) {
     s->dev_dirty = false;  // everything enqueued there has completed
     latch_hints(s);        // a sync point: later pushes decide from the pushes up to here
   }
-  return collect_errors(s, st, first_bad);
+  if (h->min_bad_enc == 0) return GLINT_OK;
+  s->last_bad = (i64)~h->min_bad_enc;
+  if (first_bad) *first_bad = s->last_bad;
+  HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), st));
+  HIPCHK(hipStreamSynchronize(st));
+  return GLINT_EOUTOFRANGE;
 }
 
 // ---- device-resident ---------------------------------------------------------------------------

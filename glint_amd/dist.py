@@ -27,6 +27,7 @@ the partition it hosts, which needs no exchange.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 import threading
 from typing import Callable, List, Optional
@@ -373,14 +374,33 @@ class _Distributed:
                 ev.record(st)
                 cur.wait_event(ev)
                 done.append((sh, st))
-            for sh, st in done:
-                sh.sync(st.cuda_stream)
+            self._sync_all(done)
             return
         touched = []
         for _, sh, t, call in ops:
             call()
             touched.append((sh, t))
         self._sync(touched)
+
+    @staticmethod
+    def _sync_all(done) -> None:
+        """Each (shard, stream)'s sync, with one library call for all of them (glint_shards_sync: every
+        error-state copy enqueued before the first wait), raising as the first failing shard's sync."""
+        lib = N.load()
+        if len(done) < 2 or getattr(lib, "glint_shards_sync", None) is None:
+            for sh, st in done:
+                sh.sync(st.cuda_stream)
+            return
+        n = len(done)
+        hs = (C.c_void_p * n)(*[sh.handle for sh, _ in done])
+        ss = (C.c_void_p * n)(*[st.cuda_stream for _, st in done])
+        rcs = (C.c_int * n)()
+        bad = (C.c_int64 * n)(*([-1] * n))
+        lib.glint_shards_sync(hs, ss, n, rcs, bad)
+        for i, (sh, _) in enumerate(done):
+            if rcs[i] == N.GLINT_EOUTOFRANGE:
+                raise ArrayIndexOutOfBoundsException(f"record {bad[i]} is outside the partition", bad[i])
+            check(rcs[i], sh.handle)
 
     def _push_gated(self, keys: torch.Tensor, args: tuple, deterministic: bool) -> bool:
         """A world of one with one partition: the batch is the shard's push as it is. The key check

@@ -154,6 +154,12 @@ int glint_mat_push_dev_gated(glint_shard_t shard, const int64_t* rows, const int
  * device-resident call since the last sync saw an out-of-range record (first_bad_record = its
  * index within the call that saw it, may be NULL). Clears the device error state. */
 int glint_shard_sync(glint_shard_t shard, void* stream, int64_t* first_bad_record);
+/* glint_shard_sync for n DISTINCT shards at once, shard i's calls on streams[i] (the local pushes of one
+ * exchange step, each on a stream of its own): every error-state copy is enqueued before the first
+ * wait, so the n waits overlap. rcs[i] / first_bad[i] (may be NULL): what glint_shard_sync(shards[i],
+ * streams[i], ...) returns and reports. Returns GLINT_OK when every rcs[i] is, else the first other
+ * code (GLINT_EINVAL for a NULL or repeated shard, before anything is waited for). */
+int glint_shards_sync(glint_shard_t* shards, void** streams, int n, int* rcs, int64_t* first_bad);
 
 /* Device pointer to the shard's data (row-major, row pitch from glint_shard_pitch) for
  * stream-ordered consumers (RCCL exchange buffers, checkpoint dumps, tests). */

@@ -438,3 +438,40 @@ def test_wide_row_pull_answers_bypass_the_ring(gpu):
         t, out = sh.pull_async(q, rows=True)
         sh.wait(t)
         np.testing.assert_array_equal(out, full[q])
+
+
+def test_shards_sync_reports_each_shard(gpu):
+    """glint_shards_sync: the syncs of several shards, each on its own stream, in one call (the
+    exchange layer's local pushes): each shard's result is what its own glint_shard_sync reports --
+    the rejected record of the one bad push, nothing for the others -- the error state is cleared,
+    and a repeated shard is refused before anything is waited for."""
+    import ctypes as C
+    import torch
+    lib = N.load()
+    d = torch.device("cuda", gpu)
+    shards = [PartialVector(RangePartition(i, i * 1000, (i + 1) * 1000), "long", gpu) for i in range(3)]
+    streams = [torch.cuda.Stream(d) for _ in shards]
+    try:
+        for i, (sh, st) in enumerate(zip(shards, streams)):
+            k = torch.arange(i * 1000, (i + 1) * 1000, dtype=torch.int64, device=d)
+            if i == 1:
+                k[17] = 5  # shard 0's key: outside shard 1
+            with torch.cuda.stream(st):
+                sh.update(k, torch.ones(1000, dtype=torch.int64, device=d), sync=False)
+        n = len(shards)
+        hs = (C.c_void_p * n)(*[sh.handle for sh in shards])
+        ss = (C.c_void_p * n)(*[st.cuda_stream for st in streams])
+        rcs, bad = (C.c_int * n)(), (C.c_int64 * n)(*([-1] * n))
+        assert lib.glint_shards_sync(hs, ss, n, rcs, bad) == N.GLINT_EOUTOFRANGE
+        assert list(rcs) == [0, N.GLINT_EOUTOFRANGE, 0] and bad[1] == 17 and bad[0] == -1
+        assert lib.glint_shards_sync(hs, ss, n, rcs, bad) == 0 and list(rcs) == [0, 0, 0]  # cleared
+        want = np.ones(1000, np.int64)
+        np.testing.assert_array_equal(shards[0].to_numpy(), want)
+        np.testing.assert_array_equal(shards[2].to_numpy(), want)
+        got1 = shards[1].to_numpy()  # in-range records applied, as the reference's loop did before it threw
+        assert got1[17] == 0 and got1.sum() == 999
+        dup = (C.c_void_p * 2)(shards[0].handle, shards[0].handle)
+        assert lib.glint_shards_sync(dup, (C.c_void_p * 2)(ss[0], ss[1]), 2, (C.c_int * 2)(), None) == N.GLINT_EINVAL
+    finally:
+        for sh in shards:
+            sh.destroy()

@@ -18,6 +18,7 @@
 #   latency   tools/host_latency.py (per-call cost of the host-pointer entry points)
 #   ring      tools/ring_probe.py: pipelined message-sized wire pushes, timed and with kernel stats
 #   loopback  tools/loopback/build/glint_loopback, HBM shards vs the oracle's CPU loop (cfg1, cfg4 shapes)
+#   lbspin    cfg4b thread-per-connection pulls with GLINT_LOCK_SPIN 0 / 200 / 2000, cfg1 actor rows, CPU loop beside
 set -o pipefail
 TAG=${TAG:-r05}
 R=$(pwd)
@@ -167,6 +168,21 @@ for s in ${STAGES:-tests bench}; do
         i=$((i + 1))
       done
       cat $OUT/lba_*.log | grep '^{' > $OUT/loopback_actor.jsonl || true
+      ;;
+    lbspin)  # cfg4b pulls under the thread-per-connection harness with the shard lock tried before blocking
+             # (GLINT_LOCK_SPIN) and without, then cfg1 under the actor model; the CPU loop beside each
+      LB=tools/loopback/build/glint_loopback
+      A4="--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"
+      for r in $(seq ${ROUNDS:-2}); do
+        for sp in 0 ${SPINS:-200 2000}; do
+          step lbspin_${sp}_$r 200 env GLINT_LOCK_SPIN=$sp $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so $A4 --cpu-stats
+        done
+        step lbspin_oracle_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so $A4 --cpu-stats
+        step lbactor1_gpu_$r 200 $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so --server actor --answers direct --cpu-stats
+        step lbactor1_oracle_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so --server actor --cpu-stats
+      done
+      cat $OUT/lbspin_*.log | grep '^{' > $OUT/loopback_lockspin.jsonl || true
+      cat $OUT/lbactor1_*.log | grep '^{' > $OUT/loopback_actor_cfg1.jsonl || true
       ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
