@@ -1619,7 +1619,7 @@ template <bool SC1>
 __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* __restrict__ T, const u32* __restrict__ Bb,
                                             const u32* __restrict__ Ib, const u32* off2, BinCtl* bc,
                                             uint4* __restrict__ units, uint2* __restrict__ runs, int group_on,
-                                            PlanLds& L) {
+                                            PlanLds& L, u32 item) {
   static_assert(kMaxDigit == kPlanTPB, "one slab per thread");
   uint16_t* const rows = L.rows;
   u32* const ptab = L.ptab;
@@ -1628,7 +1628,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   uint8_t* const spanv = L.spanv;
   u32& ubase = L.ubase;
   const int tid = threadIdx.x;
-  const u32 J = bucket_items(T[b], kSItem), I = Ib[b], nf1 = g.nf + 1, bb = Bb[b];
+  const u32 J = bucket_items(T[b], item), I = Ib[b], nf1 = g.nf + 1, bb = Bb[b];
   const u32 jt = kPlanLds / 2 / nf1;  // items per staged tile (>= 31 for nf <= 1024)
   const u32 f = tid;                  // this thread's slab
   auto stage = [&](u32 j0, u32 j1) {  // rows of items [j0, j1): every load of a round in flight together
@@ -1666,7 +1666,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
         const uint16_t* r = rows + (j - j0) * nf1 + f;
         const u32 o0 = r[0];
         u32 c = (u32)r[span] - o0;
-        u32 st = bb + j * kSItem + o0;
+        u32 st = bb + j * item + o0;
         t += c;
         while (c) {
           const u32 take = min(c, kUnitCap - acc);
@@ -1770,7 +1770,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
         const uint16_t* r = rows + j * nf1 + ff;
         const u32 o0 = r[0];
         c = (u32)r[sp] - o0;
-        st = bb + j * kSItem + o0;
+        st = bb + j * item + o0;
         P = ptab[j * ps + ff];
       }
       const u32 nus = sp == 0u ? 0u : sp > 1u ? 1u : (tot + kUnitCap - 1) / kUnitCap;
@@ -1798,9 +1798,9 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
 __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32* __restrict__ T, const u32* __restrict__ Bb,
                                                             const u32* __restrict__ Ib, const u32* __restrict__ off2,
                                                             BinCtl* bc, uint4* __restrict__ units, uint2* __restrict__ runs,
-                                                            int group_on) {
+                                                            int group_on, u32 item) {
   __shared__ PlanLds L;
-  plan_bucket<false>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L);
+  plan_bucket<false>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item);
 }
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
@@ -1814,7 +1814,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
                                                           u32* __restrict__ off2, u64* hint, u64* whole_hint,
                                                           u32 whole_n, const u32* __restrict__ Ib, u32* done,
                                                           uint4* __restrict__ units, uint2* __restrict__ runs,
-                                                          int group_on) {
+                                                          int group_on, u32 item) {
   constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
   constexpr size_t kSortLds = 4 * kMaxDigit + kStage;
   constexpr size_t kLds = FUSED && sizeof(PlanLds) > kSortLds ? sizeof(PlanLds) : kSortLds;
@@ -1836,7 +1836,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
   if (it >= bc->nfitems) return;  // the grid is the item count's upper bound
   const uint2 d = fitems[it];
   const u32 b = d.x;
-  const u32 s0 = Bb[b] + d.y * kSItem, s1 = Bb[b] + min(T[b], (d.y + 1) * kSItem);
+  const u32 s0 = Bb[b] + d.y * item, s1 = Bb[b] + min(T[b], (d.y + 1) * item);
   const u32 nf1 = g.nf + 1;
   u32* const orow = off2 + (size_t)it * nf1;
   auto put_row = [&](u32 f, u32 x) {  // (fused: sc1 stores, read by the bucket's planner with sc1 loads)
@@ -1847,9 +1847,10 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
     if (!FUSED) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its stores done
     __syncthreads();
-    if (tid == 0) last_flag = atomicAdd(&done[b], 1u) + 1u == bucket_items(T[b], kSItem);
+    if (tid == 0) last_flag = atomicAdd(&done[b], 1u) + 1u == bucket_items(T[b], item);
     __syncthreads();
-    if (last_flag) plan_bucket<true>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, *reinterpret_cast<PlanLds*>(smem));
+    if (last_flag)
+      plan_bucket<true>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, *reinterpret_cast<PlanLds*>(smem), item);
   };
   for (u32 f = tid; f < g.nf; f += kSTPB) hist[f] = 0;
   if (s1 == s0) {  // an empty bucket's one item
@@ -1864,9 +1865,13 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
   for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
     const u32 i = s0 + q * kSTPB + tid;
     const u32 ii = i < s1 ? i : s1 - 1;
-    a[q] = ld_in(addr_in + ii);
-    v[q] = ld_in(val_in + ii);
-    if (i >= s1) a[q] = kEmptySlot;
+    if ((u32)q * kSTPB < item) {  // launch-uniform (an item of fewer records than the registers hold)
+      a[q] = ld_in(addr_in + ii);
+      v[q] = ld_in(val_in + ii);
+    } else {
+      v[q] = A(0);
+    }
+    if (i >= s1 || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
   }
   __syncthreads();
   ph.mark(32);
@@ -2330,7 +2335,15 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const int wpc = dedup ? kPartWgPerCuDedup : front == 1 ? std::min(plain_wpc, hot_occ) : plain_wpc;
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * wpc));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
-  const i64 max_fitems = (i64)g.nb + n / kSItem + 1;
+  // fine items: kSItem records, or (GLINT_FSORT_ITEM, a multiple of the fine sort's workgroup up to
+  // kSItem) fewer for a small push, whose items then spread over more of the chip
+  static EnvKnob item_knob("GLINT_FSORT_ITEM");
+  const bool small_push = (i64)g.nb + n / kSItem + 1 <= (i64)4 * s->cus;
+  const u32 item = small_push ? (u32)item_knob.get([](const char* e) -> long long {
+    const long long v = e ? atoll(e) : (long long)kSItem;
+    return v >= kSTPB && v <= (long long)kSItem && v % kSTPB == 0 ? v : (long long)kSItem;
+  }) : kSItem;
+  const i64 max_fitems = (i64)g.nb + n / item + 1;
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
   // floor(H / cap) + floor(runs / kRunMax) + 1 per non-empty slab
   const i64 max_units = (i64)g.nslab + n / kUnitCap + std::min<i64>(n, max_fitems * g.nf) / kRunMax + 1;
@@ -2441,12 +2454,12 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   if (dedup) {
     auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
-                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data, kSItem, Roff, Bb, Ib);
+                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data, item, Roff, Bb, Ib);
   } else {
     auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
                                  : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
-                              val_a, a.err, bc, T, fitems, wbest, wpart, kSItem, Roff, Bb, Ib);
+                              val_a, a.err, bc, T, fitems, wbest, wpart, item, Roff, Bb, Ib);
   }
   HIPCHK(hipGetLastError());
   if (front == 1) {
@@ -2465,20 +2478,20 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   // itself in costs more: cfg3 1.067 -> 1.078, cfg4b 2.375 -> 2.44 ms, cfg5 0.347 -> 0.335,
   // profiles/r05/ab_fused_plan.txt. GLINT_BIN_FUSED_PLAN=0 / 1 forces it off / on)
   const long long fz = fused_knob.get([](const char* e) -> long long { return e ? atoi(e) : -1; });
-  const bool fused = fz == 1 || (fz < 0 && max_fitems <= (i64)4 * s->cus);
+  const bool fused = fz == 1 || (fz < 0 && small_push);
   u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
   u64* const whint = whole_next ? s->d_hint : nullptr;
   if (fused) {
     bin_fsort_kernel<A, true><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
                                                                       off2, bhint, whint, (u32)n, Ib, done, units, runs,
-                                                                      group_on);
+                                                                      group_on, item);
     HIPCHK(hipGetLastError());
   } else {
     bin_fsort_kernel<A, false><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
                                                                        off2, bhint, whint, (u32)n, Ib, done, units, runs,
-                                                                       group_on);
+                                                                       group_on, item);
     HIPCHK(hipGetLastError());
-    bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on);
+    bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on, item);
     HIPCHK(hipGetLastError());
   }
   // a persistent grid of the resident workgroups: each pipelines its units two deep

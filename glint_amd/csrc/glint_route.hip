@@ -49,8 +49,9 @@ struct RangeDesc {
 };
 
 // floor(x / dv) for 0 <= x < 2^52 and 0 < dv < 2^31, from inv = 1.0 / dv: the estimate is within one of
-// the quotient (both roundings are relative 2^-53), and one step each way fixes it. (An i64 division
-// is a ~100-instruction sequence: per record it bound route_hist and route_scatter.)
+// the quotient (both roundings are relative 2^-53), and one step each way fixes it, in place of an i64
+// division's ~100-instruction sequence per record (the route kernels timed the same either way: they
+// are bound by their memory traffic, not by this).
 __device__ __forceinline__ i64 div_fast(i64 x, i64 dv, double inv) {
   i64 o = (i64)((double)x * inv);
   const i64 r = x - o * dv;
@@ -130,50 +131,6 @@ __global__ __launch_bounds__(kRT) void route_hist(const i64* __restrict__ keys, 
   }
   __syncthreads();
   for (int p = threadIdx.x; p < d.nparts; p += kRT) hist[(i64)p * nblocks + blockIdx.x] = h[p];  // partition-major
-}
-
-// route_hist for 4096-record chunks (rounds == kMinRounds) on a persistent grid: each block takes the
-// chunks blockIdx, blockIdx + grid, ... and loads the next chunk's keys before counting this one, so a
-// block always has a chunk's loads in flight (one chunk per block and launch left the chip's memory
-// pipe half empty between a block's load and its exit: 160 us for 2^26 keys, ~3.3 TB/s).
-__global__ __launch_bounds__(kRT) void route_hist_p(const i64* __restrict__ keys, i64 n, RangeDesc d,
-                                                    const int32_t* __restrict__ slot_of, int nbits,
-                                                    u32* __restrict__ hist, i64 nblocks, u64* __restrict__ bad) {
-  extern __shared__ u32 h[];
-  const int lane = threadIdx.x & 63;
-  constexpr int R = kMinRounds;
-  auto load = [&](i64 c, i64 (&k)[R]) {
-    const i64 cc = c < nblocks ? c : nblocks - 1;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {  // clamped, unconditional: every load in flight at once
-      const i64 i = cc * (R * kRT) + (i64)r * kRT + threadIdx.x;
-      k[r] = keys[i < n ? i : n - 1];
-    }
-  };
-  i64 ka[R], kb[R];
-  i64 c = blockIdx.x;
-  load(c, ka);
-  for (; c < nblocks; c += gridDim.x) {
-    for (int p = threadIdx.x; p < d.nparts; p += kRT) h[p] = 0;
-    load(c + gridDim.x, kb);  // the next chunk: in flight while this one is counted
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const i64 i = c * (R * kRT) + (i64)r * kRT + threadIdx.x;
-      int32_t o = d.nparts;  // sentinel: past the end
-      if (i < n) {
-        o = slot_of_key(d, slot_of, ka[r]);
-        if (o < 0) { atomicMax(bad, ~(u64)i); o = d.nparts; }
-      }
-      const u64 m = match_owner(o, nbits);
-      if (o < d.nparts && (m & ((1ull << lane) - 1)) == 0) atomicAdd(&h[o], (u32)__popcll(m));
-    }
-    __syncthreads();
-    for (int p = threadIdx.x; p < d.nparts; p += kRT) hist[(i64)p * nblocks + c] = h[p];  // partition-major
-#pragma unroll
-    for (int r = 0; r < R; ++r) ka[r] = kb[r];
-    __syncthreads();  // h is cleared for the next chunk
-  }
 }
 
 // Send-order outputs of the fused route (each may be null): the record indices (order) and the
@@ -603,27 +560,8 @@ int route_launch(const int64_t* keys, int64_t n, int kind, int32_t nparts, int64
   if (n == 0) {
     if (hipMemsetAsync(counts, 0, (size_t)nparts * 8, st) != hipSuccess) return GLINT_EDEVICE;
   } else {
-    static const int cus = [] {
-      int dv = 0, c = 0;
-      if (hipGetDevice(&dv) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dv) !=
-                                                  hipSuccess || c <= 0) {
-        (void)hipGetLastError();
-        c = 256;
-      }
-      return c;
-    }();
-    int bpc = 0;  // resident blocks per CU: the persistent grid
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, route_hist_p, kRT, (size_t)nparts * 4) != hipSuccess ||
-        bpc < 1) {
-      (void)hipGetLastError();
-      bpc = 1;
-    }
-    if (rounds == kMinRounds)
-      route_hist_p<<<(unsigned)std::min<i64>(nblocks, (i64)cus * bpc), kRT, (size_t)nparts * 4, st>>>(
-          keys, n, d, slot_of, nbits, hist, nblocks, bad_dev);
-    else
-      route_hist<<<(unsigned)nblocks, kRT, (size_t)nparts * 4, st>>>(keys, n, d, slot_of, nbits, rounds, hist, nblocks,
-                                                                   bad_dev);
+    route_hist<<<(unsigned)nblocks, kRT, (size_t)nparts * 4, st>>>(keys, n, d, slot_of, nbits, rounds, hist, nblocks,
+                                                                 bad_dev);
     route_row_sums<<<(unsigned)nparts, kST, 0, st>>>(hist, nblocks, tot, counts);
     // no output requested (a single partition: the batch is its own send buffer): counts and the
     // status word only

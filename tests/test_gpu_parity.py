@@ -973,6 +973,34 @@ def test_binned_fronts_matrix(gpu, monkeypatch, front):
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
+@pytest.mark.parametrize("item,fused,group", [("4096", "1", "0"), ("8192", "0", "1"), ("16384", "0", "0"),
+                                              ("16384", "1", "1")])
+def test_binned_small_push_shapes(gpu, monkeypatch, item, fused, group):
+    """A small push's fine stage in each of its shapes: fine items of 4096 / 8192 / 16384 records
+    (GLINT_FSORT_ITEM), the plan fused into the fine sort or launched on its own
+    (GLINT_BIN_FUSED_PLAN), sparse-slab groups on or off (GLINT_BIN_GROUP): Zipf rows x uniform
+    columns with hot rows (units split across a slab, flushed by atomics) and cold sparse slabs,
+    bit-exact (Long) against the oracle."""
+    monkeypatch.setenv("GLINT_FSORT_ITEM", item)
+    monkeypatch.setenv("GLINT_BIN_FUSED_PLAN", fused)
+    monkeypatch.setenv("GLINT_BIN_GROUP", group)
+    N.reload_env()
+    rng = np.random.default_rng(29)
+    rows_n, cols_n = 1 << 13, 512
+    part = RangePartition(0, 0, rows_n)
+    r = np.minimum(np.floor(np.power(float(rows_n), rng.random(1 << 21))).astype(np.int64) - 1, rows_n - 1)  # Zipf(1.0)
+    r = rng.permutation(rows_n)[r].astype(np.int64)
+    c = rng.integers(0, cols_n, r.size).astype(np.int32)
+    v = rng.integers(-1000, 1000, r.size).astype(np.int64)
+    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE["long"])
+    assert ref.update(r, c, v) == -1
+    with PartialMatrix(part, cols_n, "long", gpu) as sh:
+        for _ in range(2):
+            sh.update(r, c, v, unordered=True)
+        assert ref.update(r, c, v) == -1
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
 def test_loopback_harness_gpu_backend(gpu):
     """configs[0] over loopback TCP with HBM shards fed the raw wire images (glint_push_wire /
     glint_pull_wire): pulled values equal the pushed ones bit for bit."""

@@ -92,10 +92,13 @@ def main():
     cal, cal_src = calibration()
     kernels = {}
     total = 0.0
-    # pushes profiled: push_check runs once per push (the apply may run once per window of records,
-    # so a kernel's bytes per push = its mean per dispatch x dispatches / pushes)
-    checks = [c for k, c in nf.items() if k.startswith("glint::push_check_kernel")]
-    pushes = max(checks) if checks else max(list(nf.values()) + [1])
+    # pushes profiled: the most dispatched of the kernels that run once per push -- push_check (the
+    # checked path), bin_count (every binned push; whole-push bins run no check) and push_scatter (a
+    # whole-push scatter runs alone) -- (the apply may run once per window of records, so a kernel's
+    # bytes per push = its mean per dispatch x dispatches / pushes)
+    once = [c for k, c in nf.items()
+            if k.startswith(("glint::push_check_kernel", "glint::bin_count_kernel", "glint::push_scatter_kernel"))]
+    pushes = max(once) if once else max(list(nf.values()) + [1])
     for name in sorted(set(fetch) | set(write)):
         per = nf.get(name, 0) / pushes
         rfac, wfac, shapes, note = kernel_factor(name, cal)
