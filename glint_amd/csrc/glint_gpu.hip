@@ -1196,7 +1196,7 @@ int glint_shards_sync(glint_shard_t* shards, void** streams, int n, int* rcs, in
       for (size_t i = 0; i < k; ++i) v[i]->mu.unlock();
     }
   } locks{order};
-  for (; locks.k < order.size(); ++locks.k) lock_spin(order[locks.k]->mu);
+  for (; locks.k < order.size(); ++locks.k) order[locks.k]->mu.lock();
   std::vector<ErrState> local((size_t)n);
   std::vector<ErrState*> h((size_t)n);
   for (int i = 0; i < n; ++i) {  // the error states ride behind each stream's work

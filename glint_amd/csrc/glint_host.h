@@ -10,7 +10,6 @@
 #include <atomic>
 #include <chrono>
 #include <functional>
-#include <sched.h>
 #include <cstdlib>
 #include <memory>
 #include <mutex>
@@ -228,30 +227,16 @@ inline u64 host_ns() {
 
 // The shard's lock (one message at a time per shard, as the actor); with GLINT_HOST_PROF it also
 // accounts the time spent waiting for it and holding it.
-// GLINT_LOCK_SPIN=N: try the shard's lock up to N times (pausing, yielding every 64th) before blocking
-// on it. Many connection threads per shard (the loopback harness's thread-per-connection servers)
-// convoy on a blocking lock: every hand-off wakes a descheduled thread. 0 (default): block at once.
-inline void lock_spin(std::mutex& mu) {
-  static EnvKnob k("GLINT_LOCK_SPIN");
-  const long long spin = k.get([](const char* e) -> long long { return e ? std::max(0ll, atoll(e)) : 0ll; });
-  for (long long i = 0; i < spin; ++i) {
-    if (mu.try_lock()) return;
-    if ((i & 63) == 63) sched_yield();
-    else __builtin_ia32_pause();
-  }
-  mu.lock();
-}
-
 struct ShardLock {
   glint_shard* s;
   u64 t1 = 0;
   explicit ShardLock(glint_shard* s_) : s(s_) {
     if (!s->hprof) {
-      lock_spin(s->mu);
+      s->mu.lock();
       return;
     }
     const u64 t0 = host_ns();
-    lock_spin(s->mu);
+    s->mu.lock();
     t1 = host_ns();
     s->hp.lock_wait.fetch_add(t1 - t0, std::memory_order_relaxed);
     s->hp.nlock.fetch_add(1, std::memory_order_relaxed);

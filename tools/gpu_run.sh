@@ -18,7 +18,8 @@
 #   latency   tools/host_latency.py (per-call cost of the host-pointer entry points)
 #   ring      tools/ring_probe.py: pipelined message-sized wire pushes, timed and with kernel stats
 #   loopback  tools/loopback/build/glint_loopback, HBM shards vs the oracle's CPU loop (cfg1, cfg4 shapes)
-#   lbspin    cfg4b thread-per-connection pulls with GLINT_LOCK_SPIN 0 / 200 / 2000, cfg1 actor rows, CPU loop beside
+#   lbspin    cfg4b thread-per-connection pulls with GLINT_LOCK_SPIN 0 / 200 / 2000 (a round-5 build knob,
+#             removed after this A/B), cfg1 actor rows, CPU loop beside
 set -o pipefail
 TAG=${TAG:-r05}
 R=$(pwd)
