@@ -92,8 +92,6 @@ struct BinCtl {
   u32 cold;    // valid records that were not hot (the dedup front end's input; m for the others)
   u32 nunits;  // v2: apply units written by bin_plan (each bucket takes its range with one atomic)
   u32 disorder;  // v2, a whole-push bin (no push_check): some wave saw two adjacent records out of order
-  u32 nchunks3;  // v3: partition chunks of the tail (bin_part3's workgroup 0)
-  u32 scan3_done;  // v3: bin_scan3's finished workgroups (the last one lays out the items)
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -911,246 +909,6 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
     for (int sl = tid; sl < kWideSlots; sl += kATPB) hot_partial[(size_t)w * kWideSlots + sl] = hacc[sl];
   }
   ph.flush(8);
-}
-
-// ---- v3: the partition with no count pass ----------------------------------------------------------
-// bin_part3 writes each 8192-record chunk in place -- records [c * kAChunk, c * kAChunk + valid) of the
-// partition buffer, sorted by bucket in LDS, every store a whole-chunk run -- and its per-bucket count
-// and offset inside the chunk (bucket-major tables cnt3 / off3). bin_scan3 turns a bucket's counts into
-// its record prefix over the chunks (P) and total (T), and notes the chunk holding each fine item's
-// first record; the last of its workgroups lays out the items (fitems, Bb, Ib) as bin_part's
-// workgroup 0 does in v2. A fine item is then the same 16 384 consecutive records of its bucket as in
-// v2 -- only gathered from the chunks' runs (bin_fsort<..., GATHER>) instead of one contiguous range --
-// so bin_plan and bin_apply2 do not change. What goes is bin_count's pass over the keys.
-template <typename A, int P>
-__device__ __forceinline__ u32 part_emit3(const u32 (&ad)[P], const A (&va)[P], u32 valid, const BinGeom& g, u32* dcnt,
-                                          u32* st_a, A* st_v, const BufOut& oa, const BufOut& ov, u32 cbase,
-                                          u32* __restrict__ cnt3, u32* __restrict__ off3, u32 c, u32 nchm,
-                                          PhaseClock& ph, int pb) {
-  const int tid = threadIdx.x;
-  u32 rank[P];
-#pragma unroll
-  for (int j = 0; j < P; ++j)
-    if (valid & (1u << j)) rank[j] = atomicAdd(&dcnt[bucket_of(ad[j], g)], 1u);
-  __syncthreads();
-  ph.mark(pb);
-  const u32 total = block_scan<kATPB, 1>(
-      g.nb, [&](u32 d) { return dcnt[d]; },
-      [&](u32 d, u32 excl) {
-        cnt3[(size_t)d * nchm + c] = dcnt[d];  // bucket-major: bin_scan3 and the gathers read a bucket's row
-        off3[(size_t)d * nchm + c] = excl;
-        dcnt[d] = excl;
-      });
-  ph.mark(pb + 1);
-#pragma unroll
-  for (int j = 0; j < P; ++j) {
-    if (valid & (1u << j)) {
-      const u32 p = dcnt[bucket_of(ad[j], g)] + rank[j];
-      st_a[p] = ad[j];
-      st_v[p] = va[j];
-    }
-  }
-  __syncthreads();
-  ph.mark(pb + 2);
-#pragma unroll
-  for (int j = 0; j < P; ++j) {  // the chunk's sorted records, one contiguous run
-    if ((u32)(j * kATPB) >= total) break;  // workgroup-uniform
-    const u32 p = tid + j * kATPB;
-    const bool on = p < total;
-    bput(oa, (cbase + p) * 4u, on, st_a[p]);
-    bput(ov, (cbase + p) * (u32)sizeof(A), on, st_v[p]);
-  }
-  __syncthreads();
-  ph.mark(pb + 3);
-  for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
-  __syncthreads();
-  ph.mark(pb + 4);
-  return total;
-}
-
-// The plain (HOT: plain + hot split) front end of v3. Also does what bin_count did besides counting:
-// the next push's [BinCtl | T | done] header zeroed (block 0), and for a whole-push bin the next
-// LaunchCtl slot and the sampled order check.
-template <typename V, bool MAT, bool HOT, int KIND>
-__global__ __launch_bounds__(kATPB) void bin_part3_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
-                                                          const V* __restrict__ vals, i64 n, PartDesc part,
-                                                          const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
-                                                          u32* __restrict__ addr_out,
-                                                          typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
-                                                          BinCtl* bc, const unsigned long long* __restrict__ hot_best,
-                                                          typename LdsAcc<V>::T* __restrict__ hot_partial,
-                                                          u32* __restrict__ cnt3, u32* __restrict__ off3, u32 nchm,
-                                                          BinCtl* next_bc, u32* __restrict__ next_T, LaunchCtl* next_ctl) {
-  typedef typename LdsAcc<V>::T A;
-  __shared__ u32 dcnt[kMaxDigit];
-  __shared__ u32 st_a[kAChunk];
-  __shared__ A st_v[kAChunk];
-  constexpr int kHS = HOT ? kWideSlots : 1;
-  __shared__ u32 htag[kHS];
-  __shared__ A hacc[kHS];
-  const int tid = threadIdx.x;
-  const u32 w = blockIdx.x;
-  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
-  const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
-  if (w == 0) {
-    for (u32 b = tid; b < g.nb; b += kATPB) {
-      next_T[b] = 0;
-      next_T[kMaxDigit + b] = 0;
-    }
-    if (tid < (int)(sizeof(BinCtl) / 4)) reinterpret_cast<u32*>(next_bc)[tid] = 0;
-    if (next_ctl && tid == 0) {
-      next_ctl->brk_enc = 0u;
-      next_ctl->nonaffine = 0u;
-      next_ctl->cancel = 0u;
-      next_ctl->bad = 0ull;
-    }
-    if (tid == 0) bc->nchunks3 = (u32)max<i64>(0, nchunks);
-  }
-  if constexpr (HOT) {
-    for (int sl = tid; sl < kWideSlots; sl += kATPB) {
-      const unsigned long long b = hot_best[sl];
-      htag[sl] = b ? (u32)b : kEmptySlot;
-      hacc[sl] = hot_zero<A>();
-    }
-  }
-  for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
-  __syncthreads();
-  PhaseClock ph(0);
-  const i64 G = gridDim.x;
-  const BufOut oa = buf_out(addr_out, (u32)(nchm * kAChunk) * 4u), ov = buf_out(val_out, (u32)(nchm * kAChunk) * (u32)sizeof(A));
-  BadRecs bad;
-  u32 emitted = 0, nvalid = 0;
-  bool dis = false;
-  auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
-    const i64 cc = min(c, nchunks - 1);
-    const i64 c0 = r0 + cc * kAChunk, c1 = min(n, r0 + (cc + 1) * kAChunk);
-    if constexpr (KIND == 0) {
-#pragma unroll
-      for (int q = 0; q < kAPer; ++q) {
-        const i64 i = c0 + q * kATPB + threadIdx.x;
-        const i64 ii = i < c1 ? i : c1 - 1;
-        r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
-        r.cl[q] = MAT ? ld_in(cols + ii) : 0;
-        r.v[q] = ld_in(vals + ii);
-      }
-    } else {
-      load_recs<V, MAT>(keys, cols, vals, c0, c1, r);
-    }
-  };
-  auto step = [&](i64 c, RecRegs<V, MAT>& r) {
-    const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
-    u32 ad[kAPer];
-    A va[kAPer];
-    u32 valid = 0;
-#pragma unroll
-    for (int q = 0; q < kAPer; ++q) {
-      const i64 i = c0 + q * kATPB + tid;
-      i64 a64;
-      ad[q] = 0;
-      va[q] = (A)r.v[q];
-      const bool in = i < c1;
-      bool ok = false;
-      if (in) {
-        if (rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64)) {
-          ad[q] = (u32)a64;
-          valid |= 1u << q;
-          ok = true;
-        } else {
-          bad.add(i);
-        }
-      }
-      if (next_ctl && q == 0) {  // the whole-push bin's sampled order check (as bin_count's)
-        const u32 a32 = ok ? ad[q] : 0xFFFFFFFFu, prev = __shfl_up(a32, 1);
-        dis = dis || (in && (!ok || ((threadIdx.x & 63) && prev >= a32)));
-      }
-    }
-    nvalid += (u32)__popc(valid);
-    if constexpr (HOT) {
-#pragma unroll
-      for (int q = 0; q < kAPer; ++q) {
-        const u32 hs = wide_slot(ad[q]);
-        if ((valid & (1u << q)) && htag[hs] == ad[q]) {
-          lds_add(&hacc[hs], va[q]);
-          valid &= ~(1u << q);
-        }
-      }
-    }
-    ph.mark(1);
-    if (c < nchunks)
-      emitted += part_emit3<A, kAPer>(ad, va, valid, g, dcnt, st_a, st_v, oa, ov, (u32)(c * kAChunk), cnt3, off3,
-                                      (u32)c, nchm, ph, 3);
-    load_chunk(c + 2 * G, r);
-    ph.mark(2);
-  };
-  RecRegs<V, MAT> ra, rb;
-  i64 c = w;
-  if (c < nchunks) {
-    load_chunk(c, ra);
-    load_chunk(c + G, rb);
-    for (; c < nchunks; c += 2 * G) {
-      step(c, ra);
-      if (c + G < nchunks) step(c + G, rb);  // (workgroup-uniform)
-    }
-  }
-  const u32 tot = block_sum<kATPB>(nvalid);
-  if (tid == 0) {
-    if (tot) atomicAdd(&bc->tail, tot);
-    if (emitted) {
-      atomicAdd(&bc->m, emitted);
-      atomicAdd(&bc->cold, emitted);
-    }
-  }
-  if (next_ctl && __syncthreads_or(dis) && tid == 0) atomicOr(&bc->disorder, 1u);
-  bad.report(err);
-  if constexpr (HOT) {
-    __syncthreads();
-    for (int sl = tid; sl < kWideSlots; sl += kATPB) hot_partial[(size_t)w * kWideSlots + sl] = hacc[sl];
-  }
-  ph.flush(8);
-}
-
-// Per bucket (one workgroup each): P[b][c] = the bucket's records in chunks before c, T[b] = its total,
-// itc[b][k] = the chunk holding its record k * item (a chunk holds at most 8192 < item of one bucket,
-// so at most one such k per chunk). The last workgroup to finish (sc1 stores of T and a counter, the
-// guide's hand-off) lays out the fine items, as bin_part's workgroup 0 does for v2.
-__global__ __launch_bounds__(kATPB) void bin_scan3_kernel(BinGeom g, const u32* __restrict__ cnt3, u32 nchm,
-                                                          u32* __restrict__ P, u32* __restrict__ itc, u32 kmax, u32 item,
-                                                          BinCtl* bc, u32* T, uint2* __restrict__ fitems,
-                                                          u32* __restrict__ Bb, u32* __restrict__ Ib) {
-  __shared__ u32 last;
-  const u32 b = blockIdx.x, nch = bc->nchunks3;
-  const u32* row = cnt3 + (size_t)b * nchm;
-  u32* prow = P + (size_t)b * (nchm + 1);
-  u32* irow = itc + (size_t)b * kmax;
-  const u32 total = block_scan<kATPB, 4>(nch, [&](u32 c) { return row[c]; },
-                                         [&](u32 c, u32 excl) {
-                                           prow[c] = excl;
-                                           const u32 v = row[c];
-                                           const u32 k = (excl + item - 1) / item;  // the first multiple >= excl
-                                           if (v && k * item < excl + v) irow[k] = c;
-                                         });
-  if (threadIdx.x == 0) {
-    prow[nch] = total;
-    __hip_atomic_store(T + b, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&bc->scan3_done, 1u) + 1u == gridDim.x;
-  __syncthreads();
-  if (!last) return;
-  // the items: bucket b gets bucket_items(T[b]) of them ({b, j}), Ib[b] its first, Bb[b] its first record
-  __shared__ u32 tl[kMaxDigit];
-  for (u32 x = threadIdx.x; x < g.nb; x += kATPB) tl[x] = __hip_atomic_load(T + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  block_scan<kATPB, 1>(g.nb, [&](u32 x) { return tl[x]; }, [&](u32 x, u32 excl) { Bb[x] = excl; });
-  const u32 nit = block_scan<kATPB, 1>(
-      g.nb, [&](u32 x) { return bucket_items(tl[x], item); },
-      [&](u32 x, u32 excl) {
-        const u32 J = bucket_items(tl[x], item);
-        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(x, j);
-        Ib[x] = excl;
-      });
-  if (threadIdx.x == 0) bc->nfitems = nit;
 }
 
 // Dedup front end for duplicate-heavy tails: per chunk, equal elements are summed in an LDS hash
@@ -2048,12 +1806,7 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
 // (plan_bucket<true>), so no plan launch follows and the buckets' plans overlap the other items' sorts.
 constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
-// GATHER (v3): the item's records are gathered from the partition chunks' runs of its bucket (bin_part3:
-// chunk c holds them at c * kAChunk + off3[b][c], P[b][c] of the bucket's records before it): each
-// record finds its run by a fixed-step binary search over the item's runs, staged in LDS (or, for an
-// item spread over more than kGatherRuns chunks, over the bucket's prefix row itself).
-constexpr u32 kGatherRuns = 4095;
-template <typename A, bool FUSED, bool GATHER = false>
+template <typename A, bool FUSED>
 __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
                                                           const u32* __restrict__ T, const u32* __restrict__ Bb,
                                                           const u32* __restrict__ addr_in, const A* __restrict__ val_in,
@@ -2061,10 +1814,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
                                                           u32* __restrict__ off2, u64* hint, u64* whole_hint,
                                                           u32 whole_n, const u32* __restrict__ Ib, u32* done,
                                                           uint4* __restrict__ units, uint2* __restrict__ runs,
-                                                          int group_on, u32 item, const u32* __restrict__ P3 = nullptr,
-                                                          const u32* __restrict__ off3 = nullptr,
-                                                          const u32* __restrict__ itc = nullptr, u32 nchm = 0,
-                                                          u32 kmax = 0) {
+                                                          int group_on, u32 item) {
   constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
   constexpr size_t kSortLds = 4 * kMaxDigit + kStage;
   constexpr size_t kLds = FUSED && sizeof(PlanLds) > kSortLds ? sizeof(PlanLds) : kSortLds;
@@ -2111,98 +1861,17 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
   PhaseClock ph(32);
   u32 a[kSPer];
   A v[kSPer];
-  if constexpr (GATHER) {
-    const u32 nch = bc->nchunks3, J = bucket_items(T[b], item);
-    const u32* prow = P3 + (size_t)b * (nchm + 1);
-    const u32* orow3 = off3 + (size_t)b * nchm;
-    const u32 clo = itc[(size_t)b * kmax + d.y];
-    const u32 chi = d.y + 1 < J ? itc[(size_t)b * kmax + d.y + 1] : nch - 1;
-    const u32 nr = chi - clo + 1;
-    const u32 r0 = d.y * item, cnt = s1 - s0;  // the item's first record within its bucket, its records
-    // LDS (the stage buffer): the runs' record prefixes and sources, and the run of every item position
-    // (a marker at each non-empty run's first position, then a prefix maximum)
-    u32* const rpre = reinterpret_cast<u32*>(stage);
-    u32* const rbase = rpre + (kGatherRuns + 1);
-    uint16_t* const run_of = reinterpret_cast<uint16_t*>(rbase + kGatherRuns + 1);
-    static_assert((2 * (kGatherRuns + 1)) * 4 + kSItem * 2 <= kStage, "the gather tables fit the stage buffer");
-    const bool lds = nr <= kGatherRuns;  // block-uniform
-    if (lds) {
-      for (u32 x = tid; x <= nr; x += kSTPB) {
-        const u32 c = clo + x;
-        rpre[x] = prow[c];  // (x == nr: the prefix after the item's last run)
-        if (x < nr) rbase[x] = c * (u32)kAChunk + orow3[c];
-      }
-      for (u32 x = tid; x < kSItem / 2; x += kSTPB) reinterpret_cast<u32*>(run_of)[x] = 0u;
-      __syncthreads();
-      for (u32 x = tid; x < nr; x += kSTPB) {  // distinct starts: only non-empty runs mark
-        const u32 lo = max(rpre[x], r0) - r0, hi = min(rpre[x + 1] - r0, cnt);
-        if (rpre[x + 1] > r0 && hi > lo) run_of[lo] = (uint16_t)x;
-      }
-      __syncthreads();
-      // prefix maximum over the item's positions: 16 consecutive per thread, then across the workgroup
-      constexpr int kPos = (int)kSItem / kSTPB;
-      __shared__ u32 wmax[kSTPB / 64];
-      u32 m = 0, loc[kPos];
 #pragma unroll
-      for (int i = 0; i < kPos; ++i) {
-        m = max(m, (u32)run_of[tid * kPos + i]);
-        loc[i] = m;
-      }
-      u32 incl = m;
-#pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        const u32 y = __shfl_up(incl, dd);
-        if ((tid & 63) >= dd) incl = max(incl, y);
-      }
-      if ((tid & 63) == 63) wmax[tid >> 6] = incl;
-      __syncthreads();
-      u32 carry = __shfl_up(incl, 1);
-      if ((tid & 63) == 0) carry = 0;
-      for (int w = 0; w < (tid >> 6); ++w) carry = max(carry, wmax[w]);
-#pragma unroll
-      for (int i = 0; i < kPos; ++i) run_of[tid * kPos + i] = (uint16_t)max(carry, loc[i]);
-      __syncthreads();
+  for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
+    const u32 i = s0 + q * kSTPB + tid;
+    const u32 ii = i < s1 ? i : s1 - 1;
+    if ((u32)q * kSTPB < item) {  // launch-uniform (an item of fewer records than the registers hold)
+      a[q] = ld_in(addr_in + ii);
+      v[q] = ld_in(val_in + ii);
+    } else {
+      v[q] = A(0);
     }
-    u32 span = 1;
-    while (span < nr) span <<= 1;
-#pragma unroll
-    for (int q = 0; q < kSPer; ++q) {
-      const u32 i = s0 + q * kSTPB + tid;
-      const u32 pos = min(i, s1 - 1) - s0;  // clamped, branch-free
-      const u32 R = r0 + pos;
-      u32 src;
-      if (lds) {
-        const u32 x = run_of[pos];
-        src = rbase[x] + (R - rpre[x]);
-      } else {  // an item spread over more chunks than the tables hold: search the bucket's prefix row
-        u32 x = 0;
-        for (u32 st = span >> 1; st > 0; st >>= 1) {
-          const u32 m2 = x + st;
-          if (m2 < nr && prow[clo + m2] <= R) x = m2;
-        }
-        src = (clo + x) * (u32)kAChunk + orow3[clo + x] + (R - prow[clo + x]);
-      }
-      if ((u32)q * kSTPB < item) {  // launch-uniform
-        a[q] = ld_in(addr_in + src);
-        v[q] = ld_in(val_in + src);
-      } else {
-        v[q] = A(0);
-      }
-      if (i >= s1 || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
-      const u32 i = s0 + q * kSTPB + tid;
-      const u32 ii = i < s1 ? i : s1 - 1;
-      if ((u32)q * kSTPB < item) {  // launch-uniform (an item of fewer records than the registers hold)
-        a[q] = ld_in(addr_in + ii);
-        v[q] = ld_in(val_in + ii);
-      } else {
-        v[q] = A(0);
-      }
-      if (i >= s1 || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
-    }
+    if (i >= s1 || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
   }
   __syncthreads();
   ph.mark(32);
@@ -2688,20 +2357,8 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const size_t b_units = pad256((size_t)max_units * 16) + pad256((size_t)max_units * kRunMax * 8);
   const size_t b_hot = pad256((size_t)kHotSlots * 4);
   const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
-  // v3 (GLINT_BIN_V3=1; measured slower, off): no count pass for the plain and plain + hot front ends of a push
-  // that is not validated inside (the dedup front end and the validating count keep v2); the chunks are
-  // partitioned in place, so the coarse buffer holds whole chunks
-  static EnvKnob v3_knob("GLINT_BIN_V3");
-  const u32 nchm = (u32)nchunks_max;
-  const bool v3 = !hook && front != 2 && (u64)nchm * kAChunk * sizeof(A) < ((u64)1 << 32) &&  // (one buffer window)
-                  v3_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 0; }) != 0;
-  const u32 kmax = (u32)(n / item + 2);
-  const size_t cap = v3 ? (size_t)nchm * kAChunk : (size_t)n;
-  const size_t b_a = pad256(cap * 4), b_v = pad256(cap * sizeof(A)), b_e = pad256((size_t)n * 2);
-  const size_t b_c3 = v3 ? pad256((size_t)g.nb * nchm * 4) : 0, b_p3 = v3 ? pad256((size_t)g.nb * (nchm + 1) * 4) : 0;
-  const size_t b_i3 = v3 ? pad256((size_t)g.nb * kmax * 4) : 0;
-  const size_t need = 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + b_wpart + b_a + 2 * b_v + b_e +
-                      2 * b_c3 + b_p3 + b_i3;
+  const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(A)), b_e = pad256((size_t)n * 2);
+  const size_t need = 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + b_wpart + b_a + 2 * b_v + b_e;
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   constexpr size_t kHdr = 12288;  // one [BinCtl (256 B) | T (<= kMaxDigit u32) | done (<= kMaxDigit u32)] header
@@ -2755,11 +2412,6 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   A* val_a = (A*)(p + b_a);
   A* val_b = (A*)(p + b_a + b_v);
   uint16_t* e_b = (uint16_t*)(p + b_a + 2 * b_v);
-  p += b_a + 2 * b_v + pad256((size_t)n * 2);
-  u32* cnt3 = (u32*)p;
-  u32* off3 = (u32*)(p + b_c3);
-  u32* P3 = (u32*)(p + 2 * b_c3);
-  u32* itc = (u32*)(p + 2 * b_c3 + b_p3);
 
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   const int fb = from_break ? 1 : (hook && whole_next ? 2 : 0);
@@ -2782,16 +2434,7 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const unsigned long long* count_hot = front == 1 ? wbest : nullptr;  // the hot records are not partitioned
   BinCtl* const nbc = (BinCtl*)nhdr;
   u32* const nT = (u32*)(nhdr + 256);
-  if (v3) {  // partition in place, then the per-bucket prefixes and the items
-    auto kern = a.part.kind == 0 ? (front == 1 ? bin_part3_kernel<V, MAT, true, 0> : bin_part3_kernel<V, MAT, false, 0>)
-                                 : (front == 1 ? bin_part3_kernel<V, MAT, true, -1> : bin_part3_kernel<V, MAT, false, -1>);
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, addr_a, val_a, a.err, bc,
-                              wbest, wpart, cnt3, off3, nchm, nbc, nT, whole_next);
-    HIPCHK(hipGetLastError());
-    s->bin_par ^= 1;  // bin_part3 zeroed the other header for the next push
-    bin_scan3_kernel<<<g.nb, kATPB, 0, st>>>(g, cnt3, nchm, P3, itc, kmax, item, bc, T, fitems, Bb, Ib);
-    HIPCHK(hipGetLastError());
-  } else if (hook) {  // a validating gated push: the count validates the tail records
+  if (hook) {  // a validating gated push: the count validates the tail records
     auto kern = a.part.kind == 0 ? bin_count_kernel<MAT, 0, true> : bin_count_kernel<MAT, -1, true>;
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff, count_hot, nbc, nT,
                               a.ctl, whole_next);
@@ -2802,7 +2445,6 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
     bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
                                                    count_hot, nbc, nT, nullptr, whole_next);
   }
-  if (!v3) {
   HIPCHK(hipGetLastError());
   s->bin_par ^= 1;  // this push's header is [hdr]; bin_count zeroed the other one for the next push
   if (hook) {  // the verdict (and a rejected batch's cancel) and the head's apply, before any partition
@@ -2820,7 +2462,6 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
                               val_a, a.err, bc, T, fitems, wbest, wpart, item, Roff, Bb, Ib);
   }
   HIPCHK(hipGetLastError());
-  }
   if (front == 1) {
     bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, 0);
     HIPCHK(hipGetLastError());
@@ -2841,14 +2482,14 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
   u64* const whint = whole_next ? s->d_hint : nullptr;
   if (fused) {
-    auto kern = v3 ? bin_fsort_kernel<A, true, true> : bin_fsort_kernel<A, true, false>;
-    kern<<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b, off2, bhint, whint,
-                                                 (u32)n, Ib, done, units, runs, group_on, item, P3, off3, itc, nchm, kmax);
+    bin_fsort_kernel<A, true><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
+                                                                      off2, bhint, whint, (u32)n, Ib, done, units, runs,
+                                                                      group_on, item);
     HIPCHK(hipGetLastError());
   } else {
-    auto kern = v3 ? bin_fsort_kernel<A, false, true> : bin_fsort_kernel<A, false, false>;
-    kern<<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b, off2, bhint, whint,
-                                                 (u32)n, Ib, done, units, runs, group_on, item, P3, off3, itc, nchm, kmax);
+    bin_fsort_kernel<A, false><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
+                                                                       off2, bhint, whint, (u32)n, Ib, done, units, runs,
+                                                                       group_on, item);
     HIPCHK(hipGetLastError());
     bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on, item);
     HIPCHK(hipGetLastError());
