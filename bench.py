@@ -99,7 +99,9 @@ def sparse_floor(workload_tag: str, ms_per_step: float):
     partitioning were free. frac = floor / ms_per_step; None for lines without one."""
     # (case, shard pushes per step): the 8-partition line's step is eight shard pushes, each floored alone
     case, per_step = {"zipf_2p28": ("cfg3", 1), "exchange_2p28": ("cfg4b", 1), "matrix_2p17x512": ("cfg5", 1),
-                      "exchange_2p28_mps8": ("cfg4_mps8_shard", 8)}.get(workload_tag, (None, 1))
+                      "exchange_2p28_mps8": ("cfg4_mps8_shard", 8),
+                      # the eight partitions in one slab: one push of the whole batch, cfg4b's floor
+                      "exchange_2p28_mps8_slab": ("cfg4b", 1)}.get(workload_tag, (None, 1))
     files = [f for f in sorted(glob.glob(str(ROOT / "profiles" / "*" / "micro_sparse_floor.json")))
              if case and f'"{case}"' in Path(f).read_text()]
     if not case or not files:
@@ -242,8 +244,16 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     else:
         my_parts = [partitioner.all()[rank]]
     part = my_parts[0]
-    shards = [PartialMatrix(p, cols_n, "double", device=local) if mat else PartialVector(p, "double", device=local)
-              for p in my_parts]
+    slab = None
+    if exch and mps > 1:  # the rank's partitions as views of one slab (dist.slab_shards; GLINT_DIST_SLAB=0: off)
+        from glint_amd.dist import slab_shards
+        sv = slab_shards("vector", my_parts, 0, "double", local)
+        if sv is not None:
+            slab, shards = sv
+    if slab is None:
+        shards = [PartialMatrix(p, cols_n, "double", device=local) if mat else PartialVector(p, "double", device=local)
+                  for p in my_parts]
+    handles = shards + ([slab] if slab is not None else [])  # every shard a push may launch on
     shard = shards[0]
     n = part.size
     gen = torch.Generator(device=dev)
@@ -290,7 +300,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         # space), so each push is route + gather (glint_route_gather_dev) + all_to_all_single + the
         # local push. Keys and values come from per-rank generators that every rank can replay.
         from glint_amd.dist import DistributedBigVector
-        dv = DistributedBigVector(partitioner, shards, partitioner.size, np.float64, None, dev)
+        dv = DistributedBigVector(partitioner, shards, partitioner.size, np.float64, None, dev, slab=slab)
         nrec = 1 << 26
 
         def batch(src):
@@ -311,7 +321,8 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
         workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({P}, "
                     f"{partitioner.size}), {mps} partition(s) per GPU; route + gather + RCCL all-to-all + "
-                    f"local push" + ("es" if mps > 1 else ""))
+                    f"local push" + ("es" if mps > 1 and slab is None else "") +
+                    (f" (the rank's {mps} partitions in one slab: one push at world size 1)" if slab is not None else ""))
     elif pat in ("dense", "pull"):
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
         vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
@@ -374,9 +385,9 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         # one push at a time, each ended by the shard's sync point: the adaptive tail switch decides
         # from the previous push's tail as published at its sync, so the timed pushes take the path
         # the warm-up settled on (and its one-time scratch allocation lands in the warm-up)
-        for sh in shards:
+        for sh in handles:
             sh.sync(stream)
-    for sh in shards:
+    for sh in handles:
         sh.sync(stream)
         lib.glint_prof_reset(sh.handle)
         lib.glint_prof_enable(sh.handle, 1)
@@ -390,7 +401,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    for sh in shards:
+    for sh in handles:
         lib.glint_prof_enable(sh.handle, 0)
         sh.sync(stream)
     if world > 1:
@@ -402,7 +413,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         """Device time of one kernel kind per step (a large push runs its check and apply as one
         launch per window of records: the launches of a step are summed) and its launch count."""
         tot_ms, tot_n = 0.0, 0
-        for sh in shards:  # every local shard's launches of this kind (the exchange line may host several)
+        for sh in handles:  # every local shard's launches of this kind (the exchange line may host several)
             ms, cnt = C.c_double(), C.c_int64()
             lib.glint_prof_read(sh.handle, kid, C.byref(ms), C.byref(cnt))
             tot_ms, tot_n = tot_ms + ms.value, tot_n + cnt.value
@@ -548,11 +559,13 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
                      else "summed device time of the step's kernels"},
         "check": ok,
     }
-    floor = sparse_floor(tag, dt / steps * 1e3)
+    floor = sparse_floor(tag + ("_slab" if slab is not None else ""), dt / steps * 1e3)
     if floor is not None:
         line["practical_floor"] = floor
     for sh in shards:
         sh.destroy()
+    if slab is not None:  # after its views
+        slab.destroy()
     return line
 
 

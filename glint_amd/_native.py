@@ -31,6 +31,7 @@ _SZ = C.c_size_t
 SIGNATURES = {
     "glint_shard_create": (_I, [_I, _I, _I64, _I64, _I32, C.POINTER(_P)]),
     "glint_shard_create_cyclic": (_I, [_I, _I, _I32, _I32, _I64, _I32, C.POINTER(_P)]),
+    "glint_shard_create_in": (_I, [_P, _I64, _I64, _I64, C.POINTER(_P)]),
     "glint_shard_destroy": (_I, [_P]),
     "glint_shard_zero": (_I, [_P]),
     "glint_shard_info": (_I, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I), C.POINTER(_I)]),
@@ -61,6 +62,7 @@ SIGNATURES = {
     "glint_pull_wire": (_I, [_P, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     "glint_route_dev": (_I, [_P, _I64, _I, _I32, _I64, _P, _P, C.POINTER(_I64), _P]),
     "glint_route_gather_dev": (_I, [_P, _P, _P, _I, _I64, _I, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "glint_route_gather_rebased_dev": (_I, [_P, _P, _P, _I, _I64, _I, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "glint_scatter_rows_dev": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "glint_copy_segments_dev": (_I, [_P, _P, C.POINTER(_I64), _I, _P]),
     "glint_send_matrix_dev": (_I, [_P, _P, _I32, _I32, _P, _P, _P]),

@@ -890,7 +890,7 @@ int push_mat_t(glint_shard* s, const i64* k, const int32_t* c, const void* v, i6
   return launch_push<V, true>(s, k, c, v, n, f, st);
 }
 
-int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
+int create_common(glint_shard* s, int device, int dtype, int32_t cols, void* view_data = nullptr) {
   if (dtype < GLINT_I32 || dtype > GLINT_F64 || cols < 0) return GLINT_EINVAL;
   static EnvKnob hprof_knob("GLINT_HOST_PROF");
   s->hprof = hprof_knob.pos_or(0) != 0;
@@ -915,7 +915,9 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
   HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
   // +16 B: a slab-wide pair load may touch one element past an odd-sized shard's end
   const size_t bytes = (size_t)s->elems * s->vsize + 16;
-  if (hipMalloc(&s->data, bytes) != hipSuccess) {
+  if (view_data) {
+    s->data = view_data;  // a slab's elements, as they are (glint_shard_create_in)
+  } else if (hipMalloc(&s->data, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return GLINT_ENOMEM;
   }
@@ -939,7 +941,7 @@ int create_common(glint_shard* s, int device, int dtype, int32_t cols) {
     (void)hipGetLastError();
     s->h_err = nullptr;  // host calls then read the error state with a pageable copy
   }
-  HIPCHK(hipMemsetAsync(s->data, 0, bytes, s->stream));  // new Array[V](size) is zeroed
+  if (!view_data) HIPCHK(hipMemsetAsync(s->data, 0, bytes, s->stream));  // new Array[V](size) is zeroed
   HIPCHK(hipMemsetAsync(s->d_err, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipMemsetAsync(s->d_err_host, 0, sizeof(ErrState), s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
@@ -963,7 +965,7 @@ void free_shard(glint_shard* s) {
     DeviceGuard g(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     prof_drain(s);
-    if (s->data) (void)hipFree(s->data);
+    if (s->data && !s->slab) (void)hipFree(s->data);
     if (s->d_err) (void)hipFree(s->d_err);
     if (s->d_err_host) (void)hipFree(s->d_err_host);
     if (s->d_ctl) (void)hipFree(s->d_ctl);
@@ -1108,8 +1110,44 @@ int glint_shard_create_cyclic(int device, int dtype, int32_t index, int32_t num_
   return GLINT_OK;
 }
 
+int glint_shard_create_in(glint_shard_t slab, int64_t offset, int64_t start, int64_t end, glint_shard_t* out) {
+  if (!out) return GLINT_EINVAL;
+  *out = nullptr;
+  if (!slab || slab->slab || offset < 0 || end < start || end - start > INT32_MAX) return GLINT_EINVAL;
+  ShardLock lk(slab);
+  const i64 rows = end - start;
+  if (offset + rows > (i64)slab->part.size) return GLINT_EINVAL;
+  const i64 first = offset * (slab->part.cols > 0 ? slab->part.pitch : 1);  // the view's first element
+  if ((first * (i64)slab->vsize) % 256 != 0) return GLINT_EINVAL;  // kernels take 256 B-aligned shards
+  glint_shard* s = new (std::nothrow) glint_shard();
+  if (!s) return GLINT_ENOMEM;
+  s->part.kind = 0;
+  s->part.start = start;
+  s->part.size = (int32_t)rows;
+  s->slab = slab;  // set first: a failed create does not free the slab's memory
+  int rc = create_common(s, slab->device, slab->dtype, slab->part.cols, (char*)slab->data + first * (i64)slab->vsize);
+  if (rc == GLINT_OK) {
+    try {
+      slab->views.push_back(s);
+    } catch (...) {
+      rc = GLINT_ENOMEM;
+    }
+  }
+  if (rc) { free_shard(s); return rc; }
+  *out = s;
+  return GLINT_OK;
+}
+
 int glint_shard_destroy(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
+  if (s->slab) {  // a view: off its slab's list first
+    ShardLock lk(s->slab);
+    auto& v = s->slab->views;
+    v.erase(std::remove(v.begin(), v.end(), s), v.end());
+  } else {
+    ShardLock lk(s);
+    if (!s->views.empty()) return GLINT_EINVAL;  // its views read and write its memory: destroy them first
+  }
   free_shard(s);
   return GLINT_OK;
 }
@@ -1118,7 +1156,8 @@ int glint_shard_zero(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
   ShardLock lk(s);
   DeviceGuard g(s->device);
-  int rc = ring_flush_locked(s);  // the restart comes after every message enqueued before it
+  int rc = refuse_slab(s);
+  if (rc == GLINT_OK) rc = ring_flush_locked(s);  // the restart comes after every message enqueued before it
   if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(s->data, 0, (size_t)s->elems * s->vsize, s->stream));
@@ -2025,6 +2064,14 @@ int ring_wait_locked(glint_shard* s, u64 ticket, i64* first_bad) {
 // A device-resident call runs on the caller's stream: it first waits for the ring entries enqueued
 // on the shard's stream (they share the data array and the error state).
 int dev_order_after_host(glint_shard* s, hipStream_t st) {
+  // a slab's call reads or writes its views' elements: it waits for their host-pointer work, and
+  // their later host-pointer calls wait for it (lock order: slab, then view)
+  for (glint_shard* v : s->views) {
+    ShardLock lv(v);
+    if (int rc = dev_order_after_host(v, st)) return rc;
+    v->last_dev_stream = st;
+    v->dev_dirty = true;
+  }
   int rc = ring_flush_locked(s);
   if (rc) return rc;
   if (!s->host_pending) return GLINT_OK;
@@ -2069,7 +2116,8 @@ int host_push(glint_shard* s, bool mat, const int64_t* keys, const int32_t* cols
   if (n == 0) return GLINT_OK;
   ShardLock lk(s);
   DeviceGuard g(s->device);
-  int rc = order_after_dev(s);
+  int rc = refuse_slab(s);
+  if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) return rc;
   if (batchable(s, n)) {  // Akka-sized: into the open batch (read in place by the kernel), then wait
     u64 ticket = 0;
@@ -2110,7 +2158,8 @@ int host_pull(glint_shard* s, int kind, const int64_t* keys, const int32_t* cols
   if (n == 0) return GLINT_OK;
   ShardLock lk(s);
   DeviceGuard g(s->device);
-  int rc = ring_flush_locked(s);
+  int rc = refuse_slab(s);
+  if (rc == GLINT_OK) rc = ring_flush_locked(s);
   if (rc == GLINT_OK) rc = order_after_dev(s);
   if (rc) return rc;
   if (n <= GLINT_ZERO_COPY_MAX && pull_bytes(s, kind, n) <= kRingAnswerMax) {
@@ -2211,7 +2260,8 @@ int glint_stage_acquire(glint_shard_t s, int64_t n, void** keys, void** cols, vo
   if (!s || !keys || !vals || !slot) return GLINT_EINVAL;
   ShardLock lk(s);
   DeviceGuard g(s->device);
-  int rc = ring_acquire_locked(s, n, slot);
+  int rc = refuse_slab(s);
+  if (rc == GLINT_OK) rc = ring_acquire_locked(s, n, slot);
   if (rc) return rc;
   glint_shard::RingSlot& r = s->ring[*slot];
   const StageLayout L = stage_layout(s, n);
@@ -2225,6 +2275,7 @@ int glint_push_staged(glint_shard_t s, int slot, int64_t n, int flags, uint64_t*
   if (!s) return GLINT_EINVAL;
   ShardLock lk(s);
   DeviceGuard g(s->device);
+  if (int rc = refuse_slab(s)) return rc;
   return ring_push_locked(s, slot, n, flags, (u64*)ticket);
 }
 
@@ -2262,6 +2313,7 @@ int glint_push_wire_async(glint_shard_t s, const uint8_t* payload, size_t len, i
   const i64 bad = small ? host_first_bad(s, kp, mat ? kp + (size_t)n * 8 : nullptr, n) : -1;
   ShardLock lk(s);
   DeviceGuard g(s->device);
+  if (int rc = refuse_slab(s)) return rc;
   if (bad >= 0) {
     s->last_bad = bad;
     return GLINT_EOUTOFRANGE;
@@ -2333,6 +2385,7 @@ int glint_pull_async(glint_shard_t s, int kind, const int64_t* keys, const int32
   const i64 bad = n > 0 ? host_first_bad(s, keys, kind == 1 ? cols : nullptr, n) : -1;
   ShardLock lk(s);
   DeviceGuard g(s->device);
+  if (int rc = refuse_slab(s)) return rc;
   if (bad >= 0) {
     s->last_bad = bad;
     return GLINT_EOUTOFRANGE;

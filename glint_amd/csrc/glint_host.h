@@ -188,6 +188,11 @@ struct glint_shard {
     std::atomic<u64> retire_wait{0}, nretire_wait{0};         // ns waiting for an entry to retire
     std::atomic<u64> copy{0};                                  // ns copying answers out of ring slots
   } hp;
+  // slabs (glint_shard_create_in): a view's elements live inside its slab's allocation (not owned);
+  // the slab lists its views (under its mu) so that its device-resident calls are ordered after the
+  // views' host-pointer work and the views' later host-pointer calls after them
+  glint_shard* slab = nullptr;
+  std::vector<glint_shard*> views;
   std::mutex mu;
 };
 
@@ -317,6 +322,10 @@ inline hipStream_t pick(glint_shard* s, void* stream) {
 // A host-pointer call runs on the shard's private stream: it first waits for everything the
 // caller has enqueued on the last device-resident call's stream (that call's kernels share the
 // shard's data, control words and error state with this one).
+// A slab with views (glint_shard_create_in) takes device-resident calls only: host-pointer work on
+// its private stream would not be ordered with the views' (they take that traffic). Under s->mu.
+inline int refuse_slab(const glint_shard* s) { return s->views.empty() ? GLINT_OK : GLINT_EINVAL; }
+
 inline int order_after_dev(glint_shard* s) {
   if (!s->dev_dirty) return GLINT_OK;
   if (!s->order_ev && hipEventCreateWithFlags(&s->order_ev, hipEventDisableTiming) != hipSuccess) {

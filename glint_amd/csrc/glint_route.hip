@@ -143,6 +143,9 @@ struct RouteOut {
   const int32_t* in_cols;
   const void* in_vals;
   int vsize;  // 4 or 8
+  // added to each key written out, per slot (nullable): a partition's keys rebased to its place in
+  // the receiving rank's slab (glint_route_gather_rebased_dev)
+  const i64* key_delta;
 };
 
 __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ keys, i64 n, RangeDesc d,
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(kRT) void route_scatter(const i64* __restrict__ key
       const int lead = __ffsll((long long)m) - 1;
       const i64 pos = (i64)offs[(i64)o * nblocks + blockIdx.x] + grp_base[wid * 64 + lead] + __popcll(below);
       if (out.order) out.order[pos] = i;
-      if (out.keys) out.keys[pos] = key;
+      if (out.keys) out.keys[pos] = key + (out.key_delta ? out.key_delta[o] : 0);
       if (out.cols) out.cols[pos] = out.in_cols[i];
       if (out.vals) {
         if (out.vsize == 8) reinterpret_cast<u64*>(out.vals)[pos] = reinterpret_cast<const u64*>(out.in_vals)[i];
@@ -210,9 +213,11 @@ __global__ __launch_bounds__(kRT) void route_scatter_small(const i64* __restrict
   __shared__ uint8_t ob[kSChunk];        // owner of each sorted position
   __shared__ u32 goff[kSmallParts + 1];  // per owner: its first output slot minus its first sorted position
   __shared__ u32 wt[kRT / 64];
+  __shared__ i64 kd[kSmallParts];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const i64 base = (i64)blockIdx.x * kSChunk;
   const int np = d.nparts;
+  if (tid < np) kd[tid] = out.key_delta ? out.key_delta[tid] : 0;
   i64 k[R];
   u64 v[R];
   int32_t c[R];
@@ -290,7 +295,7 @@ __global__ __launch_bounds__(kRT) void route_scatter_small(const i64* __restrict
     }
     __syncthreads();
   };
-  if (out.keys) emit([&](int r) { return (u64)k[r]; }, out.keys);
+  if (out.keys) emit([&](int r) { return (u64)(k[r] + kd[o[r]]); }, out.keys);
   if (out.vals) {
     if (out.vsize == 8) emit([&](int r) { return v[r]; }, reinterpret_cast<u64*>(out.vals));
     else emit([&](int r) { return v[r]; }, reinterpret_cast<u32*>(out.vals));
@@ -604,6 +609,24 @@ extern "C" int glint_route_dev(const int64_t* keys, int64_t n, int kind, int32_t
   if (rc) return rc;
   *first_bad = enc ? (int64_t)~enc : -1;
   return enc ? GLINT_EOUTOFRANGE : GLINT_OK;
+}
+
+extern "C" int glint_route_gather_rebased_dev(const int64_t* keys, const int32_t* cols, const void* vals, int vsize,
+                                              int64_t n, int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of,
+                                              const int64_t* key_delta, int64_t* counts, int64_t* order,
+                                              int64_t* out_keys, int32_t* out_cols, void* out_vals, uint64_t* bad_dev,
+                                              void* stream) {
+  if (!key_delta || (!out_keys && n > 0) || nparts <= 1) return GLINT_EINVAL;  // (one partition: no scatter pass to rebase in)
+  RouteOut out{};
+  out.order = order;
+  out.keys = out_keys;
+  out.cols = out_cols;
+  out.vals = out_vals;
+  out.in_cols = cols;
+  out.in_vals = vals;
+  out.vsize = vsize;
+  out.key_delta = key_delta;
+  return route_launch(keys, n, kind, nparts, nkeys, slot_of, counts, out, bad_dev, (hipStream_t)stream);
 }
 
 extern "C" int glint_route_gather_dev(const int64_t* keys, const int32_t* cols, const void* vals, int vsize, int64_t n,

@@ -28,6 +28,7 @@ the partition it hosts, which needs no exchange.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import threading
 from typing import Callable, List, Optional
@@ -39,7 +40,7 @@ import torch.distributed as dist
 from . import _native as N
 from .client import bucket
 from .errors import ArrayIndexOutOfBoundsException, IndexOutOfBoundsException, ModelCreationException
-from .partitioning import CyclicPartitioner, RangePartitioner
+from .partitioning import CyclicPartitioner, RangePartition, RangePartitioner
 from .shard import PartialMatrix, PartialVector, check, resolve_dtype
 
 _TORCH_DTYPES = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
@@ -80,10 +81,11 @@ class Router:
             self._dev[device] = t
         return t
 
-    def route(self, keys: torch.Tensor, cols=None, vals=None, want_order: bool = False):
+    def route(self, keys: torch.Tensor, cols=None, vals=None, want_order: bool = False, key_delta=None):
         """Device batch -> records in send order, in ONE kernel pass (glint_route_gather_dev) with no
         host synchronisation: (counts, order, keys, cols, vals, bad), all device tensors; counts in
-        slot (send) order, bad = ~first bad record index or 0."""
+        slot (send) order, bad = ~first bad record index or 0. key_delta (device int64 per slot, with
+        nparts >= 2): keys written as key + key_delta[slot] (glint_route_gather_rebased_dev)."""
         n = keys.numel()
         dev = keys.device
         slot_of, _ = self._device_tables(dev)
@@ -102,10 +104,16 @@ class Router:
         sc = torch.empty(n, dtype=torch.int32, device=dev) if cols is not None else None
         sv = torch.empty(n, dtype=vals.dtype, device=dev) if vals is not None else None
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-        rc = N.load().glint_route_gather_dev(
-            keys.data_ptr(), ptr(cols), ptr(vals), vals.element_size() if vals is not None else 0, n, self.kind,
-            self.nparts, self.nkeys, ptr(slot_of), counts.data_ptr(), ptr(order), sk.data_ptr(), ptr(sc), ptr(sv),
-            bad.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        vsize = vals.element_size() if vals is not None else 0
+        st = torch.cuda.current_stream(dev).cuda_stream
+        if key_delta is not None:
+            rc = N.load().glint_route_gather_rebased_dev(
+                keys.data_ptr(), ptr(cols), ptr(vals), vsize, n, self.kind, self.nparts, self.nkeys, ptr(slot_of),
+                key_delta.data_ptr(), counts.data_ptr(), ptr(order), sk.data_ptr(), ptr(sc), ptr(sv), bad.data_ptr(), st)
+        else:
+            rc = N.load().glint_route_gather_dev(
+                keys.data_ptr(), ptr(cols), ptr(vals), vsize, n, self.kind, self.nparts, self.nkeys, ptr(slot_of),
+                counts.data_ptr(), ptr(order), sk.data_ptr(), ptr(sc), ptr(sv), bad.data_ptr(), st)
         check(rc)
         return counts, order, sk, sc, sv, bad
 
@@ -284,8 +292,56 @@ class _Exchange:
         return resp
 
 
+def slab_layout(parts, cols: int, dtype):
+    """Where a rank's partitions sit in its slab -> (start, end, rows), or None when they do not
+    qualify (fewer than two, not all RangePartitions, more than an Int of rows): the slab is
+    RangePartition(start, end) and partition j's first row in it is rows[j], each 256-byte aligned.
+    * Side by side in key order (a rank's partitions at world 1), aligned: the slab spans their keys,
+      so a key is its own slab key (delta 0) and a batch needs no route at all.
+    * Otherwise (rank r of W hosts r, r + W, ...): one after another from row 0, each at the next
+      256-byte boundary; the route rebases keys into it (glint_route_gather_rebased_dev).
+    The same function of (parts, cols, dtype) on every rank, so each rank knows every slab's layout."""
+    if len(parts) < 2 or not all(isinstance(p, RangePartition) for p in parts):
+        return None
+    _, np_dtype = resolve_dtype(dtype)
+    vsize = np.dtype(np_dtype).itemsize
+    pitch = -(-int(cols) // (16 // vsize)) * (16 // vsize) if cols else 1  # the library's row pitch
+    step = 256 // math.gcd(256, pitch * vsize)  # rows per 256-byte boundary
+    rows = [p.start - parts[0].start for p in parts]
+    if all(a.end == b.start for a, b in zip(parts, parts[1:])) and all(r % step == 0 for r in rows):
+        start, end = parts[0].start, parts[-1].end
+    else:
+        rows, r = [], 0
+        for p in parts:
+            rows.append(r)
+            r = -(-(r + p.end - p.start) // step) * step
+        start, end = 0, rows[-1] + parts[-1].end - parts[-1].start
+    if end - start >= 2 ** 31:
+        return None
+    return start, end, rows
+
+
+def slab_shards(kind: str, parts, cols: int, dtype, device: int):
+    """The partitions one rank hosts as views of ONE slab (glint_shard_create_in, laid out by
+    slab_layout) -> (slab, views), or None. A push whose records all belong to the rank is then one
+    device-resident call on the slab -- one launch sequence for all of its partitions, where the
+    reference sends a message per partition (AsyncBigVector.scala:96-98): _Distributed._push_gated
+    (world 1, the slab spans the key space) and DistributedBigVector._push_slab (the route rebases
+    keys into every rank's slab). GLINT_DIST_SLAB=0: no slabs (A/B)."""
+    if os.environ.get("GLINT_DIST_SLAB", "1") == "0":
+        return None
+    lay = slab_layout(parts, cols, dtype)
+    if lay is None:
+        return None
+    start, end, rows = lay
+    whole = RangePartition(parts[0].index, start, end)
+    slab = PartialVector(whole, dtype, device) if kind == "vector" else PartialMatrix(whole, cols, dtype, device)
+    views = [type(slab).view(slab, p, r) for p, r in zip(parts, rows)]
+    return slab, views
+
+
 class _Distributed:
-    def __init__(self, partitioner, shards, group, device):
+    def __init__(self, partitioner, shards, group, device, slab=None):
         self.partitioner = partitioner
         self.group = group
         self.rank = dist.get_rank(group)
@@ -293,6 +349,8 @@ class _Distributed:
         self.router = Router(partitioner, self.world)
         self.shards = list(shards)  # local shards, in rank_parts[rank] order
         self.device = device
+        # the slab the local shards are views of (slab_shards), or None
+        self.slab = slab
 
     @property
     def nrOfPartitions(self) -> int:
@@ -316,9 +374,15 @@ class _Distributed:
                        self._comm(keys), bad_exc=exc)
         return order, ex
 
-    def _begin_fused(self, keys, cols=None, vals=None, want_order=False):
-        """Device route: the fused route writes the send buffers; one host read for the splits."""
-        counts, order, sk, sc, sv, bad = self.router.route(keys, cols, vals, want_order)
+    def _begin_fused(self, keys, cols=None, vals=None, want_order=False, rebase=False):
+        """Device route: the fused route writes the send buffers; one host read for the splits.
+        rebase: keys written as their slab keys (_slab_plan's deltas)."""
+        delta = None
+        if rebase:
+            if getattr(self, "_delta_dev", None) is None or self._delta_dev.device != keys.device:
+                self._delta_dev = torch.from_numpy(self._delta).to(keys.device)
+            delta = self._delta_dev
+        counts, order, sk, sc, sv, bad = self.router.route(keys, cols, vals, want_order, key_delta=delta)
         ex = _Exchange(self.router, self.rank, counts, self.group, self._comm(keys), bad)
         return ex, order, sk, sc, sv
 
@@ -402,8 +466,49 @@ class _Distributed:
                 raise ArrayIndexOutOfBoundsException(f"record {bad[i]} is outside the partition", bad[i])
             check(rcs[i], sh.handle)
 
+    def _gated_shard(self):
+        """The one shard a world-of-one push goes to as it is: the only partition's, or the slab that
+        holds every partition side by side (its range is the key space, so its key check is the
+        route's; vectors only, _slab_plan)."""
+        if self.world != 1:
+            return None
+        if self.router.nparts == 1:
+            return self.shards[0]
+        return self.slab if getattr(self, "_slab_keyed", False) else None
+
+    def _slab_plan(self, np_dtype) -> None:
+        """Vectors: whether pushes go to slabs, and the route's per-slot key deltas (key -> the key of
+        its row in the hosting rank's slab, slab_layout). Decided the same way on every rank: the
+        layouts are a function of the partitioner, and at world > 1 the ranks agree by one MIN
+        all-reduce that every rank joins (a rank without a slab -- another shard factory,
+        GLINT_DIST_SLAB=0 -- turns it off for all). (A matrix keeps per-partition pushes: a batch with
+        a bad column fails only that partition's message in the reference.)"""
+        self._delta, self._slab_keyed = None, False
+        if not isinstance(self.partitioner, RangePartitioner) or self.router.maxp < 2:
+            return
+        parts = self.partitioner.all()
+        lays = [slab_layout([parts[p] for p in self.router.rank_parts[r]], 0, np_dtype) for r in range(self.world)]
+        if any(lay is None for lay in lays):
+            return
+        ok = self.slab is not None and self.slab.partition.start == lays[self.rank][0] and \
+            self.slab.partition.end == lays[self.rank][1]
+        if self.world > 1:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int64,
+                             device="cpu" if dist.get_backend(self.group) == "gloo" else self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            ok = bool(t.item())
+        if not ok:
+            return
+        d = np.zeros(self.router.nparts, np.int64)
+        for r, (start, _, rows) in enumerate(lays):
+            for j, p in enumerate(self.router.rank_parts[r]):
+                d[self.router.slot_of[p]] = start + rows[j] - parts[p].start
+        self._slab_keyed = self.world == 1 and not d.any()
+        self._delta = d
+
     def _push_gated(self, keys: torch.Tensor, args: tuple, deterministic: bool) -> bool:
-        """A world of one with one partition: the batch is the shard's push as it is. The key check
+        """A world of one with one partition (or a slab holding all of them, slab_shards): the batch
+        is the shard's push as it is. The key check
         (the route's validation pass) and the push are enqueued back to back -- the push gated on the
         route's status word on the device (glint_*_push_dev_gated: a batch with an out-of-range key
         applies nothing, as mapPartitions throws before sending, AsyncBigVector.scala:96-98) -- and the
@@ -412,14 +517,14 @@ class _Distributed:
         and writes the word, so the route's pass over the keys is gone too (GLINT_GATE_ROUTE=1: the
         route in front, for A/B). Returns False when the call does not qualify (the general path then
         runs)."""
-        if not (self.world == 1 and self.router.nparts == 1 and keys.is_cuda and not deterministic
-                and self._on_shard_device(keys) and hasattr(self.shards[0], "handle")
+        sh = self._gated_shard()
+        if not (sh is not None and keys.is_cuda and not deterministic
+                and self._on_shard_device(keys) and hasattr(sh, "handle")
                 and getattr(N.load(), "glint_vec_push_dev_gated", None) is not None):  # (an older A/B library)
             return False
         esz = args[-1].element_size()
         if keys.data_ptr() % 16 or args[-1].data_ptr() % (2 * esz) or (len(args) == 3 and args[1].data_ptr() % 8):
             return False
-        sh = self.shards[0]
         lib = N.load()
         sup = getattr(lib, "glint_push_flags_supported", None)
         if sup is not None and sup() & N.GLINT_PUSH_VALIDATE and os.environ.get("GLINT_GATE_ROUTE", "0") != "1":
@@ -503,6 +608,8 @@ class _Distributed:
     def destroy(self) -> bool:
         for sh in self.shards:
             sh.destroy()
+        if self.slab is not None:  # after its views
+            self.slab.destroy()
         if getattr(self, "_gate_buf", None) is not None:
             self._gate_buf.free()
             self._gate_buf = None
@@ -512,10 +619,28 @@ class _Distributed:
 class DistributedBigVector(_Distributed):
     """AsyncBigVector over the ranks of a process group (push / pull of any keys from any rank)."""
 
-    def __init__(self, partitioner, shards, size: int, np_dtype, group=None, device=None):
-        super().__init__(partitioner, shards, group, device)
+    def __init__(self, partitioner, shards, size: int, np_dtype, group=None, device=None, slab=None):
+        super().__init__(partitioner, shards, group, device, slab)
         self.size = int(size)
         self.dtype = _TORCH_DTYPES[np.dtype(np_dtype)]
+        self._slab_plan(np_dtype)
+
+    def _push_slab(self, keys: torch.Tensor, values: torch.Tensor) -> bool:
+        """Every rank's partitions in one slab (_slab_plan): the route writes each key rebased into
+        the hosting rank's slab (glint_route_gather_rebased_dev), the exchange sends the records as
+        usual, and each rank pushes ALL it received as one unordered call on its slab -- no
+        per-partition split, no per-partition push. Keys were checked by the route (a batch with a bad
+        one sends nothing and raises after the collectives), so the slab push cannot reject any."""
+        if self._delta is None or not (keys.is_cuda and self._on_shard_device(keys) and values.device == keys.device):
+            return False
+        ex, _, sk, _, sv = self._begin_fused(keys, vals=values.contiguous(), rebase=True)
+        rk, rv = ex.forward(sk), ex.forward(sv)
+        if rk.numel():
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            self.slab.update(self._to_shard(rk), self._to_shard(rv), sync=False, unordered=True)
+            self.slab.sync(stream)
+        ex.raise_if_bad(keys, self.router.nkeys)
+        return True
 
     def push(self, keys: torch.Tensor, values: torch.Tensor, deterministic: bool = False) -> bool:
         keys = keys.reshape(-1).to(torch.int64)
@@ -523,6 +648,8 @@ class DistributedBigVector(_Distributed):
         if keys.numel() != values.numel():
             raise ValueError("keys and values differ in length")
         if values.device == keys.device and self._push_gated(keys, (keys, values.contiguous()), deterministic):
+            return True
+        if not deterministic and self._push_slab(keys, values):
             return True
         if keys.is_cuda and values.device == keys.device:
             ex, _, sk, _, sv = self._begin_fused(keys, vals=values.contiguous())
@@ -555,8 +682,8 @@ class DistributedBigVector(_Distributed):
 class DistributedBigMatrix(_Distributed):
     """AsyncBigMatrix over the ranks of a process group."""
 
-    def __init__(self, partitioner, shards, rows: int, cols: int, np_dtype, group=None, device=None):
-        super().__init__(partitioner, shards, group, device)
+    def __init__(self, partitioner, shards, rows: int, cols: int, np_dtype, group=None, device=None, slab=None):
+        super().__init__(partitioner, shards, group, device, slab)
         self.rows, self.cols = int(rows), int(cols)
         self.dtype = _TORCH_DTYPES[np.dtype(np_dtype)]
 
@@ -640,20 +767,24 @@ class DistributedClient:
         partitioner = createPartitioner(nparts, keys)
         mine = Router(partitioner, self.world).rank_parts[self.rank]
         parts = partitioner.all()
+        if self.shard_factory == self._hbm_shard and self.device.type == "cuda":
+            sv = slab_shards(kind, [parts[p] for p in mine], cols, dtype, self.device.index)
+            if sv is not None:  # the rank's partitions side by side in one slab
+                return partitioner, sv[1], sv[0]
         shards = [self.shard_factory(kind, parts[p], cols, dtype, self.device) for p in mine]
-        return partitioner, shards
+        return partitioner, shards, None
 
     def vector(self, keys: int, dtype="double", modelsPerServer: int = 1,
                createPartitioner: Callable = RangePartitioner.apply) -> DistributedBigVector:
         _, np_dtype = resolve_dtype(dtype)
-        partitioner, shards = self._create(keys, modelsPerServer, createPartitioner, "vector", 0, dtype)
-        return DistributedBigVector(partitioner, shards, keys, np_dtype, self.group, self.device)
+        partitioner, shards, slab = self._create(keys, modelsPerServer, createPartitioner, "vector", 0, dtype)
+        return DistributedBigVector(partitioner, shards, keys, np_dtype, self.group, self.device, slab)
 
     def matrix(self, rows: int, cols: int, dtype="double", modelsPerServer: int = 1,
                createPartitioner: Callable = RangePartitioner.apply) -> DistributedBigMatrix:
         _, np_dtype = resolve_dtype(dtype)
-        partitioner, shards = self._create(rows, modelsPerServer, createPartitioner, "matrix", cols, dtype)
-        return DistributedBigMatrix(partitioner, shards, rows, cols, np_dtype, self.group, self.device)
+        partitioner, shards, slab = self._create(rows, modelsPerServer, createPartitioner, "matrix", cols, dtype)
+        return DistributedBigMatrix(partitioner, shards, rows, cols, np_dtype, self.group, self.device, slab)
 
 
-__all__ = ["Router", "DistributedClient", "DistributedBigVector", "DistributedBigMatrix"]
+__all__ = ["Router", "DistributedClient", "DistributedBigVector", "DistributedBigMatrix", "slab_shards"]

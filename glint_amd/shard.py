@@ -130,6 +130,26 @@ class _Shard:
         self.size = sz.value
         self.cols = cl.value
 
+    @classmethod
+    def view(cls, slab: "_Shard", partition: RangePartition, offset: int):
+        """A shard over ``partition`` whose elements are rows [offset, offset + size) of ``slab``
+        (glint_shard_create_in): the partitions a server hosts, kept in one allocation so that one
+        device-resident call on the slab serves all of them. Destroy views before their slab."""
+        if not isinstance(partition, RangePartition):
+            raise TypeError("a slab view takes a RangePartition")
+        self = cls.__new__(cls)
+        self.lib, self.partition, self.device = slab.lib, partition, slab.device
+        self.code, self.np_dtype = slab.code, slab.np_dtype
+        self._h = C.c_void_p()
+        check(self.lib.glint_shard_create_in(slab.handle, int(offset), partition.start, partition.end, C.byref(self._h)))
+        sz, cl = C.c_int32(), C.c_int32()
+        check(self.lib.glint_shard_info(self._h, C.byref(sz), C.byref(cl), None, None), self._h)
+        self.size, self.cols = sz.value, cl.value
+        if cl.value:
+            self.rows = self.size
+        self.slab = slab
+        return self
+
     # lifetime -------------------------------------------------------------------------------
     @property
     def handle(self) -> C.c_void_p:
@@ -139,7 +159,7 @@ class _Shard:
 
     def destroy(self) -> None:
         if self._h:
-            self.lib.glint_shard_destroy(self._h)
+            check(self.lib.glint_shard_destroy(self._h))  # (a slab with live views refuses: EINVAL)
             self._h = C.c_void_p()
 
     close = destroy

@@ -88,6 +88,22 @@ int glint_shard_create(int device, int dtype, int64_t start, int64_t end, int32_
 int glint_shard_create_cyclic(int device, int dtype, int32_t index, int32_t num_partitions,
                               int64_t num_keys, int32_t cols, glint_shard_t* out);
 
+/* Slabs: the partitions one server hosts, kept in one allocation. A range shard (vector, or matrix
+ * rows of the slab's width) over RangePartition(start, end) whose elements are the slab's rows
+ * [offset, offset + end - start) -- a view: it reads and writes them as they are, and is a shard like
+ * any other (its own partition, key check, stream, error state). The slab keeps its own partition, so
+ * a batch whose records all fall in the views can be pushed or pulled as ONE device-resident call on
+ * the slab when the views' partitions lie side by side in key order (the Client's partitions of one
+ * rank at world size 1: DistributedClient's slab) -- one launch sequence for all of them, where the
+ * reference sends one message per partition (AsyncBigVector.scala:96-98, one actor per partition,
+ * Client.scala:71-85). The view's first element must be 256-byte aligned in the slab. While it has
+ * views the slab takes device-resident calls only (its host-pointer calls, and glint_shard_zero,
+ * return GLINT_EINVAL), each ordered after the views' host-pointer work and before their later
+ * host-pointer calls; device-resident calls on the slab and its views are ordered by their streams,
+ * as for any shard. A view is destroyed before its slab (GLINT_EINVAL until then). */
+int glint_shard_create_in(glint_shard_t slab, int64_t offset, int64_t start, int64_t end,
+                          glint_shard_t* out);
+
 /* Frees the device memory (actor postStop / `destroy()`, AsyncBigVector.scala:135-140). */
 int glint_shard_destroy(glint_shard_t shard);
 
@@ -262,6 +278,17 @@ int glint_route_gather_dev(const int64_t* keys, const int32_t* cols, const void*
                            int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of, int64_t* counts,
                            int64_t* order, int64_t* out_keys, int32_t* out_cols, void* out_vals,
                            uint64_t* bad_dev, void* stream);
+
+/* glint_route_gather_dev with every key written to out_keys as key + key_delta[group] (device array
+ * of nparts int64, indexed like the groups): a partition's keys rebased to their rows in the slab of
+ * the rank that hosts it (glint_shard_create_in), so the receiving rank pushes everything it receives
+ * as ONE call on its slab instead of one per partition (the reference's one message per partition,
+ * AsyncBigVector.scala:96-116). out_keys and key_delta non-NULL, nparts >= 2. */
+int glint_route_gather_rebased_dev(const int64_t* keys, const int32_t* cols, const void* vals, int vsize,
+                                   int64_t n, int kind, int32_t nparts, int64_t nkeys, const int32_t* slot_of,
+                                   const int64_t* key_delta, int64_t* counts, int64_t* order,
+                                   int64_t* out_keys, int32_t* out_cols, void* out_vals, uint64_t* bad_dev,
+                                   void* stream);
 
 /* ---- exchange glue (device) ----------------------------------------------------------------- *
  * The client side of a routed pull: AsyncBigVector.pull writes each partition's answer back to the

@@ -87,7 +87,7 @@ def run_case(rank, world, port, backend, case, use_gpu):
             dev = torch.device("cpu")
             from glint_amd.dist import DistributedClient
             client = DistributedClient(device=dev, shard_factory=_oracle_factory)
-        CASES[case](client, rank, world, dev)
+        (CASES.get(case) or GPU_CASES[case])(client, rank, world, dev)
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -201,6 +201,77 @@ def _matrix_case(nrows, ncols, mps, dtype="double", n=2500):
         mat.destroy()
     return body
 
+
+def _slab_case(nkeys, mps, dtype, keyed, n=60_000):
+    """The rank's partitions in one slab (dist.slab_shards). World 1, partitions side by side and
+    aligned (keyed): an unordered device push is ONE validating push on the slab (_push_gated);
+    otherwise (unaligned partitions, or world > 1 where rank r hosts r, r + W, ...) the route
+    rebases keys into every rank's slab and each rank pushes what it receives as one call
+    (_push_slab). Interleaved with deterministic pushes (the views, through the route) and, at
+    world 1, with the views' own host-pointer pushes left in flight -- against the oracle's replay
+    (every rank pushes the same batches). Long: bit-exact; Double: within 1e-12 of each element's
+    sum of magnitudes (unordered sums)."""
+    def body(client, rank, world, dev):
+        _, np_dtype = resolve_dtype(dtype)
+        vec = client.vector(nkeys, dtype, modelsPerServer=mps)
+        assert vec.slab is not None and all(sh.slab is vec.slab for sh in vec.shards)
+        assert vec._delta is not None and vec._slab_keyed == (keyed and world == 1), (vec._slab_keyed, keyed)
+        ref = O.OracleVector(O.part_range(0, nkeys), resolve_dtype(dtype)[0])
+        mag = np.zeros(nkeys, np.float64)
+        tickets = []
+        for step, how in enumerate(["device", "host", "device", "deterministic", "device"]):
+            k, v = _batch(3000 + step, n, nkeys, np_dtype)
+            if how == "host" and world == 1:
+                # each view's records through its host-pointer path, enqueued and NOT waited for: the
+                # slab's next push must order itself after them (dev_order_after_host over its views)
+                for sh in vec.shards:
+                    m = (k >= sh.partition.start) & (k < sh.partition.end)
+                    tickets.append((sh, sh.push_async(k[m], v[m])))
+            else:
+                vec.push(torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev), deterministic=how == "deterministic")
+            for _ in range(1 if how == "host" and world == 1 else world):
+                assert ref.update(k, v) == -1
+                np.add.at(mag, k, np.abs(v.astype(np.float64)))
+            if step == 2:
+                for sh, t in tickets:
+                    sh.wait(t)
+        allk = np.arange(nkeys, dtype=np.int64)
+        want, _ = ref.get(allk)
+        got = vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy()
+        if np.dtype(np_dtype).kind == "f":
+            assert np.all(np.abs(got - want) <= 1e-12 * mag), np.max(np.abs(got - want) - 1e-12 * mag)
+        else:
+            np.testing.assert_array_equal(got, want)
+        # each local view holds its partition's elements (the slab's rows at its place)
+        for sh in vec.shards:
+            p = sh.partition
+            np.testing.assert_array_equal(sh.get(torch.arange(p.start, p.end, device=dev)).cpu().numpy(),
+                                          got[p.start:p.end])
+        # a bad key on rank 0: it sends nothing and raises (after the collectives); the others land
+        bad = np.array([5, nkeys, 7], dtype=np.int64) if rank == 0 else np.array([5, 7], dtype=np.int64)
+        try:
+            vec.push(torch.from_numpy(bad).to(dev), torch.from_numpy(np.ones(bad.size, np_dtype)).to(dev))
+            assert rank != 0, "out-of-range key accepted"
+        except IndexOutOfBoundsException:
+            assert rank == 0
+        for _ in range(world - 1):
+            assert ref.update(np.array([5, 7], np.int64), np.ones(2, np_dtype)) == -1
+        want, _ = ref.get(allk)
+        got = vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy()
+        if np.dtype(np_dtype).kind != "f":
+            np.testing.assert_array_equal(got, want)
+        vec.destroy()
+    return body
+
+
+# HBM shards only (test_gpu_parity.test_dist_exchange_on_gpu): world 1 with the partitions in one slab
+GPU_CASES = {
+    "vec_slab_long_mps8": _slab_case(8 * 4096, 8, "long", keyed=True),
+    "vec_slab_double_mps4": _slab_case(4 * 8192, 4, "double", keyed=True),
+    "vec_slab_long_mps3_unaligned": _slab_case(3 * 1000 + 1, 3, "long", keyed=False),  # (rebased route)
+    "vec_range_mps4_aligned": _vector_case(4 * 4096, 4, RangePartitioner.apply, "double"),
+    "mat_range_mps4_aligned": _matrix_case(1_024, 17, 4),
+}
 
 CASES = {
     "vec_range": _vector_case(10_007, 1, RangePartitioner.apply, "double"),

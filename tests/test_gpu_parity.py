@@ -637,7 +637,12 @@ def test_route_out_of_range_reports_first_bad(gpu):
 @pytest.mark.parametrize("backend,world,case", [
     ("gloo", 2, "vec_range"), ("gloo", 2, "vec_range_mps3"), ("gloo", 2, "vec_cyclic_mps2"),
     ("gloo", 2, "vec_long_few_keys"), ("gloo", 2, "mat_range_mps2"),
-    ("nccl", 1, "vec_range_mps3"), ("nccl", 1, "vec_range"), ("nccl", 1, "mat_range")])
+    ("nccl", 1, "vec_range_mps3"), ("nccl", 1, "vec_range"), ("nccl", 1, "mat_range"),
+    # the partitions of a rank in one slab (dist.slab_shards)
+    ("nccl", 1, "vec_slab_long_mps8"), ("nccl", 1, "vec_slab_double_mps4"), ("nccl", 1, "vec_slab_long_mps3_unaligned"),
+    ("nccl", 1, "vec_range_mps4_aligned"), ("nccl", 1, "mat_range_mps4_aligned"),
+    # world 2: every rank's slab, keys rebased by the route (rank r hosts r, r + 2, ...)
+    ("gloo", 2, "vec_slab_long_mps8"), ("gloo", 2, "vec_slab_long_mps3_unaligned"), ("gloo", 2, "vec_range_mps4_aligned")])
 def test_dist_exchange_on_gpu(gpu, backend, world, case):
     import socket
     import torch.multiprocessing as mp

@@ -1,0 +1,129 @@
+"""Slabs (glint_shard_create_in): the partitions one server hosts, as views of one allocation.
+
+A view is a shard like any other -- its own RangePartition, key check, stream and error state --
+whose elements are rows of the slab. These tests pin the C ABI's contract (include/glint_gpu.h): the
+views and the slab see one memory; a slab with views takes device-resident calls only, each ordered
+after the views' host-pointer work; views are destroyed first; offsets are checked. The world-1
+exchange on top of it (one push on the slab for all partitions) is dist_workers' slab cases."""
+import numpy as np
+import pytest
+import torch
+
+from glint_amd.errors import ArrayIndexOutOfBoundsException
+from glint_amd.partitioning import RangePartition
+from glint_amd.shard import PartialMatrix, PartialVector
+
+pytestmark = pytest.mark.gpu
+
+
+def _vec_slab(gpu, dtype="long", start=100, rows=1024, nviews=3):
+    slab = PartialVector(RangePartition(0, start, start + rows * nviews), dtype, gpu)
+    views = [PartialVector.view(slab, RangePartition(j, start + rows * j, start + rows * (j + 1)), rows * j)
+             for j in range(nviews)]
+    return slab, views
+
+
+def test_views_and_slab_share_elements(gpu):
+    dev = torch.device("cuda", gpu)
+    slab, views = _vec_slab(gpu)
+    one = lambda n, x: torch.full((n,), x, dtype=torch.int64, device=dev)  # noqa: E731
+    views[1].update(torch.arange(1124, 2148, device=dev), one(1024, 1))         # device push on a view
+    views[2].update(np.arange(2148, 3172), np.full(1024, 2, np.int64))          # host push on another
+    t = views[0].push_async(np.arange(100, 1124), np.full(1024, 5, np.int64))   # enqueued, not waited for
+    slab.update(torch.arange(100, 3172, device=dev), one(3072, 10))             # one push on the slab
+    views[0].wait(t)
+    want = 10 + np.repeat(np.array([5, 1, 2], np.int64), 1024)
+    np.testing.assert_array_equal(slab.get(torch.arange(100, 3172, device=dev)).cpu().numpy(), want)
+    for j, v in enumerate(views):
+        lo = 100 + 1024 * j
+        np.testing.assert_array_equal(v.get(np.arange(lo, lo + 1024)), want[1024 * j:1024 * (j + 1)])
+    # a view checks its own partition
+    with pytest.raises(ArrayIndexOutOfBoundsException):
+        views[0].update(np.array([1124]), np.array([1], np.int64))
+    for v in views:
+        v.destroy()
+    slab.destroy()
+
+
+def test_slab_takes_device_calls_only_while_it_has_views(gpu):
+    dev = torch.device("cuda", gpu)
+    slab, views = _vec_slab(gpu, nviews=2)
+    with pytest.raises(ValueError):
+        slab.update(np.array([100]), np.array([1], np.int64))
+    with pytest.raises(ValueError):
+        slab.get(np.array([100]))
+    with pytest.raises(ValueError):
+        slab.push_async(np.array([100]), np.array([1], np.int64))
+    with pytest.raises(ValueError):
+        slab.zero()
+    with pytest.raises(ValueError):  # its views read and write its memory
+        slab.destroy()
+    slab.update(torch.tensor([100], device=dev), torch.tensor([3], dtype=torch.int64, device=dev))
+    views[1].destroy()
+    with pytest.raises(ValueError):
+        slab.destroy()
+    views[0].destroy()
+    # no views left: a shard like any other again
+    slab.update(np.array([100]), np.array([1], np.int64))
+    assert slab.get(np.array([100]))[0] == 4
+    slab.destroy()
+
+
+def test_view_offsets_are_checked(gpu):
+    slab = PartialVector(RangePartition(0, 0, 4096), "double", gpu)
+    with pytest.raises(ValueError):  # 8 bytes into the slab: not 256-byte aligned
+        PartialVector.view(slab, RangePartition(0, 0, 10), 1)
+    with pytest.raises(ValueError):  # past the slab's end
+        PartialVector.view(slab, RangePartition(0, 0, 64), 4096 - 32)
+    v = PartialVector.view(slab, RangePartition(0, 0, 64), 32)
+    with pytest.raises(ValueError):  # a view of a view
+        PartialVector.view(v, RangePartition(0, 0, 32), 0)
+    v.destroy()
+    slab.destroy()
+
+
+@pytest.mark.parametrize("unordered", [False, True])
+def test_odd_view_writes_stay_inside(gpu, unordered):
+    """A 1023-element view followed by a gap element and the next view: dense and unordered pushes
+    into the odd-sized view (the slab-wide pair paths) leave the gap and the neighbour untouched."""
+    dev = torch.device("cuda", gpu)
+    slab = PartialVector(RangePartition(0, 0, 2048), "double", gpu)
+    a = PartialVector.view(slab, RangePartition(0, 0, 1023), 0)
+    b = PartialVector.view(slab, RangePartition(1, 1024, 2048), 1024)
+    k = torch.arange(0, 1023, device=dev)
+    if unordered:
+        k = k[torch.randperm(1023, device=dev)]
+    for _ in range(3):
+        a.update(k, torch.ones(1023, dtype=torch.float64, device=dev), unordered=unordered)
+    b.update(torch.arange(1024, 2048, device=dev), torch.full((1024,), 7.0, dtype=torch.float64, device=dev))
+    for v in (a, b):
+        v.destroy()
+    got = slab.get(torch.arange(0, 2048, device=dev)).cpu().numpy()
+    np.testing.assert_array_equal(got[:1023], np.full(1023, 3.0))
+    assert got[1023] == 0.0
+    np.testing.assert_array_equal(got[1024:], np.full(1024, 7.0))
+    slab.destroy()
+
+
+def test_matrix_views(gpu):
+    """Rows of a 17-column Double slab (row pitch 18 elements = 144 B: views start every 16 rows)."""
+    dev = torch.device("cuda", gpu)
+    slab = PartialMatrix(RangePartition(0, 0, 64), 17, "double", gpu)
+    views = [PartialMatrix.view(slab, RangePartition(j, 16 * j, 16 * (j + 1)), 16 * j) for j in range(4)]
+    with pytest.raises(ValueError):  # 8 rows in: 1152 B, not 256-byte aligned
+        PartialMatrix.view(slab, RangePartition(9, 8, 16), 8)
+    rng = np.random.default_rng(5)
+    want = np.zeros((64, 17))
+    for j, v in enumerate(views):
+        r = rng.integers(16 * j, 16 * (j + 1), 500).astype(np.int64)
+        c = rng.integers(0, 17, 500).astype(np.int32)
+        x = rng.integers(-50, 50, 500).astype(np.float64)  # small integers: exact in any order
+        v.update(torch.from_numpy(r).to(dev), torch.from_numpy(c).to(dev), torch.from_numpy(x).to(dev))
+        np.add.at(want, (r, c), x)
+    got = slab.getRows(torch.arange(0, 64, device=dev)).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    with pytest.raises(ArrayIndexOutOfBoundsException):  # a view's own column check
+        views[2].update(np.array([33]), np.array([17], np.int32), np.array([1.0]))
+    for v in views:
+        v.destroy()
+    slab.destroy()
