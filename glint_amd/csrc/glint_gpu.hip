@@ -1245,6 +1245,17 @@ int glint_shards_sync(glint_shard_t* shards, void** streams, int n, int* rcs, in
     rcs[i] = hipMemcpyAsync(h[i], s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, (hipStream_t)streams[i]) ==
                      hipSuccess ? GLINT_OK : GLINT_EDEVICE;
   }
+  static EnvKnob flush_knob("GLINT_SYNC_FLUSH");
+  if (flush_knob.get([](const char* e) { return e ? atoll(e) : 1LL; }) != 0) {
+    // a query submits what the runtime holds back for the stream, so every copy is on its queue
+    // before the first wait (without it the copies of streams sharing a hardware queue went out one
+    // per wait, ~25 us apart, after the last push)
+    for (int i = 0; i < n; ++i) {
+      DeviceGuard g(shards[i]->device);
+      (void)hipStreamQuery((hipStream_t)streams[i]);
+    }
+    (void)hipGetLastError();
+  }
   int rc = GLINT_OK;
   for (int i = 0; i < n; ++i) {
     glint_shard* s = shards[i];
