@@ -32,6 +32,7 @@ SIGNATURES = {
     "glint_shard_create": (_I, [_I, _I, _I64, _I64, _I32, C.POINTER(_P)]),
     "glint_shard_create_cyclic": (_I, [_I, _I, _I32, _I32, _I64, _I32, C.POINTER(_P)]),
     "glint_shard_create_in": (_I, [_P, _I64, _I64, _I64, C.POINTER(_P)]),
+    "glint_vec_push_dev_shards": (_I, [_P, _I, _P, _P, _I64, _P, _P]),
     "glint_shard_destroy": (_I, [_P]),
     "glint_shard_zero": (_I, [_P]),
     "glint_shard_info": (_I, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I), C.POINTER(_I)]),

@@ -414,6 +414,107 @@ __global__ __launch_bounds__(kTPB) void push_scatter_kernel(PushArgs<V> a, int f
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// several range shards in one push (glint_vec_push_dev_shards): the partitions one server hosts, as
+// one launch sequence -- a validation pass over the keys, then one scatter that sends each record's
+// aggregate to the shard whose range holds its key
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxSetShards = 64;
+template <typename V>
+struct ShardSet {
+  int n;
+  i64 start[kMaxSetShards];  // ascending, ranges disjoint
+  i64 end[kMaxSetShards];
+  V* data[kMaxSetShards];
+};
+
+// index of the shard whose [start, end) holds key, or -1 (RangePartitioner.partition restated over the
+// shards' own ranges: the first start > key, one back)
+__device__ __forceinline__ int set_find(const i64* st, const i64* en, int n, i64 key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (st[mid] <= key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo > 0 && key < en[lo - 1] ? lo - 1 : -1;
+}
+
+// *bad = ~(first record whose key is in no shard), 0 if none (atomicMax of ~index)
+template <typename V>
+__global__ __launch_bounds__(kTPB) void set_validate_kernel(const i64* __restrict__ keys, i64 n, ShardSet<V> set,
+                                                            u64* bad) {
+  __shared__ i64 st[kMaxSetShards], en[kMaxSetShards];
+  if (threadIdx.x < set.n) {
+    st[threadIdx.x] = set.start[threadIdx.x];
+    en[threadIdx.x] = set.end[threadIdx.x];
+  }
+  __syncthreads();
+  u64 b = 0;
+  const i64 stride = (i64)gridDim.x * kTPB;
+  for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
+    if (set_find(st, en, set.n, keys[i]) < 0) b = max(b, ~(u64)i);
+  for (int d = 32; d > 0; d >>= 1) b = max(b, (u64)__shfl_xor((unsigned long long)b, d));
+  if ((threadIdx.x & 63) == 0 && b) atomicMax((unsigned long long*)bad, (unsigned long long)b);
+}
+
+__global__ void set_gate_kernel(const u64* bad, u64* gate) {
+  if (threadIdx.x == 0) *gate = *bad;
+}
+
+// push_scatter over the set: the LDS hash aggregates by key, and each aggregate goes to its shard
+template <typename V>
+__global__ __launch_bounds__(kTPB) void set_scatter_kernel(const i64* __restrict__ keys, const V* __restrict__ vals,
+                                                           i64 n, ShardSet<V> set, const u64* bad) {
+  if (*bad != 0ull) return;  // a key outside every shard: nothing is applied
+  const i64 nchunks = (n + kScatterChunk - 1) / kScatterChunk;
+  typedef typename LdsAcc<V>::T A;
+  __shared__ u64 hk[kHashSlots];
+  __shared__ A hv[kHashSlots];
+  __shared__ i64 st[kMaxSetShards], en[kMaxSetShards];
+  __shared__ V* dp[kMaxSetShards];
+  const int tid = threadIdx.x;
+  if (tid < set.n) {
+    st[tid] = set.start[tid];
+    en[tid] = set.end[tid];
+    dp[tid] = set.data[tid];
+  }
+  for (int q = tid; q < kHashSlots; q += kTPB) { hk[q] = kEmpty; hv[q] = A(0); }
+  __syncthreads();
+  for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const i64 cbase = ch * kScatterChunk;
+#pragma unroll 2
+    for (int q = tid; q < kScatterChunk; q += kTPB) {
+      const i64 i = cbase + q;
+      if (i >= n) break;
+      const u64 ua = (u64)keys[i];  // in some shard (validated)
+      const V val = vals[i];
+      u32 h = (u32)((ua * 0x9E3779B97F4A7C15ull) >> (64 - 12));
+      for (;;) {
+        const u64 cur = __hip_atomic_load(&hk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == ua) break;
+        if (cur == kEmpty) {
+          const u64 prev = atomicCAS(&hk[h], kEmpty, ua);
+          if (prev == kEmpty || prev == ua) break;
+        }
+        h = (h + 1) & (kHashSlots - 1);
+      }
+      lds_add(&hv[h], (A)val);
+    }
+    __syncthreads();
+    for (int q = tid; q < kHashSlots; q += kTPB) {
+      const u64 key = hk[q];
+      if (key != kEmpty) {
+        const int j = set_find(st, en, set.n, (i64)key);
+        gadd(dp[j] + ((i64)key - st[j]), (V)hv[q]);
+        hk[q] = kEmpty;
+        hv[q] = A(0);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // A gated push (glint_vec_push_dev_gated): its LaunchCtl learns, on the device, whether the gate word
 // is set; push_check and push_apply then do nothing, and the tail is empty (brk_enc stays 0).
 __global__ void push_gate_kernel(const u64* gate, LaunchCtl* ctl) {
@@ -890,6 +991,35 @@ int push_mat_t(glint_shard* s, const i64* k, const int32_t* c, const void* v, i6
   return launch_push<V, true>(s, k, c, v, n, f, st);
 }
 
+// glint_vec_push_dev_shards' launches: the set's ranges and data pointers by value, its verdict in the
+// first shard's scratch word
+template <typename V>
+int launch_set_push(glint_shard* const* sh, int m, const i64* keys, const void* vals, i64 n, u64* gate,
+                    hipStream_t st) {
+  glint_shard* s0 = sh[0];
+  ShardSet<V> set{};
+  set.n = m;
+  for (int j = 0; j < m; ++j) {
+    set.start[j] = sh[j]->part.start;
+    set.end[j] = sh[j]->part.start + sh[j]->part.size;
+    set.data[j] = (V*)sh[j]->data;
+  }
+  if (!s0->d_word && hipMalloc((void**)&s0->d_word, 256) != hipSuccess) {
+    (void)hipGetLastError();
+    s0->d_word = nullptr;
+    return GLINT_ENOMEM;
+  }
+  HIPCHK(hipMemsetAsync(s0->d_word, 0, sizeof(u64), st));
+  const unsigned gv = grid_for(n, (i64)kTPB * 16, (i64)s0->cus * 8);
+  HIPCHK(launch_k(s0, GLINT_K_PUSH_CHECK, set_validate_kernel<V>, gv, kTPB, st, keys, n, set, s0->d_word));
+  set_gate_kernel<<<1, 64, 0, st>>>(s0->d_word, gate);
+  HIPCHK(hipGetLastError());
+  const unsigned g2 = grid_for(n, kScatterChunk, (i64)s0->cus * 2);
+  HIPCHK(launch_k(s0, GLINT_K_PUSH_SCATTER, set_scatter_kernel<V>, g2, kTPB, st, keys, (const V*)vals, n, set,
+                  (const u64*)s0->d_word));
+  return GLINT_OK;
+}
+
 int create_common(glint_shard* s, int device, int dtype, int32_t cols, void* view_data = nullptr) {
   if (dtype < GLINT_I32 || dtype > GLINT_F64 || cols < 0) return GLINT_EINVAL;
   static EnvKnob hprof_knob("GLINT_HOST_PROF");
@@ -978,6 +1108,7 @@ void free_shard(glint_shard* s) {
     for (auto& e : s->det_ev)
       if (e) (void)hipEventDestroy(e);
     if (s->d_bin) (void)hipFree(s->d_bin);
+    if (s->d_word) (void)hipFree(s->d_word);
     if (s->d_binctl) (void)hipFree(s->d_binctl);
     if (s->d_hot) (void)hipFree(s->d_hot);
     if (s->h_hint) (void)hipHostFree(s->h_hint);
@@ -1364,6 +1495,47 @@ int glint_mat_push_dev_gated(glint_shard_t s, const int64_t* rows, const int32_t
     return GLINT_OK;
   }
   GLINT_DISPATCH(s->dtype, push_mat_t, s, (const i64*)rows, cols, vals, n, flags, pick(s, stream));
+}
+
+int glint_vec_push_dev_shards(glint_shard_t* shards, int m, const int64_t* keys, const void* vals, int64_t n,
+                              uint64_t* gate, void* stream) {
+  if (!shards || m <= 0 || m > kMaxSetShards || n < 0 || !gate || (n > 0 && (!keys || !vals))) return GLINT_EINVAL;
+  std::vector<glint_shard*> v(shards, shards + m);
+  for (glint_shard* s : v)
+    if (!s || s->part.cols != 0 || s->part.kind != 0 || s->dtype != v[0]->dtype || s->device != v[0]->device)
+      return GLINT_EINVAL;
+  std::sort(v.begin(), v.end(), [](const glint_shard* a, const glint_shard* b) { return a->part.start < b->part.start; });
+  for (int j = 1; j < m; ++j)  // disjoint ranges (each once)
+    if (v[j - 1]->part.start + v[j - 1]->part.size > v[j]->part.start || v[j - 1] == v[j]) return GLINT_EINVAL;
+  std::vector<glint_shard*> order(v);  // every shard's lock, taken in address order, for the whole call
+  std::sort(order.begin(), order.end());
+  struct Locks {
+    std::vector<glint_shard*>& o;
+    size_t k = 0;
+    ~Locks() {
+      for (size_t i = 0; i < k; ++i) o[i]->mu.unlock();
+    }
+  } locks{order};
+  for (; locks.k < order.size(); ++locks.k) order[locks.k]->mu.lock();
+  DeviceGuard g(v[0]->device);
+  hipStream_t st = (hipStream_t)stream;
+  for (glint_shard* s : v) {
+    if (int rc = dev_order_after_host(s, st)) return rc;
+    (void)pick(s, stream);
+  }
+  u64* gd = (u64*)host_dev_ptr(gate, sizeof(u64), sizeof(u64));
+  if (!gd) gd = (u64*)gate;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(gd, 0, sizeof(u64), st));
+    return GLINT_OK;
+  }
+  switch (v[0]->dtype) {
+    case GLINT_F64: return launch_set_push<double>(v.data(), m, (const i64*)keys, vals, n, gd, st);
+    case GLINT_F32: return launch_set_push<float>(v.data(), m, (const i64*)keys, vals, n, gd, st);
+    case GLINT_I64: return launch_set_push<long long>(v.data(), m, (const i64*)keys, vals, n, gd, st);
+    case GLINT_I32: return launch_set_push<int>(v.data(), m, (const i64*)keys, vals, n, gd, st);
+    default: return GLINT_EINVAL;
+  }
 }
 
 int glint_vec_pull_dev(glint_shard_t s, const int64_t* keys, void* out, int64_t n, void* stream) {

@@ -148,6 +148,7 @@ struct glint_shard {
   const PullDst* pull_tab = nullptr;  // set only while a pull batch with direct answers dispatches
   int pull_nm = 0;
   u64* gate = nullptr;  // set only while a gated device push launches (glint_*_push_dev_gated)
+  u64* d_word = nullptr;  // device scratch of glint_vec_push_dev_shards (the set's verdict), 256 B
   int ring_next = 0;
   uint64_t ticket_next = 0;
   // tickets of ring entries whose launch failed after their tickets were handed out: a wait that

@@ -506,6 +506,16 @@ class _Distributed:
         self._slab_keyed = self.world == 1 and not d.any()
         self._delta = d
 
+    def _gate(self):
+        """(address, int64 view) of the pinned host word a gated push writes its verdict into: one per
+        model, used under _gate_lock."""
+        if getattr(self, "_gate_buf", None) is None:
+            from .shard import HostBuffer
+            self._gate_lock = threading.Lock()
+            self._gate_buf = HostBuffer(64)
+            self._gate_arr = self._gate_buf.array(np.int64, 1)
+        return self._gate_buf.ptr, self._gate_arr
+
     def _push_gated(self, keys: torch.Tensor, args: tuple, deterministic: bool) -> bool:
         """A world of one with one partition (or a slab holding all of them, slab_shards): the batch
         is the shard's push as it is. The key check
@@ -532,15 +542,11 @@ class _Distributed:
             # The verdict word lives in pinned host memory (a HostBuffer): read after the one wait,
             # with no device-to-host copy (GLINT_GATE_HOST=0: a device word and a copy, for A/B)
             if os.environ.get("GLINT_GATE_HOST", "1") != "0":
-                if getattr(self, "_gate_buf", None) is None:
-                    from .shard import HostBuffer
-                    self._gate_lock = threading.Lock()  # one word per model: one gated push at a time
-                    self._gate_buf = HostBuffer(64)
-                    self._gate_word = self._gate_buf.array(np.int64, 1)
-                with self._gate_lock:
-                    sh.update(*args, gate=self._gate_buf.ptr, validate=True, sync=False)
+                gptr, word = self._gate()
+                with self._gate_lock:  # one word per model: one gated push at a time
+                    sh.update(*args, gate=gptr, validate=True, sync=False)
                     sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
-                    b = int(self._gate_word[0])
+                    b = int(word[0])
             else:
                 bad = torch.empty(1, dtype=torch.int64, device=keys.device)
                 sh.update(*args, gate=bad, validate=True, sync=False)
@@ -625,6 +631,43 @@ class DistributedBigVector(_Distributed):
         self.dtype = _TORCH_DTYPES[np.dtype(np_dtype)]
         self._slab_plan(np_dtype)
 
+
+    def _push_set(self, keys: torch.Tensor, values: torch.Tensor) -> bool:
+        """World 1, several partitions, no key-spanning slab, a sparse batch (fewer records than 1/8 of
+        the keys, where every shard push would take the atomic scatter anyway): ONE launch sequence for
+        all local shards (glint_vec_push_dev_shards) -- the keys checked against the shards' ranges,
+        then one scatter sending each aggregate to its shard -- in place of the route, the split and a
+        push per partition. A key outside the key space applies nothing and raises as the route would.
+        GLINT_DIST_SET=0: off (A/B)."""
+        lib = N.load()
+        m = len(self.shards)
+        if not (self.world == 1 and m > 1 and m <= 64 and isinstance(self.partitioner, RangePartitioner)
+                and keys.is_cuda and self._on_shard_device(keys) and values.device == keys.device
+                and all(hasattr(sh, "handle") for sh in self.shards)
+                and getattr(lib, "glint_vec_push_dev_shards", None) is not None
+                and os.environ.get("GLINT_DIST_SET", "1") != "0"):
+            return False
+        n = keys.numel()
+        if n * 8 >= self.router.nkeys:
+            return False
+        keys = keys.contiguous()
+        values = values.contiguous()
+        for sh in self.shards:  # (their dtype and device: the library checks the set agrees)
+            sh._check_dev(n, keys, values=values)
+        hs = getattr(self, "_set_handles", None)
+        if hs is None:
+            hs = self._set_handles = (C.c_void_p * m)(*[sh.handle for sh in self.shards])
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        gptr, word = self._gate()
+        with self._gate_lock:
+            check(lib.glint_vec_push_dev_shards(hs, m, keys.data_ptr(), values.data_ptr(), n, gptr, stream))
+            self.shards[0].sync(stream)
+            b = int(word[0])
+        if b != 0:
+            i = ~b
+            raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.router.nkeys})")
+        return True
+
     def _push_slab(self, keys: torch.Tensor, values: torch.Tensor) -> bool:
         """Every rank's partitions in one slab (_slab_plan): the route writes each key rebased into
         the hosting rank's slab (glint_route_gather_rebased_dev), the exchange sends the records as
@@ -649,7 +692,7 @@ class DistributedBigVector(_Distributed):
             raise ValueError("keys and values differ in length")
         if values.device == keys.device and self._push_gated(keys, (keys, values.contiguous()), deterministic):
             return True
-        if not deterministic and self._push_slab(keys, values):
+        if not deterministic and (self._push_set(keys, values) or self._push_slab(keys, values)):
             return True
         if keys.is_cuda and values.device == keys.device:
             ex, _, sk, _, sv = self._begin_fused(keys, vals=values.contiguous())

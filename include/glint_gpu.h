@@ -88,6 +88,19 @@ int glint_shard_create(int device, int dtype, int64_t start, int64_t end, int32_
 int glint_shard_create_cyclic(int device, int dtype, int32_t index, int32_t num_partitions,
                               int64_t num_keys, int32_t cols, glint_shard_t* out);
 
+/* One device-resident push into several range vector shards of one device and type at once (up to
+ * 64, disjoint ranges, any order): each record goes to the shard whose range holds its key -- the
+ * partitions one server hosts, applied by one launch sequence where the reference sends a message per
+ * partition (AsyncBigVector.scala:96-98) and each partition's actor applies its own
+ * (PartialVector.scala:35-43). The batch is checked first: a key in no shard's range applies NOTHING
+ * (mapPartitions throws before sending, AsyncBigVector.scala:96-98) and *gate receives ~(first such
+ * record), else 0 -- gate is a device word or a glint_host_alloc word the caller reads after waiting on
+ * `stream`. Unordered sums (as GLINT_PUSH_UNORDERED; exact for Int/Long). Every shard's lock is held
+ * for the call; each is ordered after its host-pointer work and marked for the next sync like any
+ * device-resident call (glint_shards_sync / glint_shard_sync on `stream`). */
+int glint_vec_push_dev_shards(glint_shard_t* shards, int n_shards, const int64_t* keys, const void* vals,
+                              int64_t n, uint64_t* gate, void* stream);
+
 /* Slabs: the partitions one server hosts, kept in one allocation. A range shard (vector, or matrix
  * rows of the slab's width) over RangePartition(start, end) whose elements are the slab's rows
  * [offset, offset + end - start) -- a view: it reads and writes them as they are, and is a shard like

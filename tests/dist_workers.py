@@ -264,6 +264,40 @@ def _slab_case(nkeys, mps, dtype, keyed, n=60_000):
     return body
 
 
+def _set_case(nkeys, mps, dtype, n=20_000):
+    """World 1, sparse unordered device pushes (fewer records than nkeys / 8): one push for all local
+    shards (glint_vec_push_dev_shards via DistributedBigVector._push_set), against the oracle's replay;
+    a bad key applies nothing and raises the route's exception."""
+    def body(client, rank, world, dev):
+        assert world == 1
+        _, np_dtype = resolve_dtype(dtype)
+        vec = client.vector(nkeys, dtype, modelsPerServer=mps)
+        assert not vec._slab_keyed and n * 8 < nkeys
+        calls = []
+        orig = vec._push_set
+        vec._push_set = lambda k, v: calls.append(1) or orig(k, v)
+        ref = O.OracleVector(O.part_range(0, nkeys), resolve_dtype(dtype)[0])
+        for step in range(3):
+            k, v = _batch(7000 + step, n, nkeys, np_dtype)
+            vec.push(torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev))
+            assert ref.update(k, v) == -1
+        allk = np.arange(nkeys, dtype=np.int64)
+        want, _ = ref.get(allk)
+        got = vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy()
+        np.testing.assert_array_equal(got, want)
+        for bad in ([3, nkeys, 9], [-1, 4], [nkeys + 2**32]):
+            b = np.array(bad, dtype=np.int64)
+            try:
+                vec.push(torch.from_numpy(b).to(dev), torch.from_numpy(np.ones(b.size, np_dtype)).to(dev))
+                raise AssertionError(f"bad key {bad} accepted")
+            except IndexOutOfBoundsException as e:
+                assert f"record {[i for i, x in enumerate(bad) if not 0 <= x < nkeys][0]})" in str(e), str(e)
+        np.testing.assert_array_equal(vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy(), want)
+        assert len(calls) == 6
+        vec.destroy()
+    return body
+
+
 # HBM shards only (test_gpu_parity.test_dist_exchange_on_gpu): world 1 with the partitions in one slab
 GPU_CASES = {
     "vec_slab_long_mps8": _slab_case(8 * 4096, 8, "long", keyed=True),
@@ -271,6 +305,7 @@ GPU_CASES = {
     "vec_slab_long_mps3_unaligned": _slab_case(3 * 1000 + 1, 3, "long", keyed=False),  # (rebased route)
     "vec_range_mps4_aligned": _vector_case(4 * 4096, 4, RangePartitioner.apply, "double"),
     "mat_range_mps4_aligned": _matrix_case(1_024, 17, 4),
+    "vec_set_long_mps8": _set_case(8 * 50_000 + 5, 8, "long"),
 }
 
 CASES = {

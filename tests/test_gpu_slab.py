@@ -4,7 +4,9 @@ A view is a shard like any other -- its own RangePartition, key check, stream an
 whose elements are rows of the slab. These tests pin the C ABI's contract (include/glint_gpu.h): the
 views and the slab see one memory; a slab with views takes device-resident calls only, each ordered
 after the views' host-pointer work; views are destroyed first; offsets are checked. The world-1
-exchange on top of it (one push on the slab for all partitions) is dist_workers' slab cases."""
+exchange on top of it (one push on the slab for all partitions) is dist_workers' slab cases. Last, the
+other way to push a server's partitions at once: glint_vec_push_dev_shards (one launch sequence over
+several separately allocated shards; dist_workers' set case drives it through DistributedBigVector)."""
 import numpy as np
 import pytest
 import torch
@@ -127,3 +129,72 @@ def test_matrix_views(gpu):
     for v in views:
         v.destroy()
     slab.destroy()
+
+
+# ---- several shards in one push (glint_vec_push_dev_shards) --------------------------------------------
+def _set_push(shards, keys, vals, gate):
+    import ctypes as C
+    from glint_amd import _native as N
+    hs = (C.c_void_p * len(shards))(*[s.handle for s in shards])
+    st = torch.cuda.current_stream(keys.device).cuda_stream
+    return N.load().glint_vec_push_dev_shards(hs, len(shards), keys.data_ptr(), vals.data_ptr(), keys.numel(),
+                                              gate.data_ptr(), st)
+
+
+@pytest.mark.parametrize("dtype", ["long", "double"])
+def test_set_push_routes_each_record_to_its_shard(gpu, dtype):
+    """Three range shards given out of order, with a gap between two ranges: each record lands in the
+    shard that holds its key (duplicates summed); a key in the gap or outside applies nothing and the
+    gate holds ~(first such record). Long: bit-exact; Double: small integers, exact in any order."""
+    dev = torch.device("cuda", gpu)
+    ranges = [(5000, 9000), (0, 3000), (3000, 4500)]  # (4500, 5000) belongs to no shard
+    shards = [PartialVector(RangePartition(i, a, b), dtype, gpu) for i, (a, b) in enumerate(ranges)]
+    tdt = torch.int64 if dtype == "long" else torch.float64
+    rng = np.random.default_rng(11)
+    k = np.concatenate([rng.integers(0, 4500, 30_000), rng.integers(5000, 9000, 30_000)]).astype(np.int64)
+    rng.shuffle(k)
+    v = rng.integers(-20, 20, k.size)
+    gate = torch.full((1,), 7, dtype=torch.int64, device=dev)
+    kt, vt = torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev).to(tdt)
+    for _ in range(2):
+        assert _set_push(shards, kt, vt, gate) == 0
+    shards[0].sync(torch.cuda.current_stream(dev).cuda_stream)
+    assert int(gate.item()) == 0
+    want = np.zeros(9000, np.int64)
+    np.add.at(want, k, 2 * v)
+    for sh, (a, b) in zip(shards, ranges):
+        got = sh.get(torch.arange(a, b, device=dev)).cpu().numpy()
+        np.testing.assert_array_equal(got.astype(np.int64), want[a:b])
+    # a key in the gap (record 2) and one past the end (record 4): nothing applied
+    bad = torch.tensor([10, 20, 4700, 30, 9000], dtype=torch.int64, device=dev)
+    assert _set_push(shards, bad, torch.ones(5, dtype=tdt, device=dev), gate) == 0
+    shards[0].sync(torch.cuda.current_stream(dev).cuda_stream)
+    assert int(gate.item()) == ~2
+    for sh, (a, b) in zip(shards, ranges):
+        np.testing.assert_array_equal(sh.get(torch.arange(a, b, device=dev)).cpu().numpy().astype(np.int64), want[a:b])
+    # an empty batch: verdict 0
+    gate.fill_(5)
+    assert _set_push(shards, torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, dtype=tdt, device=dev),
+                     gate) == 0
+    torch.cuda.synchronize(dev)
+    assert int(gate.item()) == 0
+    for sh in shards:
+        sh.destroy()
+
+
+def test_set_push_rejects_bad_sets(gpu):
+    from glint_amd import _native as N
+    dev = torch.device("cuda", gpu)
+    a = PartialVector(RangePartition(0, 0, 100), "double", gpu)
+    b = PartialVector(RangePartition(1, 50, 150), "double", gpu)   # overlaps a
+    c = PartialVector(RangePartition(2, 200, 300), "float", gpu)   # another type
+    m = PartialMatrix(RangePartition(3, 400, 500), 4, "double", gpu)
+    d = PartialVector(RangePartition(4, 100, 200), "double", gpu)
+    k = torch.tensor([1], dtype=torch.int64, device=dev)
+    x = torch.ones(1, dtype=torch.float64, device=dev)
+    g = torch.zeros(1, dtype=torch.int64, device=dev)
+    for bad in ([a, b], [a, c], [a, m], [a, a], []):  # overlap, mixed types, a matrix, twice, none
+        assert _set_push(bad, k, x, g) == N.GLINT_EINVAL
+    assert _set_push([d, a], k, x, g) == 0
+    for s in (a, b, c, m, d):
+        s.destroy()
