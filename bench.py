@@ -319,10 +319,21 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         u_note = " (U estimated)"
         tag = f"exchange_2p{log2_keys}" + (f"_mps{mps}" if mps > 1 else "")
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
+        # the path DistributedBigVector.push takes (dist.py: _push_gated, _push_set, _push_slab, the route)
+        set_path = (slab is None and world == 1 and 1 < mps <= 64 and nrec * 8 < partitioner.size
+                    and os.environ.get("GLINT_DIST_SET", "1") != "0")
+        if world == 1 and mps == 1:
+            how = "one validating push (the push checks the keys), no route"
+        elif slab is not None and world == 1:
+            how = f"the rank's {mps} partitions in one slab: one validating push, no route"
+        elif slab is not None:
+            how = f"route (keys rebased into each rank's slab) + RCCL all-to-all + one slab push per rank"
+        elif set_path:
+            how = f"one validated scatter over the {mps} local shards (glint_vec_push_dev_shards), no route"
+        else:
+            how = "route + gather + RCCL all-to-all + local push" + ("es" if mps > 1 else "")
         workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({P}, "
-                    f"{partitioner.size}), {mps} partition(s) per GPU; route + gather + RCCL all-to-all + "
-                    f"local push" + ("es" if mps > 1 and slab is None else "") +
-                    (f" (the rank's {mps} partitions in one slab: one push at world size 1)" if slab is not None else ""))
+                    f"{partitioner.size}), {mps} partition(s) per GPU; {how}")
     elif pat in ("dense", "pull"):
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
         vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1

@@ -632,26 +632,24 @@ class DistributedBigVector(_Distributed):
         self._slab_plan(np_dtype)
 
 
-    def _push_set(self, keys: torch.Tensor, values: torch.Tensor) -> bool:
-        """World 1, several partitions, no key-spanning slab, a sparse batch (fewer records than 1/8 of
-        the keys, where every shard push would take the atomic scatter anyway): ONE launch sequence for
-        all local shards (glint_vec_push_dev_shards) -- the keys checked against the shards' ranges,
-        then one scatter sending each aggregate to its shard -- in place of the route, the split and a
-        push per partition. A key outside the key space applies nothing and raises as the route would.
-        GLINT_DIST_SET=0: off (A/B)."""
-        lib = N.load()
+    def _set_ok(self, n: int) -> bool:
+        """Whether a sparse batch of n records (fewer than 1/8 of this rank's keys, where every shard
+        push would take the atomic scatter anyway) can go to all local shards in ONE launch sequence
+        (glint_vec_push_dev_shards): range vector shards on this GPU, 2..64 of them. GLINT_DIST_SET=0:
+        off (A/B)."""
         m = len(self.shards)
-        if not (self.world == 1 and m > 1 and m <= 64 and isinstance(self.partitioner, RangePartitioner)
-                and keys.is_cuda and self._on_shard_device(keys) and values.device == keys.device
+        if not (1 < m <= 64 and isinstance(self.partitioner, RangePartitioner) and self.device.type == "cuda"
                 and all(hasattr(sh, "handle") for sh in self.shards)
-                and getattr(lib, "glint_vec_push_dev_shards", None) is not None
+                and getattr(N.load(), "glint_vec_push_dev_shards", None) is not None
                 and os.environ.get("GLINT_DIST_SET", "1") != "0"):
             return False
+        return n * 8 < sum(sh.size for sh in self.shards)
+
+    def _set_push(self, keys: torch.Tensor, values: torch.Tensor) -> int:
+        """glint_vec_push_dev_shards over the local shards, then the one wait: -> the verdict word
+        (0, or ~ the first record whose key is in no local shard; nothing applied then)."""
         n = keys.numel()
-        if n * 8 >= self.router.nkeys:
-            return False
-        keys = keys.contiguous()
-        values = values.contiguous()
+        m = len(self.shards)
         for sh in self.shards:  # (their dtype and device: the library checks the set agrees)
             sh._check_dev(n, keys, values=values)
         hs = getattr(self, "_set_handles", None)
@@ -660,9 +658,20 @@ class DistributedBigVector(_Distributed):
         stream = torch.cuda.current_stream(self.device).cuda_stream
         gptr, word = self._gate()
         with self._gate_lock:
-            check(lib.glint_vec_push_dev_shards(hs, m, keys.data_ptr(), values.data_ptr(), n, gptr, stream))
+            check(N.load().glint_vec_push_dev_shards(hs, m, keys.data_ptr(), values.data_ptr(), n, gptr, stream))
             self.shards[0].sync(stream)
-            b = int(word[0])
+            return int(word[0])
+
+    def _push_set(self, keys: torch.Tensor, values: torch.Tensor) -> bool:
+        """World 1, several partitions, no key-spanning slab, a sparse batch: one call for all local
+        shards (_set_push) -- the keys checked against the shards' ranges, then one scatter sending each
+        aggregate to its shard -- in place of the route, the split and a push per partition. A key
+        outside the key space applies nothing and raises as the route would."""
+        if not (self.world == 1 and keys.is_cuda and self._on_shard_device(keys) and values.device == keys.device
+                and self._set_ok(keys.numel())):
+            return False
+        keys = keys.contiguous()
+        b = self._set_push(keys, values.contiguous())
         if b != 0:
             i = ~b
             raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.router.nkeys})")
@@ -701,6 +710,13 @@ class DistributedBigVector(_Distributed):
             order, ex = self._begin(keys)
             rk = ex.forward(keys.index_select(0, order))
             rv = ex.forward(values.index_select(0, order.to(values.device)))
+        if not deterministic and self._set_ok(rk.numel()) and rk.numel():
+            # a sparse receive: every local partition's records in one call, no split (keys validated by
+            # the route, so the verdict is 0)
+            if self._set_push(self._to_shard(rk).contiguous(), self._to_shard(rv).contiguous()) != 0:
+                raise RuntimeError("routed records outside the local shards")
+            ex.raise_if_bad(keys, self.router.nkeys)
+            return True
         ops = []
         for j, sh, (k, v) in self._split(ex, rk, rv):
             if k.numel():

@@ -265,22 +265,29 @@ def _slab_case(nkeys, mps, dtype, keyed, n=60_000):
 
 
 def _set_case(nkeys, mps, dtype, n=20_000):
-    """World 1, sparse unordered device pushes (fewer records than nkeys / 8): one push for all local
-    shards (glint_vec_push_dev_shards via DistributedBigVector._push_set), against the oracle's replay;
-    a bad key applies nothing and raises the route's exception."""
+    """Sparse unordered device pushes (fewer records than a rank's keys / 8): one push for all local
+    shards (glint_vec_push_dev_shards, DistributedBigVector._set_push) -- at world 1 in place of the
+    route (_push_set), at world > 1 (slabs off) for everything a rank receives -- against the oracle's
+    replay (every rank pushes the same batches); a bad key applies nothing and raises the route's
+    exception."""
     def body(client, rank, world, dev):
-        assert world == 1
         _, np_dtype = resolve_dtype(dtype)
-        vec = client.vector(nkeys, dtype, modelsPerServer=mps)
-        assert not vec._slab_keyed and n * 8 < nkeys
+        if world > 1:
+            os.environ["GLINT_DIST_SLAB"] = "0"  # (the slab's rebased route would take these pushes)
+        try:
+            vec = client.vector(nkeys, dtype, modelsPerServer=mps)
+        finally:
+            os.environ.pop("GLINT_DIST_SLAB", None)
+        assert not vec._slab_keyed and n * 8 * world < nkeys
         calls = []
-        orig = vec._push_set
-        vec._push_set = lambda k, v: calls.append(1) or orig(k, v)
+        orig = vec._set_push
+        vec._set_push = lambda k, v: calls.append(1) or orig(k, v)
         ref = O.OracleVector(O.part_range(0, nkeys), resolve_dtype(dtype)[0])
         for step in range(3):
             k, v = _batch(7000 + step, n, nkeys, np_dtype)
             vec.push(torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev))
-            assert ref.update(k, v) == -1
+            for _ in range(world):
+                assert ref.update(k, v) == -1
         allk = np.arange(nkeys, dtype=np.int64)
         want, _ = ref.get(allk)
         got = vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy()
@@ -293,7 +300,9 @@ def _set_case(nkeys, mps, dtype, n=20_000):
             except IndexOutOfBoundsException as e:
                 assert f"record {[i for i, x in enumerate(bad) if not 0 <= x < nkeys][0]})" in str(e), str(e)
         np.testing.assert_array_equal(vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy(), want)
-        assert len(calls) == 6
+        # world 1: three good and three bad batches through the set push; world > 1: the bad batches
+        # send nothing (every rank's is bad), so only the good ones arrive
+        assert len(calls) == (6 if world == 1 else 3), len(calls)
         vec.destroy()
     return body
 

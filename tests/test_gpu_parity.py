@@ -642,7 +642,8 @@ def test_route_out_of_range_reports_first_bad(gpu):
     ("nccl", 1, "vec_slab_long_mps8"), ("nccl", 1, "vec_slab_double_mps4"), ("nccl", 1, "vec_slab_long_mps3_unaligned"),
     ("nccl", 1, "vec_range_mps4_aligned"), ("nccl", 1, "mat_range_mps4_aligned"), ("nccl", 1, "vec_set_long_mps8"),
     # world 2: every rank's slab, keys rebased by the route (rank r hosts r, r + 2, ...)
-    ("gloo", 2, "vec_slab_long_mps8"), ("gloo", 2, "vec_slab_long_mps3_unaligned"), ("gloo", 2, "vec_range_mps4_aligned")])
+    ("gloo", 2, "vec_slab_long_mps8"), ("gloo", 2, "vec_slab_long_mps3_unaligned"), ("gloo", 2, "vec_range_mps4_aligned"),
+    ("gloo", 2, "vec_set_long_mps8")])
 def test_dist_exchange_on_gpu(gpu, backend, world, case):
     import socket
     import torch.multiprocessing as mp
