@@ -1517,6 +1517,8 @@ int glint_vec_push_dev_shards(glint_shard_t* shards, int m, const int64_t* keys,
     }
   } locks{order};
   for (; locks.k < order.size(); ++locks.k) order[locks.k]->mu.lock();
+  for (glint_shard* s : v)  // a slab with views orders itself through their locks (held here if in the set)
+    if (!s->views.empty()) return GLINT_EINVAL;
   DeviceGuard g(v[0]->device);
   hipStream_t st = (hipStream_t)stream;
   for (glint_shard* s : v) {

@@ -97,7 +97,8 @@ int glint_shard_create_cyclic(int device, int dtype, int32_t index, int32_t num_
  * record), else 0 -- gate is a device word or a glint_host_alloc word the caller reads after waiting on
  * `stream`. Unordered sums (as GLINT_PUSH_UNORDERED; exact for Int/Long). Every shard's lock is held
  * for the call; each is ordered after its host-pointer work and marked for the next sync like any
- * device-resident call (glint_shards_sync / glint_shard_sync on `stream`). */
+ * device-resident call (glint_shards_sync / glint_shard_sync on `stream`). A slab with views is not
+ * a member (GLINT_EINVAL): push to its views, or to the slab alone. */
 int glint_vec_push_dev_shards(glint_shard_t* shards, int n_shards, const int64_t* keys, const void* vals,
                               int64_t n, uint64_t* gate, void* stream);
 

@@ -196,5 +196,12 @@ def test_set_push_rejects_bad_sets(gpu):
     for bad in ([a, b], [a, c], [a, m], [a, a], []):  # overlap, mixed types, a matrix, twice, none
         assert _set_push(bad, k, x, g) == N.GLINT_EINVAL
     assert _set_push([d, a], k, x, g) == 0
+    slab = PartialVector(RangePartition(5, 1000, 1064), "double", gpu)
+    view = PartialVector.view(slab, RangePartition(6, 600, 632), 32)
+    assert _set_push([slab, a], k, x, g) == N.GLINT_EINVAL  # a slab with views
+    assert _set_push([view, a], k, x, g) == 0                # its view is a shard like any other
+    torch.cuda.synchronize(dev)
+    view.destroy()
+    slab.destroy()
     for s in (a, b, c, m, d):
         s.destroy()

@@ -43,6 +43,10 @@ SHAPES = {
     "bin_fsort": (["ld4", "ld8"], ["st8"]),
     "bin_plan": (["ld4"], ["st8"]),
     "bin_apply2": (["*ld4", "*ld8", "rmw16"], ["rmw16"]),
+    # one push over several shards (glint_vec_push_dev_shards): the key check streams the keys, the
+    # scatter is push_scatter's shape
+    "set_validate": (["ld8"], []),
+    "set_scatter": (["ld8", "*gather8"], ["*atomic8"]),
 }
 
 
@@ -97,7 +101,8 @@ def main():
     # whole-push scatter runs alone) -- (the apply may run once per window of records, so a kernel's
     # bytes per push = its mean per dispatch x dispatches / pushes)
     once = [c for k, c in nf.items()
-            if k.startswith(("glint::push_check_kernel", "glint::bin_count_kernel", "glint::push_scatter_kernel"))]
+            if k.startswith(("glint::push_check_kernel", "glint::bin_count_kernel", "glint::push_scatter_kernel",
+                             "glint::set_scatter_kernel"))]
     pushes = max(once) if once else max(list(nf.values()) + [1])
     for name in sorted(set(fetch) | set(write)):
         per = nf.get(name, 0) / pushes
@@ -111,7 +116,7 @@ def main():
                          "correction": {"read_factor": rfac, "write_factor": wfac, "read_shapes": shapes[0],
                                         "write_shapes": shapes[1], "source": (cal_src or "MI355X_MICROARCH.md")
                                         + ": " + note}}
-        counted = ("push_" in name or "bin_" in name) and nf.get(name, 0) * 2 >= pushes
+        counted = ("push_" in name or "bin_" in name or "set_" in name) and nf.get(name, 0) * 2 >= pushes
         kernels[name]["counted"] = counted
         if counted:
             total += rd + wr
