@@ -260,6 +260,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     gen.manual_seed(42 + rank)
     cols = out = None
     push = pat in ("dense", "zipf", "matrix", "exchange")
+    how = ""  # the exchange line's push path (named below)
     scope = "per GPU" if not strong else f"1/{world} of the vector per GPU"
     fill_v = None
     u_note = ""
@@ -559,7 +560,9 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         "config": {"workload": workload + u_note, "keys_per_gpu": n * (cols_n if mat else 1) * len(shards),
                    "records_per_step_per_gpu": nrec, "records_received_per_step_per_gpu": recv,
                    "distinct_keys_per_step_per_gpu": uniq, "key_dtype": "i64", "value_dtype": "f64",
-                   "parallelism": f"range-sharded x{world}, " + ("route + all-to-all exchange" if exch else "no exchange")},
+                   "parallelism": f"range-sharded x{world}, " + (
+                       "route + all-to-all exchange" if exch and world > 1 else
+                       "no exchange (world 1: " + how.split(",")[0] + ")" if exch else "no exchange")},
         "pct_hbm_peak_per_gpu": round(100.0 * value / world / HBM_PEAK_GBS, 2),
         "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
