@@ -451,9 +451,33 @@ __global__ __launch_bounds__(kTPB) void set_validate_kernel(const i64* __restric
   }
   __syncthreads();
   u64 b = 0;
-  const i64 stride = (i64)gridDim.x * kTPB;
-  for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
-    if (set_find(st, en, set.n, keys[i]) < 0) b = max(b, ~(u64)i);
+  if (((uintptr_t)keys & 15) == 0) {  // two keys per 16-B load, four loads in flight per lane
+    typedef __attribute__((ext_vector_type(2))) long long KP;
+    const i64 np = n >> 1, stride = (i64)gridDim.x * kTPB;
+    i64 p = (i64)blockIdx.x * kTPB + threadIdx.x;
+    for (; p + 3 * stride < np; p += 4 * stride) {
+      KP k[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) k[u] = __builtin_nontemporal_load(reinterpret_cast<const KP*>(keys) + p + u * stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const i64 i = 2 * (p + u * stride);
+        if (set_find(st, en, set.n, k[u].y) < 0) b = max(b, ~(u64)(i + 1));
+        if (set_find(st, en, set.n, k[u].x) < 0) b = max(b, ~(u64)i);
+      }
+    }
+    for (; p < np; p += stride) {
+      const KP k = __builtin_nontemporal_load(reinterpret_cast<const KP*>(keys) + p);
+      if (set_find(st, en, set.n, k.y) < 0) b = max(b, ~(u64)(2 * p + 1));
+      if (set_find(st, en, set.n, k.x) < 0) b = max(b, ~(u64)(2 * p));
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0 && set_find(st, en, set.n, keys[n - 1]) < 0)
+      b = max(b, ~(u64)(n - 1));
+  } else {
+    const i64 stride = (i64)gridDim.x * kTPB;
+    for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
+      if (set_find(st, en, set.n, keys[i]) < 0) b = max(b, ~(u64)i);
+  }
   for (int d = 32; d > 0; d >>= 1) b = max(b, (u64)__shfl_xor((unsigned long long)b, d));
   if ((threadIdx.x & 63) == 0 && b) atomicMax((unsigned long long*)bad, (unsigned long long)b);
 }
@@ -1010,7 +1034,7 @@ int launch_set_push(glint_shard* const* sh, int m, const i64* keys, const void* 
     return GLINT_ENOMEM;
   }
   HIPCHK(hipMemsetAsync(s0->d_word, 0, sizeof(u64), st));
-  const unsigned gv = grid_for(n, (i64)kTPB * 16, (i64)s0->cus * 8);
+  const unsigned gv = grid_for(n, (i64)kTPB * 16, (i64)s0->cus * 4);
   HIPCHK(launch_k(s0, GLINT_K_PUSH_CHECK, set_validate_kernel<V>, gv, kTPB, st, keys, n, set, s0->d_word));
   set_gate_kernel<<<1, 64, 0, st>>>(s0->d_word, gate);
   HIPCHK(hipGetLastError());

@@ -158,15 +158,20 @@ def test_set_push_routes_each_record_to_its_shard(gpu, dtype):
     kt, vt = torch.from_numpy(k).to(dev), torch.from_numpy(v).to(dev).to(tdt)
     for _ in range(2):
         assert _set_push(shards, kt, vt, gate) == 0
+    assert _set_push(shards, kt[1:], vt[1:], gate) == 0  # keys 8 B off a 16-B boundary, odd count
     shards[0].sync(torch.cuda.current_stream(dev).cuda_stream)
     assert int(gate.item()) == 0
     want = np.zeros(9000, np.int64)
     np.add.at(want, k, 2 * v)
+    np.add.at(want, k[1:], v[1:])
     for sh, (a, b) in zip(shards, ranges):
         got = sh.get(torch.arange(a, b, device=dev)).cpu().numpy()
         np.testing.assert_array_equal(got.astype(np.int64), want[a:b])
     # a key in the gap (record 2) and one past the end (record 4): nothing applied
     bad = torch.tensor([10, 20, 4700, 30, 9000], dtype=torch.int64, device=dev)
+    assert _set_push(shards, bad[3:], torch.ones(2, dtype=tdt, device=dev), gate) == 0  # unaligned, bad last
+    shards[0].sync(torch.cuda.current_stream(dev).cuda_stream)
+    assert int(gate.item()) == ~1
     assert _set_push(shards, bad, torch.ones(5, dtype=tdt, device=dev), gate) == 0
     shards[0].sync(torch.cuda.current_stream(dev).cuda_stream)
     assert int(gate.item()) == ~2
