@@ -727,8 +727,37 @@ class DistributedBigVector(_Distributed):
         ex.raise_if_bad(keys, self.router.nkeys)
         return True
 
+    def _pull_slab(self, keys: torch.Tensor) -> torch.Tensor:
+        """World 1 with every partition side by side in one slab (_slab_keyed): the batch's keys are
+        checked as the route checks them (glint_route_gather_dev with one partition: a read of the
+        keys, the raw 64-bit range) and the slab answers them in the caller's order in one gather --
+        no grouping, no per-partition pulls, no scatter back. A bad key raises the route's exception
+        (the slab's own check, which the gather makes on its (key - start).toInt, is not the one
+        reported)."""
+        keys = keys.contiguous()
+        n, dev = keys.numel(), keys.device
+        st = torch.cuda.current_stream(dev).cuda_stream
+        counts = torch.empty(1, dtype=torch.int64, device=dev)
+        bad = torch.empty(1, dtype=torch.int64, device=dev)
+        check(N.load().glint_route_gather_dev(keys.data_ptr(), None, None, 0, n, N.GLINT_ROUTE_RANGE, 1,
+                                              self.router.nkeys, None, counts.data_ptr(), None, None, None, None,
+                                              bad.data_ptr(), st))
+        out = torch.empty(n, dtype=self.dtype, device=dev)
+        try:
+            self.slab.get(keys, out=out)  # (one wait, on this stream: the check above is done too)
+        except ArrayIndexOutOfBoundsException:
+            pass  # outside the slab = outside the key space: the route's word names the record
+        b = int(bad.item())
+        if b != 0:
+            i = ~b
+            raise IndexOutOfBoundsException(f"key {int(keys[i])} (record {i}) outside [0, {self.router.nkeys})")
+        return out
+
     def pull(self, keys: torch.Tensor) -> torch.Tensor:
         keys = keys.reshape(-1).to(torch.int64)
+        if keys.is_cuda and self._slab_keyed and self._on_shard_device(keys) and \
+                os.environ.get("GLINT_DIST_SLAB_PULL", "1") != "0":
+            return self._pull_slab(keys)
         if keys.is_cuda:
             ex, order, sk, _, _ = self._begin_fused(keys, want_order=True)
             rk = ex.forward(sk)

@@ -260,6 +260,16 @@ def _slab_case(nkeys, mps, dtype, keyed, n=60_000):
         got = vec.pull(torch.from_numpy(allk).to(dev)).cpu().numpy()
         if np.dtype(np_dtype).kind != "f":
             np.testing.assert_array_equal(got, want)
+        # pulls of keys 2^32 away from real ones (a keyed slab's gather would alias them): the route's
+        # check rejects them on every path
+        for wrap in ([2**32 + 5], [3, -(2**32) + 1], [nkeys]):
+            try:
+                vec.pull(torch.tensor(wrap, dtype=torch.int64, device=dev))
+                raise AssertionError(f"pull of {wrap} accepted")
+            except IndexOutOfBoundsException as e:
+                assert f"(record {len(wrap) - 1})" in str(e), str(e)
+        q = torch.from_numpy(np.random.default_rng(5).integers(0, nkeys, 999)).to(dev)
+        np.testing.assert_array_equal(vec.pull(q).cpu().numpy(), got[q.cpu().numpy()])
         vec.destroy()
     return body
 
