@@ -321,7 +321,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         tag = f"exchange_2p{log2_keys}" + (f"_mps{mps}" if mps > 1 else "")
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
         # the path DistributedBigVector.push takes (dist.py: _push_gated, _push_set, _push_slab, the route)
-        set_path = (slab is None and world == 1 and 1 < mps <= 64 and nrec * 8 < partitioner.size
+        set_path = (slab is None and 1 < mps <= 64 and nrec * 8 < mps * n
                     and os.environ.get("GLINT_DIST_SET", "1") != "0")
         if world == 1 and mps == 1:
             how = "one validating push (the push checks the keys), no route"
@@ -329,8 +329,11 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
             how = f"the rank's {mps} partitions in one slab: one validating push, no route"
         elif slab is not None:
             how = f"route (keys rebased into each rank's slab) + RCCL all-to-all + one slab push per rank"
-        elif set_path:
+        elif set_path and world == 1:
             how = f"one validated scatter over the {mps} local shards (glint_vec_push_dev_shards), no route"
+        elif set_path:
+            how = (f"route + RCCL all-to-all + one validated scatter over the rank's {mps} shards "
+                   f"(glint_vec_push_dev_shards)")
         else:
             how = "route + gather + RCCL all-to-all + local push" + ("es" if mps > 1 else "")
         workload = (f"cfg4b: {world} GPU(s), {nrec} uniform keys per rank over RangePartitioner({P}, "
