@@ -32,6 +32,15 @@ shard of RangePartitioner(N, N * 2^17) rows (8 x 2^17 = the 2^20-row matrix at N
 DistributedBigVector.push (route + all-to-all + local push, AsyncBigVector.scala:96-121); the
 post-run check regenerates every rank's batches and compares the rank's shard with a torch fp64
 segment sum, and U (distinct elements a shard receives) is counted, not estimated.
+
+--batches K (push patterns): K batches of the same distribution from distinct seeds (the same
+permutation of the shard, fresh Zipf / uniform samples and values), pre-generated in HBM and rotated
+per step -- every push is a new message, as a server sees them (AsyncBigVector.scala:107-121) -- so
+no state the binned push keeps across pushes (the hot table, the latched front-end and whole-push
+hints) meets the same batch twice in a row. The post-run check replays all K batches.
+
+At N > 1 the line carries `devices`: every rank's device index and PCI address (all-gathered), and a
+run over RCCL fails if two ranks share a GPU.
 """
 from __future__ import annotations
 
@@ -70,6 +79,8 @@ def parse():
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the extra cfg2 (2^28) leg of the default 1-GPU run")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run shard check")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="push patterns: K different batches of the same distribution, rotated per step")
     ap.add_argument("--parts-per-gpu", type=int, default=1,
                     help="exchange only: range partitions hosted per GPU (modelsPerServer, Client.scala:63); "
                          "8 at one GPU is cfg4's own key space, RangePartitioner(8, 2^31)")
@@ -215,7 +226,7 @@ def segment_sums(v, counts, chunk: int = 1 << 22):
 
 
 def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: int, check: bool,
-             mps: int = 1) -> dict:
+             mps: int = 1, nb: int = 1) -> dict:
     """Builds the workload of one bench line, times `steps` pushes (or pulls) after `warmup`, checks
     the shard afterwards and returns the line's fields (without the CPU baseline)."""
     import numpy as np
@@ -245,7 +256,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         my_parts = [partitioner.all()[rank]]
     part = my_parts[0]
     slab = None
-    if exch and mps > 1:  # the rank's partitions as views of one slab (dist.slab_shards; GLINT_DIST_SLAB=0: off)
+    if exch and mps > 1:  # the rank's partitions as views of one slab (dist.slab_shards)
         from glint_amd.dist import slab_shards
         sv = slab_shards("vector", my_parts, 0, "double", local)
         if sv is not None:
@@ -264,16 +275,21 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     scope = "per GPU" if not strong else f"1/{world} of the vector per GPU"
     fill_v = None
     u_note = ""
+    batches = []  # [(keys, cols, vals, distinct elements)] of --batches K
     if pat == "matrix":
         # cfg5: rows Zipf(1.0) through a seeded permutation of the shard's rows, cols uniform [0, 512)
         rng = np.random.default_rng(42 + rank)
         nrec = 1 << 23
-        r = rng.permutation(n)[zipf_rows(rng, n, nrec)].astype(np.int64)
-        c = rng.integers(0, cols_n, nrec).astype(np.int32)
-        uniq = int(np.unique(r * cols_n + c).size)
-        keys = torch.from_numpy(r + part.start).to(dev)
-        cols = torch.from_numpy(c).to(dev)
-        vals = torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+        perm = rng.permutation(n)
+        for b in range(nb):
+            rb = rng if b == 0 else np.random.default_rng(100042 + 1000 * b + rank)
+            r = perm[zipf_rows(rb, n, nrec)].astype(np.int64)
+            c = rb.integers(0, cols_n, nrec).astype(np.int32)
+            batches.append((torch.from_numpy(r + part.start).to(dev), torch.from_numpy(c).to(dev),
+                            torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1,
+                            int(np.unique(r * cols_n + c).size)))
+        keys, cols, vals, uniq = batches[0]
+        uniq = int(np.mean([bt[3] for bt in batches]))
         tag = "matrix_2p17x512"
         bytes_per_step = 20.0 * nrec + 16.0 * uniq  # n(8+4+8) + U(8+8)
         workload = (f"cfg5 per GPU: {nrec} Zipf(1.0)-row x uniform-col triplets into a 2^17 x 512 Double "
@@ -304,15 +320,18 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         dv = DistributedBigVector(partitioner, shards, partitioner.size, np.float64, None, dev, slab=slab)
         nrec = 1 << 26
 
-        def batch(src):
+        def batch(src, b=0):
             kg = torch.Generator(device=dev)
-            kg.manual_seed(1042 + src)
+            kg.manual_seed(1042 + src + 100000 * b)
             vg = torch.Generator(device=dev)
-            vg.manual_seed(2042 + src)
+            vg.manual_seed(2042 + src + 100000 * b)
             k = torch.randint(0, partitioner.size, (nrec,), dtype=torch.int64, device=dev, generator=kg)
             return k, torch.rand(nrec, dtype=torch.float64, device=dev, generator=vg) * 2 - 1
 
-        keys, vals = batch(rank)
+        for b in range(nb):
+            kb, vb = batch(rank, b)
+            batches.append((kb, None, vb, None))
+        keys, vals = batches[0][0], batches[0][2]
         # distinct elements a rank receives per push: counted over all ranks' batches by the check,
         # the expected value until then
         P = world * mps
@@ -321,8 +340,7 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         tag = f"exchange_2p{log2_keys}" + (f"_mps{mps}" if mps > 1 else "")
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
         # the path DistributedBigVector.push takes (dist.py: _push_gated, _push_set, _push_slab, the route)
-        set_path = (slab is None and 1 < mps <= 64 and nrec * 8 < mps * n
-                    and os.environ.get("GLINT_DIST_SET", "1") != "0")
+        set_path = slab is None and 1 < mps <= 64 and nrec * 8 < mps * n
         if world == 1 and mps == 1:
             how = "one validating push (the push checks the keys), no route"
         elif slab is not None and world == 1:
@@ -342,6 +360,10 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         keys = torch.arange(part.start, part.end, dtype=torch.int64, device=dev)
         vals = torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
         nrec, uniq = n, n
+        if pat == "dense":  # K batches: the same keys, fresh values
+            batches = [(keys, None, vals, n)] + [
+                (keys, None, torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 2 - 1, n)
+                for _ in range(nb - 1)]
         if pat == "pull":  # PartialVector.get (PartialVector.scala:51-60) of every key of the shard
             shard.update(keys, vals)
             out = torch.empty(n, dtype=torch.float64, device=dev)
@@ -370,17 +392,30 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         ranks = ranks[ranks <= n][:nrec] - 1
         nrec = ranks.size
         perm = rng.permutation(n)
-        k = perm[ranks].astype(np.int64) + part.start
-        uniq = int(np.unique(k).size)
-        keys = torch.from_numpy(k).to(dev)
-        vals = torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+        for b in range(nb):
+            if b:  # a fresh sample of the same law, the same number of records
+                rb = np.random.default_rng(100042 + 1000 * b + rank)
+                ranks = rb.zipf(1.1, size=int(nrec * 1.4))
+                ranks = ranks[ranks <= n][:nrec] - 1
+                assert ranks.size == nrec
+            k = perm[ranks].astype(np.int64) + part.start
+            batches.append((torch.from_numpy(k).to(dev), None,
+                            torch.rand(nrec, dtype=torch.float64, device=dev, generator=gen) * 2 - 1,
+                            int(np.unique(k).size)))
+        keys, _, vals, _ = batches[0]
+        uniq = int(np.mean([bt[3] for bt in batches]))
         tag = f"zipf_2p{log2_keys}"
         bytes_per_step = 16.0 * nrec + 16.0 * uniq
         workload = f"cfg3: Zipf(1.1) push of {nrec} records into a 2^{log2_keys}-key Double shard"
     stream = torch.cuda.current_stream(dev).cuda_stream
     h = shard.handle
+    nstep = [0]  # pushes so far: step s pushes batch s % K
 
     def step():
+        nonlocal keys, cols, vals
+        if batches:
+            keys, cols, vals = batches[nstep[0] % len(batches)][:3]
+        nstep[0] += 1
         if exch:
             dv.push(keys, vals)
             return
@@ -441,12 +476,14 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     # equal what was pushed, bit for bit (a row pull: the dense fill's rows).
     ok = None
     reps = warmup + steps
+    # pushes of each batch: step s pushed batch s % K
+    times = [len(range(b, reps, len(batches))) for b in range(len(batches))] if batches else [reps]
     recv = nrec  # records this rank's shard takes per push
     if check:
         if pat == "dense":
             acc = torch.zeros_like(vals)
-            for _ in range(reps):
-                acc += vals
+            for s_ in range(reps):  # (in push order: the same rounding as the shard's ordered adds)
+                acc += batches[s_ % len(batches)][2]
             ok = bool(torch.equal(shard.get(keys), acc))
             del acc
         elif pat == "pull":
@@ -454,38 +491,45 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
         elif pat == "rowpull":
             ok = bool(torch.equal(out, fill_v.view(n, cols_n)[keys - part.start]))
         else:
+            # every batch's records (value x the times it was pushed), in addresses local to the shard
+            # (exchange: to the concatenation of the rank's shards, shard j's elements at j * n ...)
+            addr_l, val_l = [], []
+            recv_b = []
+            for b, tb in enumerate(times):
+                if exch:
+                    # every rank's batch b, replayed: the records of this rank's partitions
+                    r0 = sum(int(x.numel()) for x in addr_l)
+                    for src in range(world):
+                        k_s, v_s = (batches[b][0], batches[b][2]) if src == rank else batch(src, b)
+                        for j, p in enumerate(my_parts):
+                            m = (k_s >= p.start) & (k_s < p.end)
+                            addr_l.append(k_s[m] - p.start + j * n)
+                            val_l.append(v_s[m] * tb)
+                        del k_s, v_s, m
+                    recv_b.append(sum(int(x.numel()) for x in addr_l) - r0)
+                else:
+                    kb, cb, vb = batches[b][:3] if batches else (keys, cols, vals)
+                    addr_l.append((kb - part.start) * cols_n + cb.to(torch.int64) if mat else kb - part.start)
+                    val_l.append(vb * tb)
+            addr, v_all = torch.cat(addr_l), torch.cat(val_l)
+            mag_all = torch.cat([v.abs() for v in val_l])
+            del addr_l, val_l
             if exch:
-                # every rank's batch, replayed: the records of this rank's partitions, in addresses local
-                # to the concatenation of its shards (shard j's elements at j * n ...)
-                addr_l, val_l = [], []
-                for src in range(world):
-                    k_s, v_s = (keys, vals) if src == rank else batch(src)
-                    for j, p in enumerate(my_parts):
-                        m = (k_s >= p.start) & (k_s < p.end)
-                        addr_l.append(k_s[m] - p.start + j * n)
-                        val_l.append(v_s[m])
-                    del k_s, v_s, m
-                addr, v_all = torch.cat(addr_l), torch.cat(val_l)
-                del addr_l, val_l
-                recv = int(addr.numel())
+                recv = int(np.mean(recv_b))
                 got = torch.cat([sh.get(torch.arange(p.start, p.end, dtype=torch.int64, device=dev))
                                  for sh, p in zip(shards, my_parts)])
             elif mat:
-                addr = (keys - part.start) * cols_n + cols.to(torch.int64)
-                v_all = vals
                 got = shard.getRows(torch.arange(part.start, part.end, dtype=torch.int64, device=dev)).reshape(-1)
             else:
-                addr = keys - part.start
-                v_all = vals
                 got = shard.get(torch.arange(part.start, part.end, dtype=torch.int64, device=dev))
             # segment sums over the sorted addresses (an atomic index_add_ serialises on Zipf's hot key)
             a, order = torch.sort(addr)
             uq, counts = torch.unique_consecutive(a, return_counts=True)
-            sums = segment_sums(v_all[order], counts) * reps
+            sums = segment_sums(v_all[order], counts)
             # 1e-9 of each element's sum of magnitudes: the scale any summation order of a Double sum
             # is accurate to (~n eps sum |v|), far inside the north star's 1e-6 relative, while a lost
             # or duplicated record cannot pass
-            mags = segment_sums(v_all[order].abs(), counts) * reps
+            mags = segment_sums(mag_all[order], counts)
             close = (got[uq] - sums).abs() <= 1e-9 * mags
             ok = bool(close.all())
             if not ok:
@@ -497,10 +541,10 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
                 ok = False
                 print(f"check: {int((got != 0).sum())} elements outside the pushed addresses are nonzero",
                       file=sys.stderr)
-            if exch:
+            if exch and len(times) == 1:
                 uniq, u_note = int(uq.numel()), ""
                 bytes_per_step = 16.0 * recv + 16.0 * uniq
-            del a, order, uq, counts, sums, mags, addr, v_all, got
+            del a, order, uq, counts, sums, mags, addr, v_all, mag_all, got
     if check and world > 1:  # every rank's verdict: the line's check holds for all of them
         t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -576,6 +620,10 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
                      else "summed device time of the step's kernels"},
         "check": ok,
     }
+    if batches and len(batches) > 1:
+        line["batches"] = {"k": len(batches), "rotation": "step s pushes batch s % K",
+                           "distinct_keys_per_batch": [bt[3] for bt in batches] if not exch else None,
+                           "check": "every batch replayed (value x times pushed) into one fp64 segment sum"}
     floor = sparse_floor(tag + ("_slab" if slab is not None else ""), dt / steps * 1e3)
     if floor is not None:
         line["practical_floor"] = floor
@@ -584,6 +632,26 @@ def run_line(ctx, pat: str, log2_keys: int, scaling: str, steps: int, warmup: in
     if slab is not None:  # after its views
         slab.destroy()
     return line
+
+
+def rank_devices(dev, backend: str, local_pinned: bool) -> dict:
+    """Every rank's GPU as the ranks see it (all-gathered to every rank): device index, PCI address and
+    UUID. Over RCCL two ranks on one GPU are an error -- the line would not be N GPUs' throughput; the
+    gloo rehearsal (GLINT_BENCH_DEVICE pins every rank to one GPU) is marked as such."""
+    import torch
+    import torch.distributed as dist
+    p = torch.cuda.get_device_properties(dev)
+    me = {"rank": dist.get_rank(), "device": torch.cuda.current_device(),
+          "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                 f"{getattr(p, 'pci_device_id', 0):02x}",
+          "uuid": str(getattr(p, "uuid", ""))}
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, me)
+    distinct = len({(d["pci"], d["uuid"]) for d in allr})
+    if backend == "nccl" and distinct != len(allr):
+        raise SystemExit(f"{len(allr)} ranks on {distinct} distinct GPUs: {allr}")
+    return {"ranks": allr, "distinct_gpus": distinct, "backend": backend,
+            "rehearsal": bool(local_pinned or backend != "nccl")}
 
 
 def main():
@@ -622,8 +690,13 @@ def main():
         raise SystemExit("--parts-per-gpu applies to --pattern exchange")
     headline = args.log2_keys is None and args.pattern == "dense" and args.scaling == "weak"
     log2_keys = args.log2_keys if args.log2_keys is not None else (30 if headline else 28)
+    if args.batches > 1 and args.pattern not in ("dense", "zipf", "matrix", "exchange"):
+        raise SystemExit("--batches applies to the push patterns")
     line = run_line(ctx, args.pattern, log2_keys, args.scaling, args.steps, args.warmup, not args.no_check,
-                    args.parts_per_gpu)
+                    args.parts_per_gpu, max(1, args.batches))
+    if world > 1:
+        line["world_size"] = dist.get_world_size()
+        line["devices"] = rank_devices(dev, backend, local_pinned="GLINT_BENCH_DEVICE" in os.environ)
     # BASELINE.json configs[1] (cfg2: 2^28 keys) beside the north-star line, with its own roofline and check
     if world == 1 and headline and not args.no_north_star:
         torch.cuda.empty_cache()

@@ -9,19 +9,20 @@
 // in LDS and written back with one coalesced read-modify-write of the touched element pairs.
 // Nothing is reserved across workgroups at run time: every writer owns its output range.
 //
-//   bin_count   per partition workgroup w (the grid of bin_part, same chunk -> w mapping): raw
-//               records per coarse bucket of w's chunks -> R[w][b], and per bucket -> T[b].
-//   bin_part    workgroup w owns the range of its chunks' records; inside it bucket b starts at the
-//               exclusive scan of R[w][*]. Per 4096-record chunk it (optionally) sums duplicate
-//               elements in an LDS hash table, then appends the chunk's records to its bucket
-//               ranges, staged in LDS so the stores are runs. -> segment (w, b): offset and length.
-//   bin_fpart   one workgroup per coarse bucket: counts its records per slab, writes the apply items
-//               of its slabs, then moves the records into slab order (LDS-staged tiles, LDS cursors).
-//               Bucket b's output starts at sum(T[0..b)), its item slots at
-//               sum(nf + ceil(T[b']/16384)) over b' < b.
-//   bin_apply   per apply item: LDS accumulation of the slab, coalesced RMW of touched pairs (items
-//               of a slab cut into several flush with device atomics instead).
-// Capacities come from raw counts, so dedup leaves holes only at range ends.
+//   bin_count   per partition workgroup w: records per coarse bucket of w's chunks -> R[w][b]; its add
+//               to the bucket total T[b] returns where w's records of b start inside the bucket
+//               (Roff[w][b]), so every bucket is one contiguous range of the partition buffer.
+//   bin_part    per 8192-record chunk (optionally after summing duplicate elements in an LDS hash
+//               table), the chunk's records ranked by bucket in LDS and appended to the bucket ranges
+//               as runs (u32 address + value).
+//   bin_fsort   per fine item (<= 16384 records of one bucket): ranked by slab in LDS and written back
+//               slab-sorted (u16 slab offset + value), with the item's per-slab offsets (off2).
+//   bin_plan    per bucket: every slab's runs (one per item) cut into apply units (fused into
+//               bin_fsort for small pushes).
+//   bin_apply2  per apply unit: LDS accumulation of the slab, coalesced RMW of the touched lines
+//               (units of a slab cut into several flush with device atomics instead).
+// Record indices are u32 (a push of < 2^32 records); buffer offsets are 64-bit wherever a push's
+// buffers pass 4 GiB (WIDE partition stores).
 #include "glint_device.h"
 #include "glint_host.h"
 
@@ -52,27 +53,12 @@ static_assert((1 << kASlotBits) == kASlots, "dedup table size");
 constexpr int kPartWgPerCuDedup = kATPB == 1024 ? 1 : 2;
 constexpr int kPartWgPerCuPlain = kATPB == 1024 ? 1 : 2;  // what fits (VGPRs): a second round of
                                                            // workgroups measured 3-9 % slower
-constexpr int kMaxSegs = 1024;         // partition workgroups at most (segments per bucket)
-#ifndef GLINT_FPART_WAVES
-#define GLINT_FPART_WAVES 4  // bin_fpart's register budget: waves per SIMD (build-time knob)
-#endif
-constexpr int kFPer = 8;               // records per thread per fine-partition tile (tile = TPB * kFPer;
-                                       // bin_fpart runs at 256 or 512 threads, chosen per push)
-constexpr u32 kFItem = 16384;          // records per fine-partition item at most (a bucket has >= 1)
-// bin_fcount, two shapes: a push with more items than the resident 256-thread workgroups walks each
-// item in 2048-record tiles (one tile in flight ahead); a small push (cfg5: ~640 items) takes one
-// 512-thread workgroup per item with the item's 16384 addresses in flight at once (the tile walk was 8
-// dependent round trips per item there: cfg5 0.435 -> 0.406 ms; cfg3's ~1500 items lost 3 % with it)
-constexpr int kFCTPB = 256;
-constexpr int kFCTPBWhole = 512;
-constexpr int kFCPer = (int)kFItem / kFCTPBWhole;
+constexpr int kMaxSegs = 1024;         // partition workgroups at most
 #ifndef GLINT_APPLY_TPB
 #define GLINT_APPLY_TPB 256
 #endif
 constexpr int kCTPB = GLINT_APPLY_TPB;  // slab-apply workgroup size (build-time knob)
-constexpr u32 kCItem = 16384;          // records per apply item at most
 constexpr u32 kEmptySlot = 0xFFFFFFFFu;
-constexpr u32 kItemEmpty = 2u;         // apply item slot left unused
 
 struct BinGeom {
   u32 fb;     // fine digit bits
@@ -86,12 +72,10 @@ __device__ __forceinline__ u32 fine_of(u32 a, const BinGeom& g) { return (a >> k
 struct BinCtl {
   u32 m;       // records the partition emitted (after dedup)
   u32 tail;    // valid records in the tail
-  u32 nslots;  // apply item slots written by bin_fpart (the last bucket's first item knows the total)
-  u32 nfitems; // fine-partition items (written by bin_part's workgroup 0)
-  u32 fnext;   // bin_fpart's item queue: the next item to take
+  u32 nfitems; // fine items (written by bin_part's workgroup 0)
   u32 cold;    // valid records that were not hot (the dedup front end's input; m for the others)
-  u32 nunits;  // v2: apply units written by bin_plan (each bucket takes its range with one atomic)
-  u32 disorder;  // v2, a whole-push bin (no push_check): some wave saw two adjacent records out of order
+  u32 nunits;  // apply units written by bin_plan (each bucket takes its range with one atomic)
+  u32 disorder;  // a whole-push bin (no push_check): some wave saw two adjacent records out of order
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -171,6 +155,24 @@ __device__ __forceinline__ void bput(const BufOut& b, u32 off, bool on, T v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, v), b.r, o, 0, 0);
   }
 }
+// A record array of T through one buffer window: element `rel` at byte rel * sizeof(T) (< 2^32 bytes).
+template <typename T>
+struct RecOut {
+  BufOut b;
+  __device__ __forceinline__ void put(u32 rel, bool on, T v) const { bput(b, rel * (u32)sizeof(T), on, v); }
+};
+// The same for a push whose buffers pass 4 GiB (a window offset is 32 bits): plain 64-bit-addressed
+// stores, and a lane with nothing to store writes its own slot of a dump area instead, so every path
+// still issues one store per call.
+template <typename T>
+struct WideOut {
+  T* base;
+  T* dump;  // >= 64 elements, never read
+  __device__ __forceinline__ void put(u32 rel, bool on, T v) const {
+    T* const p = on ? base + rel : dump + (threadIdx.x & 63);
+    *p = v;
+  }
+};
 struct BadRecs {  // this thread's rejected records: the first one and how many
   i64 first = -1;
   u32 count = 0;
@@ -253,13 +255,6 @@ __device__ __forceinline__ i64 tail_start(const LaunchCtl* lctl, u32 ntiles, int
   return brk == 0u ? n : (i64)(ntiles - brk) * kTile;
 }
 
-// chunk c of the tail belongs to partition workgroup c % G; workgroup w's records start at
-// chunk_base(w) * kAChunk within the partition buffer (every chunk counted full: an upper bound)
-__device__ __forceinline__ u32 chunk_base(u32 w, u32 G, i64 nchunks) {
-  const u32 q = (u32)(nchunks / G), r = (u32)(nchunks % G);
-  return w * q + min(w, r);
-}
-
 // One partition chunk's records, kAPer per thread, in registers. The partition kernels keep two of
 // these in flight (chunks c + G and c + 2G load while chunk c is partitioned): one chunk of loads per
 // workgroup left too little in flight per CU to cover HBM latency.
@@ -298,10 +293,10 @@ __device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
   return x;
 }
 
-// v2 (push_binned_v2): Roff[w][b] = where workgroup w's records of bucket b start inside the bucket (the
-// value its add to T[b] returned), so every bucket is one contiguous range of the partition buffer; and
-// with hot_best the push's hot elements are not counted (the hot front end sums them in LDS), so the
-// counts are exact and the buffer has no holes.
+// Roff[w][b] = where workgroup w's records of bucket b start inside the bucket (the value its add to
+// T[b] returned), so every bucket is one contiguous range of the partition buffer; and with hot_best
+// the push's hot elements are not counted (the hot front end sums them in LDS), so the counts are
+// exact and the buffer has no holes.
 constexpr int kWideSlots = 8192;  // the plain + hot front end's hot table (see bin_hot_select)
 __device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
 // VALIDATE (a validating gated push, GLINT_PUSH_VALIDATE, whose tail is binned): the count also checks
@@ -324,7 +319,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   const u32 hc = (u32)((tid >> 6) % kCopies) * g.nb;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
-  if (next_bc && blockIdx.x == 0) {  // v2: the next push's header (the previous push used it; it is done)
+  if (blockIdx.x == 0) {  // the next push's header (the previous push used it; it is done)
     for (u32 b = tid; b < g.nb; b += kATPB) {
       next_T[b] = 0;
       next_T[kMaxDigit + b] = 0;  // the fused plan's per-bucket item counters (push_binned_v2's header)
@@ -415,8 +410,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
 #pragma unroll
     for (int cpy = 0; cpy < kCopies; ++cpy) x += h[cpy * g.nb + b];
     R[blockIdx.x * g.nb + b] = x;
-    const u32 o = x ? atomicAdd(&T[b], x) : 0u;
-    if (Roff) Roff[blockIdx.x * g.nb + b] = o;
+    Roff[blockIdx.x * g.nb + b] = x ? atomicAdd(&T[b], x) : 0u;
   }
   const u32 tot = block_sum<kATPB>(nvalid);
   if (tid == 0 && tot) atomicAdd(&bc->tail, tot);
@@ -543,10 +537,11 @@ __device__ __forceinline__ void hot_flush(int* p, int x) { gadd(p, x); }
 // ---- bin_part -------------------------------------------------------------------------------------
 // Appends a chunk's records (P per thread in registers, `valid` bit mask) to this workgroup's bucket
 // ranges: cur[b] = next free slot of bucket b. dcnt and gpos are scratch (dcnt zero on entry/exit).
-template <typename A, int P>
+// OA / OV: where the addresses / values go (RecOut, or WideOut for a push past 4 GiB of buffer).
+template <typename A, int P, typename OA, typename OV>
 __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u32 valid, const BinGeom& g,
-                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v, const BufOut& oa,
-                                         const BufOut& ov, u32 wbase, PhaseClock& ph, int pb) {
+                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v, const OA& oa,
+                                         const OV& ov, PhaseClock& ph, int pb) {
   const int tid = threadIdx.x;
   u32 rank[P];
 #pragma unroll
@@ -580,14 +575,9 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
     const u32 p = tid + j * kATPB;
     const bool on = p < total;
     const u32 a = st_a[p];
-    const u32 rel = gpos[on ? bucket_of(a, g) : 0u] + p - wbase;  // within this workgroup's range
-#ifdef GLINT_BIN_NOSTORE  // timing experiment only: every partition store dropped
-    bput(oa, rel * 4u, false, a);
-    bput(ov, rel * (u32)sizeof(A), false, st_v[p]);
-#else
-    bput(oa, rel * 4u, on, a);
-    bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
-#endif
+    const u32 rel = gpos[on ? bucket_of(a, g) : 0u] + p;  // record index in the partition buffer
+    oa.put(rel, on, a);
+    ov.put(rel, on, st_v[p]);
   }
   __syncthreads();
   ph.mark(pb + 3);
@@ -597,37 +587,24 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   return total;
 }
 
-// Workgroup w's bucket ranges: cur[b] = chunk_base(w) * kAChunk + exclusive scan of R[w][*], also
-// published bucket-major as segoff[b][w] for the fine partition.
-// v2 (Roff set): bucket b is the contiguous range [Bb[b], Bb[b] + T[b]) with Bb the exclusive scan of T
-// (written once, by workgroup 0); this workgroup's records of b start at Bb[b] + Roff[w][b].
-__device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, i64 nchunks, const u32* __restrict__ R,
-                                           u32* __restrict__ segoff, u32* cur, u32* dcnt, const u32* __restrict__ T,
+// Workgroup w's bucket ranges: bucket b is the contiguous range [Bb[b], Bb[b] + T[b]) with Bb the
+// exclusive scan of T (written once, by workgroup 0); this workgroup's records of b start at
+// Bb[b] + Roff[w][b].
+__device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, u32* cur, u32* dcnt, const u32* __restrict__ T,
                                            const u32* __restrict__ Roff, u32* __restrict__ Bb) {
-  if (Roff) {
-    block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; },
-                         [&](u32 b, u32 excl) {
-                           cur[b] = excl + Roff[w * g.nb + b];
-                           dcnt[b] = 0;
-                           if (w == 0) Bb[b] = excl;
-                         });
-    return;
-  }
-  const u32 base = chunk_base(w, gridDim.x, nchunks) * (u32)kAChunk;
-  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return R[w * g.nb + b]; },
+  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; },
                        [&](u32 b, u32 excl) {
-                         cur[b] = base + excl;
-                         segoff[b * gridDim.x + w] = base + excl;  // bucket-major: bin_fpart reads a row
+                         cur[b] = excl + Roff[w * g.nb + b];
                          dcnt[b] = 0;
+                         if (w == 0) Bb[b] = excl;
                        });
 }
 
-// Workgroup 0 of bin_part: the fine-partition items -- bucket b gets max(1, ceil(T[b] / kFItem))
-// of them ({b, j}: its records [j * kFItem, (j + 1) * kFItem) in segment order).
-// fine-partition items of a bucket of t records: ceil(t / kFItem), at least one (the bucket's first
-// item writes its apply items)
-__device__ __forceinline__ u32 bucket_items(u32 t, u32 item = kFItem) { return max(1u, (t + item - 1) / item); }
-// (v2: items of `item` records; Ib[b] = the bucket's first item)
+// fine items of a bucket of t records: ceil(t / item), at least one (an empty bucket's one item writes
+// its empty offset row)
+__device__ __forceinline__ u32 bucket_items(u32 t, u32 item) { return max(1u, (t + item - 1) / item); }
+// Workgroup 0 of bin_part: the fine items -- {b, j}: bucket b's records [j * item, (j + 1) * item) --
+// and Ib[b] = the bucket's first item.
 __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
                                            BinCtl* bc, u32 item, u32* __restrict__ Ib) {
   const u32 tot = block_scan<kATPB, 1>(
@@ -635,19 +612,12 @@ __device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restri
       [&](u32 b, u32 excl) {
         const u32 J = bucket_items(T[b], item);
         for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
-        if (Ib) Ib[b] = excl;
+        Ib[b] = excl;
       });
   if (threadIdx.x == 0) bc->nfitems = tot;
 }
 
-__device__ __forceinline__ void part_finish(const BinGeom& g, u32 w, const u32* __restrict__ segoff, const u32* cur,
-                                            u32* __restrict__ seglen, u32 emitted, BinCtl* bc) {
-  if (segoff)
-    for (u32 b = threadIdx.x; b < g.nb; b += kATPB) seglen[b * gridDim.x + w] = cur[b] - segoff[b * gridDim.x + w];
-  if (threadIdx.x == 0 && emitted) atomicAdd(&bc->m, emitted);
-}
-
-// v2, dedup front end: the chunk tables merged records, so this workgroup's bucket ranges end short of
+// Dedup front end: the chunk tables merged records, so this workgroup's bucket ranges end short of
 // what bin_count counted; the rest of each range is marked empty for bin_fsort.
 __device__ __forceinline__ void part_fill_holes(const BinGeom& g, u32 w, const u32* __restrict__ T,
                                                 const u32* __restrict__ R, const u32* __restrict__ Roff, const u32* cur,
@@ -744,12 +714,11 @@ __global__ __launch_bounds__(256) void bin_hot_select_kernel(u32* __restrict__ g
 // each sum a contiguous range of workgroups (coalesced rows, loads issued back to back), then the
 // group sums are added in group order -- the result is the same on every run.
 constexpr int kRedSlots = 64, kRedTPB = 1024, kRedGroups = kRedTPB / kRedSlots;
+// (the picks stay for the next pushes: push_binned clears them itself before it samples again)
 template <typename V>
-// clear: empty the picks after reading them (v1: every push samples; v2 keeps them for the next pushes
-// and clears the table itself before it samples again)
-__global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(unsigned long long* __restrict__ best, u32 G,
+__global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned long long* __restrict__ best, u32 G,
                                                                  const typename LdsAcc<V>::T* __restrict__ partial,
-                                                                 V* __restrict__ data, int clear) {
+                                                                 V* __restrict__ data) {
   typedef typename LdsAcc<V>::T A;
   __shared__ A gs[kRedGroups][kRedSlots];
   __shared__ u32 gany[kRedGroups][kRedSlots];
@@ -778,7 +747,6 @@ __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(unsigned long l
   if (grp != 0) return;
   const unsigned long long b = best[sl];
   if (!b) return;
-  if (clear) best[sl] = 0ull;  // the picks' last reader empties them for the next push (no memset)
   A tot = hot_zero<A>();
   bool seen = false;
   for (int q = 0; q < kRedGroups; ++q) {
@@ -790,24 +758,35 @@ __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(unsigned long l
   if (seen) data[a] = acc_add(data[a], tot);
 }
 
+// The partition's outputs: buffer windows (RecOut), or for a push whose buffers pass 4 GiB WideOut with
+// the dump area (kDumpBytes: values, then addresses)
+constexpr size_t kDumpBytes = 1024;
+template <bool WIDE, typename T>
+__device__ __forceinline__ auto part_out(T* base, u32 n, void* dump, size_t dump_off) {
+  if constexpr (WIDE) {
+    return WideOut<T>{base, reinterpret_cast<T*>(reinterpret_cast<char*>(dump) + dump_off)};
+  } else {
+    return RecOut<T>{buf_out(base, n * (u32)sizeof(T))};
+  }
+}
+
 // Plain front end: every valid record is appended as it is. HOT: the push's hot elements (the wide
 // table, bin_hot_select) are summed in LDS over all of the workgroup's chunks and stored per
 // workgroup for bin_hot_reduce; only the cold records are appended. Once the hot elements are off,
 // a Zipf-like tail has almost no duplicates left inside a chunk (cfg3: the chunk dedup would merge
 // 0.6 % of the cold records), so the hash table is not worth its time there.
-template <typename V, bool MAT, bool HOT, int KIND>
+template <typename V, bool MAT, bool HOT, int KIND, bool WIDE>
 __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                          const V* __restrict__ vals, i64 n, PartDesc part,
                                                          const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
-                                                         const u32* __restrict__ R, u32* __restrict__ segoff,
-                                                         u32* __restrict__ seglen, u32* __restrict__ addr_out,
+                                                         u32* __restrict__ addr_out,
                                                          typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
                                                          BinCtl* bc, const u32* __restrict__ T,
                                                          uint2* __restrict__ fitems,
                                                          const unsigned long long* __restrict__ hot_best,
                                                          typename LdsAcc<V>::T* __restrict__ hot_partial, u32 fitem,
                                                          const u32* __restrict__ Roff, u32* __restrict__ Bb,
-                                                         u32* __restrict__ Ib) {
+                                                         u32* __restrict__ Ib, void* dump) {
   typedef typename LdsAcc<V>::T A;
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
   __shared__ u32 st_a[kAChunk];
@@ -828,13 +807,12 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   }
   PhaseClock ph(0);
   if (w == 0) part_items(g, T, fitems, bc, fitem, Ib);
-  part_setup(g, w, nchunks, R, segoff, cur, dcnt, T, Roff, Bb);
+  part_setup(g, w, cur, dcnt, T, Roff, Bb);
   ph.mark(0);
   const i64 G = gridDim.x;
-  // output window: v1 this workgroup's own range; v2 the whole buffer (bucket ranges; n * sizeof(A) < 2^32)
-  const u32 wbase = Roff ? 0u : chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
-  const u32 wlen = Roff ? (u32)(n - r0) : chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
-  const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
+  // output: the whole buffer (the bucket ranges)
+  const auto oa = part_out<WIDE>(addr_out, (u32)(n - r0), dump, 512);
+  const auto ov = part_out<WIDE>(val_out, (u32)(n - r0), dump, 0);
   BadRecs bad;
   u32 emitted = 0;
   // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
@@ -886,7 +864,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
       }
     }
     ph.mark(1);
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 3);
+    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 3);
     // two chunks ahead, into the registers just consumed: in flight across the next chunk's work
     load_chunk(c + 2 * G, r);
     ph.mark(2);
@@ -901,8 +879,10 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
       step(c + G, rb);  // past the end: no valid record, nothing stored
     }
   }
-  part_finish(g, w, segoff, cur, seglen, emitted, bc);
-  if (tid == 0 && emitted) atomicAdd(&bc->cold, emitted);  // cold records: all of them were appended
+  if (tid == 0 && emitted) {
+    atomicAdd(&bc->m, emitted);
+    atomicAdd(&bc->cold, emitted);  // cold records: all of them were appended
+  }
   bad.report(err);
   if constexpr (HOT) {
     __syncthreads();  // every chunk's hot sums are in; bin_hot_reduce adds them up
@@ -918,14 +898,13 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
 
 // KIND: the partition layout (0 range: only the keys' low words are loaded, as in bin_count -- the
 // register budget of this kernel is tight; -1 read at run time)
-template <typename V, bool MAT, int KIND>
+template <typename V, bool MAT, int KIND, bool WIDE>
 __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     const i64* __restrict__ keys, const int32_t* __restrict__ cols, const V* __restrict__ vals, i64 n, PartDesc part,
     const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, const u32* __restrict__ R,
-    u32* __restrict__ segoff, u32* __restrict__ seglen, u32* __restrict__ addr_out,
-    typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc, const u32* __restrict__ T,
-    uint2* __restrict__ fitems, const u32* __restrict__ hot_tags, V* __restrict__ data, u32 fitem,
-    const u32* __restrict__ Roff, u32* __restrict__ Bb, u32* __restrict__ Ib) {
+    u32* __restrict__ addr_out, typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc,
+    const u32* __restrict__ T, uint2* __restrict__ fitems, const u32* __restrict__ hot_tags, V* __restrict__ data,
+    u32 fitem, const u32* __restrict__ Roff, u32* __restrict__ Bb, u32* __restrict__ Ib, void* dump) {
   typedef typename LdsAcc<V>::T A;
   static_assert(kAChunk * (4 + sizeof(A)) <= kASlots * sizeof(A), "staging must fit the value table");
   __shared__ u32 hk[kASlots];
@@ -953,13 +932,12 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   if (tid == 0) nused = 0;
   PhaseClock ph(8);
   if (w == 0) part_items(g, T, fitems, bc, fitem, Ib);
-  part_setup(g, w, nchunks, R, segoff, cur, dcnt, T, Roff, Bb);
+  part_setup(g, w, cur, dcnt, T, Roff, Bb);
   ph.mark(8);
   const u64 below = (1ull << lane) - 1ull;
   const i64 G = gridDim.x;
-  const u32 wbase = Roff ? 0u : chunk_base(w, (u32)G, nchunks) * (u32)kAChunk;
-  const u32 wlen = Roff ? (u32)(n - r0) : chunk_base(w + 1, (u32)G, nchunks) * (u32)kAChunk - wbase;
-  const BufOut oa = buf_out(addr_out + wbase, wlen * 4u), ov = buf_out(val_out + wbase, wlen * (u32)sizeof(A));
+  const auto oa = part_out<WIDE>(addr_out, (u32)(n - r0), dump, 512);
+  const auto ov = part_out<WIDE>(val_out, (u32)(n - r0), dump, 0);
   BadRecs bad;
   u32 emitted = 0, ncold = 0;
   // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
@@ -1056,7 +1034,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     __syncthreads();
     if (tid == 0) nused = 0;
     ph.mark(11);
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, wbase, ph, 12);
+    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 12);
     for (int sl = tid; sl < kStageA; sl += kATPB) hv[sl] = A(0);  // staging overlaid these
 #pragma unroll
     for (int j = 0; j < kAPer; ++j) {  // and the table's own slots of this chunk
@@ -1079,8 +1057,8 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
       step(c + G, rb);  // past the end: no valid record, nothing stored
     }
   }
-  part_finish(g, w, segoff, cur, seglen, emitted, bc);
-  if (Roff) part_fill_holes(g, w, T, R, Roff, cur, dcnt, addr_out);
+  if (tid == 0 && emitted) atomicAdd(&bc->m, emitted);
+  part_fill_holes(g, w, T, R, Roff, cur, dcnt, addr_out);
   bad.report(err);
   {  // records that entered the hash table (valid, not hot): the host's measure of what chunk dedup merges
     const u32 tot = block_sum<kATPB>(ncold);
@@ -1092,463 +1070,6 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     if (a != kEmptySlot && !hot_untouched<A>(hacc[sl])) hot_flush(data + a, hacc[sl]);
   }
   ph.flush(10);
-}
-
-// ---- fine partition ---------------------------------------------------------------------------------
-// Record v of bucket b (0 <= v < M_b, segments in partition-workgroup order) lives at
-// segst[s] + v - segpre[s]. Each thread visits increasing v, so it walks the segment list with a cursor.
-__device__ __forceinline__ u32 seg_addr(u32 v, u32& s, const u32* segpre, const u32* segst) {
-  while (segpre[s + 1] <= v) ++s;
-  return segst[s] + (v - segpre[s]);
-}
-
-// the addresses of records [t0, t0 + TPB * kFPer) of a bucket; returns which are valid (< v1) as a
-// mask (selecting on the loaded registers would make the compiler wait for the loads at once); s is
-// the thread's segment cursor (its records only move forward)
-// (clamped and branch-free: every lane issues kFPer loads; needs v1 > 0)
-template <int TPB>
-__device__ __forceinline__ u32 fetch_addr(u32 t0, u32 v1, u32& s, const u32* segpre, const u32* segst,
-                                          const u32* __restrict__ addr_in, u32 (&a)[kFPer]) {
-  u32 valid = 0;
-#pragma unroll
-  for (int q = 0; q < kFPer; ++q) {
-    const u32 v = t0 + q * TPB + threadIdx.x;
-    a[q] = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
-    valid |= (v < v1 ? 1u : 0u) << q;
-  }
-  return valid;
-}
-
-// bucket b's segment table into LDS; returns M_b
-template <int TPB>
-__device__ __forceinline__ u32 load_segments(const BinGeom& g, u32 G, u32 b, const u32* __restrict__ segoff,
-                                             const u32* __restrict__ seglen, u32* segpre, u32* segst) {
-  const u32 M = block_scan<TPB, 4>(
-      G, [&](u32 w) { return seglen[b * G + w]; },
-      [&](u32 w, u32 excl) {
-        segpre[w] = excl;
-        segst[w] = segoff[b * G + w];
-      });
-  if (threadIdx.x == 0) segpre[G] = M;
-  __syncthreads();
-  return M;
-}
-
-// per item: records per slab -> H[slab] (exact counts after dedup). WHOLE: see kFCTPBWhole.
-template <bool WHOLE>
-__global__ __launch_bounds__(WHOLE ? kFCTPBWhole : kFCTPB) void bin_fcount_kernel(
-    BinGeom g, u32 G, const uint2* __restrict__ fitems, const BinCtl* bc, const u32* __restrict__ segoff,
-    const u32* __restrict__ seglen, const u32* __restrict__ addr_in, u32* __restrict__ H, u32* __restrict__ IH) {
-  constexpr int TPB = WHOLE ? kFCTPBWhole : kFCTPB;
-  __shared__ u32 segst[kMaxSegs], segpre[kMaxSegs + 1];
-  __shared__ u32 fh[kMaxDigit];
-  const int tid = threadIdx.x;
-  const u32 nit = bc->nfitems;
-  for (u32 it = blockIdx.x; it < nit; it += gridDim.x) {
-    const uint2 d = fitems[it];
-    const u32 b = d.x;
-    for (u32 f = tid; f < g.nf; f += TPB) fh[f] = 0;
-    const u32 M = load_segments<TPB>(g, G, b, segoff, seglen, segpre, segst);
-    const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
-    u32 s = 0;
-    if (WHOLE) {
-      if (v1 > v0) {
-        u32 a[kFCPer];
-#pragma unroll
-        for (int q = 0; q < kFCPer; ++q) {
-          const u32 v = v0 + (u32)q * TPB + (u32)tid;
-          a[q] = ld_in(addr_in + seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst));
-        }
-#pragma unroll
-        for (int q = 0; q < kFCPer; ++q)
-          if (v0 + (u32)q * TPB + (u32)tid < v1) atomicAdd(&fh[fine_of(a[q], g)], 1u);
-      }
-    } else {
-      u32 a[kFPer], avalid = 0;
-      if (v1 > v0) avalid = fetch_addr<TPB>(v0, v1, s, segpre, segst, addr_in, a);
-      for (u32 t0 = v0; t0 < v1; t0 += TPB * kFPer) {
-        u32 cur[kFPer];
-        const u32 cvalid = avalid;
-#pragma unroll
-        for (int q = 0; q < kFPer; ++q) cur[q] = a[q];
-        avalid = fetch_addr<TPB>(t0 + TPB * kFPer, v1, s, segpre, segst, addr_in, a);  // the next tile, in flight meanwhile
-#pragma unroll
-        for (int q = 0; q < kFPer; ++q)
-          if ((cvalid >> q) & 1u) atomicAdd(&fh[fine_of(cur[q], g)], 1u);
-      }
-    }
-    __syncthreads();
-    for (u32 f = tid; f < g.nf; f += TPB) {
-      const u32 c = fh[f];
-      IH[(size_t)it * g.nf + f] = c;  // this item's own histogram: bin_fpart reserves from it
-      if (c) atomicAdd(&H[b * g.nf + f], c);
-    }
-    __syncthreads();
-  }
-}
-
-// per item: its records moved to their slab ranges. Slab f of bucket b starts at
-// ob(b) + exclusive scan of H[b][*]; an item reserves its share of each slab with one returning
-// atomic (cur2), then moves tiles of TPB * kFPer records, staged in LDS so the stores are runs. The
-// bucket's first item also writes the apply items of its slabs.
-// LDS: the tile staging is static; the segment table (2G + 1 words) and the four per-slab arrays
-// (4 nf words) are sized at launch (fpart_dyn_bytes), so that small geometries fit more blocks per CU
-__host__ __device__ constexpr size_t fpart_dyn_bytes(u32 G, u32 nf) { return ((size_t)2 * G + 1 + (size_t)4 * nf) * 4; }
-
-template <typename A, int TPB>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GLINT_FPART_WAVES))) void bin_fpart_kernel(BinGeom g, u32 G, const uint2* __restrict__ fitems,
-                                                          BinCtl* bc, const u32* __restrict__ T,
-                                                          const u32* __restrict__ H, u32* __restrict__ cur2,
-                                                          const u32* __restrict__ segoff,
-                                                          const u32* __restrict__ seglen,
-                                                          const u32* __restrict__ addr_in,
-                                                          const A* __restrict__ val_in, u32* __restrict__ addr_out,
-                                                          A* __restrict__ val_out, uint4* __restrict__ cdesc,
-                                                          u64* hint, const u32* __restrict__ IH) {
-  extern __shared__ u32 fdyn[];
-  u32* const segst = fdyn;
-  u32* const segpre = fdyn + G;
-  u32* const sst = fdyn + 2 * G + 1;
-  u32* const fcur = sst + g.nf;
-  u32* const tcnt = fcur + g.nf;
-  u32* const tpos = tcnt + g.nf;
-  __shared__ u32 st_a[(TPB * kFPer)];
-  __shared__ A st_v[(TPB * kFPer)];
-  const int tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0 && hint)  // for the host's next binned push: how much did dedup keep?
-  {
-    __hip_atomic_store(hint, ((u64)bc->m << 32) | (u64)bc->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(hint + 1, (u64)bc->cold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  const u32 nit = bc->nfitems;
-  PhaseClock ph(20);
-  // items are taken from a queue (one returning atomic per item, fetched one item ahead): the grid
-  // is the resident block count, and items differ in size (a bucket's last item, skewed buckets)
-  __shared__ u32 s_next;
-  if (tid == 0) s_next = atomicAdd(&bc->fnext, 1u);
-  __syncthreads();
-  for (u32 it = s_next; it < nit; it = s_next) {
-    __syncthreads();  // every thread has read s_next
-    if (tid == 0) s_next = atomicAdd(&bc->fnext, 1u);  // the next item, in flight meanwhile
-    const uint2 d = fitems[it];
-    const u32 b = d.x;
-    // where the bucket's records go (raw capacities: holes only at bucket ends) and its item slots
-    u32 ob = 0, ib = 0;
-    for (u32 x = tid; x < b; x += TPB) {
-      const u32 t = T[x];
-      ob += t;
-      ib += g.nf + (t + kCItem - 1) / kCItem;
-    }
-    ob = block_sum<TPB>(ob);
-    ib = block_sum<TPB>(ib);
-    for (u32 f = tid; f < g.nf; f += TPB) tcnt[f] = 0;
-    block_scan<TPB, 4>(g.nf, [&](u32 f) { return H[b * g.nf + f]; }, [&](u32 f, u32 excl) { sst[f] = ob + excl; });
-    ph.mark(20);
-    if (d.y == 0) {  // the bucket's apply items {slab, first, end, exclusive}, then unused slots
-      const u32 nslots = g.nf + (T[b] + kCItem - 1) / kCItem;
-      if (b == g.nb - 1 && tid == 0) bc->nslots = ib + nslots;  // bin_apply's item count
-      const u32 used_slots = block_scan<TPB, 4>(
-          g.nf, [&](u32 f) { return (H[b * g.nf + f] + kCItem - 1) / kCItem; },
-          [&](u32 f, u32 excl) {
-            const u32 c = H[b * g.nf + f], s0 = sst[f];
-            const u32 m = (c + kCItem - 1) / kCItem;
-            for (u32 q = 0; q < m; ++q)
-              cdesc[ib + excl + q] =
-                  make_uint4(b * g.nf + f, s0 + q * kCItem, s0 + min(c, (q + 1) * kCItem), m == 1u ? 1u : 0u);
-          });
-      for (u32 x = used_slots + tid; x < nslots; x += TPB) cdesc[ib + x] = make_uint4(0u, 0u, 0u, kItemEmpty);
-    }
-    ph.mark(21);
-    const u32 M = load_segments<TPB>(g, G, b, segoff, seglen, segpre, segst);
-    const u32 v0 = d.y * kFItem, v1 = min(M, v0 + kFItem);
-    ph.mark(22);
-    // this item's records per slab (counted by bin_fcount); reserve the item's share of each slab
-    __syncthreads();
-    ph.mark(23);
-    for (u32 f = tid; f < g.nf; f += TPB) {
-      const u32 c = IH[(size_t)it * g.nf + f];
-      fcur[f] = c ? sst[f] + atomicAdd(&cur2[b * g.nf + f], c) : 0u;
-      tcnt[f] = 0;
-    }
-    __syncthreads();
-    ph.mark(24);
-    // pass 2: tiles moved to their slab ranges
-    u32 s = 0;
-    u32 na[kFPer], nvalid = 0;
-    A nv[kFPer];
-    // a tile's addresses and values (clamped, branch-free); which are valid goes to a separate mask
-    // (selecting on a loaded register would make the compiler wait for the load at once)
-    auto fetch = [&](u32 t0) {
-      nvalid = 0;
-#pragma unroll
-      for (int q = 0; q < kFPer; ++q) {
-        const u32 v = t0 + q * TPB + tid;
-        const u32 r = seg_addr(v < v1 ? v : v1 - 1, s, segpre, segst);
-        na[q] = ld_in(addr_in + r);
-        nv[q] = ld_in(val_in + r);
-        nvalid |= (v < v1 ? 1u : 0u) << q;
-      }
-    };
-    // the bucket's output range as buffer descriptors (counted stores)
-    const BufOut oa = buf_out(addr_out + ob, T[b] * 4u), ov = buf_out(val_out + ob, T[b] * (u32)sizeof(A));
-    if (v1 > v0) fetch(v0);
-    for (u32 t0 = v0; t0 < v1; t0 += (TPB * kFPer)) {
-      u32 a[kFPer], rank[kFPer];
-      A val[kFPer];
-      const u32 valid = nvalid;
-#pragma unroll
-      for (int q = 0; q < kFPer; ++q) {
-        a[q] = na[q];
-        val[q] = nv[q];
-      }
-      fetch(t0 + (TPB * kFPer));  // the next tile, in flight during this one's ranking, scan and stores
-      ph.mark(25);
-#pragma unroll
-      for (int q = 0; q < kFPer; ++q)
-        if ((valid >> q) & 1u) rank[q] = atomicAdd(&tcnt[fine_of(a[q], g)], 1u);
-      __syncthreads();
-      ph.mark(26);
-      const u32 total = block_scan<TPB, 4>(
-          g.nf, [&](u32 f) { return tcnt[f]; },
-          [&](u32 f, u32 excl) {
-            tpos[f] = fcur[f] - excl;  // output slot of staging position p (slab f) = tpos[f] + p
-            fcur[f] += tcnt[f];
-            tcnt[f] = excl;
-          });
-      ph.mark(27);
-#pragma unroll
-      for (int q = 0; q < kFPer; ++q) {
-        if ((valid >> q) & 1u) {
-          const u32 p = tcnt[fine_of(a[q], g)] + rank[q];
-          st_a[p] = a[q];
-          st_v[p] = val[q];
-        }
-      }
-      __syncthreads();
-      ph.mark(28);
-#pragma unroll
-      for (int j = 0; j < kFPer; ++j) {  // total <= (TPB * kFPer)
-        if ((u32)(j * TPB) >= total) break;  // workgroup-uniform: no store instructions past the tile
-        const u32 p = tid + j * TPB;
-        const bool on = p < total;
-        const u32 x = st_a[p];
-        const u32 rel = tpos[on ? fine_of(x, g) : 0u] + p - ob;
-        bput(oa, rel * 4u, on, x);
-        bput(ov, rel * (u32)sizeof(A), on, st_v[p]);
-      }
-      __syncthreads();
-      ph.mark(29);
-      for (u32 f = tid; f < g.nf; f += TPB) tcnt[f] = 0;
-      __syncthreads();
-      ph.mark(30);
-    }
-    __syncthreads();  // s_next is written
-  }
-  ph.flush(11);
-}
-
-// ---- slab apply ----------------------------------------------------------------------------------------
-constexpr int kCRB = 4;  // records per thread per batch: loads issue together, then the LDS adds
-constexpr u32 kSparseCap = 2040;  // sparse apply items hold at most this many records (touched list; 4 workgroups per CU fit in LDS)
-
-// One work item = up to kCItem records of one slab: summed in LDS (A, a byte flag per touched
-// element), then one coalesced read-modify-write of the touched pairs (exclusive items) or device
-// atomics (items of a slab that was cut into several). Software-pipelined: the next item's
-// descriptor and first record batch are loaded before this item's read-modify-write, so their
-// latencies overlap.
-template <typename A>
-__device__ __forceinline__ void apply_fetch(const uint4& d, const u32* __restrict__ addr, const A* __restrict__ val,
-                                            u32 (&ad)[kCRB], A (&v)[kCRB]) {
-#pragma unroll
-  for (int q = 0; q < kCRB; ++q) {  // clamped, branch-free loads
-    const u32 j = d.y + q * kCTPB + threadIdx.x;
-    const u32 jj = j < d.z ? j : d.z - 1;
-    ad[q] = kEmptySlot;
-    v[q] = A(0);
-    if (d.w != kItemEmpty && d.z > d.y) {
-      ad[q] = ld_in(addr + jj);
-      v[q] = ld_in(val + jj);
-      if (j >= d.z) ad[q] = kEmptySlot;
-    }
-  }
-}
-
-template <typename V>
-__global__ __launch_bounds__(kCTPB) void bin_apply_kernel(const u32* __restrict__ addr,
-                                                          const typename LdsAcc<V>::T* __restrict__ val,
-                                                          const uint4* __restrict__ cdesc, const BinCtl* bc, i64 elems,
-                                                          V* __restrict__ data, u32 pre_min, u32 sparse_max,
-                                                          u32 list_max, bool line_wb) {
-  typedef typename Vec2<V>::T V2;
-  typedef typename LdsAcc<V>::T A;
-  __shared__ A acc[kSlab];
-  __shared__ uint8_t touched[kSlab];  // plain byte stores: no atomic serialisation on hot elements
-  // sparse items (<= sparse_max records): the elements they touch, listed once each (first touch)
-  __shared__ uint16_t tlist[kSparseCap];
-  __shared__ u32 ntl[2];  // list lengths, alternating per item (the other one is reset meanwhile)
-  constexpr int kPairsPerThread = kSlab / 2 / kCTPB;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const u64 below = (1ull << lane) - 1ull;
-  u32 par = 0;
-  if (tid < 2) ntl[tid] = 0;
-  const uint4 kEmpty4 = make_uint4(0u, 0u, 0u, kItemEmpty);
-  const u32 nslots = bc->nslots;  // written by bin_fpart: slots past it hold an older push's items
-  u32 it = blockIdx.x;
-  uint4 nd = it < nslots ? cdesc[it] : kEmpty4;
-  u32 pa[kCRB];
-  A pv[kCRB];
-  apply_fetch<A>(nd, addr, val, pa, pv);
-  // acc and touched are zero between items: cleared once here, then by each item's write-back as it
-  // reads them (no clearing pass and no barrier for it per item)
-  for (int e = tid; e < kSlab; e += kCTPB) acc[e] = A(0);
-  for (int w = tid; w < kSlab / 16; w += kCTPB) reinterpret_cast<uint4*>(touched)[w] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  PhaseClock ph(40);
-  for (; it < nslots; it += gridDim.x) {
-    const uint4 d4 = nd;
-    u32 ca[kCRB];
-    A cv[kCRB];
-#pragma unroll
-    for (int q = 0; q < kCRB; ++q) {
-      ca[q] = pa[q];
-      cv[q] = pv[q];
-    }
-    nd = it + gridDim.x < nslots ? cdesc[it + gridDim.x] : kEmpty4;
-    if (d4.w == kItemEmpty) {  // block-uniform
-      apply_fetch<A>(nd, addr, val, pa, pv);
-      continue;
-    }
-    const u32 slab = d4.x;
-    const bool exclusive = d4.w == 1u;
-    const u32 r_lo = d4.y, r_hi = d4.z;
-    const i64 sbase_g = (i64)slab << kSlabBits;
-    V* const sbase = data + sbase_g;
-    // an item with many records touches most of the slab's lines: pull the slab into L2 now (one
-    // dword per 128-B line), so the fetch overlaps the record phase and the RMW's loads hit
-    const bool pre = exclusive && r_hi - r_lo >= pre_min;
-    u32 warm = 0;
-    if (pre) {
-      constexpr int kLines = kSlab * (int)sizeof(V) / 128;
-      constexpr int kPerLine = 128 / (int)sizeof(V);
-      for (int l = tid; l < kLines; l += kCTPB)
-        if (sbase_g + (i64)l * kPerLine < elems) warm ^= *reinterpret_cast<const u32*>(sbase + (i64)l * kPerLine);
-    }
-    ph.mark(40);
-    ph.mark(41);
-    // block-uniform: a sparse item lists its elements at first touch (a returning LDS OR on the
-    // byte's word), so the write-back visits those alone instead of sweeping the slab's 4096 flags
-    const bool sparse = exclusive && r_hi - r_lo <= sparse_max;
-    for (u32 j0 = r_lo;;) {  // the first batch came with the prefetch
-      if (sparse) {
-#pragma unroll
-        for (int q = 0; q < kCRB; ++q) {
-          bool first = false;
-          u32 e = 0;
-          if (ca[q] != kEmptySlot) {
-            e = ca[q] & (kSlab - 1);
-            lds_add(&acc[e], cv[q]);
-            const u32 sh = 8u * (e & 3u);
-            first = ((atomicOr(reinterpret_cast<u32*>(touched) + (e >> 2), 1u << sh) >> sh) & 0xFFu) == 0u;
-          }
-          const u64 b = __ballot(first);
-          if (b) {
-            u32 base = 0;
-            if (lane == 0) base = atomicAdd(&ntl[par], (u32)__popcll(b));
-            base = __shfl(base, 0);
-            if (first) tlist[base + (u32)__popcll(b & below)] = (uint16_t)e;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < kCRB; ++q) {
-          if (ca[q] == kEmptySlot) continue;
-          const u32 e = ca[q] & (kSlab - 1);
-          lds_add(&acc[e], cv[q]);
-          touched[e] = 1;
-        }
-      }
-      j0 += (u32)kCTPB * kCRB;
-      if (j0 >= r_hi) break;
-      apply_fetch<A>(make_uint4(0u, j0, r_hi, 0u), addr, val, ca, cv);
-    }
-    asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
-    ph.mark(42);
-    __syncthreads();
-    ph.mark(43);
-    apply_fetch<A>(nd, addr, val, pa, pv);  // the next item's first batch: in flight during the RMW
-    bool sweep_wb = exclusive && !sparse;
-    if (sparse) {
-      // the other parity's list was read by the previous item, before the barrier that ended it,
-      // and is appended to only after the barrier that ends this one
-      if (tid == 0) ntl[par ^ 1u] = 0;
-      const u32 L = ntl[par];  // block-uniform (read after the barrier)
-      if (L > list_max) {
-        sweep_wb = true;  // many distinct elements: most lines are touched, so whole-line write-back
-      } else {
-        for (u32 i = tid; i < L; i += kCTPB) {
-          const u32 e = tlist[i];
-          if (sbase_g + e < elems) sbase[e] = acc_add(sbase[e], acc[e]);
-          acc[e] = A(0);
-          touched[e] = 0;
-        }
-      }
-      par ^= 1u;
-    }
-    if (sweep_wb) {
-      // one coalesced RMW of the slab's touched 128-B lines: every pair of a line with a touched
-      // element is read and written back (the untouched ones unchanged -- the slab is this item's), so
-      // the stores are whole lines, not byte-masked pairs. Lanes of a line-less pair load the slab's
-      // first pair instead (one cached line), so all loads issue back to back without a branch.
-      // (GLINT_BIN_LINE_WB=0: the touched pairs only.)
-      constexpr int kPPL = 128 / (2 * (int)sizeof(V));  // pairs per line: 8 lanes (Double), 16 (Float)
-      const u64 gmask = (kPPL >= 64 ? ~0ull : ((1ull << kPPL) - 1ull)) << (lane & ~(kPPL - 1));
-      V2 dd[kPairsPerThread];
-      u32 t[kPairsPerThread];
-      bool wb[kPairsPerThread];
-#pragma unroll
-      for (int q = 0; q < kPairsPerThread; ++q) {
-        const int e0 = 2 * (tid + q * kCTPB);
-        t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
-        wb[q] = line_wb ? (__ballot(t[q] != 0u) & gmask) != 0ull : t[q] != 0u;  // wave-uniform loop
-      }
-#pragma unroll
-      for (int q = 0; q < kPairsPerThread; ++q) {
-        const int e0 = 2 * (tid + q * kCTPB);
-        const bool vec = wb[q] && sbase_g + e0 + 1 < elems;
-        dd[q] = *reinterpret_cast<const V2*>(vec ? sbase + e0 : sbase);
-        if (t[q]) *reinterpret_cast<uint16_t*>(touched + e0) = 0;
-      }
-#pragma unroll
-      for (int q = 0; q < kPairsPerThread; ++q) {
-        if (!wb[q]) continue;
-        const int e0 = 2 * (tid + q * kCTPB);
-        if (sbase_g + e0 + 1 < elems) {
-          V2 r = dd[q];
-          if (t[q] & 1u) r.x = acc_add((V)r.x, acc[e0]);
-          if (t[q] & 2u) r.y = acc_add((V)r.y, acc[e0 + 1]);
-          *reinterpret_cast<V2*>(sbase + e0) = r;
-        } else if (t[q]) {  // the shard's last element, odd count
-          sbase[e0] = acc_add(sbase[e0], acc[e0]);
-        }
-        if (t[q]) {
-          acc[e0] = A(0);
-          acc[e0 + 1] = A(0);
-        }
-      }
-    } else if (!exclusive) {
-      for (int e = tid; e < kSlab; e += kCTPB) {
-        if (touched[e]) {
-          gadd(sbase + e, (V)acc[e]);
-          acc[e] = A(0);
-          touched[e] = 0;
-        }
-      }
-    }
-    ph.mark(44);
-    __syncthreads();
-    ph.mark(45);
-  }
-  ph.flush(6);
 }
 
 // ==== v2 fine stage: one sort pass per fine item, a plan per bucket, an apply that gathers runs =========
@@ -1574,6 +1095,12 @@ constexpr u32 kSItem = (u32)kSTPB * kSPer;  // records per fine item (v2)
 static_assert(kSItem <= 32768, "u16 slab offsets and the u16 staging of one item");
 constexpr u32 kUnitExcl = 1u;  // apply unit descriptor {slab, runs, records, flags}: the slab's only unit
 constexpr u32 kSparseCap2 = 1024;  // bin_apply2's touched list (4 workgroups per CU fit in LDS)
+// An exclusive slab unit of at most kSparseMax2 records lists its touched elements (first touch) and
+// writes back those alone -- unless it touched more than kListMax distinct elements: at 768 of a slab's
+// 4096 ~95 % of its lines are touched, and the whole-line sweep beats byte-masked element stores
+// (cfg4b exchange 2.91 -> 2.84-2.88 ms, profiles/r04/ab_apply_writeback.txt; 256 / 512 slowed cfg5)
+constexpr u32 kSparseMax2 = kSparseCap2;
+constexpr u32 kListMax = 768;
 
 // One workgroup per bucket: every slab's runs (one per item of the bucket, from the bucket's off2 rows,
 // staged in LDS) cut into apply units of <= kUnitCap records and <= kRunMax runs (a run longer than
@@ -1919,8 +1446,8 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
 
 // Per apply unit: the records of its runs (record r lives in run i = the last one whose prefix is <= r:
 // a binary search over the unit's run table in LDS), kCRB2 per thread per batch. A slab unit sums them
-// in LDS and is written back as in bin_apply (exclusive: one coalesced RMW of the touched lines, or the
-// touched list of a sparse unit; shared: device atomics). A group unit (several sparse slabs) sums them
+// in LDS and is written back (exclusive: one coalesced RMW of the touched 128-B lines, or the touched
+// list of a sparse unit; shared: device atomics). A group unit (several sparse slabs) sums them
 // in an LDS hash table keyed by element (overlaying the slab accumulator) and read-modify-writes each
 // distinct element. Element write-backs issue all their loads before any store (a loop of dependent
 // load / store pairs would wait one round trip per element). Software-pipelined per workgroup: the
@@ -1929,9 +1456,6 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
 #ifndef GLINT_APPLY2_WAVES
 #define GLINT_APPLY2_WAVES 4  // bin_apply2's register budget: waves per SIMD (4 workgroups per CU fit in LDS)
 #endif
-#ifndef GLINT_APPLY2_WARM
-#define GLINT_APPLY2_WARM 0  // slab warm-up: 0 off, 1 one unit ahead, 2 at the unit's own start
-#endif
 #ifndef GLINT_CRB2
 #define GLINT_CRB2 4  // (8: 18 spilled VGPRs; A/B profiles/r05: cfg5 0.383 vs 0.403 ms, cfg3 1.130 vs 1.136, cfg4b 2.508 vs 2.501)
 #endif
@@ -1939,8 +1463,7 @@ constexpr int kCRB2 = GLINT_CRB2;  // records per thread per batch
 template <typename V>
 __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APPLY2_WAVES))) void bin_apply2_kernel(
     const uint16_t* __restrict__ e_in, const typename LdsAcc<V>::T* __restrict__ v_in, const uint4* __restrict__ units,
-    const uint2* __restrict__ runs, const BinCtl* bc, i64 elems, V* __restrict__ data, u32 pre_min, u32 sparse_max,
-    u32 list_max, bool line_wb, int xcd_map, u32 nf) {
+    const uint2* __restrict__ runs, const BinCtl* bc, i64 elems, V* __restrict__ data, int xcd_map, u32 nf) {
   typedef typename Vec2<V>::T V2;
   typedef typename LdsAcc<V>::T A;
   static_assert(kRunMax <= kCTPB, "one run per loading thread");
@@ -2023,17 +1546,6 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
     }
     return valid;
   };
-  auto warm_slab = [&](const uint4& d) -> u32 {  // most of the slab's lines will be touched: into L2 now
-    u32 w = 0;
-    if ((d.w & (kUnitExcl | kUnitGroup)) == kUnitExcl && d.z >= pre_min) {
-      constexpr int kLines = kSlab * (int)sizeof(V) / 128;
-      constexpr int kPerLine = 128 / (int)sizeof(V);
-      const i64 sb = (i64)d.x << kSlabBits;
-      for (int l = tid; l < kLines; l += kCTPB)
-        if (sb + (i64)l * kPerLine < elems) w ^= *reinterpret_cast<const u32*>(data + sb + (i64)l * kPerLine);
-    }
-    return w;
-  };
   // a wave's claimed list entries: one LDS atomic per wave for all its lanes' new entries
   auto list_append = [&](bool first, u32 val, u32 par_, uint16_t* list) {
     const u64 bl = __ballot(first);
@@ -2055,7 +1567,6 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
   u32 pa[kCRB2];
   A pv[kCRB2];
   u32 pvalid = fetch(0, dcur, 0u, pa, pv);
-  u32 warm = GLINT_APPLY2_WARM == 1 ? warm_slab(dcur) : 0u;
   int cs = 0;  // LDS table slot of unit u
   u32 par = 0;
   PhaseClock ph(56);
@@ -2066,8 +1577,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
     const bool exclusive = (d.w & kUnitExcl) != 0;
     const i64 sbase_g = (i64)slab << kSlabBits;
     V* const sbase = data + sbase_g;
-    const bool sparse = !group && exclusive && cnt <= sparse_max;
-    if (GLINT_APPLY2_WARM == 2) warm = warm_slab(d);
+    const bool sparse = !group && exclusive && cnt <= kSparseMax2;
     u32 ca[kCRB2];
     A cv[kCRB2];
     u32 valid = pvalid;
@@ -2126,7 +1636,6 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
       if (r0 >= cnt) break;
       valid = fetch(cs, d, r0, ca, cv);
     }
-    asm volatile("" ::"v"(warm));  // the warm-up loads complete here, after the record phase
     ph.mark(56);
     // the next unit's run table into the other slot; the one after it starts loading
     publish(cs ^ 1, dnext, rnext);
@@ -2135,15 +1644,14 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
     __syncthreads();
     ph.mark(57);
     if (tid == 0) ntl[par ^ 1u] = 0;  // the next list unit's count (the last one read it before a barrier)
-    // the next unit's first batch (and warm-up): in flight during this unit's write-back
+    // the next unit's first batch: in flight during this unit's write-back
     pvalid = fetch(cs ^ 1, dcur, 0u, pa, pv);
-    if (GLINT_APPLY2_WARM == 1) warm = warm_slab(dcur);
     ph.mark(58);
     bool sweep_wb = exclusive && !sparse && !group;
     if (group || sparse) {
       const u32 L = ntl[par];  // block-uniform (read after the barrier)
       par ^= 1u;
-      if (sparse && L > list_max) {
+      if (sparse && L > kListMax) {
         sweep_wb = true;  // many distinct elements: whole-line write-back
       } else {
         // element read-modify-writes: every load of a pass (kListPass per thread, 1024 elements)
@@ -2181,7 +1689,11 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
         }
       }
     }
-    if (sweep_wb) {  // as bin_apply: whole touched lines, read and written back
+    if (sweep_wb) {
+      // one coalesced RMW of the slab's touched 128-B lines: every pair of a line with a touched
+      // element is read and written back (the untouched ones unchanged -- the slab is this unit's), so
+      // the stores are whole lines, not byte-masked pairs. Lanes of a line-less pair load the slab's
+      // first pair instead (one cached line), so all loads issue back to back without a branch.
       constexpr int kPPL = 128 / (2 * (int)sizeof(V));
       const u64 gmask = (kPPL >= 64 ? ~0ull : ((1ull << kPPL) - 1ull)) << (lane & ~(kPPL - 1));
       V2 dd[kPairsPerThread];
@@ -2191,7 +1703,7 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
       for (int q = 0; q < kPairsPerThread; ++q) {
         const int e0 = 2 * (tid + q * kCTPB);
         t[q] = (u32)touched[e0] | ((u32)touched[e0 + 1] << 1);
-        wb[q] = line_wb ? (__ballot(t[q] != 0u) & gmask) != 0ull : t[q] != 0u;
+        wb[q] = (__ballot(t[q] != 0u) & gmask) != 0ull;  // wave-uniform per line
       }
 #pragma unroll
       for (int q = 0; q < kPairsPerThread; ++q) {
@@ -2231,44 +1743,10 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
     ph.mark(60);
     cs ^= 1;
   }
-  asm volatile("" ::"v"(warm));
   ph.flush(5);
 }
 
 // ---- host side ----------------------------------------------------------------------------------------
-// records per slab item from which bin_apply warms the whole slab into L2 (GLINT_BIN_PREFETCH_MIN;
-// 0xFFFFFFFF disables)
-u32 bin_prefetch_min() {
-  static EnvKnob k("GLINT_BIN_PREFETCH_MIN");
-  return (u32)k.get([](const char* e) -> long long { return e ? (long long)strtoul(e, nullptr, 10) : kSlab / 4; });
-}
-
-// records per exclusive slab item up to which bin_apply lists the touched elements instead of
-// sweeping the slab (GLINT_BIN_SPARSE_MAX; 0 disables; at most kSparseCap)
-u32 bin_sparse_max() {
-  static EnvKnob k("GLINT_BIN_SPARSE_MAX");
-  return (u32)k.get([](const char* e) -> long long {
-    return std::min<u32>(kSparseCap, e ? (u32)strtoul(e, nullptr, 10) : 1024u);
-  });
-}
-
-// a sparse item whose list holds more distinct elements than this writes back by the line sweep
-// instead (GLINT_BIN_LIST_MAX, default 768; 0xFFFFFFFF disables): at 768 of a slab's 4096 elements
-// ~95 % of its lines are touched, and element stores would leave them byte-masked. Same box, 3 rounds
-// (profiles/r04/ab_apply_writeback.txt): cfg4b exchange 2.91 -> 2.84-2.88 ms, cfg3 unchanged, cfg5
-// within its run-to-run spread (0.43-0.46 ms either way); lower thresholds (256, 512) slowed cfg5
-u32 bin_list_max() {
-  static EnvKnob k("GLINT_BIN_LIST_MAX");
-  return (u32)k.get([](const char* e) -> long long { return e ? (long long)strtoul(e, nullptr, 10) : 768ll; });
-}
-
-// bin_apply's swept items write back whole touched lines (GLINT_BIN_LINE_WB, default 1) or the
-// touched pairs only (0)
-bool bin_line_wb() {
-  static EnvKnob k("GLINT_BIN_LINE_WB");
-  return k.get([](const char* e) -> long long { return e ? atoll(e) : 1ll; }) != 0;
-}
-
 // resident blocks per CU of a kernel at its block size (occupancy query)
 template <typename K>
 int resident_per_cu(K kernel, int tpb, size_t dyn_lds = 0) {
@@ -2280,21 +1758,17 @@ int resident_per_cu(K kernel, int tpb, size_t dyn_lds = 0) {
   return b;
 }
 
+// 128 coarse buckets (few enough that a partition chunk's records form runs per bucket, and a fine
+// item's runs per slab stay as long: 32 records each way for uniform keys into 2^28), more only when
+// the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses). Same box, two runs each
+// (profiles/r03/bench_binned_cb.txt): 2^7 against 2^8 buckets cfg5 0.418 -> 0.398 ms, cfg3 1.648 ->
+// 1.636 ms, cfg4b exchange 3.005 -> 3.005 ms; 2^6 slower on all
+constexpr u32 kCoarseBitsMin = 7;
 BinGeom bin_geometry(i64 elems) {
   const i64 slabs = (elems + kSlab - 1) / kSlab;
   u32 sb = 0;
   while (((i64)1 << sb) < slabs) ++sb;
-  // 128 coarse buckets (few enough that a partition chunk's records form runs per bucket, and a
-  // fine-partition item's runs per slab stay as long: 32 records each way for uniform keys into
-  // 2^28), more only when the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses).
-  // Same box, two runs each (profiles/r03/bench_binned_cb.txt): 2^7 against 2^8 buckets cfg5
-  // 0.418 -> 0.398 ms, cfg3 1.648 -> 1.636 ms, cfg4b exchange 3.005 -> 3.005 ms; 2^6 slower on all
-  static EnvKnob cb_knob("GLINT_BIN_CB");  // coarse digit bits at least (tuning knob, 4..10)
-  const u32 cb_min = (u32)cb_knob.get([](const char* e) -> long long {
-    const int v = e ? atoi(e) : 0;
-    return v >= 4 && v <= 10 ? v : 7;
-  });
-  const u32 cb = std::min<u32>(sb, std::max<u32>(cb_min, sb > 10u ? sb - 10u : 0u));
+  const u32 cb = std::min<u32>(sb, std::max<u32>(kCoarseBitsMin, sb > 10u ? sb - 10u : 0u));
   BinGeom g;
   g.fb = sb - cb;
   g.nb = 1u << cb;
@@ -2303,15 +1777,9 @@ BinGeom bin_geometry(i64 elems) {
   return g;
 }
 
-// The v2 binned push (front: 0 plain, 1 plain + hot split, 2 chunk dedup; see push_binned).
-bool bin_v1() {
-  static EnvKnob v1_knob("GLINT_BIN_V1");
-  return v1_knob.get([](const char* e) -> long long { return e && atoi(e) != 0; }) != 0;
-}
-
-bool push_binned_fusable(const glint_shard* s, i64 n, size_t asize) {
-  return !bin_v1() && (u64)n * asize < ((u64)1 << 32) && n < ((i64)1 << 32) - 2 * kAChunk &&
-         s->elems < ((i64)1 << 32) - 1;
+// u32 record indices and element addresses
+bool push_binnable(const glint_shard* s, i64 n) {
+  return n < ((i64)1 << 32) - 2 * kAChunk && s->elems < ((i64)1 << 32) - 1;
 }
 
 int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32 nb, hipStream_t st) {
@@ -2320,37 +1788,79 @@ int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32
   return GLINT_OK;
 }
 
+// Front end of a binned push (0 plain, 1 plain + hot split, 2 chunk dedup + hot split), from what the
+// last dedup push measured (the device reports m, the tail size and the cold records of each push
+// through host-mapped words, taken at the shard's last sync point, so the choice does not depend on
+// timing): chunk dedup when it kept < 80 % of the cold records it saw; otherwise the plain front end,
+// with the hot-element split when the hot elements took >= 25 % of the tail (cfg3 ~65 %; cfg5's ~10 %
+// does not pay for the sampling launch and the per-record check). A dedup push re-measures every 16
+// pushes (and the first one). GLINT_BIN_FRONT = dedup | hot | prep forces one (tests).
+int bin_front(glint_shard* s) {
+  {
+    const u64 w = s->hint_bin;
+    const u32 m = (u32)(w >> 32), tail = (u32)w;
+    const u32 cold = (u32)s->hint_bin_cold;
+    if (tail > 0 && s->hint_bin_front == 2) {
+      s->bin_chunk_ratio = cold ? (double)m / (double)cold : 1.0;
+      s->bin_hot_frac = 1.0 - (double)cold / (double)tail;
+    }
+  }
+  const bool probe = (s->bin_pushes++ & 15) == 0;
+  const int front = probe || s->bin_chunk_ratio < 0.8 ? 2 : (s->bin_hot_frac >= 0.25 ? 1 : 0);
+  static EnvKnob front_knob("GLINT_BIN_FRONT");
+  const int forced = (int)front_knob.get([](const char* e) -> long long {
+    if (!e) return -1;
+    if (!strcmp(e, "dedup")) return 2;
+    if (!strcmp(e, "hot")) return 1;
+    if (!strcmp(e, "prep")) return 0;
+    return -1;
+  });
+  return forced >= 0 ? forced : front;
+}
+
+// The wide hot table (front 1) is sampled every kHotEvery-th push and kept in between: a push's hot
+// set only decides how much work leaves the partition path (any set gives the same sums), and a
+// Zipf-like stream keeps its hot elements from push to push. A shard coming from another front end
+// samples at once. (tests/test_gpu_parity.py::test_binned_stream_of_batches pushes a stream of
+// different batches through the kept table.)
+constexpr u32 kHotEvery = 8;
+constexpr u32 kWideMin = 3;  // samples (of 262 144) that make an element hot in the wide table
+constexpr u32 kHotMin = 2;   // samples (of 16 384) that make an element hot in the dedup front end's table
+
 template <typename V, bool MAT>
-int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, int front, bool hot_on,
-                   const BinHook* hook, LaunchCtl* whole_next, bool hot_refresh) {
+int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook,
+                LaunchCtl* whole_next) {
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
+  if (!push_binnable(s, n)) return GLINT_EINVAL;
   const BinGeom g = bin_geometry(s->elems);
+  const int front = bin_front(s);
   const bool dedup = front == 2;
+  bool hot_refresh = true;
+  if (front == 1) {
+    hot_refresh = s->bin_last_front != 1 || s->hot_age == 0 || s->hot_age >= kHotEvery;
+    s->hot_age = hot_refresh ? 1u : s->hot_age + 1u;
+  }
+  s->bin_last_front = front;
+  // a push whose partition buffers pass 4 GiB stores through 64-bit addresses (WideOut)
+  const bool wide = (u64)n * sizeof(A) >= ((u64)1 << 32);
   const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
-  static EnvKnob wpc_knob("GLINT_PART_WPC");
   // partition workgroups per CU: what fits at once (the hot front end's LDS table allows fewer)
-  static const int hot_occ = resident_per_cu(bin_part_kernel<V, MAT, true, 0>, kATPB);
-  const int plain_wpc = (int)wpc_knob.pos_or(kPartWgPerCuPlain);
-  const int wpc = dedup ? kPartWgPerCuDedup : front == 1 ? std::min(plain_wpc, hot_occ) : plain_wpc;
+  static const int hot_occ = resident_per_cu(bin_part_kernel<V, MAT, true, 0, false>, kATPB);
+  const int wpc = dedup ? kPartWgPerCuDedup : front == 1 ? std::min(kPartWgPerCuPlain, hot_occ) : kPartWgPerCuPlain;
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * wpc));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
-  // fine items: kSItem records, or (GLINT_FSORT_ITEM, a multiple of the fine sort's workgroup up to
-  // kSItem) fewer for a small push, whose items then spread over more of the chip
-  static EnvKnob item_knob("GLINT_FSORT_ITEM");
+  // a small push (at most ~4 fine items per CU, cfg5) plans its buckets inside bin_fsort
   const bool small_push = (i64)g.nb + n / kSItem + 1 <= (i64)4 * s->cus;
-  const u32 item = small_push ? (u32)item_knob.get([](const char* e) -> long long {
-    const long long v = e ? atoll(e) : (long long)kSItem;
-    return v >= kSTPB && v <= (long long)kSItem && v % kSTPB == 0 ? v : (long long)kSItem;
-  }) : kSItem;
+  const u32 item = kSItem;
   const i64 max_fitems = (i64)g.nb + n / item + 1;
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
   // floor(H / cap) + floor(runs / kRunMax) + 1 per non-empty slab
   const i64 max_units = (i64)g.nslab + n / kUnitCap + std::min<i64>(n, max_fitems * g.nf) / kRunMax + 1;
-  // R, Roff, Bb, Ib, the fine items, off2, the apply units, the dedup front end's hot tags and the
-  // record buffers (coarse: u32 address + A value; fine: u16 slab offset + A value). The [BinCtl | T]
-  // headers and the hot front end's tables live in buffers of their own (stable addresses: emptied by
-  // the kernels of the push before, not by memsets)
+  // R, Roff, Bb, Ib, the fine items, off2, the apply units, the dedup front end's hot tags, the dump
+  // area of wide stores and the record buffers (coarse: u32 address + A value; fine: u16 slab offset + A
+  // value). The [BinCtl | T] headers and the hot front end's tables live in buffers of their own (stable
+  // addresses: emptied by the kernels of the push before, not by memsets)
   const size_t b_seg = pad256((size_t)G * g.nb * 4);
   const size_t b_nb = pad256((size_t)g.nb * 4);
   const size_t b_fit = pad256((size_t)max_fitems * 8), b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 4);
@@ -2358,7 +1868,8 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   const size_t b_hot = pad256((size_t)kHotSlots * 4);
   const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
   const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(A)), b_e = pad256((size_t)n * 2);
-  const size_t need = 2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + b_wpart + b_a + 2 * b_v + b_e;
+  const size_t need =
+      2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + kDumpBytes + b_wpart + b_a + 2 * b_v + b_e;
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   constexpr size_t kHdr = 12288;  // one [BinCtl (256 B) | T (<= kMaxDigit u32) | done (<= kMaxDigit u32)] header
@@ -2403,6 +1914,8 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   p += b_units;
   u32* hot_tags = (u32*)p;
   p += b_hot;
+  void* dump = p;
+  p += kDumpBytes;
   u32* wkey = front == 1 ? (u32*)s->d_hot : nullptr;
   u32* wcnt = front == 1 ? (u32*)((char*)s->d_hot + b_wk) : nullptr;
   unsigned long long* wbest = front == 1 ? (unsigned long long*)((char*)s->d_hot + 2 * b_wk) : nullptr;
@@ -2416,19 +1929,15 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
   ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
   const int fb = from_break ? 1 : (hook && whole_next ? 2 : 0);
   if (front == 1 && hot_refresh) {  // the wide hot table: sample, count, pick (the count table starts empty)
-    static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");
-    const u32 wide_min = (u32)wide_knob.pos_or(3);
     HIPCHK(hipMemsetAsync(wbest, 0, b_wbest, st));  // the picks of the pushes before (kept for reuse)
     bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
                                                                 wcnt);
     HIPCHK(hipGetLastError());
-    bin_hot_select_kernel<<<(1u << kWideHashBits) / 256u, 256, 0, st>>>(wkey, wcnt, wide_min, wbest);
+    bin_hot_select_kernel<<<(1u << kWideHashBits) / 256u, 256, 0, st>>>(wkey, wcnt, kWideMin, wbest);
     HIPCHK(hipGetLastError());
   }
-  if (dedup && hot_on) {
-    static EnvKnob hmin_knob("GLINT_BIN_HOT_MIN");
-    const u32 hot_min = (u32)hmin_knob.pos_or(2);
-    bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, hot_min, hot_tags);
+  if (dedup) {
+    bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, kHotMin, hot_tags);
     HIPCHK(hipGetLastError());
   }
   const unsigned long long* count_hot = front == 1 ? wbest : nullptr;  // the hot records are not partitioned
@@ -2452,33 +1961,33 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
     if (rc) return rc;
   }
   if (dedup) {
-    auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
-                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data, item, Roff, Bb, Ib);
+    auto kern = a.part.kind == 0 ? (wide ? bin_part_dedup_kernel<V, MAT, 0, true> : bin_part_dedup_kernel<V, MAT, 0, false>)
+                                 : (wide ? bin_part_dedup_kernel<V, MAT, -1, true> : bin_part_dedup_kernel<V, MAT, -1, false>);
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, addr_a, val_a, a.err, bc, T,
+                              fitems, hot_tags, a.data, item, Roff, Bb, Ib, dump);
   } else {
-    auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
-                                 : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, nullptr, nullptr, addr_a,
-                              val_a, a.err, bc, T, fitems, wbest, wpart, item, Roff, Bb, Ib);
+    auto kern = a.part.kind == 0
+                    ? (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, 0, true> : bin_part_kernel<V, MAT, true, 0, false>)
+                                  : (wide ? bin_part_kernel<V, MAT, false, 0, true> : bin_part_kernel<V, MAT, false, 0, false>))
+                    : (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, -1, true> : bin_part_kernel<V, MAT, true, -1, false>)
+                                  : (wide ? bin_part_kernel<V, MAT, false, -1, true> : bin_part_kernel<V, MAT, false, -1, false>));
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, addr_a, val_a, a.err, bc, T,
+                              fitems, wbest, wpart, item, Roff, Bb, Ib, dump);
   }
   HIPCHK(hipGetLastError());
   if (front == 1) {
-    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, 0);
+    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
     HIPCHK(hipGetLastError());
   }
   // Groups of sparse slabs for vector shards; a matrix shard's sparse slabs stay units of their own: its
   // records cluster in a slab's few hot rows, and grouping cost cfg5 0.309 -> 0.337 ms while it takes
-  // cfg3 1.077 -> 1.038 (profiles/r05/ab_group_unitcap.txt). GLINT_BIN_GROUP=0 / 1 forces it.
-  static EnvKnob group_knob("GLINT_BIN_GROUP");
-  const long long gk = group_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : -1; });
-  const int group_on = gk < 0 ? (MAT ? 0 : 1) : (int)gk;
-  static EnvKnob fused_knob("GLINT_BIN_FUSED_PLAN");  // 0: the plan as a launch of its own (A/B)
-  // (fused: a push of at most 4 items per CU -- cfg5's 641 -- where the plan launch and its tail are a
-  // real share of the push; with many items per CU every item's wait for its stores before counting
-  // itself in costs more: cfg3 1.067 -> 1.078, cfg4b 2.375 -> 2.44 ms, cfg5 0.347 -> 0.335,
-  // profiles/r05/ab_fused_plan.txt. GLINT_BIN_FUSED_PLAN=0 / 1 forces it off / on)
-  const long long fz = fused_knob.get([](const char* e) -> long long { return e ? atoi(e) : -1; });
-  const bool fused = fz == 1 || (fz < 0 && small_push);
+  // cfg3 1.077 -> 1.038 (profiles/r05/ab_group_unitcap.txt).
+  const int group_on = MAT ? 0 : 1;
+  // The plan fused into bin_fsort for a push of at most ~4 items per CU (cfg5's 641), where the plan
+  // launch and its tail are a real share of the push; with many items per CU every item's wait for its
+  // stores before counting itself in costs more: cfg3 1.067 -> 1.078, cfg4b 2.375 -> 2.44 ms, cfg5
+  // 0.347 -> 0.335 (profiles/r05/ab_fused_plan.txt)
+  const bool fused = small_push;
   u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
   u64* const whint = whole_next ? s->d_hint : nullptr;
   if (fused) {
@@ -2494,210 +2003,12 @@ int push_binned_v2(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStr
     bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on, item);
     HIPCHK(hipGetLastError());
   }
-  // a persistent grid of the resident workgroups: each pipelines its units two deep
+  // a persistent grid of the resident workgroups: each pipelines its units two deep, in XCD-grouped
+  // order (see bin_apply2_kernel)
   static const int apply2_occ = resident_per_cu(bin_apply2_kernel<V>, kCTPB);
-  static EnvKnob apply2_knob("GLINT_BIN_APPLY2_BPC");
-  static EnvKnob xcd_knob("GLINT_BIN_XCD");  // XCD-grouped unit order (see bin_apply2_kernel); 2 = off
-  const int apply2_bpc = (int)apply2_knob.pos_or(apply2_occ);
-  const unsigned apply2_grid = (unsigned)std::min<i64>(max_units, (i64)s->cus * apply2_bpc);
-  bin_apply2_kernel<V><<<apply2_grid, kCTPB, 0, st>>>(
-      e_b, val_b, units, runs, bc, s->elems, a.data, bin_prefetch_min(), std::min<u32>(bin_sparse_max(), kSparseCap2),
-      bin_list_max(), bin_line_wb(), apply2_grid % 8 == 0 && xcd_knob.pos_or(1) == 1 ? 1 : 0, g.nf);
-  HIPCHK(hipGetLastError());
-  return GLINT_OK;
-}
-
-template <typename V, bool MAT>
-int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream_t st, const BinHook* hook,
-                LaunchCtl* whole_next) {
-  typedef typename LdsAcc<V>::T A;
-  const i64 n = a.n;
-  if (n >= ((i64)1 << 32) - 2 * kAChunk || s->elems >= ((i64)1 << 32) - 1) return GLINT_EINVAL;  // u32 addresses
-  const BinGeom g = bin_geometry(s->elems);
-  // Front end, from what the last dedup push measured (the device reports m, the tail size and the
-  // cold records of each push through host-mapped words, taken at the shard's last sync point, so the
-  // choice does not depend on timing): chunk dedup when it kept < 80 % of the cold records it saw;
-  // otherwise the plain front end, with the hot-element split when the hot elements took >= 25 % of
-  // the tail (cfg3 ~65 %; cfg5's ~10 % does not pay for the sampling launch and the per-record check).
-  // A dedup push re-measures every 16 pushes (and the first one).
-  // GLINT_BIN_FRONT = dedup | hot | prep forces one (tests, tuning).
-  static EnvKnob hot_knob("GLINT_BIN_HOT");  // GLINT_BIN_HOT=0: no hot-element split (A/B, tests)
-  const bool hot_on = hot_knob.get([](const char* e) -> long long { return !(e && atoi(e) == 0); }) != 0;
-  {
-    const u64 w = s->hint_bin;
-    const u32 m = (u32)(w >> 32), tail = (u32)w;
-    const u32 cold = (u32)s->hint_bin_cold;
-    if (tail > 0 && s->hint_bin_front == 2) {
-      s->bin_chunk_ratio = cold ? (double)m / (double)cold : 1.0;
-      s->bin_hot_frac = 1.0 - (double)cold / (double)tail;
-    }
-  }
-  const bool probe = (s->bin_pushes++ & 15) == 0;
-  int front = probe || s->bin_chunk_ratio < 0.8 ? 2 : (hot_on && s->bin_hot_frac >= 0.25 ? 1 : 0);
-  static EnvKnob front_knob("GLINT_BIN_FRONT");
-  const int forced = (int)front_knob.get([](const char* e) -> long long {
-    if (!e) return -1;
-    if (!strcmp(e, "dedup")) return 2;
-    if (!strcmp(e, "hot")) return 1;
-    if (!strcmp(e, "prep")) return 0;
-    return -1;
-  });
-  if (forced == 2 || forced == 0) front = forced;
-  else if (forced == 1) front = hot_on ? 1 : 0;
-  const bool dedup = front == 2;
-  // The wide hot table (front 1) is sampled every GLINT_BIN_HOT_EVERY-th push (default 8) and kept in
-  // between: a push's hot set only decides how much work leaves the partition path (any set gives the
-  // same sums), and a Zipf-like stream keeps its hot elements from push to push. A shard coming from
-  // another front end samples at once.
-  static EnvKnob hot_every_knob("GLINT_BIN_HOT_EVERY");
-  const u32 hot_every = (u32)hot_every_knob.pos_or(8);
-  bool hot_refresh = true;
-  if (front == 1) {
-    hot_refresh = s->bin_last_front != 1 || s->hot_age == 0 || s->hot_age >= hot_every;
-    s->hot_age = hot_refresh ? 1u : s->hot_age + 1u;
-  }
-  s->bin_last_front = front;
-  // the v2 fine stage (bin_fsort / bin_plan / bin_apply2) unless GLINT_BIN_V1=1; its coarse partition
-  // addresses the whole buffer through one 32-bit buffer window
-  if (hook || whole_next || push_binned_fusable(s, n, sizeof(A)))
-    return push_binned_v2<V, MAT>(s, a, from_break, st, front, hot_on, hook, whole_next, hot_refresh);
-  // the partition grid: one dedup workgroup per CU (its LDS table), two plain ones; bin_count runs
-  // on the same grid so that its per-workgroup counts are the partition's capacities
-  const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
-  static EnvKnob wpc_knob("GLINT_PART_WPC");  // plain partition workgroups per CU (tuning knob)
-  const int plain_wpc = (int)wpc_knob.pos_or(kPartWgPerCuPlain);
-  const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * (dedup ? kPartWgPerCuDedup : plain_wpc)));
-  if (G > (u32)kMaxSegs) return GLINT_EINVAL;
-  const i64 nslots = (i64)g.nslab + g.nb + n / kCItem + 1;  // apply item slots (bucket b: nf + ceil(T[b]/16384))
-  const i64 max_fitems = (i64)g.nb + n / kFItem + 1;
-  // [BinCtl | T | H | cur2] zeroed per push; then R, segoff, seglen, item maps, the record buffers
-  const size_t b_ctl = 256, b_T = pad256((size_t)g.nb * 4), b_seg = pad256((size_t)G * g.nb * 4);
-  const size_t b_H = pad256((size_t)g.nslab * 4);
-  const size_t b_cd = pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8) +
-                      pad256((size_t)max_fitems * g.nf * 4);  // + per-item slab histograms
-  const size_t cap_a = (size_t)nchunks_max * kAChunk;  // the partition's capacity (every chunk full)
-  const size_t b_a = pad256(cap_a * 4), b_v = pad256(cap_a * sizeof(A));
-  const size_t b_zero = b_ctl + b_T + 2 * b_H;
-  const size_t b_hot = pad256((size_t)kHotSlots * 4);
-  // the wide hot table of the plain + hot front end: global count table (keys, counts), the picked
-  // elements per slot, the partition workgroups' per-slot sums
-  const size_t b_wk = front == 1 ? pad256(((size_t)4 << kWideHashBits)) : 0;
-  const size_t b_wbest = front == 1 ? pad256((size_t)kWideSlots * 8) : 0;
-  const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
-  const size_t need = b_zero + 3 * b_seg + b_cd + b_hot + 2 * b_wk + b_wbest + b_wpart + 2 * (b_a + b_v);
-  int rc = grow(&s->d_bin, &s->bin_bytes, need);
-  if (rc) return rc;
-  char* p = (char*)s->d_bin;
-  BinCtl* bc = (BinCtl*)p;
-  u32* T = (u32*)(p + b_ctl);
-  u32* H = (u32*)(p + b_ctl + b_T);
-  u32* cur2 = (u32*)(p + b_ctl + b_T + b_H);
-  p += b_zero;
-  u32* R = (u32*)p;
-  u32* segoff = (u32*)(p + b_seg);
-  u32* seglen = (u32*)(p + 2 * b_seg);
-  p += 3 * b_seg;
-  uint4* cdesc = (uint4*)p;
-  uint2* fitems = (uint2*)(p + pad256((size_t)nslots * 16));
-  u32* IH = (u32*)(p + pad256((size_t)nslots * 16) + pad256((size_t)max_fitems * 8));
-  p += b_cd;
-  u32* hot_tags = (u32*)p;
-  p += b_hot;
-  u32* wkey = (u32*)p;
-  u32* wcnt = (u32*)(p + b_wk);
-  unsigned long long* wbest = (unsigned long long*)(p + 2 * b_wk);
-  A* wpart = (A*)(p + 2 * b_wk + b_wbest);
-  p += 2 * b_wk + b_wbest + b_wpart;
-  u32* addr_a = (u32*)p;
-  A* val_a = (A*)(p + b_a);
-  u32* addr_b = (u32*)(p + b_a + b_v);
-  A* val_b = (A*)(p + 2 * b_a + b_v);
-
-  ProfScope ps(s, GLINT_K_PUSH_BINNED, st);
-  HIPCHK(hipMemsetAsync(s->d_bin, 0, b_zero, st));
-  const int fb = from_break ? 1 : 0;
-  if (front == 1) {  // the wide hot table: sample, count, pick
-    static EnvKnob wide_knob("GLINT_BIN_WIDE_MIN");  // sample count that makes an element hot (tuning)
-    const u32 wide_min = (u32)wide_knob.pos_or(3);
-    HIPCHK(hipMemsetAsync(wkey, 0xFF, b_wk, st));
-    HIPCHK(hipMemsetAsync(wcnt, 0, b_wk + b_wbest, st));  // counts and picks
-    bin_hot_sample_kernel<MAT><<<kWideSampleWgs, 256, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, wkey,
-                                                                wcnt);
-    HIPCHK(hipGetLastError());
-    bin_hot_select_kernel<<<(1u << kWideHashBits) / 256u, 256, 0, st>>>(wkey, wcnt, wide_min, wbest);
-    HIPCHK(hipGetLastError());
-  }
-  if (dedup && hot_on) {
-    static EnvKnob hmin_knob("GLINT_BIN_HOT_MIN");  // sample count that makes an element hot (tuning)
-    const u32 hot_min = (u32)hmin_knob.pos_or(2);
-    bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, hot_min,
-                                                    hot_tags);
-    HIPCHK(hipGetLastError());
-  }
-  if (a.part.kind == 0)
-    bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, nullptr,
-                                                  nullptr, nullptr, nullptr);
-  else
-    bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, nullptr,
-                                                   nullptr, nullptr, nullptr);
-  HIPCHK(hipGetLastError());
-  if (dedup) {
-    auto kern = a.part.kind == 0 ? bin_part_dedup_kernel<V, MAT, 0> : bin_part_dedup_kernel<V, MAT, -1>;
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
-                              val_a, a.err, bc, T, fitems, hot_on ? hot_tags : nullptr, a.data, kFItem, nullptr,
-                              nullptr, nullptr);
-  } else {
-    auto kern = a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0> : bin_part_kernel<V, MAT, false, 0>)
-                                 : (front == 1 ? bin_part_kernel<V, MAT, true, -1> : bin_part_kernel<V, MAT, false, -1>);
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, segoff, seglen, addr_a,
-                              val_a, a.err, bc, T, fitems, wbest, wpart, kFItem, nullptr, nullptr, nullptr);
-  }
-  HIPCHK(hipGetLastError());
-  if (front == 1) {
-    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, 1);
-    HIPCHK(hipGetLastError());
-  }
-  static EnvKnob fcount_knob("GLINT_FCOUNT_BPC");
-  static const int fcount_occ = resident_per_cu(bin_fcount_kernel<false>, kFCTPB);
-  static const int fcount_whole_occ = resident_per_cu(bin_fcount_kernel<true>, kFCTPBWhole);
-  if (max_fitems <= (i64)s->cus * fcount_whole_occ) {  // every item gets its own workgroup at once
-    bin_fcount_kernel<true><<<(unsigned)max_fitems, kFCTPBWhole, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H,
-                                                                        IH);
-  } else {
-    const int fcount_rpc = (int)fcount_knob.pos_or(fcount_occ);
-    const unsigned gf = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * fcount_rpc);
-    bin_fcount_kernel<false><<<gf, kFCTPB, 0, st>>>(g, G, fitems, bc, segoff, seglen, addr_a, H, IH);
-  }
-  HIPCHK(hipGetLastError());
-  const size_t fdyn = fpart_dyn_bytes(G, g.nf);
-  // workgroup size: 512 threads (4096-record tiles, whole-line runs) unless the push has no more
-  // items than 256-thread blocks fit at once (small pushes: parallelism beats tile size)
-  static std::atomic<int> fpart_rpc[2][kMaxSegs + 1][11] = {};  // resident blocks per CU by (TPB, G, log2 nf)
-  static EnvKnob fpart_knob("GLINT_FPART_BPC");
-  auto rpc_of = [&](int w, auto kernel, int tpb) {
-    int r = fpart_rpc[w][G][g.fb].load(std::memory_order_relaxed);
-    if (!r) {  // the occupancy query once per geometry; the knob applies on top
-      r = resident_per_cu(kernel, tpb, fdyn);
-      fpart_rpc[w][G][g.fb].store(r, std::memory_order_relaxed);
-    }
-    return (int)fpart_knob.pos_or(r);
-  };
-  const int r256 = rpc_of(0, bin_fpart_kernel<A, 256>, 256);
-  if (max_fitems <= (i64)s->cus * r256) {
-    const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * r256);
-    bin_fpart_kernel<A, 256><<<gp, 256, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
-                                            val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
-  } else {
-    const int r512 = rpc_of(1, bin_fpart_kernel<A, 512>, 512);
-    const unsigned gp = (unsigned)std::min<i64>(max_fitems, (i64)s->cus * r512);
-    bin_fpart_kernel<A, 512><<<gp, 512, fdyn, st>>>(g, G, fitems, bc, T, H, cur2, segoff, seglen, addr_a, val_a, addr_b,
-                                            val_b, cdesc, s->d_hint ? s->d_hint + 1 : nullptr, IH);
-  }
-  HIPCHK(hipGetLastError());
-  static EnvKnob apply_knob("GLINT_BIN_APPLY_BPC");  // work-item blocks per CU (tuning knob)
-  const int apply_bpc = (int)apply_knob.pos_or(64);
-  bin_apply_kernel<V><<<(unsigned)std::min<i64>(nslots, (i64)s->cus * apply_bpc), kCTPB, 0, st>>>(
-      addr_b, val_b, cdesc, bc, s->elems, a.data, bin_prefetch_min(), bin_sparse_max(), bin_list_max(), bin_line_wb());
+  const unsigned apply2_grid = (unsigned)std::min<i64>(max_units, (i64)s->cus * apply2_occ);
+  bin_apply2_kernel<V><<<apply2_grid, kCTPB, 0, st>>>(e_b, val_b, units, runs, bc, s->elems, a.data,
+                                                      apply2_grid % 8 == 0 ? 1 : 0, g.nf);
   HIPCHK(hipGetLastError());
   return GLINT_OK;
 }

@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kTPB) void set_scatter_kernel(const i64* __restrict
       const u64 key = hk[q];
       if (key != kEmpty) {
         const int j = set_find(st, en, set.n, (i64)key);
-        gadd(dp[j] + ((i64)key - st[j]), (V)hv[q]);
+        if (j >= 0) gadd(dp[j] + ((i64)key - st[j]), (V)hv[q]);  // (validated: always found)
         hk[q] = kEmpty;
         hv[q] = A(0);
       }
@@ -741,25 +741,15 @@ using namespace glint;
 namespace {
 
 // ---- push -------------------------------------------------------------------------------------
-// blocks per CU in the affine sweep (GLINT_SWEEP_BPC overrides; 1 measured best on MI355X)
-int sweep_blocks_per_cu() {
-  static EnvKnob k("GLINT_SWEEP_BPC");
-  return (int)k.pos_or(1);
-}
+// blocks per CU in the affine sweep (1 measured best on MI355X)
+constexpr int kSweepBlocksPerCu = 1;
 
-// The apply of a large push runs as one launch per window of 2^26 records (GLINT_SWEEP_WINDOW =
-// log2 records overrides; 0 = one launch). A grid-stride sweep over a whole 2^30-record push lets its
-// blocks drift apart across gigabytes, and the 2-read + 1-write stream then runs 6-11 % slower than
-// the same bytes swept window by window (tools/microbench_stream.hip mode 6: 2^30 records whole
-// 5.90 TB/s, in 2^26-record launches 6.56 TB/s; 2^28 whole 6.21 TB/s; profiles/r03/micro_stream_2p30.txt).
-u32 sweep_window_tiles() {
-  static EnvKnob k("GLINT_SWEEP_WINDOW");
-  return (u32)k.get([](const char* e) -> long long {
-    const int lg = e ? atoi(e) : 26;
-    if (lg <= 10 || lg >= 42) return 0xFFFFFFFFll;
-    return ((i64)1 << lg) / kTile;
-  });
-}
+// The apply of a large push runs as one launch per window of 2^26 records. A grid-stride sweep over a
+// whole 2^30-record push lets its blocks drift apart across gigabytes, and the 2-read + 1-write stream
+// then runs 6-11 % slower than the same bytes swept window by window (tools/microbench_stream.hip mode
+// 6: 2^30 records whole 5.90 TB/s, in 2^26-record launches 6.56 TB/s; 2^28 whole 6.21 TB/s;
+// profiles/r03/micro_stream_2p30.txt).
+constexpr u32 kSweepWindowTiles = ((u32)1 << 26) / kTile;
 
 // GLINT_BINNED: 0 = never bin, 1 = bin every large push, unset = bin when the previous push on the
 // shard left a large unordered tail (read from the host-mapped word push_apply writes)
@@ -781,12 +771,8 @@ i64 bin_density() {
   static EnvKnob k("GLINT_BIN_DENSITY");
   return k.get([](const char* e) -> long long { return e ? std::max(0ll, atoll(e)) : 512ll; });
 }
-// records: up to this many, a (non-deterministic) push is the single scatter launch.
-// GLINT_SMALL_PUSH overrides it (0 = always check + apply).
-i64 small_push_max() {
-  static EnvKnob k("GLINT_SMALL_PUSH");
-  return k.get([](const char* e) -> long long { return e ? std::strtoll(e, nullptr, 10) : 4096ll; });
-}
+// records: up to this many, a (non-deterministic) push is the single scatter launch
+constexpr i64 kSmallPushMax = 4096;
 
 template <typename V, bool MAT>
 int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void* vals, i64 n, int flags,
@@ -842,7 +828,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   const int bmode = binned_mode();
   const i64 last_tail = (i64)s->hint_tail;  // the previous push's unordered tail, as of the last sync point
   const i64 slabs = (s->elems + 4095) / 4096;
-  const bool binned = !det && vec_ok && n < ((i64)1 << 32) && s->elems < ((i64)1 << 32) - 1 && bmode != 0 &&
+  const bool binned = !det && vec_ok && push_binnable(s, n) && bmode != 0 &&
                       (unordered || (n >= kBinMin && (bmode == 1 || (last_tail >= kBinMin &&
                                                                      last_tail >= bin_density() * slabs))));
   if (binned && unordered && !gated) return push_binned<V, MAT>(s, a, false, st);
@@ -855,8 +841,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   // of order, so an ordered push is followed by the checked path again. GLINT_BIN_WHOLE=0: always check.
   static EnvKnob whole_knob("GLINT_BIN_WHOLE");
   const bool whole = binned && (!gated || validate) && s->hint_tail > 0 && s->hint_head == 0 &&
-                     whole_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; }) != 0 &&
-                     push_binned_fusable(s, n, sizeof(typename LdsAcc<V>::T));
+                     whole_knob.get([](const char* e) -> long long { return e ? atoi(e) != 0 : 1; }) != 0;
   if (whole) {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
     const BinHook hook = [&](void* bc, u32* T, u32 nb) -> int {
@@ -870,7 +855,7 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
   // the scatter handles every record, instead of check + apply + scatter. Launch latency is the
   // whole cost at this size, so two fewer launches is the win; results are those of the scatter
   // path (bit-exact for unique keys and for Int/Long, unordered sums otherwise).
-  const bool small = !det && !gated && n <= small_push_max();
+  const bool small = !det && !gated && n <= kSmallPushMax;
   // Whole-push scatter: the sparse counterpart of the whole-push bin. When the last checked push broke
   // order in its first tile and this one stays below the binned density, the scatter takes every record
   // from 0 with no push_check / push_apply in front (they found only that). Its hint words say so (the
@@ -885,20 +870,19 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     HIPCHK(launch_k(s, GLINT_K_PUSH_SCATTER, push_scatter_kernel<V, MAT>, g2, kTPB, st, a, whole_scatter ? 2 : 1));
     return GLINT_OK;
   }
-  const u64 win = std::min<u64>(sweep_window_tiles(), a.ntiles);
+  const u64 win = std::min<u64>(kSweepWindowTiles, a.ntiles);
   // a validating push whose tail is binned reads its keys once: push_check validates the records up to
   // the break, the tail's count pass the rest, and the verdict comes after that count (BinHook)
-  const bool fuse = validate && binned && !det && push_binned_fusable(s, n, sizeof(typename LdsAcc<V>::T));
+  const bool fuse = validate && binned && !det;
   {
     LaunchCtl* const next = slots + (s->ctl_par ^ 1);
-    static EnvKnob check_bpc("GLINT_CHECK_BPC");
     if (gated && !validate) {
       push_gate_kernel<<<1, 64, 0, st>>>(s->gate, a.ctl);
       HIPCHK(hipGetLastError());
     }
     // one launch: the key stream alone lost 3-6 % when windowed (each short launch ramps up and drains)
     const unsigned gc =
-        grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu<push_check_kernel<MAT, 0>>(2, &check_bpc));
+        grid_for(a.ntiles, kTPB / 64, (i64)s->cus * blocks_per_cu<push_check_kernel<MAT, 0>>(2));
     HIPCHK(a.part.kind == 0 ? launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 0>, gc, kTPB, st, keys, cols, n,
                                        a.part, a.ctl, next, desc, a.ntiles, 0u, a.ntiles, validate ? (fuse ? 2 : 1) : 0)
                             : launch_k(s, GLINT_K_PUSH_CHECK, push_check_kernel<MAT, 1>, gc, kTPB, st, keys, cols, n,
@@ -910,12 +894,11 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
     s->ctl_par ^= 1;  // only once the check that zeroes the other slot is on the stream
   }
   auto apply_head = [&]() -> int {  // the records before the break (every record of an ordered push)
-    static EnvKnob apply_bpc("GLINT_APPLY_BPC");
-    const i64 bpc = blocks_per_cu<push_apply_kernel<V, MAT>>(2, &apply_bpc);
+    const i64 bpc = blocks_per_cu<push_apply_kernel<V, MAT>>(2);
     for (u64 t0 = 0; t0 < a.ntiles; t0 += win) {
       const u32 t1 = (u32)std::min<u64>(a.ntiles, t0 + win);
       const unsigned ga = grid_for(t1 - t0, kTPB / 64, (i64)s->cus * bpc);
-      a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * sweep_blocks_per_cu()));
+      a.sweep_blocks = std::min<u32>(ga, (u32)((i64)s->cus * kSweepBlocksPerCu));
       HIPCHK(launch_k(s, GLINT_K_PUSH_APPLY, push_apply_kernel<V, MAT>, ga, kTPB, st, a, (const i64*)desc, (u32)t0, t1));
     }
     return GLINT_OK;
@@ -953,7 +936,7 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
     // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5); one launch per
     // window of records, as the push's apply sweep (sweep_window_tiles)
     const i64 npairs = (n + 1) / 2;
-    const i64 win = sig.done ? npairs : std::min<i64>(npairs, (i64)sweep_window_tiles() * (kTile / 2));
+    const i64 win = sig.done ? npairs : std::min<i64>(npairs, (i64)kSweepWindowTiles * (kTile / 2));
     for (i64 p0 = 0; p0 < npairs; p0 += win) {
       const i64 p1 = std::min<i64>(npairs, p0 + win);
       const unsigned g = sig.done ? 1u : grid_for(p1 - p0, kTPB, (i64)s->cus * 4);
@@ -1016,7 +999,7 @@ int push_mat_t(glint_shard* s, const i64* k, const int32_t* c, const void* v, i6
 }
 
 // glint_vec_push_dev_shards' launches: the set's ranges and data pointers by value, its verdict in the
-// first shard's scratch word
+// first shard's scratch word for this stream (under the locks of every member)
 template <typename V>
 int launch_set_push(glint_shard* const* sh, int m, const i64* keys, const void* vals, i64 n, u64* gate,
                     hipStream_t st) {
@@ -1028,19 +1011,24 @@ int launch_set_push(glint_shard* const* sh, int m, const i64* keys, const void* 
     set.end[j] = sh[j]->part.start + sh[j]->part.size;
     set.data[j] = (V*)sh[j]->data;
   }
-  if (!s0->d_word && hipMalloc((void**)&s0->d_word, 256) != hipSuccess) {
-    (void)hipGetLastError();
-    s0->d_word = nullptr;
-    return GLINT_ENOMEM;
+  u64* word = nullptr;
+  for (auto& sw : s0->set_words)
+    if (sw.first == st) word = sw.second;
+  if (!word) {
+    if (hipMalloc((void**)&word, sizeof(u64)) != hipSuccess) {
+      (void)hipGetLastError();
+      return GLINT_ENOMEM;
+    }
+    s0->set_words.emplace_back(st, word);
   }
-  HIPCHK(hipMemsetAsync(s0->d_word, 0, sizeof(u64), st));
+  HIPCHK(hipMemsetAsync(word, 0, sizeof(u64), st));
   const unsigned gv = grid_for(n, (i64)kTPB * 16, (i64)s0->cus * 4);
-  HIPCHK(launch_k(s0, GLINT_K_PUSH_CHECK, set_validate_kernel<V>, gv, kTPB, st, keys, n, set, s0->d_word));
-  set_gate_kernel<<<1, 64, 0, st>>>(s0->d_word, gate);
+  HIPCHK(launch_k(s0, GLINT_K_PUSH_CHECK, set_validate_kernel<V>, gv, kTPB, st, keys, n, set, word));
+  set_gate_kernel<<<1, 64, 0, st>>>(word, gate);
   HIPCHK(hipGetLastError());
   const unsigned g2 = grid_for(n, kScatterChunk, (i64)s0->cus * 2);
   HIPCHK(launch_k(s0, GLINT_K_PUSH_SCATTER, set_scatter_kernel<V>, g2, kTPB, st, keys, (const V*)vals, n, set,
-                  (const u64*)s0->d_word));
+                  (const u64*)word));
   return GLINT_OK;
 }
 
@@ -1132,7 +1120,7 @@ void free_shard(glint_shard* s) {
     for (auto& e : s->det_ev)
       if (e) (void)hipEventDestroy(e);
     if (s->d_bin) (void)hipFree(s->d_bin);
-    if (s->d_word) (void)hipFree(s->d_word);
+    for (auto& sw : s->set_words) (void)hipFree(sw.second);
     if (s->d_binctl) (void)hipFree(s->d_binctl);
     if (s->d_hot) (void)hipFree(s->d_hot);
     if (s->h_hint) (void)hipHostFree(s->h_hint);
@@ -1270,6 +1258,7 @@ int glint_shard_create_in(glint_shard_t slab, int64_t offset, int64_t start, int
   *out = nullptr;
   if (!slab || slab->slab || offset < 0 || end < start || end - start > INT32_MAX) return GLINT_EINVAL;
   ShardLock lk(slab);
+  if (slab->dying) return GLINT_EINVAL;
   const i64 rows = end - start;
   if (offset + rows > (i64)slab->part.size) return GLINT_EINVAL;
   const i64 first = offset * (slab->part.cols > 0 ? slab->part.pitch : 1);  // the view's first element
@@ -1293,6 +1282,8 @@ int glint_shard_create_in(glint_shard_t slab, int64_t offset, int64_t start, int
   return GLINT_OK;
 }
 
+// (destroying a shard while another thread still calls into it is the caller's error, as for any handle;
+// a slab marks itself dying under its lock, so a view created after the check is refused)
 int glint_shard_destroy(glint_shard_t s) {
   if (!s) return GLINT_EINVAL;
   if (s->slab) {  // a view: off its slab's list first
@@ -1302,6 +1293,7 @@ int glint_shard_destroy(glint_shard_t s) {
   } else {
     ShardLock lk(s);
     if (!s->views.empty()) return GLINT_EINVAL;  // its views read and write its memory: destroy them first
+    s->dying = true;
   }
   free_shard(s);
   return GLINT_OK;
@@ -1383,7 +1375,8 @@ int glint_shards_sync(glint_shard_t* shards, void** streams, int n, int* rcs, in
   std::vector<glint_shard*> order(shards, shards + n);
   std::sort(order.begin(), order.end());
   if (n > 0 && (!order[0] || std::adjacent_find(order.begin(), order.end()) != order.end())) return GLINT_EINVAL;
-  struct Locks {  // every shard's lock, taken in address order, for the whole call
+  lock_order(order);
+  struct Locks {  // every shard's lock, in lock_order, for the whole call
     std::vector<glint_shard*>& v;
     size_t k = 0;
     ~Locks() {
@@ -1400,8 +1393,7 @@ int glint_shards_sync(glint_shard_t* shards, void** streams, int n, int* rcs, in
     rcs[i] = hipMemcpyAsync(h[i], s->d_err, sizeof(ErrState), hipMemcpyDeviceToHost, (hipStream_t)streams[i]) ==
                      hipSuccess ? GLINT_OK : GLINT_EDEVICE;
   }
-  static EnvKnob flush_knob("GLINT_SYNC_FLUSH");
-  if (flush_knob.get([](const char* e) { return e ? atoll(e) : 1LL; }) != 0) {
+  {
     // a query submits what the runtime holds back for the stream, so every copy is on its queue
     // before the first wait (without it the copies of streams sharing a hardware queue went out one
     // per wait, ~25 us apart, after the last push)
@@ -1531,8 +1523,8 @@ int glint_vec_push_dev_shards(glint_shard_t* shards, int m, const int64_t* keys,
   std::sort(v.begin(), v.end(), [](const glint_shard* a, const glint_shard* b) { return a->part.start < b->part.start; });
   for (int j = 1; j < m; ++j)  // disjoint ranges (each once)
     if (v[j - 1]->part.start + v[j - 1]->part.size > v[j]->part.start || v[j - 1] == v[j]) return GLINT_EINVAL;
-  std::vector<glint_shard*> order(v);  // every shard's lock, taken in address order, for the whole call
-  std::sort(order.begin(), order.end());
+  std::vector<glint_shard*> order(v);  // every shard's lock, in lock_order, for the whole call
+  lock_order(order);
   struct Locks {
     std::vector<glint_shard*>& o;
     size_t k = 0;
@@ -1738,19 +1730,14 @@ StageLayout stage_layout(const glint_shard* s, i64 n) {
 // against them.
 // After a short spin a lone waiter yields (a message's round trip stays ~10 us: window-1 clients);
 // when more than kBusyWaiters threads of the process are waiting at once, each sleeps between polls
-// instead (GLINT_WAIT_SLEEP_US, default 50), leaving the cores to the threads that have work: the
-// loopback servers run hundreds of connection threads on a 16-core share, and yielding waiters there
-// cost the cfg4a / cfg4b pull rows 16 % / 10 % (profiles/r04/loopback_wait_sleep.txt).
-// GLINT_WAIT_SLEEP_US=0 always yields.
+// instead (50 us), leaving the cores to the threads that have work: the loopback servers run hundreds
+// of connection threads on a 16-core share, and yielding waiters there cost the cfg4a / cfg4b pull rows
+// 16 % / 10 % (profiles/r04/loopback_wait_sleep.txt).
 std::atomic<int> g_waiters{0};
 constexpr int kBusyWaiters = 8;
-long long wait_sleep_us() {
-  static EnvKnob k("GLINT_WAIT_SLEEP_US");
-  return k.get([](const char* e) -> long long { return e ? std::max(0ll, atoll(e)) : 50ll; });
-}
+constexpr long long kWaitSleepUs = 50;
 bool poll_word(const u64* word, u64 ticket, double budget_us) {
   constexpr double kSpinUs = 4.0;
-  const long long sleep_us = wait_sleep_us();
   struct Count {
     Count() { g_waiters.fetch_add(1, std::memory_order_relaxed); }
     ~Count() { g_waiters.fetch_sub(1, std::memory_order_relaxed); }
@@ -1762,8 +1749,8 @@ bool poll_word(const u64* word, u64 ticket, double budget_us) {
       const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       if (us > budget_us) return false;
       if (us > kSpinUs) {
-        if (sleep_us > 0 && g_waiters.load(std::memory_order_relaxed) > kBusyWaiters) {
-          const struct timespec ts = {(time_t)(sleep_us / 1000000), (long)(sleep_us % 1000000) * 1000};  // tv_nsec < 1e9
+        if (g_waiters.load(std::memory_order_relaxed) > kBusyWaiters) {
+          const struct timespec ts = {0, (long)kWaitSleepUs * 1000};
           nanosleep(&ts, nullptr);
         } else {
           sched_yield();

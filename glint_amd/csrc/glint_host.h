@@ -148,7 +148,9 @@ struct glint_shard {
   const PullDst* pull_tab = nullptr;  // set only while a pull batch with direct answers dispatches
   int pull_nm = 0;
   u64* gate = nullptr;  // set only while a gated device push launches (glint_*_push_dev_gated)
-  u64* d_word = nullptr;  // device scratch of glint_vec_push_dev_shards (the set's verdict), 256 B
+  // device scratch of glint_vec_push_dev_shards (the set's verdict word), one per caller stream: calls
+  // on one stream are ordered, calls on two streams never share a word (one would clear the other's)
+  std::vector<std::pair<hipStream_t, u64*>> set_words;
   int ring_next = 0;
   uint64_t ticket_next = 0;
   // tickets of ring entries whose launch failed after their tickets were handed out: a wait that
@@ -194,11 +196,22 @@ struct glint_shard {
   // views' host-pointer work and the views' later host-pointer calls after them
   glint_shard* slab = nullptr;
   std::vector<glint_shard*> views;
+  bool dying = false;  // a slab being destroyed: no new views
   std::mutex mu;
 };
 
+// The order a call that locks several shards takes their locks in: shards that are not views (slabs
+// among them) before views, each group by address -- a slab's own device calls lock the slab, then
+// each of its views (dev_order_after_host), so every caller takes a slab's lock before its views'.
+inline void lock_order(std::vector<glint_shard*>& v) {
+  std::sort(v.begin(), v.end(), [](const glint_shard* a, const glint_shard* b) {
+    const bool va = a->slab != nullptr, vb = b->slab != nullptr;
+    return va != vb ? vb : a < b;
+  });
+}
+
 // ---- environment knobs ----------------------------------------------------------------------------
-// Tuning and test overrides (GLINT_BINNED, GLINT_BIN_FRONT, GLINT_SWEEP_WINDOW, ...) are read once per
+// Test and policy overrides (GLINT_BINNED, GLINT_BIN_FRONT, ...; DESIGN.md §8 lists them) are read once per
 // generation, so the push paths that several actor threads reach never call getenv. A test that
 // changes the environment between calls starts a new generation with glint_reload_env().
 extern std::atomic<unsigned> g_env_gen;  // glint_gpu.hip
@@ -431,11 +444,9 @@ inline unsigned grid_for(i64 units, i64 per_block, i64 cap) {
   return (unsigned)g;
 }
 
-// resident blocks per CU for a kernel (occupancy query), capped at the measured best; the
-// environment variable `knob` (e.g. GLINT_CHECK_BPC) overrides it for tuning sweeps
-// (the occupancy query runs once per kernel; `knob` is an EnvKnob the call site owns)
+// resident blocks per CU for a kernel (occupancy query, once per kernel), capped at the measured best
 template <auto Kernel>
-inline int blocks_per_cu(int cap, EnvKnob* knob = nullptr) {
+inline int blocks_per_cu(int cap) {
   static std::atomic<int> occ{0};  // one per kernel
   int b = occ.load(std::memory_order_relaxed);
   if (!b) {
@@ -445,9 +456,7 @@ inline int blocks_per_cu(int cap, EnvKnob* knob = nullptr) {
     }
     occ.store(b, std::memory_order_relaxed);
   }
-  b = std::min(b, cap);
-  if (knob) b = (int)knob->pos_or(b);
-  return b;
+  return std::min(b, cap);
 }
 
 }  // namespace
@@ -465,9 +474,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
                 LaunchCtl* whole_next = nullptr);
 // whole_next: a whole-push bin (from_break false, no push_check ran): bin_count zeroes this LaunchCtl slot
 // for the next push as push_check would, and reports through the hint words whether the push was ordered.
-// whether a push of n records (LDS partial sums of asize bytes) takes the v2 binned pipeline, whose
-// count pass can validate the tail (BinHook)
-bool push_binned_fusable(const glint_shard* s, i64 n, size_t asize);
+// whether a push of n records can be binned (u32 record indices and element addresses)
+bool push_binnable(const glint_shard* s, i64 n);
 // the verdict of a validating gated push whose tail is binned (glint_bin.hip)
 int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32 nb, hipStream_t st);
 // one-launch order-preserving push (glint_ordered.hip): n <= kOrderedMax, elems < 2^32

@@ -29,7 +29,6 @@ from __future__ import annotations
 
 import ctypes as C
 import math
-import os
 import threading
 from typing import Callable, List, Optional
 
@@ -327,8 +326,9 @@ def slab_shards(kind: str, parts, cols: int, dtype, device: int):
     device-resident call on the slab -- one launch sequence for all of its partitions, where the
     reference sends a message per partition (AsyncBigVector.scala:96-98): _Distributed._push_gated
     (world 1, the slab spans the key space) and DistributedBigVector._push_slab (the route rebases
-    keys into every rank's slab). GLINT_DIST_SLAB=0: no slabs (A/B)."""
-    if os.environ.get("GLINT_DIST_SLAB", "1") == "0":
+    keys into every rank's slab). Vectors only: a matrix keeps per-partition pushes (_slab_plan), so a
+    matrix slab would buy nothing but alignment padding and one large allocation."""
+    if kind != "vector":
         return None
     lay = slab_layout(parts, cols, dtype)
     if lay is None:
@@ -423,8 +423,7 @@ class _Distributed:
         shards run concurrently, each on a stream of its own behind the caller's stream (the shards are
         independent, so one push's short kernels -- counts, scans, tails -- overlap another's), and the
         caller's stream waits for all of them; then one wait per shard (its errors)."""
-        concurrent = os.environ.get("GLINT_DIST_STREAMS", "1") != "0"  # 0: one stream (A/B)
-        if concurrent and len(ops) > 1 and all(self._on_shard_device(t) and hasattr(sh, "handle") for _, sh, t, _ in ops):
+        if len(ops) > 1 and all(self._on_shard_device(t) and hasattr(sh, "handle") for _, sh, t, _ in ops):
             cur = torch.cuda.current_stream(self.device)
             ready = torch.cuda.Event()
             ready.record(cur)
@@ -480,8 +479,8 @@ class _Distributed:
         """Vectors: whether pushes go to slabs, and the route's per-slot key deltas (key -> the key of
         its row in the hosting rank's slab, slab_layout). Decided the same way on every rank: the
         layouts are a function of the partitioner, and at world > 1 the ranks agree by one MIN
-        all-reduce that every rank joins (a rank without a slab -- another shard factory,
-        GLINT_DIST_SLAB=0 -- turns it off for all). (A matrix keeps per-partition pushes: a batch with
+        all-reduce that every rank joins (a rank without a slab -- another shard factory, or
+        slabs=False -- turns it off for all). (A matrix keeps per-partition pushes: a batch with
         a bad column fails only that partition's message in the reference.)"""
         self._delta, self._slab_keyed = None, False
         if not isinstance(self.partitioner, RangePartitioner) or self.router.maxp < 2:
@@ -522,41 +521,23 @@ class _Distributed:
         (the route's validation pass) and the push are enqueued back to back -- the push gated on the
         route's status word on the device (glint_*_push_dev_gated: a batch with an out-of-range key
         applies nothing, as mapPartitions throws before sending, AsyncBigVector.scala:96-98) -- and the
-        host reads the word after the one wait, so no synchronisation sits between them. With a library
-        that has GLINT_PUSH_VALIDATE the push checks the keys itself (its order check reads them all)
-        and writes the word, so the route's pass over the keys is gone too (GLINT_GATE_ROUTE=1: the
-        route in front, for A/B). Returns False when the call does not qualify (the general path then
-        runs)."""
+        host reads the word after the one wait, so no synchronisation sits between them. The push checks
+        the keys itself (GLINT_PUSH_VALIDATE: its order check reads them all) and writes the word, so no
+        route pass reads them first. The word lives in pinned host memory (a HostBuffer): read after the
+        one wait, with no device-to-host copy. Returns False when the call does not qualify (the general
+        path then runs)."""
         sh = self._gated_shard()
         if not (sh is not None and keys.is_cuda and not deterministic
-                and self._on_shard_device(keys) and hasattr(sh, "handle")
-                and getattr(N.load(), "glint_vec_push_dev_gated", None) is not None):  # (an older A/B library)
+                and self._on_shard_device(keys) and hasattr(sh, "handle")):
             return False
         esz = args[-1].element_size()
         if keys.data_ptr() % 16 or args[-1].data_ptr() % (2 * esz) or (len(args) == 3 and args[1].data_ptr() % 8):
             return False
-        lib = N.load()
-        sup = getattr(lib, "glint_push_flags_supported", None)
-        if sup is not None and sup() & N.GLINT_PUSH_VALIDATE and os.environ.get("GLINT_GATE_ROUTE", "0") != "1":
-            # the push checks its own keys before applying any (GLINT_PUSH_VALIDATE): no route pass.
-            # The verdict word lives in pinned host memory (a HostBuffer): read after the one wait,
-            # with no device-to-host copy (GLINT_GATE_HOST=0: a device word and a copy, for A/B)
-            if os.environ.get("GLINT_GATE_HOST", "1") != "0":
-                gptr, word = self._gate()
-                with self._gate_lock:  # one word per model: one gated push at a time
-                    sh.update(*args, gate=gptr, validate=True, sync=False)
-                    sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
-                    b = int(word[0])
-            else:
-                bad = torch.empty(1, dtype=torch.int64, device=keys.device)
-                sh.update(*args, gate=bad, validate=True, sync=False)
-                sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
-                b = int(bad.cpu()[0])
-        else:
-            _, _, _, _, _, bad = self.router.route(keys)
-            sh.update(*args, gate=bad, sync=False)
+        gptr, word = self._gate()
+        with self._gate_lock:  # one word per model: one gated push at a time
+            sh.update(*args, gate=gptr, validate=True, sync=False)
             sh.sync(torch.cuda.current_stream(keys.device).cuda_stream)
-            b = int(bad.cpu()[0])
+            b = int(word[0])
         if b != 0:
             i = ~b
             k = int(keys[i])
@@ -635,19 +616,17 @@ class DistributedBigVector(_Distributed):
     def _set_ok(self, n: int) -> bool:
         """Whether a sparse batch of n records (fewer than 1/8 of this rank's keys, where every shard
         push would take the atomic scatter anyway) can go to all local shards in ONE launch sequence
-        (glint_vec_push_dev_shards): range vector shards on this GPU, 2..64 of them. GLINT_DIST_SET=0:
-        off (A/B)."""
+        (glint_vec_push_dev_shards): range vector shards on this GPU, 2..64 of them."""
         m = len(self.shards)
         if not (1 < m <= 64 and isinstance(self.partitioner, RangePartitioner) and self.device.type == "cuda"
-                and all(hasattr(sh, "handle") for sh in self.shards)
-                and getattr(N.load(), "glint_vec_push_dev_shards", None) is not None
-                and os.environ.get("GLINT_DIST_SET", "1") != "0"):
+                and all(hasattr(sh, "handle") for sh in self.shards)):
             return False
         return n * 8 < sum(sh.size for sh in self.shards)
 
     def _set_push(self, keys: torch.Tensor, values: torch.Tensor) -> int:
-        """glint_vec_push_dev_shards over the local shards, then the one wait: -> the verdict word
-        (0, or ~ the first record whose key is in no local shard; nothing applied then)."""
+        """glint_vec_push_dev_shards over the local shards, then one wait for all of them
+        (glint_shards_sync: each member's error state, hints latched): -> the verdict word (0, or ~ the
+        first record whose key is in no local shard; nothing applied then)."""
         n = keys.numel()
         m = len(self.shards)
         for sh in self.shards:  # (their dtype and device: the library checks the set agrees)
@@ -659,7 +638,8 @@ class DistributedBigVector(_Distributed):
         gptr, word = self._gate()
         with self._gate_lock:
             check(N.load().glint_vec_push_dev_shards(hs, m, keys.data_ptr(), values.data_ptr(), n, gptr, stream))
-            self.shards[0].sync(stream)
+            cur = torch.cuda.current_stream(self.device)
+            self._sync_all([(sh, cur) for sh in self.shards])
             return int(word[0])
 
     def _push_set(self, keys: torch.Tensor, values: torch.Tensor) -> bool:
@@ -746,7 +726,10 @@ class DistributedBigVector(_Distributed):
         try:
             self.slab.get(keys, out=out)  # (one wait, on this stream: the check above is done too)
         except ArrayIndexOutOfBoundsException:
-            pass  # outside the slab = outside the key space: the route's word names the record
+            # outside the slab = outside the key space, and the route's word names the record; a slab
+            # that rejects a key the route passed would leave `out` partly unwritten
+            if int(bad.item()) == 0:
+                raise RuntimeError("the slab rejected a key inside the key space") from None
         b = int(bad.item())
         if b != 0:
             i = ~b
@@ -755,8 +738,7 @@ class DistributedBigVector(_Distributed):
 
     def pull(self, keys: torch.Tensor) -> torch.Tensor:
         keys = keys.reshape(-1).to(torch.int64)
-        if keys.is_cuda and self._slab_keyed and self._on_shard_device(keys) and \
-                os.environ.get("GLINT_DIST_SLAB_PULL", "1") != "0":
+        if keys.is_cuda and self._slab_keyed and self._on_shard_device(keys):
             return self._pull_slab(keys)
         if keys.is_cuda:
             ex, order, sk, _, _ = self._begin_fused(keys, want_order=True)
@@ -829,9 +811,11 @@ class DistributedClient:
     """glint.Client's model factory over a process group: rank r hosts partitions r, r + W, ...
 
     ``shard_factory(kind, partition, cols, dtype, device)`` builds a local shard; the default makes
-    ``PartialVector`` / ``PartialMatrix`` HBM shards on ``device`` (this rank's GPU)."""
+    ``PartialVector`` / ``PartialMatrix`` HBM shards on ``device`` (this rank's GPU). ``slabs=False``
+    keeps a vector's local partitions in shards of their own instead of views of one slab
+    (slab_shards)."""
 
-    def __init__(self, group=None, device=None, shard_factory: Optional[Callable] = None):
+    def __init__(self, group=None, device=None, shard_factory: Optional[Callable] = None, slabs: bool = True):
         if not dist.is_initialized():
             raise ModelCreationException("torch.distributed is not initialised")
         self.group = group
@@ -841,6 +825,7 @@ class DistributedClient:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self.shard_factory = shard_factory or self._hbm_shard
+        self.slabs = bool(slabs)
 
     @staticmethod
     def _hbm_shard(kind, partition, cols, dtype, device):
@@ -855,7 +840,7 @@ class DistributedClient:
         partitioner = createPartitioner(nparts, keys)
         mine = Router(partitioner, self.world).rank_parts[self.rank]
         parts = partitioner.all()
-        if self.shard_factory == self._hbm_shard and self.device.type == "cuda":
+        if self.slabs and self.shard_factory == self._hbm_shard and self.device.type == "cuda":
             sv = slab_shards(kind, [parts[p] for p in mine], cols, dtype, self.device.index)
             if sv is not None:  # the rank's partitions side by side in one slab
                 return partitioner, sv[1], sv[0]

@@ -283,11 +283,11 @@ def _set_case(nkeys, mps, dtype, n=20_000):
     def body(client, rank, world, dev):
         _, np_dtype = resolve_dtype(dtype)
         if world > 1:
-            os.environ["GLINT_DIST_SLAB"] = "0"  # (the slab's rebased route would take these pushes)
+            client.slabs = False  # (the slab's rebased route would take these pushes)
         try:
             vec = client.vector(nkeys, dtype, modelsPerServer=mps)
         finally:
-            os.environ.pop("GLINT_DIST_SLAB", None)
+            client.slabs = True
         assert not vec._slab_keyed and n * 8 * world < nkeys
         calls = []
         orig = vec._set_push

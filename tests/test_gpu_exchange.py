@@ -127,6 +127,21 @@ def test_bench_self_launches_ranks(gpu, args):
                GLINT_BENCH_DEVICE=str(gpu), GLINT_BENCH_BACKEND="gloo")
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["check"] is True
     assert d["scaling"] == ("strong" if "strong" in args else "weak")
+    # the line names the GPU every rank ran on: here both on this one, flagged as a rehearsal
+    dv = d["devices"]
+    assert d["world_size"] == 2 and [r["rank"] for r in dv["ranks"]] == [0, 1]
+    assert all(r["device"] == gpu for r in dv["ranks"]) and dv["distinct_gpus"] == 1
+    assert dv["rehearsal"] is True and dv["backend"] == "gloo"
+
+
+@pytest.mark.parametrize("args", [["--pattern", "zipf", "--log2-keys", "22"], ["--pattern", "matrix"],
+                                  ["--pattern", "exchange", "--log2-keys", "22"],
+                                  ["--pattern", "dense", "--log2-keys", "22"]])
+def test_bench_rotated_batches(gpu, args):
+    """--batches K: K different batches of one distribution rotated per step; the post-run check
+    replays all of them (a batch pushed t times counts t times)."""
+    d = _bench(args + ["--steps", "5", "--warmup", "2", "--batches", "3", "--no-cpu-baseline"])
+    assert d["check"] is True and d["value"] > 0 and d["batches"]["k"] == 3
 
 
 @pytest.mark.parametrize("args", [["--pattern", "pull"], ["--pattern", "rowpull"],

@@ -203,15 +203,12 @@ def test_deterministic_hot_chain_split(gpu, dtype, layout, head):
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
-@pytest.mark.parametrize("n,window", [(2 * 2048 + 1, "11"), (3 * 2048 + 1, "11"), ((1 << 26) + 1, None)])
-def test_windowed_sweep_odd_record_once(gpu, monkeypatch, n, window):
-    """A dense push is applied in windows of 2^GLINT_SWEEP_WINDOW records; with n = k * 2^w + 1 the
-    window before the last also ends at pair n >> 1, and the odd last record must still be added once
-    (it was added by both windows before the fix)."""
+@pytest.mark.parametrize("n", [(1 << 26) + 1, (2 << 26) + 1])
+def test_windowed_sweep_odd_record_once(gpu, n):
+    """A dense push is applied in windows of 2^26 records; with n = k * 2^26 + 1 the window before the
+    last also ends at pair n >> 1, and the odd last record must still be added once (it was added by
+    both windows before the fix)."""
     import torch
-    if window is not None:
-        monkeypatch.setenv("GLINT_SWEEP_WINDOW", window)
-        N.reload_env()
     d = torch.device("cuda", gpu)
     for dtype in ("long", "double"):
         part = RangePartition(0, 0, n + 5)
@@ -979,32 +976,65 @@ def test_binned_fronts_matrix(gpu, monkeypatch, front):
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
-@pytest.mark.parametrize("item,fused,group", [("4096", "1", "0"), ("8192", "0", "1"), ("16384", "0", "0"),
-                                              ("16384", "1", "1")])
-def test_binned_small_push_shapes(gpu, monkeypatch, item, fused, group):
-    """A small push's fine stage in each of its shapes: fine items of 4096 / 8192 / 16384 records
-    (GLINT_FSORT_ITEM), the plan fused into the fine sort or launched on its own
-    (GLINT_BIN_FUSED_PLAN), sparse-slab groups on or off (GLINT_BIN_GROUP): Zipf rows x uniform
-    columns with hot rows (units split across a slab, flushed by atomics) and cold sparse slabs,
-    bit-exact (Long) against the oracle."""
-    monkeypatch.setenv("GLINT_FSORT_ITEM", item)
-    monkeypatch.setenv("GLINT_BIN_FUSED_PLAN", fused)
-    monkeypatch.setenv("GLINT_BIN_GROUP", group)
-    N.reload_env()
+@pytest.mark.parametrize("kind,lg", [("matrix", 21), ("vector", 21), ("matrix", 24), ("vector", 24)])
+def test_binned_fine_stage_shapes(gpu, kind, lg):
+    """The fine stage in each of its shapes, bit-exact (Long) against the oracle: a small push (2^21
+    records: <= ~4 fine items per CU) plans its buckets inside bin_fsort, a large one (2^24) launches
+    bin_plan; a vector shard groups its sparse neighbour slabs into one unit, a matrix shard does not.
+    Zipf keys with hot elements (units split across a slab, flushed by atomics) and cold sparse slabs."""
     rng = np.random.default_rng(29)
-    rows_n, cols_n = 1 << 13, 512
-    part = RangePartition(0, 0, rows_n)
-    r = np.minimum(np.floor(np.power(float(rows_n), rng.random(1 << 21))).astype(np.int64) - 1, rows_n - 1)  # Zipf(1.0)
-    r = rng.permutation(rows_n)[r].astype(np.int64)
-    c = rng.integers(0, cols_n, r.size).astype(np.int32)
-    v = rng.integers(-1000, 1000, r.size).astype(np.int64)
-    ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE["long"])
-    assert ref.update(r, c, v) == -1
-    with PartialMatrix(part, cols_n, "long", gpu) as sh:
+    nrec = 1 << lg
+    if kind == "matrix":
+        rows_n, cols_n = 1 << 13, 512
+        part = RangePartition(0, 0, rows_n)
+        r = np.minimum(np.floor(np.power(float(rows_n), rng.random(nrec))).astype(np.int64) - 1, rows_n - 1)
+        r = rng.permutation(rows_n)[r].astype(np.int64)
+        c = rng.integers(0, cols_n, r.size).astype(np.int32)
+        v = rng.integers(-1000, 1000, r.size).astype(np.int64)
+        ref = O.OracleMatrix(O.part_range(0, rows_n), cols_n, O.CODE["long"])
+        sh, args = PartialMatrix(part, cols_n, "long", gpu), (r, c, v)
+    else:
+        size = 1 << 24
+        part = RangePartition(0, 0, size)
+        k = np.minimum(np.floor(np.power(float(size), rng.random(nrec))).astype(np.int64) - 1, size - 1)
+        k = ((k.astype(np.uint64) * np.uint64(0x9E3779B1)) & np.uint64(size - 1)).astype(np.int64)
+        v = rng.integers(-1000, 1000, k.size).astype(np.int64)
+        ref = O.OracleVector(O.part_range(0, size), O.CODE["long"])
+        sh, args = PartialVector(part, "long", gpu), (k, v)
+    with sh:
         for _ in range(2):
-            sh.update(r, c, v, unordered=True)
-        assert ref.update(r, c, v) == -1
+            sh.update(*args, unordered=True)
+            assert ref.update(*args) == -1
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+@pytest.mark.parametrize("dtype", ["long", "double"])
+def test_binned_stream_of_batches(gpu, dtype):
+    """A server sees a stream of different batches (AsyncBigVector.scala:107-121: every push is a new
+    message), while the binned push keeps state across pushes: the wide hot table, resampled every 8th
+    push, the front-end choice and the whole-push hints, all latched from earlier pushes. Twelve Zipf
+    batches from distinct seeds -- with the hot set drifting between them -- pushed with the hint and
+    through the adaptive switch, against the oracle's sequential loop over the same stream (Long
+    bit-exact, Double within 1e-9 of each element's sum of magnitudes)."""
+    size = 1 << 24
+    part = RangePartition(0, 0, size)
+    ref = O.OracleVector(O.part_range(0, size), O.CODE[dtype])
+    mag = np.zeros(size)
+    with PartialVector(part, dtype, gpu) as sh:
+        for b in range(12):
+            rng = np.random.default_rng(1000 + b)
+            z = np.minimum(rng.zipf(1.1, 1 << 22) - 1, size - 1)
+            shift = (b // 4) * 977  # the hot elements move every fourth batch
+            k = (((z + shift).astype(np.uint64) * np.uint64(0x9E3779B1)) & np.uint64(size - 1)).astype(np.int64)
+            v = rand_vals(rng, dtype, k.size)
+            sh.update(k, v, unordered=b % 3 != 2)
+            assert ref.update(k, v) == -1
+            mag += np.bincount(k, np.abs(v.astype(np.float64)), minlength=size)
+        got = sh.to_numpy()
+    if dtype == "long":
+        np.testing.assert_array_equal(got, ref.data)
+    else:
+        assert not (np.abs(got - ref.data) > 1e-9 * mag).any()
 
 
 def test_loopback_harness_gpu_backend(gpu):
