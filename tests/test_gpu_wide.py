@@ -47,6 +47,13 @@ def _vals(torch, d, dtype, n, g):
     return (torch.rand(n, dtype=torch.float64, device=d, generator=g) * 2 - 1).to(tdt)
 
 
+def _launches(sh, kid):
+    import ctypes as C
+    ms, cnt = C.c_double(), C.c_int64()
+    N.load().glint_prof_read(sh.handle, kid, C.byref(ms), C.byref(cnt))
+    return cnt.value
+
+
 def _check(torch, got, ref, mag, exact):
     if exact:
         assert torch.equal(got, ref), f"{int((got != ref).sum())} elements differ"
@@ -84,8 +91,11 @@ def test_wide_binned_push(gpu, monkeypatch, dtype, front):
     # once per 2048-record chunk; a binned push once per apply unit / hot-table flush)
     hints = (True, True) if dtype == "float" else (True, False, False, True)
     with PartialVector(RangePartition(0, 0, SHARD), dtype, gpu) as sh:
+        N.load().glint_prof_enable(sh.handle, 1)
         for unordered in hints:  # (False twice: check + apply + scatter with no history, then the
             sh.update(keys, vals, unordered=unordered)  # latched tail's whole-push bin)
+        # every push but the one with no history went through the binned pipeline (its wide stores)
+        assert _launches(sh, N.GLINT_K_PUSH_BINNED) == (3 if False in hints else 2)
         got = sh.get(torch.arange(SHARD, dtype=torch.int64, device=d))
     ref *= len(hints)
     if mag is not None:
@@ -113,7 +123,8 @@ def test_wide_validating_gated_push(gpu, monkeypatch):
     ref = torch.zeros(SHARD, dtype=torch.int64, device=d)
     gate = torch.full((1,), 777, dtype=torch.int64, device=d)
     with PartialVector(RangePartition(0, 0, SHARD), "long", gpu) as sh:
-        for batch, ok in ((keys, True), (keys, True), (bad, False), (keys, True)):
+        N.load().glint_prof_enable(sh.handle, 1)
+        for i, (batch, ok) in enumerate(((keys, True), (keys, True), (bad, False), (keys, True))):
             sh.update(batch, vals, gate=gate, validate=True)
             w = int(gate.cpu()[0])
             if ok:
@@ -121,6 +132,9 @@ def test_wide_validating_gated_push(gpu, monkeypatch):
                 ref.index_add_(0, keys, vals)
             else:
                 assert ~w == first, (w, first)
+            # the first push (no history) checks, applies and scatters; the rest are whole-push bins
+            # whose count pass validates every record
+            assert _launches(sh, N.GLINT_K_PUSH_BINNED) == i
         got = sh.get(torch.arange(SHARD, dtype=torch.int64, device=d))
     assert torch.equal(got, ref)
 
