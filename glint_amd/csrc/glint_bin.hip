@@ -51,7 +51,14 @@ constexpr int kASlotBits = kASlots == 8192 ? 13 : kASlots == 4096 ? 12 : 11;
 static_assert((1 << kASlotBits) == kASlots, "dedup table size");
 // partition workgroups per CU: LDS-bound (the dedup table; the plain front end's staging)
 constexpr int kPartWgPerCuDedup = kATPB == 1024 ? 1 : 2;
-constexpr int kPartWgPerCuPlain = kATPB == 1024 ? 1 : 2;  // what fits (VGPRs): a second round of
+#ifndef GLINT_PART_WPC
+#define GLINT_PART_WPC (kATPB == 1024 ? 1 : 2)
+#endif
+#ifndef GLINT_PART_AHEAD
+#define GLINT_PART_AHEAD 2
+#endif
+constexpr int kPartAhead = GLINT_PART_AHEAD;  // partition chunks in flight per workgroup (build-time knob)
+constexpr int kPartWgPerCuPlain = GLINT_PART_WPC;  // what fits (VGPRs): a second round of
                                                            // workgroups measured 3-9 % slower
 constexpr int kMaxSegs = 1024;         // partition workgroups at most
 #ifndef GLINT_APPLY_TPB
@@ -113,12 +120,30 @@ struct PhaseClock {
 // Streaming inputs (records read once by a pass) load non-temporally (GLINT_BIN_NT, default 1), so
 // they do not evict the partially written output runs and slab lines the passes revisit. Same box,
 // two runs each (profiles/r03/ab_nt.txt): cfg3 1.43-1.50 -> 1.33-1.40 ms, cfg4b exchange -2-4 %.
+// The intermediates (the partition's output read by bin_fsort, the fine sort's read by bin_apply2) load
+// cached (GLINT_BIN_NT_MID=0): a slab's runs are gathered from every item of its bucket, and the lines
+// two neighbouring runs share stay in L2 for the unit of the next slab (XCD-grouped unit order). Same box,
+// two rounds (profiles/r06/ab_nt_mid.txt), with the per-push fine item size below: cfg4b exchange 2.42 ms
+// non-temporal -> 2.20 cached (round 5: 2.37), cfg3 1.055 -> 1.046, cfg5 0.318 -> 0.315.
+// (build-time knobs: GLINT_BIN_NT for the push's own records, read by bin_count / bin_part;
+// GLINT_BIN_NT_MID for the intermediates)
 #ifndef GLINT_BIN_NT
 #define GLINT_BIN_NT 1
+#endif
+#ifndef GLINT_BIN_NT_MID
+#define GLINT_BIN_NT_MID 0
 #endif
 template <typename T>
 __device__ __forceinline__ T ld_in(const T* p) {
 #if GLINT_BIN_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ T ld_mid(const T* p) {
+#if GLINT_BIN_NT_MID
   return __builtin_nontemporal_load(p);
 #else
   return *p;
@@ -154,6 +179,20 @@ __device__ __forceinline__ void bput(const BufOut& b, u32 off, bool on, T v) {
     static_assert(sizeof(T) == 8, "4- or 8-byte stores");
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, v), b.r, o, 0, 0);
   }
+}
+// A load through a buffer window: 0 past its end (no memory access), non-temporal as ld_mid
+template <typename T>
+__device__ __forceinline__ T bget(const BufOut& b, u32 off) {
+  constexpr int kAux = GLINT_BIN_NT_MID ? 2 : 0;  // gfx950 buffer cache policy: bit 1 = nt
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(b.r, (int)off, 0, kAux));
+  } else {
+    static_assert(sizeof(T) == 8, "4- or 8-byte loads");
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(b.r, (int)off, 0, kAux));
+  }
+}
+__device__ __forceinline__ void bput16(const BufOut& b, u32 off, bool on, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, b.r, (int)(on ? off : b.oob), 0, 0);
 }
 // A record array of T through one buffer window: element `rel` at byte rel * sizeof(T) (< 2^32 bytes).
 template <typename T>
@@ -214,13 +253,16 @@ __device__ __forceinline__ u32 block_scan(u32 N, F value, W write) {
     }
     if (lane == 63) wt[wid] = incl;
     __syncthreads();
-    u32 run = carry + incl - s, tot = 0;
+    // the waves before this one and all of them: lane l holds wave l's total, summed across the wave
+    // (two registers, where reading every wave's total into registers held TPB / 64 of them)
+    const u32 wv = lane < TPB / 64 ? wt[lane] : 0u;
+    u32 pre = lane < wid ? wv : 0u, tot = wv;
 #pragma unroll
-    for (int w = 0; w < TPB / 64; ++w) {
-      const u32 x = wt[w];
-      run += w < wid ? x : 0u;
-      tot += x;
+    for (int d = 32; d > 0; d >>= 1) {
+      pre += __shfl_xor(pre, d);
+      tot += __shfl_xor(tot, d);
     }
+    u32 run = carry + incl - s + pre;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       if (b0 + j < N) write(b0 + j, run);
@@ -775,8 +817,11 @@ __device__ __forceinline__ auto part_out(T* base, u32 n, void* dump, size_t dump
 // workgroup for bin_hot_reduce; only the cold records are appended. Once the hot elements are off,
 // a Zipf-like tail has almost no duplicates left inside a chunk (cfg3: the chunk dedup would merge
 // 0.6 % of the cold records), so the hash table is not worth its time there.
+#ifndef GLINT_PART_WAVES
+#define GLINT_PART_WAVES 4  // bin_part's register budget: waves per SIMD (build-time knob)
+#endif
 template <typename V, bool MAT, bool HOT, int KIND, bool WIDE>
-__global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
+__global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 : GLINT_PART_WAVES))) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                          const V* __restrict__ vals, i64 n, PartDesc part,
                                                          const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
                                                          u32* __restrict__ addr_out,
@@ -798,6 +843,9 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
   const u32 w = blockIdx.x;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
+  // chunks in flight: the hot front end runs one workgroup per CU (its LDS tables), two chunks ahead;
+  // the plain one kPartAhead
+  constexpr int kAhead = HOT ? 2 : kPartAhead;
   if constexpr (HOT) {
     for (int sl = tid; sl < kWideSlots; sl += kATPB) {
       const unsigned long long b = hot_best[sl];
@@ -865,18 +913,18 @@ __global__ __launch_bounds__(kATPB) void bin_part_kernel(const i64* __restrict__
     }
     ph.mark(1);
     emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 3);
-    // two chunks ahead, into the registers just consumed: in flight across the next chunk's work
-    load_chunk(c + 2 * G, r);
+    // kAhead chunks ahead, into the registers just consumed: in flight across the next chunks' work
+    load_chunk(c + kAhead * G, r);
     ph.mark(2);
   };
-  RecRegs<V, MAT> ra, rb;
+  RecRegs<V, MAT> r[kAhead];
   i64 c = w;
   if (c < nchunks) {
-    load_chunk(c, ra);
-    load_chunk(c + G, rb);
-    for (; c < nchunks; c += 2 * G) {
-      step(c, ra);
-      step(c + G, rb);  // past the end: no valid record, nothing stored
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) load_chunk(c + j * G, r[j]);
+    for (; c < nchunks; c += kAhead * G) {
+#pragma unroll
+      for (int j = 0; j < kAhead; ++j) step(c + j * G, r[j]);  // past the end: no valid record, nothing stored
     }
   }
   if (tid == 0 && emitted) {
@@ -1047,14 +1095,14 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     __syncthreads();
     ph.mark(17);
   };
-  RecRegs<V, MAT> ra, rb;
+  RecRegs<V, MAT> r[2];
   i64 c = w;
   if (c < nchunks) {
-    load_chunk(c, ra);
-    load_chunk(c + G, rb);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) load_chunk(c + j * G, r[j]);
     for (; c < nchunks; c += 2 * G) {
-      step(c, ra);
-      step(c + G, rb);  // past the end: no valid record, nothing stored
+#pragma unroll
+      for (int j = 0; j < 2; ++j) step(c + j * G, r[j]);  // past the end: no valid record, nothing stored
     }
   }
   if (tid == 0 && emitted) atomicAdd(&bc->m, emitted);
@@ -1074,7 +1122,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 
 // ==== v2 fine stage: one sort pass per fine item, a plan per bucket, an apply that gathers runs =========
 // After the coarse partition (bucket b = the contiguous range [Bb[b], Bb[b] + T[b]) of the partition
-// buffer, no holes but the dedup front end's marked ones), bucket b is cut into fine items of kSItem
+// buffer, no holes but the dedup front end's marked ones), bucket b is cut into fine items of 8 or 16 x 1024
 // records in bucket order. bin_fsort loads one item with every load in flight, ranks its records by fine
 // digit (slab of the bucket) in LDS and writes them back IN PLACE of the item's range (other buffers),
 // sorted by slab, with the item's slab offsets off2[item][0..nf] -- no count pass, no global cursor,
@@ -1086,13 +1134,22 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 #ifndef GLINT_FSORT_TPB
 #define GLINT_FSORT_TPB 1024
 #endif
-#ifndef GLINT_FSORT_PER
-#define GLINT_FSORT_PER 16
+// Records per thread of a fine item, by push size: a small push (at most ~4 items per CU, cfg5) sorts
+// items of 16 per thread at one workgroup per CU (fewer, longer runs per slab for the apply); a large one
+// items of 8 per thread at two workgroups per CU (register budget 64), so one workgroup's loads are in
+// flight while the other ranks and stores (build-time knobs GLINT_FSORT_PER_SMALL / _LARGE). Same box
+// (profiles/r06/ab_nt_mid.txt, s16 = 16 per thread for every push): cfg4b 2.28 -> 2.20 ms, cfg3 1.055 ->
+// 1.046; for cfg5 8 per thread measured 0.336 against 0.318 ms (ab_part_fsort_variants.txt, f8)
+#ifndef GLINT_FSORT_PER_SMALL
+#define GLINT_FSORT_PER_SMALL 16
+#endif
+#ifndef GLINT_FSORT_PER_LARGE
+#define GLINT_FSORT_PER_LARGE 8
 #endif
 constexpr int kSTPB = GLINT_FSORT_TPB;
-constexpr int kSPer = GLINT_FSORT_PER;
-constexpr u32 kSItem = (u32)kSTPB * kSPer;  // records per fine item (v2)
-static_assert(kSItem <= 32768, "u16 slab offsets and the u16 staging of one item");
+constexpr int kSPerSmall = GLINT_FSORT_PER_SMALL, kSPerLarge = GLINT_FSORT_PER_LARGE;
+constexpr u32 kSItemMax = (u32)kSTPB * (kSPerSmall > kSPerLarge ? kSPerSmall : kSPerLarge);
+static_assert(kSItemMax <= 32768, "u16 slab offsets and the u16 staging of one item");
 constexpr u32 kUnitExcl = 1u;  // apply unit descriptor {slab, runs, records, flags}: the slab's only unit
 constexpr u32 kSparseCap2 = 1024;  // bin_apply2's touched list (4 workgroups per CU fit in LDS)
 // An exclusive slab unit of at most kSparseMax2 records lists its touched elements (first touch) and
@@ -1113,8 +1170,12 @@ constexpr u32 kListMax = 768;
 // a few hundred records and one element round trip. Each bucket takes its range of the dense unit list
 // with one atomic.
 constexpr int kPlanTPB = 1024;
-constexpr u32 kPlanLds = 65536;  // bytes of the bucket's off2 rows staged at once
-constexpr u32 kPlanPTab = 16640; // u32 run prefixes (items x (slabs + 1)) of the wave emit
+// The plan's LDS: ROWB bytes of the bucket's off2 rows staged at once, PTAB u32 run prefixes (items x
+// (slabs + 1)) of the wave emit. The plan launch takes the large one; the plan fused into bin_fsort the
+// small one, so that the fine sort keeps two workgroups per CU (a fused push has few items per bucket
+// and <= 128 slabs per bucket: cfg5's 641 items, nf = 128)
+constexpr u32 kPlanLds = 65536, kPlanPTab = 16640;
+constexpr u32 kPlanLdsFused = 32768, kPlanPTabFused = 8320;
 constexpr int kRunMax = 128;     // runs per apply unit at most
 #ifndef GLINT_UNIT_CAP
 #define GLINT_UNIT_CAP 4096
@@ -1130,9 +1191,11 @@ constexpr u32 kGroupMax = 16;        // slabs per group (the record's u16 carrie
 static_assert(kSlabBits + 4 <= 16, "a slab offset and 4 slab bits in one u16");
 constexpr u32 kUnitGroup = 2u;       // unit flag: a group of sparse slabs (hash-table path)
 static_assert(kGroupCap <= kUnitCap && kGroupMax <= 64, "a group is one unit, inside one wave's lanes");
+template <u32 ROWB, u32 PTAB>
 struct PlanLds {
-  uint16_t rows[kPlanLds / 2];
-  u32 ptab[kPlanPTab];  // (wave emit) records of the slab (group) before each item's run
+  static constexpr u32 kRowBytes = ROWB, kPTab = PTAB;
+  uint16_t rows[ROWB / 2];
+  u32 ptab[PTAB];  // (wave emit) records of the slab (group) before each item's run
   u32 nunit[kMaxDigit];
   u32 utot[kMaxDigit];
   uint8_t spanv[kMaxDigit];
@@ -1142,11 +1205,11 @@ struct PlanLds {
 // other workgroups of this launch (bin_fsort's fused plan, the last item of the bucket plans it), so
 // they are read with sc1 loads, as they were stored (the hand-off of the MI355X guide's sc1 table: each
 // storing workgroup waits for its stores, then adds to the bucket's counter; the last adder reads).
-template <bool SC1>
+template <bool SC1, typename PL>
 __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* __restrict__ T, const u32* __restrict__ Bb,
                                             const u32* __restrict__ Ib, const u32* off2, BinCtl* bc,
                                             uint4* __restrict__ units, uint2* __restrict__ runs, int group_on,
-                                            PlanLds& L, u32 item) {
+                                            PL& L, u32 item) {
   static_assert(kMaxDigit == kPlanTPB, "one slab per thread");
   uint16_t* const rows = L.rows;
   u32* const ptab = L.ptab;
@@ -1156,7 +1219,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   u32& ubase = L.ubase;
   const int tid = threadIdx.x;
   const u32 J = bucket_items(T[b], item), I = Ib[b], nf1 = g.nf + 1, bb = Bb[b];
-  const u32 jt = kPlanLds / 2 / nf1;  // items per staged tile (>= 31 for nf <= 1024)
+  const u32 jt = PL::kRowBytes / 2 / nf1;  // items per staged tile (>= 31 for nf <= 1024 at 64 KiB)
   const u32 f = tid;                  // this thread's slab
   auto stage = [&](u32 j0, u32 j1) {  // rows of items [j0, j1): every load of a round in flight together
     const u32 nx = (j1 - j0) * nf1;
@@ -1226,7 +1289,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   // a lane per item, so the run-table stores are contiguous (the per-thread walk stored one 8-byte run
   // per lane into 64 different run tables per instruction). Larger buckets take the walk.
   const u32 ps = g.nf + 1;  // ptab row stride: +1 so the lanes of one slab's column hit different banks
-  const bool wave_emit = J <= 64u && J <= jt && J * ps <= kPlanPTab;  // block-uniform
+  const bool wave_emit = J <= 64u && J <= jt && J * ps <= PL::kPTab;  // block-uniform
   u32 h = 0, nu1 = 0;
   if (wave_emit) {
     stage(0, J);
@@ -1326,15 +1389,15 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
                                                             const u32* __restrict__ Ib, const u32* __restrict__ off2,
                                                             BinCtl* bc, uint4* __restrict__ units, uint2* __restrict__ runs,
                                                             int group_on, u32 item) {
-  __shared__ PlanLds L;
+  __shared__ PlanLds<kPlanLds, kPlanPTab> L;
   plan_bucket<false>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item);
 }
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
 // (plan_bucket<true>), so no plan launch follows and the buckets' plans overlap the other items' sorts.
 constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
-template <typename A, bool FUSED>
-__global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
+template <typename A, bool FUSED, int kSPer>
+__global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(kSPer <= 8 ? 8 : 4))) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
                                                           const u32* __restrict__ T, const u32* __restrict__ Bb,
                                                           const u32* __restrict__ addr_in, const A* __restrict__ val_in,
                                                           uint16_t* __restrict__ e_out, A* __restrict__ v_out,
@@ -1344,7 +1407,8 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
                                                           int group_on, u32 item) {
   constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
   constexpr size_t kSortLds = 4 * kMaxDigit + kStage;
-  constexpr size_t kLds = FUSED && sizeof(PlanLds) > kSortLds ? sizeof(PlanLds) : kSortLds;
+  typedef PlanLds<kPlanLdsFused, kPlanPTabFused> FusedPlanLds;
+  constexpr size_t kLds = FUSED && sizeof(FusedPlanLds) > kSortLds ? sizeof(FusedPlanLds) : kSortLds;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
   __shared__ u32 last_flag;
   u32* const hist = reinterpret_cast<u32*>(smem);
@@ -1377,7 +1441,7 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
     if (tid == 0) last_flag = atomicAdd(&done[b], 1u) + 1u == bucket_items(T[b], item);
     __syncthreads();
     if (last_flag)
-      plan_bucket<true>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, *reinterpret_cast<PlanLds*>(smem), item);
+      plan_bucket<true>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, *reinterpret_cast<FusedPlanLds*>(smem), item);
   };
   for (u32 f = tid; f < g.nf; f += kSTPB) hist[f] = 0;
   if (s1 == s0) {  // an empty bucket's one item
@@ -1386,26 +1450,29 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
     return;
   }
   PhaseClock ph(32);
+  // The item's records through buffer windows over its own ranges (workgroup-uniform descriptors, 32-bit
+  // offsets: few registers, so the fine sort keeps two workgroups per CU); a load past the item reads 0
+  // without touching memory, a store at the window's end is dropped (counted stores, see BufOut)
+  const u32 cnt = s1 - s0;
+  const BufOut ain = buf_out(addr_in + s0, cnt * 4u), vin = buf_out(val_in + s0, cnt * (u32)sizeof(A));
   u32 a[kSPer];
   A v[kSPer];
 #pragma unroll
-  for (int q = 0; q < kSPer; ++q) {  // clamped, branch-free: the whole item in flight at once
-    const u32 i = s0 + q * kSTPB + tid;
-    const u32 ii = i < s1 ? i : s1 - 1;
+  for (int q = 0; q < kSPer; ++q) {  // branch-free: the whole item in flight at once
+    const u32 x = q * kSTPB + tid;
     if ((u32)q * kSTPB < item) {  // launch-uniform (an item of fewer records than the registers hold)
-      a[q] = ld_in(addr_in + ii);
-      v[q] = ld_in(val_in + ii);
+      a[q] = bget<u32>(ain, x * 4u);
+      v[q] = bget<A>(vin, x * (u32)sizeof(A));
     } else {
       v[q] = A(0);
     }
-    if (i >= s1 || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
+    if (x >= cnt || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
   }
   __syncthreads();
   ph.mark(32);
-  u32 p[kSPer];
+  u32 p[kSPer];  // the record's place in the item's slab order (kEmptySlot: no record)
 #pragma unroll
-  for (int q = 0; q < kSPer; ++q)
-    if (a[q] != kEmptySlot) p[q] = atomicAdd(&hist[fine_of(a[q], g)], 1u);
+  for (int q = 0; q < kSPer; ++q) p[q] = a[q] != kEmptySlot ? atomicAdd(&hist[fine_of(a[q], g)], 1u) : kEmptySlot;
   __syncthreads();
   ph.mark(33);
   const u32 total = block_scan<kSTPB, 1>(
@@ -1416,27 +1483,38 @@ __global__ __launch_bounds__(kSTPB) void bin_fsort_kernel(BinGeom g, const uint2
       });
   if (tid == 0) put_row(g.nf, total);
   ph.mark(34);
-#pragma unroll
-  for (int q = 0; q < kSPer; ++q)
-    if (a[q] != kEmptySlot) p[q] += hist[fine_of(a[q], g)];
   // the slab offsets (and the slab's low 4 bits: bin_apply2's groups of sparse slabs), staged as u16
   // and stored as whole-wave runs
   uint16_t* const ste = reinterpret_cast<uint16_t*>(stage);
 #pragma unroll
-  for (int q = 0; q < kSPer; ++q)
-    if (a[q] != kEmptySlot) ste[p[q]] = (uint16_t)((a[q] & (kSlab - 1)) | ((fine_of(a[q], g) & 15u) << kSlabBits));
+  for (int q = 0; q < kSPer; ++q) {
+    if (p[q] == kEmptySlot) continue;
+    const u32 f = fine_of(a[q], g);
+    p[q] += hist[f];
+    ste[p[q]] = (uint16_t)((a[q] & (kSlab - 1)) | ((f & 15u) << kSlabBits));
+  }
   __syncthreads();
-  for (u32 x = tid; x < total; x += kSTPB) e_out[s0 + x] = ste[x];
+  const BufOut eo = buf_out(e_out + s0, total * 2u), vo = buf_out(v_out + s0, total * (u32)sizeof(A));
+#pragma unroll
+  for (int q = 0; q < kSPer; ++q) {  // total <= item <= kSPer * kSTPB
+    const u32 x = q * kSTPB + tid;
+    if ((u32)q * kSTPB >= item) break;  // launch-uniform
+    bput16(eo, x * 2u, x < total, ste[x]);
+  }
   __syncthreads();
   ph.mark(35);
   A* const stv = reinterpret_cast<A*>(stage);
   for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
 #pragma unroll
     for (int q = 0; q < kSPer; ++q)
-      if (a[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
+      if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
     __syncthreads();
-    const u32 r1 = min(total, r0 + kStageV);
-    for (u32 x = r0 + tid; x < r1; x += kSTPB) v_out[s0 + x] = stv[x - r0];
+    constexpr int kRound = (int)(kStageV / kSTPB);
+#pragma unroll
+    for (int q = 0; q < kRound; ++q) {
+      const u32 x = r0 + q * kSTPB + tid;
+      bput(vo, x * (u32)sizeof(A), x < total, stv[x - r0]);
+    }
     __syncthreads();
   }
   ph.mark(36);
@@ -1540,8 +1618,8 @@ __global__ __launch_bounds__(kCTPB) __attribute__((amdgpu_waves_per_eu(GLINT_APP
 #pragma unroll
     for (int q = 0; q < kCRB2; ++q) {
       const u32 idx = rs[slot][lo[q]] + (rr[q] - (u32)rp[slot][lo[q]]);
-      ca[q] = ld_in(e_in + idx);
-      cv[q] = ld_in(v_in + idx);
+      ca[q] = ld_mid(e_in + idx);
+      cv[q] = ld_mid(v_in + idx);
       valid |= (r0 + q * kCTPB + tid < cnt ? 1u : 0u) << q;
     }
     return valid;
@@ -1851,8 +1929,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * wpc));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   // a small push (at most ~4 fine items per CU, cfg5) plans its buckets inside bin_fsort
-  const bool small_push = (i64)g.nb + n / kSItem + 1 <= (i64)4 * s->cus;
-  const u32 item = kSItem;
+  const bool small_push = (i64)g.nb + n / ((i64)kSTPB * kSPerSmall) + 1 <= (i64)4 * s->cus;
+  const u32 item = (u32)kSTPB * (small_push ? kSPerSmall : kSPerLarge);
   const i64 max_fitems = (i64)g.nb + n / item + 1;
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
   // floor(H / cap) + floor(runs / kRunMax) + 1 per non-empty slab
@@ -1991,12 +2069,12 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
   u64* const whint = whole_next ? s->d_hint : nullptr;
   if (fused) {
-    bin_fsort_kernel<A, true><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
+    bin_fsort_kernel<A, true, kSPerSmall><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
                                                                       off2, bhint, whint, (u32)n, Ib, done, units, runs,
                                                                       group_on, item);
     HIPCHK(hipGetLastError());
   } else {
-    bin_fsort_kernel<A, false><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
+    bin_fsort_kernel<A, false, kSPerLarge><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
                                                                        off2, bhint, whint, (u32)n, Ib, done, units, runs,
                                                                        group_on, item);
     HIPCHK(hipGetLastError());

@@ -563,7 +563,30 @@ __global__ void push_validate_gate_kernel(LaunchCtl* ctl, u64* gate) {
 // pulls
 // ------------------------------------------------------------------------------------------------
 // PartialVector.get (PartialVector.scala:51-60): out[i] = data(globalToLocal(keys(i)))
-// PAIRS: records [2 * p_begin, min(n, 2 * p_end)) (a large pull runs one launch per window)
+// PAIRS: records [2 * p_begin, min(n, 2 * p_end)) (a large pull runs one launch per window). Each lane
+// takes kPullUnroll pairs per iteration: every key load, then every gather, then every store, so a
+// lane's gathers are in flight together instead of one dependent key -> element round trip at a time.
+#ifndef GLINT_PULL_UNROLL
+#define GLINT_PULL_UNROLL 1
+#endif
+#ifndef GLINT_PULL_BPC
+#define GLINT_PULL_BPC 4
+#endif
+constexpr int kPullUnroll = GLINT_PULL_UNROLL;
+constexpr int kPullBlocksPerCu = GLINT_PULL_BPC;
+template <typename V>
+__device__ __forceinline__ typename Vec2<V>::T pull_pair(const K2& k, const V* data, const PartDesc& part, ErrState* err,
+                                                         i64 r) {
+  typedef typename Vec2<V>::T V2;
+  i64 l0, l1;
+  const bool o0 = rec_addr<false>(part, k.x, 0, l0);
+  const bool o1 = rec_addr<false>(part, k.y, 0, l1);
+  if (o0 && o1 && l1 == l0 + 1 && (l0 & 1) == 0)  // adjacent pair: a streamed (dense) pull -- non-temporal
+    return __builtin_nontemporal_load(reinterpret_cast<const V2*>(data + l0));
+  if (!o0) record_error(err, r);
+  if (!o1) record_error(err, r + 1);
+  return as2<V>(o0 ? data[l0] : V(0), o1 ? data[l1] : V(0));
+}
 template <typename V, bool PAIRS>
 __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, const V* data, PartDesc part,
                                                         V* out, ErrState* err, MsgSig sig, i64 p_begin, i64 p_end) {
@@ -571,23 +594,27 @@ __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, 
   const i64 stride = (i64)gridDim.x * kTPB;
   if (PAIRS) {
     const i64 npairs = p_end;
-    for (i64 p = p_begin + (i64)blockIdx.x * kTPB + threadIdx.x; p < npairs; p += stride) {
+    i64 p = p_begin + (i64)blockIdx.x * kTPB + threadIdx.x;
+    if (kPullUnroll > 1) {
+      const i64 pfull = min(npairs, n >> 1);  // pairs with both records
+      for (; p + (kPullUnroll - 1) * stride < pfull; p += kPullUnroll * stride) {
+        K2 k[kPullUnroll];
+        V2 o[kPullUnroll];
+#pragma unroll
+        for (int u = 0; u < kPullUnroll; ++u)
+          k[u] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p + u * stride);
+#pragma unroll
+        for (int u = 0; u < kPullUnroll; ++u) o[u] = pull_pair<V>(k[u], data, part, err, 2 * (p + u * stride));
+#pragma unroll
+        for (int u = 0; u < kPullUnroll; ++u)
+          __builtin_nontemporal_store(o[u], reinterpret_cast<V2*>(out + 2 * (p + u * stride)));
+      }
+    }
+    for (; p < npairs; p += stride) {
       const i64 r = 2 * p;
       if (r + 1 < n) {
         const K2 k = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p);
-        i64 l0, l1;
-        const bool o0 = rec_addr<false>(part, k.x, 0, l0);
-        const bool o1 = rec_addr<false>(part, k.y, 0, l1);
-        V2 o;
-        if (o0 && o1 && l1 == l0 + 1 && (l0 & 1) == 0) {
-          // adjacent pair: a streamed (dense) pull -- non-temporal, like the push sweep
-          o = __builtin_nontemporal_load(reinterpret_cast<const V2*>(data + l0));
-        } else {
-          if (!o0) record_error(err, r);
-          if (!o1) record_error(err, r + 1);
-          o = as2<V>(o0 ? data[l0] : V(0), o1 ? data[l1] : V(0));
-        }
-        __builtin_nontemporal_store(o, reinterpret_cast<V2*>(out + r));
+        __builtin_nontemporal_store(pull_pair<V>(k, data, part, err, r), reinterpret_cast<V2*>(out + r));
       } else {
         i64 l0;
         const bool o0 = rec_addr<false>(part, keys[r], 0, l0);
@@ -934,12 +961,12 @@ int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream
   const bool pairs = aligned(keys, 16) && aligned(out, 2 * sizeof(V));
   if (pairs) {
     // 4 blocks per CU: the dense gather's best (tools/microbench_stream.hip mode 5); one launch per
-    // window of records, as the push's apply sweep (sweep_window_tiles)
+    // window of records, as the push's apply sweep (kSweepWindowTiles)
     const i64 npairs = (n + 1) / 2;
     const i64 win = sig.done ? npairs : std::min<i64>(npairs, (i64)kSweepWindowTiles * (kTile / 2));
     for (i64 p0 = 0; p0 < npairs; p0 += win) {
       const i64 p1 = std::min<i64>(npairs, p0 + win);
-      const unsigned g = sig.done ? 1u : grid_for(p1 - p0, kTPB, (i64)s->cus * 4);
+      const unsigned g = sig.done ? 1u : grid_for(p1 - p0, kTPB, (i64)s->cus * kPullBlocksPerCu);
       HIPCHK(launch_k(s, GLINT_K_VEC_PULL, vec_pull_kernel<V, true>, g, kTPB, st, keys, n, (const V*)s->data, s->part,
                       (V*)out, err_of(s), sig, p0, p1));
     }

@@ -21,7 +21,7 @@
 #   lbspin    cfg4b thread-per-connection pulls with GLINT_LOCK_SPIN 0 / 200 / 2000 (a round-5 build knob,
 #             removed after this A/B), cfg1 actor rows, CPU loop beside
 set -o pipefail
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT

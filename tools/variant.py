@@ -1,10 +1,10 @@
 """Builds a variant of libglint_gpu.so for A/B runs on one box: glint_bin.hip (or another source)
 recompiled with extra -D defines, linked with the other objects of the current build.
 
-    python tools/variant.py NAME -DGLINT_BIN_NT=1 [--src glint_bin]   # -> tools/build/libglint_gpu_NAME.so
+    python tools/variant.py NAME -DGLINT_BIN_NT=1 [--src glint_bin]   # -> tools/ablibs/libglint_gpu_NAME.so
     python tools/variant.py NAME -DGLINT_RING_SLOTS=64 --all          # every source (layout-changing defines)
 
-Load it with GLINT_GPU_LIB=tools/build/libglint_gpu_NAME.so (the `ab` stage of tools/gpu_run.sh).
+Load it with GLINT_GPU_LIB=tools/ablibs/libglint_gpu_NAME.so (the `ab` stage of tools/gpu_run.sh).
 """
 import importlib.util
 import subprocess
@@ -30,7 +30,8 @@ def main():
         subprocess.run([b._hipcc(), *flags, "-c", "-o", str(out), str(ROOT / "glint_amd" / "csrc" / f"{sname}.hip")],
                        check=True)
         objs.append(str(out))
-    lib = ROOT / "tools" / "build" / f"libglint_gpu_{name}.so"
+    # (tools/ablibs travels to the GPU box with the tree; tools/build does not)
+    lib = ROOT / "tools" / "ablibs" / f"libglint_gpu_{name}.so"
     lib.parent.mkdir(parents=True, exist_ok=True)
     subprocess.run([b._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(lib), *objs], check=True)
     print(lib)
