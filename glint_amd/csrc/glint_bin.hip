@@ -228,6 +228,23 @@ struct BadRecs {  // this thread's rejected records: the first one and how many
 };
 
 // ---- block-level helpers ------------------------------------------------------------------------
+// The per-wave totals of a workgroup (wt[0..NW), NW <= 16 waves): lane l < NW reads wt[l], an inclusive
+// scan across the lanes of the first DPP row (row_shr 1, 2, 4, 8: register-to-register, no LDS round
+// trip) -> the waves before wave `wid` (exclusive) and all of them, both workgroup-uniform. Two registers,
+// one LDS read.
+template <int NW>
+__device__ __forceinline__ void wave_totals(const u32* wt, int lane, int wid, u32& pre, u32& tot) {
+  static_assert(NW >= 1 && NW <= 16, "one DPP row");
+  u32 x = lane < NW ? wt[lane] : 0u;
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (NW > 2) x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (NW > 4) x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (NW > 8) x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  const int w = __builtin_amdgcn_readfirstlane(wid);
+  pre = w > 0 ? (u32)__builtin_amdgcn_readlane((int)x, w - 1) : 0u;
+  tot = (u32)__builtin_amdgcn_readlane((int)x, NW - 1);
+}
+
 // Exclusive scan over N values by one workgroup of TPB threads, in tiles of TPB x PER: each thread
 // loads a run of PER values into registers (all loads in flight together), scans them and calls
 // write(i, exclusive prefix) once per i. Returns the total.
@@ -253,15 +270,8 @@ __device__ __forceinline__ u32 block_scan(u32 N, F value, W write) {
     }
     if (lane == 63) wt[wid] = incl;
     __syncthreads();
-    // the waves before this one and all of them: lane l holds wave l's total, summed across the wave
-    // (two registers, where reading every wave's total into registers held TPB / 64 of them)
-    const u32 wv = lane < TPB / 64 ? wt[lane] : 0u;
-    u32 pre = lane < wid ? wv : 0u, tot = wv;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-      pre += __shfl_xor(pre, d);
-      tot += __shfl_xor(tot, d);
-    }
+    u32 pre, tot;  // the waves before this one and all of them
+    wave_totals<TPB / 64>(wt, lane, wid, pre, tot);
     u32 run = carry + incl - s + pre;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -281,9 +291,8 @@ __device__ __forceinline__ u32 block_sum(u32 x) {
   for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = x;
   __syncthreads();
-  u32 t = 0;
-#pragma unroll
-  for (int w = 0; w < TPB / 64; ++w) t += ws[w];
+  u32 pre, t;
+  wave_totals<TPB / 64>(ws, threadIdx.x & 63, threadIdx.x >> 6, pre, t);
   __syncthreads();
   return t;
 }

@@ -12,7 +12,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 TAG = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else ""
-PROF_LIB = ROOT / "tools" / "build" / f"libglint_gpu_prof{'_' + TAG if TAG else ''}.so"
+PROF_LIB = ROOT / "tools" / "ablibs" / f"libglint_gpu_prof{'_' + TAG if TAG else ''}.so"  # (travels to the box)
 DEFINES = [a for a in sys.argv[1:] if a.startswith("-D")]
 
 PHASES = {
@@ -20,9 +20,6 @@ PHASES = {
                              "clear+sync"]),
     "bin_part (dedup)": (8, ["setup", "hash insert", "issue loads", "sync+extract+sync", "rank+sync", "scan",
                              "stage+sync", "store+sync", "clear+sync", "hv clear+sync"]),
-    "bin_fpart": (20, ["T/H scans", "item descs", "segments", "sync", "reserve", "fetch issue",
-                       "rank+sync", "scan", "stage+sync", "store+sync", "clear+sync"]),
-    "bin_apply": (40, ["desc/warm", "clear+sync", "records", "sync", "rmw", "sync"]),
     "bin_fsort (v2)": (32, ["load+sync", "rank+sync", "scan", "stage e+store", "values"]),
     "bin_plan (v2)": (48, ["stage+walk", "groups+scan", "atomic+sync", "emit+sync"]),
     "bin_apply2 (v2)": (56, ["records", "publish+sync", "prefetch issue", "write-back", "sync"]),
@@ -71,8 +68,9 @@ def run():
             else:
                 rc = lib.glint_vec_push_dev(h, keys.data_ptr(), vals.data_ptr(), keys.numel(), 0, st)
             assert rc == 0, rc
-        for _ in range(3):
-            push()
+        for _ in range(3):  # each ended by the shard's sync point, as the bench's warm-up (the front end
+            push()          # decides from the hints latched there)
+            assert lib.glint_shard_sync(h, st, None) == 0
         torch.cuda.synchronize()
         lib.glint_debug_bin_prof(buf, 1)
         reps = 5
