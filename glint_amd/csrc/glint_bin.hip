@@ -28,6 +28,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <type_traits>
 
 namespace glint {
 
@@ -45,6 +46,14 @@ constexpr int kATPB = GLINT_PART_TPB;  // partition workgroup size (build-time k
 #define GLINT_PART_PER 4
 #endif
 constexpr int kAPer = GLINT_PART_PER;  // records per thread per chunk (build-time knob)
+#ifndef GLINT_PART_PER_PLAIN
+#define GLINT_PART_PER_PLAIN 8
+#endif
+// The plain front end of a large push takes chunks of 8 records per thread (no hot or dedup table
+// beside its staging in LDS): runs of 64 records per bucket and half the barriers per record. Same box,
+// two rounds (profiles/r06/ab_part_per_plain.txt): cfg4b 2.20 -> 2.16 ms; cfg5 (a small push) 0.311 ->
+// 0.314, so a small push keeps 4
+constexpr int kAPerPlain = GLINT_PART_PER_PLAIN;
 constexpr int kAChunk = kATPB * kAPer; // records per partition chunk (and dedup table fill)
 constexpr int kASlots = 2 * kAChunk;   // dedup hash slots (load <= 0.5)
 constexpr int kASlotBits = kASlots == 8192 ? 13 : kASlots == 4096 ? 12 : 11;
@@ -309,18 +318,18 @@ __device__ __forceinline__ i64 tail_start(const LaunchCtl* lctl, u32 ntiles, int
 // One partition chunk's records, kAPer per thread, in registers. The partition kernels keep two of
 // these in flight (chunks c + G and c + 2G load while chunk c is partitioned): one chunk of loads per
 // workgroup left too little in flight per CU to cover HBM latency.
-template <typename V, bool MAT>
+template <typename V, bool MAT, int PER = kAPer>
 struct RecRegs {
-  i64 k[kAPer];
-  int32_t cl[kAPer];
-  V v[kAPer];
+  i64 k[PER];
+  int32_t cl[PER];
+  V v[PER];
 };
 
-template <typename V, bool MAT, bool VALS = true>
+template <typename V, bool MAT, bool VALS = true, int PER = kAPer>
 __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
-                                          const V* __restrict__ vals, i64 c0, i64 c1, RecRegs<V, MAT>& r) {
+                                          const V* __restrict__ vals, i64 c0, i64 c1, RecRegs<V, MAT, PER>& r) {
 #pragma unroll
-  for (int q = 0; q < kAPer; ++q) {  // clamped, branch-free loads
+  for (int q = 0; q < PER; ++q) {  // clamped, branch-free loads
     const i64 i = c0 + q * kATPB + threadIdx.x;
     const i64 ii = i < c1 ? i : c1 - 1;
     r.k[q] = ld_in(keys + ii);
@@ -355,7 +364,7 @@ __device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlot
 // first rejected one in the push's LaunchCtl (vctl->bad), as push_check does for the records before the
 // break; the push's verdict and cancel come after this kernel (push_validate_gate_binned_kernel), so the
 // keys are read once instead of by push_check and here.
-template <bool MAT, int KIND, bool VALIDATE = false>
+template <bool MAT, int KIND, bool VALIDATE = false, int PER = kAPer>
 __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                           i64 n, PartDesc part, const LaunchCtl* lctl, u32 ntiles,
                                                           int from_break, BinGeom g, u32* __restrict__ T,
@@ -368,6 +377,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   __shared__ u32 htag[kWideSlots];
   const int tid = threadIdx.x;
   const u32 hc = (u32)((tid >> 6) % kCopies) * g.nb;
+  constexpr int kChunk = kATPB * PER;  // records per chunk (the partition's, front end by front end)
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
   for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
   if (blockIdx.x == 0) {  // the next push's header (the previous push used it; it is done)
@@ -389,7 +399,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
       htag[sl] = x ? (u32)x : kEmptySlot;
     }
   __syncthreads();
-  const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
+  const i64 nchunks = (n - r0 + kChunk - 1) / kChunk;
   const i64 G = gridDim.x;
   u32 nvalid = 0;
   bool dis = false;  // (a whole-push bin) two adjacent records of one wave out of order
@@ -398,29 +408,29 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
   // (chunk index clamped; a step past the end counts nothing), so the compiler can wait for one
   // chunk's loads while the next chunk's stay in flight: with conditional loads it waited vmcnt(0).
   BadRecs bad;
-  auto load = [&](i64 c, RecRegs<double, MAT>& r) {
+  auto load = [&](i64 c, RecRegs<double, MAT, PER>& r) {
     const i64 cc = min(c, nchunks - 1);
     if constexpr (KIND == 0 && !VALIDATE) {
       // the range layout reads only the key's low word ((key - start).toInt): loading the whole key
       // left its high half dead, the compiler reused that register while the load was in flight and
       // had to wait for it (vmcnt(0)), so only one chunk was ever in flight
-      const i64 c0 = r0 + cc * kAChunk, c1 = min(n, c0 + kAChunk);
+      const i64 c0 = r0 + cc * kChunk, c1 = min(n, c0 + kChunk);
 #pragma unroll
-      for (int q = 0; q < kAPer; ++q) {
+      for (int q = 0; q < PER; ++q) {
         const i64 i = c0 + q * kATPB + threadIdx.x;
         const i64 ii = i < c1 ? i : c1 - 1;
         r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
         r.cl[q] = MAT ? ld_in(cols + ii) : 0;
       }
     } else {
-      load_recs<double, MAT, false>(keys, cols, nullptr, r0 + cc * kAChunk, min(n, r0 + (cc + 1) * kAChunk), r);
+      load_recs<double, MAT, false, PER>(keys, cols, nullptr, r0 + cc * kChunk, min(n, r0 + (cc + 1) * kChunk), r);
     }
   };
-  auto step = [&](i64 c, RecRegs<double, MAT>& r) {
-    const i64 c0 = r0 + c * kAChunk, c1 = c < nchunks ? min(n, c0 + kAChunk) : c0;
-    u32 bk[kAPer];
+  auto step = [&](i64 c, RecRegs<double, MAT, PER>& r) {
+    const i64 c0 = r0 + c * kChunk, c1 = c < nchunks ? min(n, c0 + kChunk) : c0;
+    u32 bk[PER];
 #pragma unroll
-    for (int q = 0; q < kAPer; ++q) {
+    for (int q = 0; q < PER; ++q) {
       i64 ad;
       const bool in = c0 + q * kATPB + tid < c1;
       bool ok = in && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad);
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
     }
     load(c + kCountAhead * G, r);  // kCountAhead chunks ahead, into the registers just consumed
 #pragma unroll
-    for (int q = 0; q < kAPer; ++q) {
+    for (int q = 0; q < PER; ++q) {
       if (bk[q] != kEmptySlot) {
         atomicAdd(&h[hc + bk[q]], 1u);
         ++nvalid;
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict_
     }
   };
   if ((i64)blockIdx.x < nchunks) {
-    RecRegs<double, MAT> r[kCountAhead];
+    RecRegs<double, MAT, PER> r[kCountAhead];
     i64 c = blockIdx.x;
 #pragma unroll
     for (int j = 0; j < kCountAhead; ++j) load(c + j * G, r[j]);
@@ -619,7 +629,6 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   }
   __syncthreads();
   ph.mark(pb + 2);
-  static_assert(P * kATPB == kAChunk, "the store loop covers a whole chunk");
 #pragma unroll
   for (int j = 0; j < P; ++j) {  // consecutive threads: consecutive slots of one run
     if ((u32)(j * kATPB) >= total) break;  // workgroup-uniform: no store instructions past the chunk
@@ -829,7 +838,7 @@ __device__ __forceinline__ auto part_out(T* base, u32 n, void* dump, size_t dump
 #ifndef GLINT_PART_WAVES
 #define GLINT_PART_WAVES 4  // bin_part's register budget: waves per SIMD (build-time knob)
 #endif
-template <typename V, bool MAT, bool HOT, int KIND, bool WIDE>
+template <typename V, bool MAT, bool HOT, int KIND, bool WIDE, int PER = kAPer>
 __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 : GLINT_PART_WAVES))) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
                                                          const V* __restrict__ vals, i64 n, PartDesc part,
                                                          const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
@@ -842,16 +851,17 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
                                                          const u32* __restrict__ Roff, u32* __restrict__ Bb,
                                                          u32* __restrict__ Ib, void* dump) {
   typedef typename LdsAcc<V>::T A;
+  constexpr int kChunk = kATPB * PER;  // records per chunk
   __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
-  __shared__ u32 st_a[kAChunk];
-  __shared__ A st_v[kAChunk];
+  __shared__ u32 st_a[kChunk];
+  __shared__ A st_v[kChunk];
   constexpr int kHS = HOT ? kWideSlots : 1;
   __shared__ u32 htag[kHS];
   __shared__ A hacc[kHS];
   const int tid = threadIdx.x;
   const u32 w = blockIdx.x;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
-  const i64 nchunks = (n - r0 + kAChunk - 1) / kAChunk;
+  const i64 nchunks = (n - r0 + kChunk - 1) / kChunk;
   // chunks in flight: the hot front end runs one workgroup per CU (its LDS tables), two chunks ahead;
   // the plain one kPartAhead
   constexpr int kAhead = HOT ? 2 : kPartAhead;
@@ -874,12 +884,12 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
   u32 emitted = 0;
   // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
   // compiler can wait for one chunk's loads while the next chunk's stay in flight
-  auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
+  auto load_chunk = [&](i64 c, RecRegs<V, MAT, PER>& r) {
     const i64 cc = min(c, nchunks - 1);
-    const i64 c0 = r0 + cc * kAChunk, c1 = min(n, r0 + (cc + 1) * kAChunk);
+    const i64 c0 = r0 + cc * kChunk, c1 = min(n, r0 + (cc + 1) * kChunk);
     if constexpr (KIND == 0) {  // (key - start).toInt needs the low words only (as bin_count loads them)
 #pragma unroll
-      for (int q = 0; q < kAPer; ++q) {
+      for (int q = 0; q < PER; ++q) {
         const i64 i = c0 + q * kATPB + threadIdx.x;
         const i64 ii = i < c1 ? i : c1 - 1;
         r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
@@ -887,16 +897,16 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
         r.v[q] = ld_in(vals + ii);
       }
     } else {
-      load_recs<V, MAT>(keys, cols, vals, c0, c1, r);
+      load_recs<V, MAT, true, PER>(keys, cols, vals, c0, c1, r);
     }
   };
-  auto step = [&](i64 c, RecRegs<V, MAT>& r) {
-    const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
-    u32 ad[kAPer];
-    A va[kAPer];
+  auto step = [&](i64 c, RecRegs<V, MAT, PER>& r) {
+    const i64 c0 = r0 + c * kChunk, c1 = min(n, c0 + kChunk);
+    u32 ad[PER];
+    A va[PER];
     u32 valid = 0;
 #pragma unroll
-    for (int q = 0; q < kAPer; ++q) {
+    for (int q = 0; q < PER; ++q) {
       const i64 i = c0 + q * kATPB + tid;
       i64 a64;
       ad[q] = 0;
@@ -912,7 +922,7 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
     }
     if constexpr (HOT) {
 #pragma unroll
-      for (int q = 0; q < kAPer; ++q) {
+      for (int q = 0; q < PER; ++q) {
         const u32 hs = wide_slot(ad[q]);
         if ((valid & (1u << q)) && htag[hs] == ad[q]) {  // hot: summed over all of this workgroup's chunks
           lds_add(&hacc[hs], va[q]);
@@ -921,12 +931,12 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
       }
     }
     ph.mark(1);
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 3);
+    emitted += part_emit<A, PER>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 3);
     // kAhead chunks ahead, into the registers just consumed: in flight across the next chunks' work
     load_chunk(c + kAhead * G, r);
     ph.mark(2);
   };
-  RecRegs<V, MAT> r[kAhead];
+  RecRegs<V, MAT, PER> r[kAhead];
   i64 c = w;
   if (c < nchunks) {
 #pragma unroll
@@ -1850,7 +1860,10 @@ int resident_per_cu(K kernel, int tpb, size_t dyn_lds = 0) {
 // the fine digit would exceed 10 bits (slabs < 2^20 for u32 addresses). Same box, two runs each
 // (profiles/r03/bench_binned_cb.txt): 2^7 against 2^8 buckets cfg5 0.418 -> 0.398 ms, cfg3 1.648 ->
 // 1.636 ms, cfg4b exchange 3.005 -> 3.005 ms; 2^6 slower on all
-constexpr u32 kCoarseBitsMin = 7;
+#ifndef GLINT_BIN_CB
+#define GLINT_BIN_CB 7  // (build-time knob: coarse digit bits at least)
+#endif
+constexpr u32 kCoarseBitsMin = GLINT_BIN_CB;
 BinGeom bin_geometry(i64 elems) {
   const i64 slabs = (elems + kSlab - 1) / kSlab;
   u32 sb = 0;
@@ -1866,7 +1879,7 @@ BinGeom bin_geometry(i64 elems) {
 
 // u32 record indices and element addresses
 bool push_binnable(const glint_shard* s, i64 n) {
-  return n < ((i64)1 << 32) - 2 * kAChunk && s->elems < ((i64)1 << 32) - 1;
+  return n < ((i64)1 << 32) - 2 * (i64)kATPB * (kAPer > kAPerPlain ? kAPer : kAPerPlain) && s->elems < ((i64)1 << 32) - 1;
 }
 
 int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32 nb, hipStream_t st) {
@@ -1931,14 +1944,15 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   s->bin_last_front = front;
   // a push whose partition buffers pass 4 GiB stores through 64-bit addresses (WideOut)
   const bool wide = (u64)n * sizeof(A) >= ((u64)1 << 32);
-  const i64 nchunks_max = (n + kAChunk - 1) / kAChunk;
+  // a small push (at most ~4 fine items per CU, cfg5) plans its buckets inside bin_fsort
+  const bool small_push = (i64)g.nb + n / ((i64)kSTPB * kSPerSmall) + 1 <= (i64)4 * s->cus;
+  const int per = front == 0 && !small_push ? kAPerPlain : kAPer;  // records per thread of a partition chunk
+  const i64 nchunks_max = (n + (i64)kATPB * per - 1) / ((i64)kATPB * per);
   // partition workgroups per CU: what fits at once (the hot front end's LDS table allows fewer)
   static const int hot_occ = resident_per_cu(bin_part_kernel<V, MAT, true, 0, false>, kATPB);
   const int wpc = dedup ? kPartWgPerCuDedup : front == 1 ? std::min(kPartWgPerCuPlain, hot_occ) : kPartWgPerCuPlain;
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * wpc));
   if (G > (u32)kMaxSegs) return GLINT_EINVAL;
-  // a small push (at most ~4 fine items per CU, cfg5) plans its buckets inside bin_fsort
-  const bool small_push = (i64)g.nb + n / ((i64)kSTPB * kSPerSmall) + 1 <= (i64)4 * s->cus;
   const u32 item = (u32)kSTPB * (small_push ? kSPerSmall : kSPerLarge);
   const i64 max_fitems = (i64)g.nb + n / item + 1;
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
@@ -2030,16 +2044,18 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   const unsigned long long* count_hot = front == 1 ? wbest : nullptr;  // the hot records are not partitioned
   BinCtl* const nbc = (BinCtl*)nhdr;
   u32* const nT = (u32*)(nhdr + 256);
-  if (hook) {  // a validating gated push: the count validates the tail records
-    auto kern = a.part.kind == 0 ? bin_count_kernel<MAT, 0, true> : bin_count_kernel<MAT, -1, true>;
+  {
+    // the count's chunks are the partition's (its per-workgroup counts are the partition's places)
+    // (hook: a validating gated push, whose count validates the tail records)
+    auto pick = [&](auto per) {
+      constexpr int P = decltype(per)::value;
+      if (hook) return a.part.kind == 0 ? bin_count_kernel<MAT, 0, true, P> : bin_count_kernel<MAT, -1, true, P>;
+      return a.part.kind == 0 ? bin_count_kernel<MAT, 0, false, P> : bin_count_kernel<MAT, -1, false, P>;
+    };
+    auto kern = per == kAPerPlain ? pick(std::integral_constant<int, kAPerPlain>{})
+                                  : pick(std::integral_constant<int, kAPer>{});
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff, count_hot, nbc, nT,
-                              a.ctl, whole_next);
-  } else if (a.part.kind == 0) {
-    bin_count_kernel<MAT, 0><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
-                                                  count_hot, nbc, nT, nullptr, whole_next);
-  } else {
-    bin_count_kernel<MAT, -1><<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff,
-                                                   count_hot, nbc, nT, nullptr, whole_next);
+                              hook ? a.ctl : nullptr, whole_next);
   }
   HIPCHK(hipGetLastError());
   s->bin_par ^= 1;  // this push's header is [hdr]; bin_count zeroed the other one for the next push
@@ -2053,11 +2069,15 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, addr_a, val_a, a.err, bc, T,
                               fitems, hot_tags, a.data, item, Roff, Bb, Ib, dump);
   } else {
-    auto kern = a.part.kind == 0
-                    ? (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, 0, true> : bin_part_kernel<V, MAT, true, 0, false>)
-                                  : (wide ? bin_part_kernel<V, MAT, false, 0, true> : bin_part_kernel<V, MAT, false, 0, false>))
-                    : (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, -1, true> : bin_part_kernel<V, MAT, true, -1, false>)
-                                  : (wide ? bin_part_kernel<V, MAT, false, -1, true> : bin_part_kernel<V, MAT, false, -1, false>));
+    auto pick = [&](auto pp) {
+      constexpr int PP = decltype(pp)::value;
+      return a.part.kind == 0
+                 ? (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, 0, true> : bin_part_kernel<V, MAT, true, 0, false>)
+                               : (wide ? bin_part_kernel<V, MAT, false, 0, true, PP> : bin_part_kernel<V, MAT, false, 0, false, PP>))
+                 : (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, -1, true> : bin_part_kernel<V, MAT, true, -1, false>)
+                               : (wide ? bin_part_kernel<V, MAT, false, -1, true, PP> : bin_part_kernel<V, MAT, false, -1, false, PP>));
+    };
+    auto kern = per == kAPerPlain ? pick(std::integral_constant<int, kAPerPlain>{}) : pick(std::integral_constant<int, kAPer>{});
     kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, addr_a, val_a, a.err, bc, T,
                               fitems, wbest, wpart, item, Roff, Bb, Ib, dump);
   }

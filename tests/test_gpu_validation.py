@@ -5,6 +5,7 @@ import pytest
 
 from glint_amd import PartialMatrix, PartialVector, RangePartition
 from oracle import oracle as O
+import glint_amd._native as N
 
 pytestmark = pytest.mark.gpu
 
@@ -81,3 +82,62 @@ def test_host_calls_order_after_device_calls(gpu):
             np.testing.assert_array_equal(sh.get(q), ref.get(q)[0])
         sh.sync(torch.cuda.current_stream(dev).cuda_stream)
         np.testing.assert_array_equal(sh.to_numpy(), ref.data)
+
+
+# ---- the library's environment knobs: each non-default branch (DESIGN.md §8 lists them) ----------------
+def test_host_prof_knob(gpu, monkeypatch, capfd):
+    """GLINT_HOST_PROF=1: a shard counts its lock waits, launches, retire waits and copies, and prints
+    them as one `glint_host_prof {...}` JSON line on stderr when it is destroyed (the loopback harness's
+    --cpu-stats rows read it). Without it nothing is printed."""
+    import json
+    from glint_amd import PartialVector, RangePartition
+    part = RangePartition(0, 0, 4096)
+    keys = np.arange(1000, dtype=np.int64)
+    for on in (True, False):
+        if on:
+            monkeypatch.setenv("GLINT_HOST_PROF", "1")
+        else:
+            monkeypatch.delenv("GLINT_HOST_PROF", raising=False)
+        N.reload_env()
+        with PartialVector(part, "long", gpu) as sh:
+            t = sh.push_async(keys, np.ones(keys.size, np.int64))
+            sh.wait(t)
+            assert (sh.get(keys) == 1).all()
+        err = capfd.readouterr().err
+        lines = [ln for ln in err.splitlines() if ln.startswith("glint_host_prof ")]
+        if on:
+            assert len(lines) == 1, err
+            d = json.loads(lines[0][len("glint_host_prof "):])
+            assert d["device"] == gpu and d["locks"] >= 2 and d["launches"] >= 1 and d["tickets"] >= 1
+        else:
+            assert not lines
+
+
+@pytest.mark.parametrize("stage_max", ["0", "64"])
+def test_pinned_stage_max_knob(gpu, monkeypatch, stage_max):
+    """GLINT_PINNED_STAGE_MAX (bytes): host arrays up to it are staged through the shard's pinned buffer
+    (one DMA per call), larger ones go straight from pageable memory. At 0 / 64 B every call of this test
+    takes the pageable path that only messages above the 2 MiB default take; results are the oracle's."""
+    from glint_amd import PartialMatrix, PartialVector, RangePartition
+    from oracle import oracle as O
+    monkeypatch.setenv("GLINT_PINNED_STAGE_MAX", stage_max)
+    N.reload_env()
+    rng = np.random.default_rng(3)
+    size = 50_000
+    ref = O.OracleVector(O.part_range(100, 100 + size), O.CODE["long"])
+    with PartialVector(RangePartition(0, 100, 100 + size), "long", gpu) as sh:
+        for n in (1, 1000, 70_000):
+            k = rng.integers(100, 100 + size, n).astype(np.int64)
+            v = rng.integers(-99, 99, n).astype(np.int64)
+            sh.update(k, v)
+            assert ref.update(k, v) == -1
+        q = rng.integers(100, 100 + size, 5000).astype(np.int64)
+        np.testing.assert_array_equal(sh.get(q), ref.get(q)[0])
+    mref = O.OracleMatrix(O.part_range(0, 64), 33, O.CODE["double"])
+    with PartialMatrix(RangePartition(0, 0, 64), 33, "double", gpu) as sh:
+        r = rng.integers(0, 64, 3000).astype(np.int64)
+        c = rng.integers(0, 33, 3000).astype(np.int32)
+        v = rng.uniform(-1, 1, 3000)
+        sh.update(r, c, v, deterministic=True)
+        assert mref.update(r, c, v) == -1
+        np.testing.assert_array_equal(sh.getRows(np.arange(64)), mref.data)
