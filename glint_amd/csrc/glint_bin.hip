@@ -2094,6 +2094,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // launch and its tail are a real share of the push; with many items per CU every item's wait for its
   // stores before counting itself in costs more: cfg3 1.067 -> 1.078, cfg4b 2.375 -> 2.44 ms, cfg5
   // 0.347 -> 0.335 (profiles/r05/ab_fused_plan.txt)
+  // (fused for every push, with the fine sort at two workgroups per CU: cfg4b 2.15 -> 2.50 ms, cfg3 1.02
+  // -> 1.04, profiles/r06/ab_fuse_all.txt)
   const bool fused = small_push;
   u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
   u64* const whint = whole_next ? s->d_hint : nullptr;
