@@ -1210,26 +1210,28 @@ constexpr u32 kGroupMax = 16;        // slabs per group (the record's u16 carrie
 static_assert(kSlabBits + 4 <= 16, "a slab offset and 4 slab bits in one u16");
 constexpr u32 kUnitGroup = 2u;       // unit flag: a group of sparse slabs (hash-table path)
 static_assert(kGroupCap <= kUnitCap && kGroupMax <= 64, "a group is one unit, inside one wave's lanes");
-template <u32 ROWB, u32 PTAB>
+template <u32 ROWB, u32 PTAB, u32 NSLAB = kMaxDigit>
 struct PlanLds {
   static constexpr u32 kRowBytes = ROWB, kPTab = PTAB;
   uint16_t rows[ROWB / 2];
   u32 ptab[PTAB];  // (wave emit) records of the slab (group) before each item's run
-  u32 nunit[kMaxDigit];
-  u32 utot[kMaxDigit];
-  uint8_t spanv[kMaxDigit];
+  u32 nunit[NSLAB];  // (indexed by the slab within the workgroup's range)
+  u32 utot[NSLAB];
+  uint8_t spanv[NSLAB];
   u32 ubase;
 };
 // The plan of bucket b by one workgroup of kPlanTPB threads. SC1: the bucket's off2 rows were written by
 // other workgroups of this launch (bin_fsort's fused plan, the last item of the bucket plans it), so
 // they are read with sc1 loads, as they were stored (the hand-off of the MI355X guide's sc1 table: each
 // storing workgroup waits for its stores, then adds to the bucket's counter; the last adder reads).
-template <bool SC1, typename PL>
+// The slabs [f_lo, f_hi) of the bucket (at most TPB of them, f_lo a multiple of 64: one slab per thread,
+// a wave's lanes on consecutive slabs); the plan launch splits a bucket of many slabs over several
+// workgroups, each taking its range of the unit list with one atomic.
+template <bool SC1, typename PL, int TPB>
 __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* __restrict__ T, const u32* __restrict__ Bb,
                                             const u32* __restrict__ Ib, const u32* off2, BinCtl* bc,
                                             uint4* __restrict__ units, uint2* __restrict__ runs, int group_on,
-                                            PL& L, u32 item) {
-  static_assert(kMaxDigit == kPlanTPB, "one slab per thread");
+                                            PL& L, u32 item, u32 f_lo, u32 f_hi) {
   uint16_t* const rows = L.rows;
   u32* const ptab = L.ptab;
   u32* const nunit = L.nunit;
@@ -1238,23 +1240,27 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   u32& ubase = L.ubase;
   const int tid = threadIdx.x;
   const u32 J = bucket_items(T[b], item), I = Ib[b], nf1 = g.nf + 1, bb = Bb[b];
-  const u32 jt = PL::kRowBytes / 2 / nf1;  // items per staged tile (>= 31 for nf <= 1024 at 64 KiB)
-  const u32 f = tid;                  // this thread's slab
+  // the staged rows hold this workgroup's columns only: slabs [f_lo, f_hi] (a run's end is the next
+  // slab's offset), nl u16 per item
+  const u32 nl = f_hi - f_lo + 1;
+  const u32 jt = PL::kRowBytes / 2 / nl;  // items per staged tile (>= 31 for 1024 slabs at 64 KiB)
+  const u32 f = f_lo + (u32)tid;      // this thread's slab
   auto stage = [&](u32 j0, u32 j1) {  // rows of items [j0, j1): every load of a round in flight together
-    const u32 nx = (j1 - j0) * nf1;
-    const u32* src = off2 + (size_t)(I + j0) * nf1;
+    const u32 nx = (j1 - j0) * nl;
+    const u32* src = off2 + (size_t)(I + j0) * nf1 + f_lo;
     constexpr int U = 8;
-    for (u32 x0 = 0; x0 < nx; x0 += kPlanTPB * U) {
+    for (u32 x0 = 0; x0 < nx; x0 += TPB * U) {
       uint16_t t[U];
 #pragma unroll
       for (int q = 0; q < U; ++q) {
-        const u32 x = x0 + q * kPlanTPB + tid;
-        const u32* ps = src + (x < nx ? x : nx - 1);
+        const u32 x = x0 + q * TPB + tid;
+        const u32 xx = x < nx ? x : nx - 1;
+        const u32* ps = src + (size_t)(xx / nl) * nf1 + xx % nl;
         t[q] = (uint16_t)(SC1 ? __hip_atomic_load(ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *ps);
       }
 #pragma unroll
       for (int q = 0; q < U; ++q) {
-        const u32 x = x0 + q * kPlanTPB + tid;
+        const u32 x = x0 + q * TPB + tid;
         if (x < nx) rows[x] = t[q];
       }
     }
@@ -1270,9 +1276,9 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
         stage(j0, j1);
         __syncthreads();
       }
-      if (f >= g.nf || span == 0) continue;
+      if (f >= f_hi || span == 0) continue;
       for (u32 j = j0; j < j1; ++j) {
-        const uint16_t* r = rows + (j - j0) * nf1 + f;
+        const uint16_t* r = rows + (j - j0) * nl + (f - f_lo);
         const u32 o0 = r[0];
         u32 c = (u32)r[span] - o0;
         u32 st = bb + j * item + o0;
@@ -1293,7 +1299,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
         }
       }
     }
-    if (f < g.nf && span && acc) {
+    if (f < f_hi && span && acc) {
       if (emit) units[base + nu] = make_uint4(b * g.nf + f, nr, acc, flags);
       ++nu;
     }
@@ -1307,18 +1313,19 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   // units are then written by lanes of one wave per slab (2 or 4 slabs per wave for <= 32 / 16 items),
   // a lane per item, so the run-table stores are contiguous (the per-thread walk stored one 8-byte run
   // per lane into 64 different run tables per instruction). Larger buckets take the walk.
-  const u32 ps = g.nf + 1;  // ptab row stride: +1 so the lanes of one slab's column hit different banks
+  // ptab row stride: this workgroup's slabs + 1 (so the lanes of one slab's column hit different banks)
+  const u32 ps = f_hi - f_lo + 1;
   const bool wave_emit = J <= 64u && J <= jt && J * ps <= PL::kPTab;  // block-uniform
   u32 h = 0, nu1 = 0;
   if (wave_emit) {
     stage(0, J);
     __syncthreads();
-    if (f < g.nf) {
-      const uint16_t* r = rows + f;
+    if (f < f_hi) {
+      const uint16_t* r = rows + (f - f_lo);
 #pragma unroll 8
       for (u32 j = 0; j < J; ++j) {
-        ptab[j * ps + f] = h;
-        h += (u32)r[j * nf1 + 1] - (u32)r[j * nf1];
+        ptab[j * ps + (f - f_lo)] = h;
+        h += (u32)r[j * nl + 1] - (u32)r[j * nl];
       }
     }
     nu1 = (h + kUnitCap - 1) / kUnitCap;
@@ -1329,7 +1336,7 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   // sparse neighbours: the largest aligned group (lanes f..f+gs-1 of one wave) within the caps
   u32 span = 1;
   if (group_on && J <= (u32)kRunMax) {
-    u32 s = f < g.nf ? h : 0u;
+    u32 s = f < f_hi ? h : 0u;
     for (u32 gs = 2; gs <= kGroupMax && gs <= g.nf; gs <<= 1) {
       s += __shfl_xor(s, (int)(gs >> 1));  // the sum over the aligned group of gs slabs
       if (s > 0 && s <= min(kGroupCap, gs * kGroupSlabAvg)) span = gs;
@@ -1339,22 +1346,22 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
   // (a group's units: at most one, exclusive; a single slab's: the cut above)
   const u32 nu = span > 1 ? 1u : span == 1 ? nu1 : 0u;  // a group (records > 0, <= kGroupCap): one unit
   u32 tot_f = h;
-  if (wave_emit && span > 1 && f < g.nf) {  // a group's leader: its column over the group's slabs
-    const uint16_t* r = rows + f;
+  if (wave_emit && span > 1 && f < f_hi) {  // a group's leader: its column over the group's slabs
+    const uint16_t* r = rows + (f - f_lo);
     tot_f = 0;
     for (u32 j = 0; j < J; ++j) {
-      ptab[j * ps + f] = tot_f;
-      tot_f += (u32)r[j * nf1 + span] - (u32)r[j * nf1];
+      ptab[j * ps + (f - f_lo)] = tot_f;
+      tot_f += (u32)r[j * nl + span] - (u32)r[j * nl];
     }
   }
-  if (f < g.nf) {
-    nunit[f] = nu;
-    spanv[f] = (uint8_t)span;
-    utot[f] = tot_f;
+  if (f < f_hi) {
+    nunit[f - f_lo] = nu;
+    spanv[f - f_lo] = (uint8_t)span;
+    utot[f - f_lo] = tot_f;
   }
   __syncthreads();
-  const u32 used = block_scan<kPlanTPB, 1>(g.nf, [&](u32 x) { return nunit[x]; },
-                                           [&](u32 x, u32 excl) { nunit[x] = excl; });
+  const u32 used = block_scan<TPB, 1>(f_hi - f_lo, [&](u32 x) { return nunit[x]; },
+                                      [&](u32 x, u32 excl) { nunit[x] = excl; });
   ph.mark(49);
   if (tid == 0) ubase = used ? atomicAdd(&bc->nunits, used) : 0u;
   __syncthreads();
@@ -1365,22 +1372,22 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
     const u32 lpw = 64u / spw, sub = lane / lpw, j = lane % lpw;
     const u64 gmask = lpw == 64u ? ~0ull : ((1ull << lpw) - 1ull) << (sub * lpw);
     const u64 below = (1ull << lane) - 1ull;
-    for (u32 f0 = (u32)(tid >> 6) * spw; f0 < g.nf; f0 += (kPlanTPB / 64) * spw) {
+    for (u32 f0 = f_lo + (u32)(tid >> 6) * spw; f0 < f_hi; f0 += (TPB / 64) * spw) {
       const u32 ff = f0 + sub;
       u32 sp = 0, base = 0, tot = 0;
-      if (ff < g.nf) {
-        sp = spanv[ff];
-        base = ubase + nunit[ff];
-        tot = utot[ff];
+      if (ff < f_hi) {
+        sp = spanv[ff - f_lo];
+        base = ubase + nunit[ff - f_lo];
+        tot = utot[ff - f_lo];
       }
       const bool on = sp != 0u && j < J;
       u32 c = 0, st = 0, P = 0;
       if (on) {  // this item's run of the slab (or of the group's slabs: fsort sorted the item by slab)
-        const uint16_t* r = rows + j * nf1 + ff;
+        const uint16_t* r = rows + j * nl + (ff - f_lo);
         const u32 o0 = r[0];
         c = (u32)r[sp] - o0;
         st = bb + j * item + o0;
-        P = ptab[j * ps + ff];
+        P = ptab[j * ps + (ff - f_lo)];
       }
       const u32 nus = sp == 0u ? 0u : sp > 1u ? 1u : (tot + kUnitCap - 1) / kUnitCap;
       const u32 fl = sp > 1u ? (kUnitExcl | kUnitGroup) : (nus == 1u ? kUnitExcl : 0u);
@@ -1397,19 +1404,23 @@ __device__ __forceinline__ void plan_bucket(u32 b, const BinGeom& g, const u32* 
     }
   } else {
     const u32 flags = span > 1 ? (kUnitExcl | kUnitGroup) : (nu == 1 ? kUnitExcl : 0u);
-    walk(true, ubase + (f < g.nf ? nunit[f] : 0u), flags, span, nullptr);
+    walk(true, ubase + (f < f_hi ? nunit[f - f_lo] : 0u), flags, span, nullptr);
   }
   __syncthreads();
   ph.mark(51);
   ph.flush(4);
 }
 
+// The plan launch: one workgroup of kPlanTPB threads per bucket, a slab per thread. (Split over
+// 256-slab ranges, four workgroups per bucket of 512 slabs with lighter LDS, it measured no faster:
+// cfg3 1.033 -> 1.047 ms, cfg4b 2.170 -> 2.164, profiles/r06/ab_plan_split.txt.)
 __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32* __restrict__ T, const u32* __restrict__ Bb,
                                                             const u32* __restrict__ Ib, const u32* __restrict__ off2,
                                                             BinCtl* bc, uint4* __restrict__ units, uint2* __restrict__ runs,
                                                             int group_on, u32 item) {
-  __shared__ PlanLds<kPlanLds, kPlanPTab> L;
-  plan_bucket<false>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item);
+  typedef PlanLds<kPlanLds, kPlanPTab> PL;
+  __shared__ PL L;
+  plan_bucket<false, PL, kPlanTPB>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item, 0u, g.nf);
 }
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
@@ -1460,7 +1471,8 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(kSPer <= 
     if (tid == 0) last_flag = atomicAdd(&done[b], 1u) + 1u == bucket_items(T[b], item);
     __syncthreads();
     if (last_flag)
-      plan_bucket<true>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, *reinterpret_cast<FusedPlanLds*>(smem), item);
+      plan_bucket<true, FusedPlanLds, kSTPB>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on,
+                                             *reinterpret_cast<FusedPlanLds*>(smem), item, 0u, g.nf);
   };
   for (u32 f = tid; f < g.nf; f += kSTPB) hist[f] = 0;
   if (s1 == s0) {  // an empty bucket's one item
