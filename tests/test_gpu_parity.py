@@ -726,7 +726,7 @@ def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
         with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
             sh.update(bad, vals, unordered=True)
         assert ei.value.record == 1234
-    monkeypatch.setenv("GLINT_BINNED", "0")
+    monkeypatch.setenv("GLINT_BINNED", "0")  # never bin
     N.reload_env()
     with PartialVector(part, "long", gpu) as sh:
         lib.glint_prof_enable(sh.handle, 1)
@@ -735,6 +735,18 @@ def test_binned_adaptive_switch_and_errors(gpu, monkeypatch):
         ms, cnt = C.c_double(), C.c_int64()
         lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
         assert cnt.value == 0
+    monkeypatch.setenv("GLINT_BINNED", "1")  # bin every large push, the first one (no history) too
+    N.reload_env()
+    ref = oracle_vec(part, "long")
+    with PartialVector(part, "long", gpu) as sh:
+        lib.glint_prof_enable(sh.handle, 1)
+        for i in range(2):
+            sh.update(keys, vals)
+            assert ref.update(keys, vals) == -1
+            ms, cnt = C.c_double(), C.c_int64()
+            lib.glint_prof_read(sh.handle, N.GLINT_K_PUSH_BINNED, C.byref(ms), C.byref(cnt))
+            assert cnt.value == i + 1
+        np.testing.assert_array_equal(sh.to_numpy(), ref.data)
 
 
 def test_binned_switch_density_floor(gpu, monkeypatch):

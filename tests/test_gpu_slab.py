@@ -210,3 +210,37 @@ def test_set_push_rejects_bad_sets(gpu):
     slab.destroy()
     for s in (a, b, c, m, d):
         s.destroy()
+
+
+def test_set_push_on_two_streams_keeps_each_verdict(gpu):
+    """Two pushes over the same shard set on two streams, enqueued back to back so their kernels may
+    overlap: each call's verdict lives in a word of its own stream (the set's first shard keeps one per
+    caller stream), so the clean batch is applied and reports 0 while the batch with a bad key reports
+    it and applies nothing. (With one shared word, one call's zeroing could clear the other's verdict
+    and its scatter would then apply a rejected batch.) Repeated, alternating which stream goes first."""
+    dev = torch.device("cuda", gpu)
+    ranges = [(0, 1 << 20), (1 << 20, 3 << 19)]
+    shards = [PartialVector(RangePartition(i, a, b), "long", gpu) for i, (a, b) in enumerate(ranges)]
+    rng = np.random.default_rng(17)
+    k = torch.from_numpy(rng.integers(0, 3 << 19, 1 << 20).astype(np.int64)).to(dev)
+    v = torch.from_numpy(rng.integers(-9, 9, k.numel()).astype(np.int64)).to(dev)
+    kb = k.clone()
+    kb[-1] = 3 << 19  # past the last shard
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    g1 = torch.full((1,), 3, dtype=torch.int64, device=dev)
+    g2 = torch.full((1,), 3, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    want = np.zeros(3 << 19, np.int64)
+    for rep in range(4):
+        order = [(s1, kb, g1), (s2, k, g2)] if rep % 2 else [(s2, k, g2), (s1, kb, g1)]
+        for st, keys, gate in order:
+            with torch.cuda.stream(st):
+                assert _set_push(shards, keys, v, gate) == 0
+        torch.cuda.synchronize(dev)
+        assert int(g1.item()) == ~(k.numel() - 1) and int(g2.item()) == 0, rep
+        np.add.at(want, k.cpu().numpy(), v.cpu().numpy())
+    for sh, (a, b) in zip(shards, ranges):
+        sh.sync(torch.cuda.current_stream(dev).cuda_stream)
+        np.testing.assert_array_equal(sh.get(torch.arange(a, b, device=dev)).cpu().numpy(), want[a:b])
+    for sh in shards:
+        sh.destroy()
