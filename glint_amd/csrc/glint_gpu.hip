@@ -563,17 +563,11 @@ __global__ void push_validate_gate_kernel(LaunchCtl* ctl, u64* gate) {
 // pulls
 // ------------------------------------------------------------------------------------------------
 // PartialVector.get (PartialVector.scala:51-60): out[i] = data(globalToLocal(keys(i)))
-// PAIRS: records [2 * p_begin, min(n, 2 * p_end)) (a large pull runs one launch per window). Each lane
-// takes kPullUnroll pairs per iteration: every key load, then every gather, then every store, so a
-// lane's gathers are in flight together instead of one dependent key -> element round trip at a time.
-#ifndef GLINT_PULL_UNROLL
-#define GLINT_PULL_UNROLL 1
-#endif
-#ifndef GLINT_PULL_BPC
-#define GLINT_PULL_BPC 4
-#endif
-constexpr int kPullUnroll = GLINT_PULL_UNROLL;
-constexpr int kPullBlocksPerCu = GLINT_PULL_BPC;
+// PAIRS: records [2 * p_begin, min(n, 2 * p_end)) (a large pull runs one launch per window), one pair
+// per lane per iteration at 4 blocks per CU. (2 or 4 pairs per lane per iteration -- every key load,
+// then every gather, then every store -- and 1 / 2 / 8 blocks per CU all measured slower:
+// profiles/r06/ab_pull_unroll.txt.)
+constexpr int kPullBlocksPerCu = 4;
 template <typename V>
 __device__ __forceinline__ typename Vec2<V>::T pull_pair(const K2& k, const V* data, const PartDesc& part, ErrState* err,
                                                          i64 r) {
@@ -587,41 +581,32 @@ __device__ __forceinline__ typename Vec2<V>::T pull_pair(const K2& k, const V* d
   if (!o1) record_error(err, r + 1);
   return as2<V>(o0 ? data[l0] : V(0), o1 ? data[l1] : V(0));
 }
+// the gather of record pairs [p_begin, p_end), grid-stride over the first `blocks` blocks
+template <typename V>
+__device__ __forceinline__ void pull_pairs(const i64* keys, i64 n, const V* data, const PartDesc& part, V* out,
+                                           ErrState* err, i64 p_begin, i64 p_end, i64 blocks) {
+  typedef typename Vec2<V>::T V2;
+  const i64 stride = blocks * kTPB;
+  for (i64 p = p_begin + (i64)blockIdx.x * kTPB + threadIdx.x; p < p_end; p += stride) {
+    const i64 r = 2 * p;
+    if (r + 1 < n) {
+      const K2 k = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p);
+      __builtin_nontemporal_store(pull_pair<V>(k, data, part, err, r), reinterpret_cast<V2*>(out + r));
+    } else {
+      i64 l0;
+      const bool o0 = rec_addr<false>(part, keys[r], 0, l0);
+      if (!o0) record_error(err, r);
+      out[r] = o0 ? data[l0] : V(0);
+    }
+  }
+}
+
 template <typename V, bool PAIRS>
 __global__ __launch_bounds__(kTPB) void vec_pull_kernel(const i64* keys, i64 n, const V* data, PartDesc part,
                                                         V* out, ErrState* err, MsgSig sig, i64 p_begin, i64 p_end) {
-  typedef typename Vec2<V>::T V2;
   const i64 stride = (i64)gridDim.x * kTPB;
   if (PAIRS) {
-    const i64 npairs = p_end;
-    i64 p = p_begin + (i64)blockIdx.x * kTPB + threadIdx.x;
-    if (kPullUnroll > 1) {
-      const i64 pfull = min(npairs, n >> 1);  // pairs with both records
-      for (; p + (kPullUnroll - 1) * stride < pfull; p += kPullUnroll * stride) {
-        K2 k[kPullUnroll];
-        V2 o[kPullUnroll];
-#pragma unroll
-        for (int u = 0; u < kPullUnroll; ++u)
-          k[u] = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p + u * stride);
-#pragma unroll
-        for (int u = 0; u < kPullUnroll; ++u) o[u] = pull_pair<V>(k[u], data, part, err, 2 * (p + u * stride));
-#pragma unroll
-        for (int u = 0; u < kPullUnroll; ++u)
-          __builtin_nontemporal_store(o[u], reinterpret_cast<V2*>(out + 2 * (p + u * stride)));
-      }
-    }
-    for (; p < npairs; p += stride) {
-      const i64 r = 2 * p;
-      if (r + 1 < n) {
-        const K2 k = __builtin_nontemporal_load(reinterpret_cast<const K2*>(keys) + p);
-        __builtin_nontemporal_store(pull_pair<V>(k, data, part, err, r), reinterpret_cast<V2*>(out + r));
-      } else {
-        i64 l0;
-        const bool o0 = rec_addr<false>(part, keys[r], 0, l0);
-        if (!o0) record_error(err, r);
-        out[r] = o0 ? data[l0] : V(0);
-      }
-    }
+    pull_pairs<V>(keys, n, data, part, out, err, p_begin, p_end, gridDim.x);
   } else {
     for (i64 i = (i64)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
       i64 l;
@@ -947,7 +932,10 @@ int launch_push(glint_shard* s, const i64* keys, const int32_t* cols, const void
 }
 
 // ---- pulls ------------------------------------------------------------------------------------
-// A ring launch (s->sig.done set) is one workgroup that signals its own completion.
+// A ring launch (s->sig.done set) is one workgroup that signals its own completion. (A dense pull
+// checked first -- a key pass flagging any record off one run, then a 16-B streaming copy of the run --
+// measured no faster than the gather, which is itself a dense stream for such keys: 1.006-1.054 against
+// 0.992-1.044 ms kernel time at 2^28, profiles/r06/ab_pull_checked.txt.)
 template <typename V>
 int launch_vec_pull(glint_shard* s, const i64* keys, void* out, i64 n, hipStream_t st) {
   if (n <= 0) return GLINT_OK;

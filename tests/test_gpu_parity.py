@@ -1116,3 +1116,51 @@ def test_loopback_client_bucketing_offloaded(gpu):
         assert out["groupby"]["push_messages"] == out[mode]["push_messages"]
         assert out["groupby"]["pull_messages"] == out[mode]["pull_messages"]
     assert out["device"]["device_batches"] == 2 * 64 and 0 < out["auto"]["device_batches"] <= 2 * 64
+
+
+@pytest.mark.parametrize("dtype", ["long", "double", "float", "int"])
+def test_large_pull_shapes(gpu, dtype):
+    """Large aligned pulls (>= 2^20 records, the windowed gather of record pairs) in the shapes a dense
+    stream and its edges take, against the oracle's get: an even and an odd first element (16-B element
+    pairs or two 8-B loads), an odd record count (the last record alone), a run broken in the middle and
+    at its end, a key out of range (raises with its record, the rest answered), repeated pulls, and a
+    cyclic layout whose keys are one dense run of elements."""
+    import torch
+    from glint_amd import CyclicPartition
+    d = torch.device("cuda", gpu)
+    rng = np.random.default_rng(61)
+    size = (1 << 21) + 77
+    part = RangePartition(2, 1000, 1000 + size)
+    vals = rand_vals(rng, dtype, size)
+    ref = oracle_vec(part, dtype)
+    allk = np.arange(1000, 1000 + size, dtype=np.int64)
+    assert ref.update(allk, vals) == -1
+    with PartialVector(part, dtype, gpu) as sh:
+        sh.update(allk, vals)
+        cases = [allk[:1 << 20], allk[1:(1 << 20) + 2], allk[3:(1 << 21) + 3], allk[5:]]
+        broken = allk[:1 << 21].copy()
+        broken[777_777] = broken[5]
+        cases.append(broken)
+        end = allk[:(1 << 20) + 1].copy()
+        end[-1] = allk[0]
+        cases.append(end)
+        for k in cases + cases[:2]:
+            got = sh.get(torch.from_numpy(k).to(d)).cpu().numpy()
+            want, bad = ref.get(k)
+            assert bad == -1
+            np.testing.assert_array_equal(got, want)
+        out_of_range = allk[:1 << 20].copy()
+        out_of_range[123_456] = 1000 + size + 3
+        with pytest.raises(ArrayIndexOutOfBoundsException) as ei:
+            sh.get(torch.from_numpy(out_of_range).to(d))
+        assert ei.value.record == 123_456
+        got = sh.get(torch.from_numpy(allk[:1 << 20]).to(d)).cpu().numpy()  # the shard and the flags unharmed
+        np.testing.assert_array_equal(got, ref.get(allk[:1 << 20])[0])
+    cpart = CyclicPartition(1, 3, 3 * (1 << 20))  # keys 1, 4, 7, ...: one dense run of elements
+    cref = oracle_vec(cpart, dtype)
+    ck = np.arange(1, 3 * (1 << 20), 3, dtype=np.int64)
+    cv = rand_vals(rng, dtype, ck.size)
+    assert cref.update(ck, cv) == -1
+    with PartialVector(cpart, dtype, gpu) as sh:
+        sh.update(ck, cv)
+        np.testing.assert_array_equal(sh.get(torch.from_numpy(ck).to(d)).cpu().numpy(), cref.get(ck)[0])
