@@ -24,6 +24,7 @@ set -o pipefail
 TAG=${TAG:-r06}
 R=$(pwd)
 OUT=$R/gpurun_out/$TAG
+[ -n "$GLINT_GPU_LIB" ] && export GLINT_GPU_LIB=$(realpath "$GLINT_GPU_LIB")  # (kstats / pmc run from /tmp)
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() {  # step <name> <seconds> <command...>: output to $OUT/<name>.log
@@ -115,31 +116,6 @@ for s in ${STAGES:-tests bench}; do
     phases)  # phase clocks of the binned kernels (tools/bin_phases.py, a -DGLINT_BIN_PROF build)
       step bin_phases 300 python3 tools/bin_phases.py
       ;;
-    mps8ab)  # the exchange line with 8 local partitions: local pushes on one stream / on a stream per shard
-      for r in 1 2; do
-        step mps8_seq_$r 300 env GLINT_DIST_STREAMS=0 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
-        step mps8_par_$r 300 python3 bench.py --no-cpu-baseline --pattern exchange --parts-per-gpu 8
-      done
-      ;;
-    mps8lw)  # the exchange line with 8 local partitions: bin_apply's whole-line write-back on (1) / off (0)
-      for r in 1 2; do
-        for v in 1 0; do
-          step mps8lw_${v}_$r 300 env GLINT_BIN_LINE_WB=$v python3 bench.py --no-cpu-baseline --no-north-star --pattern exchange --parts-per-gpu 8
-        done
-      done
-      ;;
-    lbsleep)  # the cfg4 loopback rows with the GPU servers' waits sleeping (GLINT_WAIT_SLEEP_US) or yielding
-      LB=tools/loopback/build/glint_loopback
-      G="--backend gpu --lib glint_amd/lib/libglint_gpu.so"
-      i=0
-      for args in "--clients 64 --servers 8 --keys 33554432" \
-                  "--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"; do
-        for r in $(seq ${ROUNDS:-2}); do
-          for us in 0 ${SLEEPS:-10 50}; do step lbs_${i}_${us}_$r 200 env GLINT_WAIT_SLEEP_US=$us $LB $G $args; done
-        done
-        i=$((i + 1))
-      done
-      ;;
     lbcpu)  # the cfg4 loopback rows with the process / server-call CPU time (--cpu-stats), both backends
       LB=tools/loopback/build/glint_loopback
       i=0
@@ -169,21 +145,6 @@ for s in ${STAGES:-tests bench}; do
         i=$((i + 1))
       done
       cat $OUT/lba_*.log | grep '^{' > $OUT/loopback_actor.jsonl || true
-      ;;
-    lbspin)  # cfg4b pulls under the thread-per-connection harness with the shard lock tried before blocking
-             # (GLINT_LOCK_SPIN) and without, then cfg1 under the actor model; the CPU loop beside each
-      LB=tools/loopback/build/glint_loopback
-      A4="--clients 64 --servers 8 --keys 33554432 --pattern uniform --records 524288 --dtype long"
-      for r in $(seq ${ROUNDS:-2}); do
-        for sp in 0 ${SPINS:-200 2000}; do
-          step lbspin_${sp}_$r 200 env GLINT_LOCK_SPIN=$sp $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so $A4 --cpu-stats
-        done
-        step lbspin_oracle_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so $A4 --cpu-stats
-        step lbactor1_gpu_$r 200 $LB --backend gpu --lib glint_amd/lib/libglint_gpu.so --server actor --answers direct --cpu-stats
-        step lbactor1_oracle_$r 200 $LB --backend oracle --lib oracle/build/libglint_oracle.so --server actor --cpu-stats
-      done
-      cat $OUT/lbspin_*.log | grep '^{' > $OUT/loopback_lockspin.jsonl || true
-      cat $OUT/lbactor1_*.log | grep '^{' > $OUT/loopback_actor_cfg1.jsonl || true
       ;;
     bintests)
       step pytest_binned 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread \
@@ -217,14 +178,6 @@ for s in ${STAGES:-tests bench}; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_det -o run \
          -- python3 $R/tools/det_probe.py > $OUT/prof_det.log 2>&1) || { tail -30 $OUT/prof_det.log >&2; exit 1; }
       find /tmp/prof_det -name "*kernel_stats.csv" -exec cp {} $OUT/kstats_det.csv \;
-      ;;
-    win)  # the dense push by sweep window (GLINT_SWEEP_WINDOW = log2 records; 0 = one launch)
-      for w in ${WINDOWS:-0 24 25 26 27}; do
-        step win_$w 300 env GLINT_SWEEP_WINDOW=$w python3 bench.py --no-cpu-baseline
-      done
-      ;;
-    pullwin)
-      for w in 0 26; do step pullwin_$w 300 env GLINT_SWEEP_WINDOW=$w python3 bench.py --no-cpu-baseline --pattern pull; done
       ;;
     micro)
       step micro_stream_2p30 300 tools/microbench_stream 30 9 6
