@@ -1427,7 +1427,7 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
 // (plan_bucket<true>), so no plan launch follows and the buckets' plans overlap the other items' sorts.
 constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
 template <typename A, bool FUSED, int kSPer>
-__global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(kSPer <= 8 ? 8 : 4))) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
+__global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
                                                           const u32* __restrict__ T, const u32* __restrict__ Bb,
                                                           const u32* __restrict__ addr_in, const A* __restrict__ val_in,
                                                           uint16_t* __restrict__ e_out, A* __restrict__ v_out,
@@ -1486,15 +1486,19 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(kSPer <= 
   // without touching memory, a store at the window's end is dropped (counted stores, see BufOut)
   const u32 cnt = s1 - s0;
   const BufOut ain = buf_out(addr_in + s0, cnt * 4u), vin = buf_out(val_in + s0, cnt * (u32)sizeof(A));
+  // (kLate: the values are loaded only in their staging rounds, not held through the ranking -- the
+  // registers of 16 records per thread then fit two workgroups per CU; cfg5 0.3118 -> 0.3073 ms,
+  // profiles/r06/ab_fsort_late.txt)
+  constexpr bool kLate = kSPer > 8;
   u32 a[kSPer];
-  A v[kSPer];
+  A v[kLate ? 1 : kSPer];
 #pragma unroll
   for (int q = 0; q < kSPer; ++q) {  // branch-free: the whole item in flight at once
     const u32 x = q * kSTPB + tid;
     if ((u32)q * kSTPB < item) {  // launch-uniform (an item of fewer records than the registers hold)
       a[q] = bget<u32>(ain, x * 4u);
-      v[q] = bget<A>(vin, x * (u32)sizeof(A));
-    } else {
+      if constexpr (!kLate) v[q] = bget<A>(vin, x * (u32)sizeof(A));
+    } else if constexpr (!kLate) {
       v[q] = A(0);
     }
     if (x >= cnt || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
@@ -1536,9 +1540,28 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(kSPer <= 
   ph.mark(35);
   A* const stv = reinterpret_cast<A*>(stage);
   for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
+    if constexpr (kLate) {
 #pragma unroll
-    for (int q = 0; q < kSPer; ++q)
-      if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
+      for (int q0 = 0; q0 < kSPer; q0 += 4) {  // four loads in flight per thread, then their LDS stores
+        A lv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = q0 + k;
+          lv[k] = A(0);
+          if ((u32)q * kSTPB < item && p[q] != kEmptySlot && p[q] - r0 < kStageV)
+            lv[k] = bget<A>(vin, (q * kSTPB + tid) * (u32)sizeof(A));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = q0 + k;
+          if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = lv[k];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kSPer; ++q)
+        if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
+    }
     __syncthreads();
     constexpr int kRound = (int)(kStageV / kSTPB);
 #pragma unroll
