@@ -1153,17 +1153,18 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 #ifndef GLINT_FSORT_TPB
 #define GLINT_FSORT_TPB 1024
 #endif
-// Records per thread of a fine item, by push size: a small push (at most ~4 items per CU, cfg5) sorts
-// items of 16 per thread at one workgroup per CU (fewer, longer runs per slab for the apply); a large one
-// items of 8 per thread at two workgroups per CU (register budget 64), so one workgroup's loads are in
-// flight while the other ranks and stores (build-time knobs GLINT_FSORT_PER_SMALL / _LARGE). Same box
-// (profiles/r06/ab_nt_mid.txt, s16 = 16 per thread for every push): cfg4b 2.28 -> 2.20 ms, cfg3 1.055 ->
-// 1.046; for cfg5 8 per thread measured 0.336 against 0.318 ms (ab_part_fsort_variants.txt, f8)
+// Records per thread of a fine item: 16 for every push (items of 16384 records: fewer, longer runs per
+// slab for the apply and half the plan's rows of 8 per thread), at two workgroups per CU -- the values
+// are loaded only in their staging rounds (kLate in bin_fsort_kernel), so one workgroup's loads are in
+// flight while the other ranks and stores. Same box, 16 against 8 per thread for large pushes
+// (profiles/r06/ab_fsort_per16.txt): cfg4b 2.170 -> 2.139 ms, cfg3 1.039 -> 1.030 (held in registers
+// at one workgroup per CU, 16 had measured slower: ab_nt_mid.txt s16). Build-time knobs
+// GLINT_FSORT_PER_SMALL / _LARGE (small: the pushes with the plan fused in, see push_binned).
 #ifndef GLINT_FSORT_PER_SMALL
 #define GLINT_FSORT_PER_SMALL 16
 #endif
 #ifndef GLINT_FSORT_PER_LARGE
-#define GLINT_FSORT_PER_LARGE 8
+#define GLINT_FSORT_PER_LARGE 16
 #endif
 constexpr int kSTPB = GLINT_FSORT_TPB;
 constexpr int kSPerSmall = GLINT_FSORT_PER_SMALL, kSPerLarge = GLINT_FSORT_PER_LARGE;
@@ -2130,7 +2131,8 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   // stores before counting itself in costs more: cfg3 1.067 -> 1.078, cfg4b 2.375 -> 2.44 ms, cfg5
   // 0.347 -> 0.335 (profiles/r05/ab_fused_plan.txt)
   // (fused for every push, with the fine sort at two workgroups per CU: cfg4b 2.15 -> 2.50 ms, cfg3 1.02
-  // -> 1.04, profiles/r06/ab_fuse_all.txt)
+  // -> 1.04, profiles/r06/ab_fuse_all.txt; again with 16-record items at two per CU: cfg4b 2.14 -> 2.35,
+  // cfg3 1.029 -> 1.028)
   const bool fused = small_push;
   u64* const bhint = s->d_hint ? s->d_hint + 1 : nullptr;
   u64* const whint = whole_next ? s->d_hint : nullptr;
