@@ -69,7 +69,6 @@ constexpr int kPartWgPerCuDedup = kATPB == 1024 ? 1 : 2;
 constexpr int kPartAhead = GLINT_PART_AHEAD;  // partition chunks in flight per workgroup (build-time knob)
 constexpr int kPartWgPerCuPlain = GLINT_PART_WPC;  // what fits (VGPRs): a second round of
                                                            // workgroups measured 3-9 % slower
-constexpr int kMaxSegs = 1024;         // partition workgroups at most
 #ifndef GLINT_APPLY_TPB
 #define GLINT_APPLY_TPB 256
 #endif
@@ -92,6 +91,8 @@ struct BinCtl {
   u32 cold;    // valid records that were not hot (the dedup front end's input; m for the others)
   u32 nunits;  // apply units written by bin_plan (each bucket takes its range with one atomic)
   u32 disorder;  // a whole-push bin (no push_check): some wave saw two adjacent records out of order
+  u32 rbase;   // bin_scan: records of the buckets placed so far (each bucket takes its range with one atomic)
+  u32 nch;     // bin_scan: partition chunks of the tail
 };
 
 // Phase timing for tuning (tools/bin_phases.py): built with -DGLINT_BIN_PROF, thread 0 of every
@@ -209,18 +210,6 @@ struct RecOut {
   BufOut b;
   __device__ __forceinline__ void put(u32 rel, bool on, T v) const { bput(b, rel * (u32)sizeof(T), on, v); }
 };
-// The same for a push whose buffers pass 4 GiB (a window offset is 32 bits): plain 64-bit-addressed
-// stores, and a lane with nothing to store writes its own slot of a dump area instead, so every path
-// still issues one store per call.
-template <typename T>
-struct WideOut {
-  T* base;
-  T* dump;  // >= 64 elements, never read
-  __device__ __forceinline__ void put(u32 rel, bool on, T v) const {
-    T* const p = on ? base + rel : dump + (threadIdx.x & 63);
-    *p = v;
-  }
-};
 struct BadRecs {  // this thread's rejected records: the first one and how many
   i64 first = -1;
   u32 count = 0;
@@ -306,6 +295,19 @@ __device__ __forceinline__ u32 block_sum(u32 x) {
   return t;
 }
 
+template <int TPB>
+__device__ __forceinline__ u32 block_max(u32 x) {
+  __shared__ u32 wm[TPB / 64];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x = max(x, (u32)__shfl_xor(x, d));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = x;
+  __syncthreads();
+  u32 m = 0;
+  for (int w = 0; w < TPB / 64; ++w) m = max(m, wm[w]);
+  __syncthreads();
+  return m;
+}
+
 // from_break: 0 the whole push; 1 from push_check's break; 2 the whole push unless its gate cancelled it
 // (a validating whole-push bin: the kernels after its verdict see an empty tail, as a cancelled break)
 __device__ __forceinline__ i64 tail_start(const LaunchCtl* lctl, u32 ntiles, int from_break, i64 n) {
@@ -338,11 +340,6 @@ __device__ __forceinline__ void load_recs(const i64* __restrict__ keys, const in
   }
 }
 
-#ifndef GLINT_COUNT_AHEAD
-#define GLINT_COUNT_AHEAD 2
-#endif
-constexpr int kCountAhead = GLINT_COUNT_AHEAD;  // bin_count: chunks in flight per workgroup
-// ---- bin_count ----------------------------------------------------------------------------------------
 // KIND: the partition layout (0 range, -1 read at run time), as push_check is specialised
 __device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
   x ^= x >> 16;
@@ -353,132 +350,8 @@ __device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
   return x;
 }
 
-// Roff[w][b] = where workgroup w's records of bucket b start inside the bucket (the value its add to
-// T[b] returned), so every bucket is one contiguous range of the partition buffer; and with hot_best
-// the push's hot elements are not counted (the hot front end sums them in LDS), so the counts are
-// exact and the buffer has no holes.
 constexpr int kWideSlots = 8192;  // the plain + hot front end's hot table (see bin_hot_select)
 __device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
-// VALIDATE (a validating gated push, GLINT_PUSH_VALIDATE, whose tail is binned): the count also checks
-// every tail record -- the key itself in the partition's key range, as key_in_part -- and records the
-// first rejected one in the push's LaunchCtl (vctl->bad), as push_check does for the records before the
-// break; the push's verdict and cancel come after this kernel (push_validate_gate_binned_kernel), so the
-// keys are read once instead of by push_check and here.
-template <bool MAT, int KIND, bool VALIDATE = false, int PER = kAPer>
-__global__ __launch_bounds__(kATPB) void bin_count_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
-                                                          i64 n, PartDesc part, const LaunchCtl* lctl, u32 ntiles,
-                                                          int from_break, BinGeom g, u32* __restrict__ T,
-                                                          u32* __restrict__ R, BinCtl* bc, u32* __restrict__ Roff,
-                                                          const unsigned long long* __restrict__ hot_best,
-                                                          BinCtl* next_bc, u32* __restrict__ next_T,
-                                                          LaunchCtl* vctl = nullptr, LaunchCtl* next_ctl = nullptr) {
-  constexpr int kCopies = 4;  // histogram copies (wave % 4): fewer LDS atomics on one hot bucket
-  __shared__ u32 h[kCopies * kMaxDigit];
-  __shared__ u32 htag[kWideSlots];
-  const int tid = threadIdx.x;
-  const u32 hc = (u32)((tid >> 6) % kCopies) * g.nb;
-  constexpr int kChunk = kATPB * PER;  // records per chunk (the partition's, front end by front end)
-  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
-  for (u32 b = tid; b < kCopies * g.nb; b += kATPB) h[b] = 0;
-  if (blockIdx.x == 0) {  // the next push's header (the previous push used it; it is done)
-    for (u32 b = tid; b < g.nb; b += kATPB) {
-      next_T[b] = 0;
-      next_T[kMaxDigit + b] = 0;  // the fused plan's per-bucket item counters (push_binned_v2's header)
-    }
-    if (tid < (int)(sizeof(BinCtl) / 4)) reinterpret_cast<u32*>(next_bc)[tid] = 0;
-    if (next_ctl && tid == 0) {  // a whole-push bin runs no push_check: the next push's control words, as it zeroes them
-      next_ctl->brk_enc = 0u;
-      next_ctl->nonaffine = 0u;
-      next_ctl->cancel = 0u;
-      next_ctl->bad = 0ull;
-    }
-  }
-  if (hot_best)
-    for (int sl = tid; sl < kWideSlots; sl += kATPB) {
-      const unsigned long long x = hot_best[sl];
-      htag[sl] = x ? (u32)x : kEmptySlot;
-    }
-  __syncthreads();
-  const i64 nchunks = (n - r0 + kChunk - 1) / kChunk;
-  const i64 G = gridDim.x;
-  u32 nvalid = 0;
-  bool dis = false;  // (a whole-push bin) two adjacent records of one wave out of order
-  // keys (and cols) only: load_recs reads no values here. Two chunks in flight per workgroup (the
-  // partition grid is one 1024-thread workgroup per CU). Every step issues its loads unconditionally
-  // (chunk index clamped; a step past the end counts nothing), so the compiler can wait for one
-  // chunk's loads while the next chunk's stay in flight: with conditional loads it waited vmcnt(0).
-  BadRecs bad;
-  auto load = [&](i64 c, RecRegs<double, MAT, PER>& r) {
-    const i64 cc = min(c, nchunks - 1);
-    if constexpr (KIND == 0 && !VALIDATE) {
-      // the range layout reads only the key's low word ((key - start).toInt): loading the whole key
-      // left its high half dead, the compiler reused that register while the load was in flight and
-      // had to wait for it (vmcnt(0)), so only one chunk was ever in flight
-      const i64 c0 = r0 + cc * kChunk, c1 = min(n, c0 + kChunk);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const i64 i = c0 + q * kATPB + threadIdx.x;
-        const i64 ii = i < c1 ? i : c1 - 1;
-        r.k[q] = (i64)(u64)ld_in(reinterpret_cast<const u32*>(keys) + 2 * ii);
-        r.cl[q] = MAT ? ld_in(cols + ii) : 0;
-      }
-    } else {
-      load_recs<double, MAT, false, PER>(keys, cols, nullptr, r0 + cc * kChunk, min(n, r0 + (cc + 1) * kChunk), r);
-    }
-  };
-  auto step = [&](i64 c, RecRegs<double, MAT, PER>& r) {
-    const i64 c0 = r0 + c * kChunk, c1 = c < nchunks ? min(n, c0 + kChunk) : c0;
-    u32 bk[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      i64 ad;
-      const bool in = c0 + q * kATPB + tid < c1;
-      bool ok = in && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], ad);
-      if constexpr (VALIDATE) {
-        ok = ok && key_in_part<KIND>(part, r.k[q]);
-        if (in && !ok) bad.add(c0 + q * kATPB + tid);
-      }
-      bk[q] = ok && !(hot_best && htag[wide_slot((u32)ad)] == (u32)ad) ? bucket_of((u32)ad, g) : kEmptySlot;
-      if (next_ctl && q == 0) {  // a wave's records are consecutive: are they strictly increasing? (one
-        // record per thread per chunk is sample enough: an unordered push shows it in every wave, a sorted
-        // one nowhere; a record before this one is in the push whenever this one is)
-        const u32 a32 = ok ? (u32)ad : 0xFFFFFFFFu, prev = __shfl_up(a32, 1);
-        dis = dis || (in && (!ok || ((threadIdx.x & 63) && prev >= a32)));
-      }
-    }
-    load(c + kCountAhead * G, r);  // kCountAhead chunks ahead, into the registers just consumed
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      if (bk[q] != kEmptySlot) {
-        atomicAdd(&h[hc + bk[q]], 1u);
-        ++nvalid;
-      }
-    }
-  };
-  if ((i64)blockIdx.x < nchunks) {
-    RecRegs<double, MAT, PER> r[kCountAhead];
-    i64 c = blockIdx.x;
-#pragma unroll
-    for (int j = 0; j < kCountAhead; ++j) load(c + j * G, r[j]);
-    for (; c < nchunks; c += kCountAhead * G) {
-#pragma unroll
-      for (int j = 0; j < kCountAhead; ++j) step(c + j * G, r[j]);
-    }
-  }
-  __syncthreads();
-  for (u32 b = tid; b < g.nb; b += kATPB) {
-    u32 x = 0;
-#pragma unroll
-    for (int cpy = 0; cpy < kCopies; ++cpy) x += h[cpy * g.nb + b];
-    R[blockIdx.x * g.nb + b] = x;
-    Roff[blockIdx.x * g.nb + b] = x ? atomicAdd(&T[b], x) : 0u;
-  }
-  const u32 tot = block_sum<kATPB>(nvalid);
-  if (tid == 0 && tot) atomicAdd(&bc->tail, tot);
-  if (next_ctl && __syncthreads_or(dis) && tid == 0) atomicOr(&bc->disorder, 1u);
-  if (VALIDATE && bad.count) atomicMax(&vctl->bad, ~(u64)bad.first);  // rare: one atomic per thread
-}
-
 // The verdict of a validating gated push whose tail is binned (after bin_count validated the tail and
 // push_check the records before the break): 0 or ~(first rejected record) to the caller's gate word; a
 // rejected batch is cancelled before anything is applied -- no head (push_apply sees cancel), no tail
@@ -596,13 +469,17 @@ __device__ __forceinline__ void hot_flush(long long* p, long long x) { gadd(p, x
 __device__ __forceinline__ void hot_flush(int* p, int x) { gadd(p, x); }
 
 // ---- bin_part -------------------------------------------------------------------------------------
-// Appends a chunk's records (P per thread in registers, `valid` bit mask) to this workgroup's bucket
-// ranges: cur[b] = next free slot of bucket b. dcnt and gpos are scratch (dcnt zero on entry/exit).
-// OA / OV: where the addresses / values go (RecOut, or WideOut for a push past 4 GiB of buffer).
-template <typename A, int P, typename OA, typename OV>
+// Chunk-local partition: chunk c of the tail (kChunk records) is written to the partition buffer's own
+// range [c * kChunk, c * kChunk + total) with its records grouped by coarse bucket, and its column of
+// the chunk table ct[b][c] = (where bucket b's run starts in the chunk) | (its length << 16). No count pass
+// runs first: the stores are one contiguous range per chunk, and bin_scan turns the table into each
+// bucket's chunk prefix afterwards. ad / va: P records per thread in registers, `valid` bit mask; dcnt
+// and gcnt are scratch (dcnt zero on entry and exit). OA / OV: the chunk's output windows.
+template <typename A, int P>
 __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u32 valid, const BinGeom& g,
-                                         u32* dcnt, u32* gpos, u32* cur, u32* st_a, A* st_v, const OA& oa,
-                                         const OV& ov, PhaseClock& ph, int pb) {
+                                         u32* dcnt, u32* gcnt, u32* st_a, A* st_v, const BufOut& ctb, u32 ctcol,
+                                         u32 ctstride, u32* __restrict__ out_a, A* __restrict__ out_v, PhaseClock& ph,
+                                         int pb) {
   const int tid = threadIdx.x;
   u32 rank[P];
 #pragma unroll
@@ -613,12 +490,13 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   const u32 total = block_scan<kATPB, 1>(
       g.nb, [&](u32 d) { return dcnt[d]; },
       [&](u32 d, u32 excl) {
-        const u32 c = dcnt[d];
-        gpos[d] = cur[d] - excl;  // slot of local staging position p (bucket d) = gpos[d] + p
-        cur[d] += c;
+        gcnt[d] = dcnt[d];
         dcnt[d] = excl;
       });
   ph.mark(pb + 1);
+  static_assert(kATPB <= kMaxDigit, "one chunk-table entry per thread");
+  // the chunk's column of the table (bucket-major rows of ctstride): one counted store per thread
+  bput(ctb, ((u32)tid * ctstride + ctcol) * 4u, (u32)tid < g.nb, dcnt[tid] | (gcnt[tid] << 16));
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     if (valid & (1u << j)) {
@@ -629,15 +507,15 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   }
   __syncthreads();
   ph.mark(pb + 2);
+  const RecOut<u32> oa{buf_out(out_a, total * 4u)};
+  const RecOut<A> ov{buf_out(out_v, total * (u32)sizeof(A))};
 #pragma unroll
-  for (int j = 0; j < P; ++j) {  // consecutive threads: consecutive slots of one run
+  for (int j = 0; j < P; ++j) {  // consecutive threads: consecutive slots of the chunk's range
     if ((u32)(j * kATPB) >= total) break;  // workgroup-uniform: no store instructions past the chunk
     const u32 p = tid + j * kATPB;
     const bool on = p < total;
-    const u32 a = st_a[p];
-    const u32 rel = gpos[on ? bucket_of(a, g) : 0u] + p;  // record index in the partition buffer
-    oa.put(rel, on, a);
-    ov.put(rel, on, st_v[p]);
+    oa.put(p, on, st_a[p]);
+    ov.put(p, on, st_v[p]);
   }
   __syncthreads();
   ph.mark(pb + 3);
@@ -647,47 +525,27 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
   return total;
 }
 
-// Workgroup w's bucket ranges: bucket b is the contiguous range [Bb[b], Bb[b] + T[b]) with Bb the
-// exclusive scan of T (written once, by workgroup 0); this workgroup's records of b start at
-// Bb[b] + Roff[w][b].
-__device__ __forceinline__ void part_setup(const BinGeom& g, u32 w, u32* cur, u32* dcnt, const u32* __restrict__ T,
-                                           const u32* __restrict__ Roff, u32* __restrict__ Bb) {
-  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; },
-                       [&](u32 b, u32 excl) {
-                         cur[b] = excl + Roff[w * g.nb + b];
-                         dcnt[b] = 0;
-                         if (w == 0) Bb[b] = excl;
-                       });
+// Workgroup 0 of the partition: the next push's header (the previous push used it; it is done) and,
+// for a whole-push bin (no push_check ran), the next push's control words as push_check zeroes them.
+__device__ __forceinline__ void part_next_header(const BinGeom& g, BinCtl* next_bc, u32* __restrict__ next_T,
+                                                 LaunchCtl* next_ctl) {
+  const int tid = threadIdx.x;
+  for (u32 b = tid; b < g.nb; b += kATPB) {
+    next_T[b] = 0;
+    next_T[kMaxDigit + b] = 0;  // the fused plan's per-bucket item counters
+  }
+  if (tid < (int)(sizeof(BinCtl) / 4)) reinterpret_cast<u32*>(next_bc)[tid] = 0;
+  if (next_ctl && tid == 0) {
+    next_ctl->brk_enc = 0u;
+    next_ctl->nonaffine = 0u;
+    next_ctl->cancel = 0u;
+    next_ctl->bad = 0ull;
+  }
 }
 
 // fine items of a bucket of t records: ceil(t / item), at least one (an empty bucket's one item writes
 // its empty offset row)
 __device__ __forceinline__ u32 bucket_items(u32 t, u32 item) { return max(1u, (t + item - 1) / item); }
-// Workgroup 0 of bin_part: the fine items -- {b, j}: bucket b's records [j * item, (j + 1) * item) --
-// and Ib[b] = the bucket's first item.
-__device__ __forceinline__ void part_items(const BinGeom& g, const u32* __restrict__ T, uint2* __restrict__ fitems,
-                                           BinCtl* bc, u32 item, u32* __restrict__ Ib) {
-  const u32 tot = block_scan<kATPB, 1>(
-      g.nb, [&](u32 b) { return bucket_items(T[b], item); },
-      [&](u32 b, u32 excl) {
-        const u32 J = bucket_items(T[b], item);
-        for (u32 j = 0; j < J; ++j) fitems[excl + j] = make_uint2(b, j);
-        Ib[b] = excl;
-      });
-  if (threadIdx.x == 0) bc->nfitems = tot;
-}
-
-// Dedup front end: the chunk tables merged records, so this workgroup's bucket ranges end short of
-// what bin_count counted; the rest of each range is marked empty for bin_fsort.
-__device__ __forceinline__ void part_fill_holes(const BinGeom& g, u32 w, const u32* __restrict__ T,
-                                                const u32* __restrict__ R, const u32* __restrict__ Roff, const u32* cur,
-                                                u32* dcnt, u32* __restrict__ addr_out) {
-  __syncthreads();
-  block_scan<kATPB, 1>(g.nb, [&](u32 b) { return T[b]; },
-                       [&](u32 b, u32 excl) { dcnt[b] = excl + Roff[w * g.nb + b] + R[w * g.nb + b]; });
-  for (u32 b = 0; b < g.nb; ++b)
-    for (u32 p = cur[b] + threadIdx.x; p < dcnt[b]; p += kATPB) addr_out[p] = kEmptySlot;
-}
 
 // The plain + hot front end keeps a wider hot table (kWideSlots tags + sums fit the plain partition
 // kernel's LDS next to its staging). Its hot elements come from a sample 16x larger than
@@ -778,8 +636,9 @@ constexpr int kRedSlots = 64, kRedTPB = 1024, kRedGroups = kRedTPB / kRedSlots;
 template <typename V>
 __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned long long* __restrict__ best, u32 G,
                                                                  const typename LdsAcc<V>::T* __restrict__ partial,
-                                                                 V* __restrict__ data) {
+                                                                 V* __restrict__ data, const LaunchCtl* gated) {
   typedef typename LdsAcc<V>::T A;
+  if (gated && gated->cancel) return;  // a validating push its verdict rejected: nothing is applied
   __shared__ A gs[kRedGroups][kRedSlots];
   __shared__ u32 gany[kRedGroups][kRedSlots];
   const int tid = threadIdx.x, ls = tid % kRedSlots, grp = tid / kRedSlots;
@@ -818,41 +677,31 @@ __global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned 
   if (seen) data[a] = acc_add(data[a], tot);
 }
 
-// The partition's outputs: buffer windows (RecOut), or for a push whose buffers pass 4 GiB WideOut with
-// the dump area (kDumpBytes: values, then addresses)
-constexpr size_t kDumpBytes = 1024;
-template <bool WIDE, typename T>
-__device__ __forceinline__ auto part_out(T* base, u32 n, void* dump, size_t dump_off) {
-  if constexpr (WIDE) {
-    return WideOut<T>{base, reinterpret_cast<T*>(reinterpret_cast<char*>(dump) + dump_off)};
-  } else {
-    return RecOut<T>{buf_out(base, n * (u32)sizeof(T))};
-  }
-}
-
 // Plain front end: every valid record is appended as it is. HOT: the push's hot elements (the wide
 // table, bin_hot_select) are summed in LDS over all of the workgroup's chunks and stored per
 // workgroup for bin_hot_reduce; only the cold records are appended. Once the hot elements are off,
 // a Zipf-like tail has almost no duplicates left inside a chunk (cfg3: the chunk dedup would merge
 // 0.6 % of the cold records), so the hash table is not worth its time there.
+// VALIDATE (a validating gated push, GLINT_PUSH_VALIDATE, whose tail is binned): every tail record is
+// also checked -- the key itself in the partition's key range, as key_in_part -- and the first rejected
+// one goes to the push's LaunchCtl (vctl->bad), as push_check does for the records before the break; the
+// verdict and cancel come after this kernel (push_validate_gate_binned_kernel), before anything is
+// applied (this kernel writes only the partition buffers and, HOT, its per-workgroup hot sums, which
+// bin_hot_reduce drops for a cancelled push). next_ctl (a whole-push bin): workgroup 0 zeroes the next
+// push's control words, and any wave that sees two adjacent records out of order says so (bc->disorder).
 #ifndef GLINT_PART_WAVES
 #define GLINT_PART_WAVES 4  // bin_part's register budget: waves per SIMD (build-time knob)
 #endif
-template <typename V, bool MAT, bool HOT, int KIND, bool WIDE, int PER = kAPer>
-__global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 : GLINT_PART_WAVES))) void bin_part_kernel(const i64* __restrict__ keys, const int32_t* __restrict__ cols,
-                                                         const V* __restrict__ vals, i64 n, PartDesc part,
-                                                         const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g,
-                                                         u32* __restrict__ addr_out,
-                                                         typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err,
-                                                         BinCtl* bc, const u32* __restrict__ T,
-                                                         uint2* __restrict__ fitems,
-                                                         const unsigned long long* __restrict__ hot_best,
-                                                         typename LdsAcc<V>::T* __restrict__ hot_partial, u32 fitem,
-                                                         const u32* __restrict__ Roff, u32* __restrict__ Bb,
-                                                         u32* __restrict__ Ib, void* dump) {
+template <typename V, bool MAT, bool HOT, int KIND, bool VALIDATE, int PER = kAPer>
+__global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 : GLINT_PART_WAVES))) void bin_part_kernel(
+    const i64* __restrict__ keys, const int32_t* __restrict__ cols, const V* __restrict__ vals, i64 n, PartDesc part,
+    const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, u32* __restrict__ addr_out,
+    typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc, u32* __restrict__ ct, u32 ctstride,
+    const unsigned long long* __restrict__ hot_best, typename LdsAcc<V>::T* __restrict__ hot_partial,
+    BinCtl* next_bc, u32* __restrict__ next_T, LaunchCtl* vctl, LaunchCtl* next_ctl) {
   typedef typename LdsAcc<V>::T A;
   constexpr int kChunk = kATPB * PER;  // records per chunk
-  __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
+  __shared__ u32 dcnt[kMaxDigit], gcnt[kMaxDigit];
   __shared__ u32 st_a[kChunk];
   __shared__ A st_v[kChunk];
   constexpr int kHS = HOT ? kWideSlots : 1;
@@ -872,22 +721,21 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
       hacc[sl] = hot_zero<A>();
     }
   }
+  for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
+  if (w == 0) part_next_header(g, next_bc, next_T, next_ctl);
+  __syncthreads();
   PhaseClock ph(0);
-  if (w == 0) part_items(g, T, fitems, bc, fitem, Ib);
-  part_setup(g, w, cur, dcnt, T, Roff, Bb);
-  ph.mark(0);
   const i64 G = gridDim.x;
-  // output: the whole buffer (the bucket ranges)
-  const auto oa = part_out<WIDE>(addr_out, (u32)(n - r0), dump, 512);
-  const auto ov = part_out<WIDE>(val_out, (u32)(n - r0), dump, 0);
+  const BufOut ctb = buf_out(ct, g.nb * ctstride * 4u);  // (< 2^32 bytes: push_binnable)
   BadRecs bad;
   u32 emitted = 0;
+  bool dis = false;  // (a whole-push bin) two adjacent records of one wave out of order
   // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
   // compiler can wait for one chunk's loads while the next chunk's stay in flight
   auto load_chunk = [&](i64 c, RecRegs<V, MAT, PER>& r) {
     const i64 cc = min(c, nchunks - 1);
     const i64 c0 = r0 + cc * kChunk, c1 = min(n, r0 + (cc + 1) * kChunk);
-    if constexpr (KIND == 0) {  // (key - start).toInt needs the low words only (as bin_count loads them)
+    if constexpr (KIND == 0 && !VALIDATE) {  // (key - start).toInt needs the low words only
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
         const i64 i = c0 + q * kATPB + threadIdx.x;
@@ -901,23 +749,26 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
     }
   };
   auto step = [&](i64 c, RecRegs<V, MAT, PER>& r) {
-    const i64 c0 = r0 + c * kChunk, c1 = min(n, c0 + kChunk);
+    const i64 c0 = r0 + c * kChunk, c1 = c < nchunks ? min(n, c0 + kChunk) : c0;
     u32 ad[PER];
     A va[PER];
     u32 valid = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const i64 i = c0 + q * kATPB + tid;
+      const bool in = i < c1;
       i64 a64;
-      ad[q] = 0;
+      bool ok = in && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64);
+      if constexpr (VALIDATE) ok = ok && key_in_part<KIND>(part, r.k[q]);
+      ad[q] = ok ? (u32)a64 : 0u;
       va[q] = (A)r.v[q];
-      if (i < c1) {
-        if (rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64)) {
-          ad[q] = (u32)a64;
-          valid |= 1u << q;
-        } else {
-          bad.add(i);
-        }
+      if (ok) valid |= 1u << q;
+      else if (in) bad.add(i);
+      if (next_ctl && q == 0) {  // a wave's records are consecutive: are they strictly increasing? (one
+        // record per thread per chunk is sample enough: an unordered push shows it in every wave, a sorted
+        // one nowhere; a record before this one is in the push whenever this one is)
+        const u32 a32 = ok ? (u32)a64 : 0xFFFFFFFFu, prev = __shfl_up(a32, 1);
+        dis = dis || (in && (!ok || ((threadIdx.x & 63) && prev >= a32)));
       }
     }
     if constexpr (HOT) {
@@ -931,7 +782,12 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
       }
     }
     ph.mark(1);
-    emitted += part_emit<A, PER>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 3);
+    const i64 cs = c < nchunks ? c : 0;  // (a step past the end emits nothing: its table row and stores land
+    // on chunk 0's, all of them dropped -- total 0 -- but its table column, which would overwrite chunk
+    // 0's: past the end the column goes to the spare one at nchunks instead)
+    const u32 crow = (u32)(c < nchunks ? c : nchunks);
+    emitted += part_emit<A, PER>(ad, va, valid, g, dcnt, gcnt, st_a, st_v, ctb, crow, ctstride,
+                                 addr_out + (size_t)cs * kChunk, val_out + (size_t)cs * kChunk, ph, 3);
     // kAhead chunks ahead, into the registers just consumed: in flight across the next chunks' work
     load_chunk(c + kAhead * G, r);
     ph.mark(2);
@@ -943,14 +799,20 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
     for (int j = 0; j < kAhead; ++j) load_chunk(c + j * G, r[j]);
     for (; c < nchunks; c += kAhead * G) {
 #pragma unroll
-      for (int j = 0; j < kAhead; ++j) step(c + j * G, r[j]);  // past the end: no valid record, nothing stored
+      for (int j = 0; j < kAhead; ++j) step(c + j * G, r[j]);  // past the end: no valid record
     }
   }
-  if (tid == 0 && emitted) {
+  if (tid == 0 && emitted) {  // (emitted is workgroup-uniform: the sum of the chunks' totals)
     atomicAdd(&bc->m, emitted);
     atomicAdd(&bc->cold, emitted);  // cold records: all of them were appended
+    atomicAdd(&bc->tail, emitted);  // valid records of the tail (the hot front end's hot ones not counted)
   }
-  bad.report(err);
+  if (next_ctl && __syncthreads_or(dis) && tid == 0) atomicOr(&bc->disorder, 1u);
+  if constexpr (VALIDATE) {
+    if (bad.count) atomicMax(&vctl->bad, ~(u64)bad.first);  // rare: one atomic per thread
+  } else {
+    bad.report(err);
+  }
   if constexpr (HOT) {
     __syncthreads();  // every chunk's hot sums are in; bin_hot_reduce adds them up
     for (int sl = tid; sl < kWideSlots; sl += kATPB) hot_partial[(size_t)w * kWideSlots + sl] = hacc[sl];
@@ -961,17 +823,19 @@ __global__ __launch_bounds__(kATPB) __attribute__((amdgpu_waves_per_eu(HOT ? 4 :
 // Dedup front end for duplicate-heavy tails: per chunk, equal elements are summed in an LDS hash
 // table first, so one record per distinct element of the chunk moves on. The staging buffer of the
 // append overlays the table's value array. Records of the push's hot elements (hot_tags) are summed
-// in LDS across all of the workgroup's chunks instead and added to the shard at the end.
+// in LDS across all of the workgroup's chunks instead and added to the shard at the end (never for a
+// validating push: its verdict comes after this kernel, so the host passes no hot tags and every record
+// is partitioned). VALIDATE, next_ctl: as bin_part_kernel.
 
-// KIND: the partition layout (0 range: only the keys' low words are loaded, as in bin_count -- the
-// register budget of this kernel is tight; -1 read at run time)
-template <typename V, bool MAT, int KIND, bool WIDE>
+// KIND: the partition layout (0 range: only the keys' low words are loaded -- the register budget of
+// this kernel is tight; -1 read at run time)
+template <typename V, bool MAT, int KIND, bool VALIDATE>
 __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     const i64* __restrict__ keys, const int32_t* __restrict__ cols, const V* __restrict__ vals, i64 n, PartDesc part,
-    const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, const u32* __restrict__ R,
-    u32* __restrict__ addr_out, typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc,
-    const u32* __restrict__ T, uint2* __restrict__ fitems, const u32* __restrict__ hot_tags, V* __restrict__ data,
-    u32 fitem, const u32* __restrict__ Roff, u32* __restrict__ Bb, u32* __restrict__ Ib, void* dump) {
+    const LaunchCtl* lctl, u32 ntiles, int from_break, BinGeom g, u32* __restrict__ addr_out,
+    typename LdsAcc<V>::T* __restrict__ val_out, ErrState* err, BinCtl* bc, u32* __restrict__ ct, u32 ctstride,
+    const u32* __restrict__ hot_tags, V* __restrict__ data, BinCtl* next_bc, u32* __restrict__ next_T,
+    LaunchCtl* vctl, LaunchCtl* next_ctl) {
   typedef typename LdsAcc<V>::T A;
   static_assert(kAChunk * (4 + sizeof(A)) <= kASlots * sizeof(A), "staging must fit the value table");
   __shared__ u32 hk[kASlots];
@@ -979,7 +843,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
   __shared__ u32 htag[kHotSlots];
   __shared__ A hacc[kHotSlots];
   __shared__ uint16_t used[kAChunk];
-  __shared__ u32 dcnt[kMaxDigit], gpos[kMaxDigit], cur[kMaxDigit];
+  __shared__ u32 dcnt[kMaxDigit], gcnt[kMaxDigit];
   __shared__ u32 nused;
   const int tid = threadIdx.x, lane = tid & 63;
   const u32 w = blockIdx.x;
@@ -996,23 +860,24 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     htag[sl] = hot_tags ? hot_tags[sl] : kEmptySlot;
     hacc[sl] = hot_zero<A>();
   }
+  for (u32 d = tid; d < g.nb; d += kATPB) dcnt[d] = 0;
   if (tid == 0) nused = 0;
+  if (w == 0) part_next_header(g, next_bc, next_T, next_ctl);
+  __syncthreads();
   PhaseClock ph(8);
-  if (w == 0) part_items(g, T, fitems, bc, fitem, Ib);
-  part_setup(g, w, cur, dcnt, T, Roff, Bb);
   ph.mark(8);
   const u64 below = (1ull << lane) - 1ull;
   const i64 G = gridDim.x;
-  const auto oa = part_out<WIDE>(addr_out, (u32)(n - r0), dump, 512);
-  const auto ov = part_out<WIDE>(val_out, (u32)(n - r0), dump, 0);
+  const BufOut ctb = buf_out(ct, g.nb * ctstride * 4u);  // (< 2^32 bytes: push_binnable)
   BadRecs bad;
-  u32 emitted = 0, ncold = 0;
+  u32 emitted = 0, ncold = 0, nvalid = 0;
+  bool dis = false;
   // chunk loads are unconditional (index clamped; a step past the end sees no valid record), so the
   // compiler can wait for one chunk's loads while the next chunk's stay in flight
   auto load_chunk = [&](i64 c, RecRegs<V, MAT>& r) {
     const i64 cc = min(c, nchunks - 1);
     const i64 c0 = r0 + cc * kAChunk, c1 = min(n, r0 + (cc + 1) * kAChunk);
-    if constexpr (KIND == 0) {  // (key - start).toInt needs the low words only
+    if constexpr (KIND == 0 && !VALIDATE) {  // (key - start).toInt needs the low words only
 #pragma unroll
       for (int q = 0; q < kAPer; ++q) {
         const i64 i = c0 + q * kATPB + threadIdx.x;
@@ -1026,7 +891,7 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     }
   };
   auto step = [&](i64 c, RecRegs<V, MAT>& r) {
-    const i64 c0 = r0 + c * kAChunk, c1 = min(n, c0 + kAChunk);
+    const i64 c0 = r0 + c * kAChunk, c1 = c < nchunks ? min(n, c0 + kAChunk) : c0;
     // the chunk's addresses, rejected records and hot hits first: the hot-table reads of all kAPer
     // records are in flight together, and a hot record is summed here and leaves the chunk
     u32 ca[kAPer];
@@ -1034,17 +899,19 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       const i64 i = c0 + q * kATPB + tid;
+      const bool in = i < c1;
       i64 a64;
-      ca[q] = 0;
-      if (i < c1) {
-        if (rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64)) {
-          ca[q] = (u32)a64;
-          cold |= 1u << q;
-        } else {
-          bad.add(i);
-        }
+      bool ok = in && rec_addr<MAT, KIND>(part, r.k[q], r.cl[q], a64);
+      if constexpr (VALIDATE) ok = ok && key_in_part<KIND>(part, r.k[q]);
+      ca[q] = ok ? (u32)a64 : 0u;
+      if (ok) cold |= 1u << q;
+      else if (in) bad.add(i);
+      if (next_ctl && q == 0) {  // (as bin_part_kernel)
+        const u32 a32 = ok ? (u32)a64 : 0xFFFFFFFFu, prev = __shfl_up(a32, 1);
+        dis = dis || (in && (!ok || ((threadIdx.x & 63) && prev >= a32)));
       }
     }
+    nvalid += (u32)__popc(cold);
 #pragma unroll
     for (int q = 0; q < kAPer; ++q) {
       const u32 hs = hot_slot(ca[q]);
@@ -1101,7 +968,10 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     __syncthreads();
     if (tid == 0) nused = 0;
     ph.mark(11);
-    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gpos, cur, st_a, st_v, oa, ov, ph, 12);
+    const i64 cs = c < nchunks ? c : 0;  // (as bin_part_kernel)
+    const u32 crow = (u32)(c < nchunks ? c : nchunks);
+    emitted += part_emit<A, kAPer>(ad, va, valid, g, dcnt, gcnt, st_a, st_v, ctb, crow, ctstride,
+                                   addr_out + (size_t)cs * kAChunk, val_out + (size_t)cs * kAChunk, ph, 12);
     for (int sl = tid; sl < kStageA; sl += kATPB) hv[sl] = A(0);  // staging overlaid these
 #pragma unroll
     for (int j = 0; j < kAPer; ++j) {  // and the table's own slots of this chunk
@@ -1125,18 +995,129 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
     }
   }
   if (tid == 0 && emitted) atomicAdd(&bc->m, emitted);
-  part_fill_holes(g, w, T, R, Roff, cur, dcnt, addr_out);
-  bad.report(err);
+  if constexpr (VALIDATE) {
+    if (bad.count) atomicMax(&vctl->bad, ~(u64)bad.first);
+  } else {
+    bad.report(err);
+  }
   {  // records that entered the hash table (valid, not hot): the host's measure of what chunk dedup merges
     const u32 tot = block_sum<kATPB>(ncold);
     if (tid == 0 && tot) atomicAdd(&bc->cold, tot);
+    const u32 tv = block_sum<kATPB>(nvalid);  // valid records of the tail, hot ones included
+    if (tid == 0 && tv) atomicAdd(&bc->tail, tv);
   }
+  if (next_ctl && __syncthreads_or(dis) && tid == 0) atomicOr(&bc->disorder, 1u);
   __syncthreads();  // every chunk's hot sums are in
   for (int sl = tid; sl < kHotSlots; sl += kATPB) {
     const u32 a = htag[sl];
     if (a != kEmptySlot && !hot_untouched<A>(hacc[sl])) hot_flush(data + a, hacc[sl]);
   }
   ph.flush(10);
+}
+
+// ---- bin_scan ---------------------------------------------------------------------------------------
+// One workgroup per coarse bucket b, after the partition (and a validating push's verdict: a cancelled
+// push's tail is empty here, so every bucket is): bucket b's records are its runs in chunk order, the
+// run of chunk c at partition-buffer index c * kChunk + start(c, b). The bucket's chunk prefix
+// P[b][c] = records of b in chunks < c (P[b][nch] = T[b]) and Q[b][c] = c * kChunk + start - P[b][c]
+// (so record v of the bucket, in chunk c, is at Q[b][c] + v), its range [Bb[b], Bb[b] + T[b]) of the
+// fine sort's output and its items [Ib[b], Ib[b] + items) -- each bucket takes both with one atomic, in
+// any order -- with cwin[item] = the chunks holding the item's first and last records. Two passes over
+// the bucket's row of the chunk table (the second one hits in cache): its total, then the prefixes.
+constexpr int kScanTPB = 1024;
+constexpr int kScanPer = 8;
+__global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32* __restrict__ ct, u32 ctstride, i64 n,
+                                                            const LaunchCtl* lctl, u32 ntiles, int from_break,
+                                                            u32 kchunk, u32 nstride, BinCtl* bc, u32* __restrict__ T,
+                                                            u32* __restrict__ Bb, u32* __restrict__ Ib,
+                                                            uint2* __restrict__ fitems, uint2* __restrict__ cwin,
+                                                            u32* __restrict__ P, u32* __restrict__ Q, u32 item) {
+  __shared__ u32 base2[2];
+  __shared__ u32 wt[kScanTPB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u32 b = blockIdx.x;
+  const i64 r0 = tail_start(lctl, ntiles, from_break, n);
+  const u32 nch = (u32)((n - r0 + kchunk - 1) / kchunk);
+  if (b == 0 && tid == 0) bc->nch = nch;
+  const u32* const row = ct + (size_t)b * ctstride;
+  u32 s = 0;
+  for (u32 base = 0; base < nch; base += (u32)kScanTPB * kScanPer) {  // kScanPer loads in flight
+    u32 w[kScanPer];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const u32 c = base + (u32)k * kScanTPB + tid;
+      w[k] = c < nch ? row[c] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) s += w[k] >> 16;
+  }
+  const u32 tb = block_sum<kScanTPB>(s);
+  const u32 J = bucket_items(tb, item);
+  if (tid == 0) {
+    T[b] = tb;
+    base2[0] = atomicAdd(&bc->rbase, tb);
+    base2[1] = atomicAdd(&bc->nfitems, J);
+    Bb[b] = base2[0];
+    Ib[b] = base2[1];
+  }
+  __syncthreads();
+  const u32 ib = base2[1];
+  u32* const Pb = P + (size_t)b * (nstride + 1);
+  u32* const Qb = Q + (size_t)b * nstride;
+  // tiles of kScanTPB x kScanPer chunks: every thread's kScanPer entries in registers, scanned, then only
+  // stores (a load between stores would wait for them: one counter for both)
+  u32 carry = 0, clast = 0;
+  for (u32 base = 0; base < nch; base += (u32)kScanTPB * kScanPer) {
+    const u32 c0 = base + (u32)tid * kScanPer;
+    u32 w[kScanPer];
+    u32 sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      w[k] = c0 + k < nch ? row[c0 + k] : 0u;
+      sum += w[k] >> 16;
+    }
+    u32 incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wt[wid] = incl;
+    __syncthreads();
+    u32 pre, tot;
+    wave_totals<kScanTPB / 64>(wt, lane, wid, pre, tot);
+    u32 run = carry + pre + incl - sum;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const u32 c = c0 + k, cnt = w[k] >> 16;
+      if (c < nch) {
+        Pb[c] = run;
+        Qb[c] = c * kchunk + (w[k] & 0xFFFFu) - run;
+      }
+      if (cnt) {
+        clast = c;
+        // items whose first record is in this run; items whose last one ((j + 1) item - 1) is
+        for (u32 j = (run + item - 1) / item; j * item < run + cnt; ++j) {
+          fitems[ib + j] = make_uint2(b, j);
+          cwin[ib + j].x = c;
+        }
+        for (u32 k1 = (run + item) / item; k1 * item <= run + cnt; ++k1) cwin[ib + k1 - 1].y = c;
+      }
+      run += cnt;
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  const u32 cl = block_max<kScanTPB>(clast);  // the bucket's last chunk with records
+  if (tid == 0) {
+    Pb[nch] = tb;
+    if (tb == 0) {  // an empty bucket's one item
+      fitems[ib] = make_uint2(b, 0u);
+      cwin[ib] = make_uint2(0u, 0u);
+    } else {
+      cwin[ib + J - 1].y = cl;  // the bucket's last record closes its last item
+    }
+  }
 }
 
 // ==== v2 fine stage: one sort pass per fine item, a plan per bucket, an apply that gathers runs =========
@@ -1161,10 +1142,10 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 // at one workgroup per CU, 16 had measured slower: ab_nt_mid.txt s16). Build-time knobs
 // GLINT_FSORT_PER_SMALL / _LARGE (small: the pushes with the plan fused in, see push_binned).
 #ifndef GLINT_FSORT_PER_SMALL
-#define GLINT_FSORT_PER_SMALL 16
+#define GLINT_FSORT_PER_SMALL 12
 #endif
 #ifndef GLINT_FSORT_PER_LARGE
-#define GLINT_FSORT_PER_LARGE 16
+#define GLINT_FSORT_PER_LARGE 12
 #endif
 constexpr int kSTPB = GLINT_FSORT_TPB;
 constexpr int kSPerSmall = GLINT_FSORT_PER_SMALL, kSPerLarge = GLINT_FSORT_PER_LARGE;
@@ -1426,7 +1407,55 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
 // (plan_bucket<true>), so no plan launch follows and the buckets' plans overlap the other items' sorts.
-constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
+#ifndef GLINT_SMALL_PER8
+#define GLINT_SMALL_PER8 0
+#endif
+#ifndef GLINT_VALIDATE_PER8
+#define GLINT_VALIDATE_PER8 1
+#endif
+#ifndef GLINT_FSORT_LATE_TRY
+#define GLINT_FSORT_LATE_TRY 0
+#endif
+constexpr u32 kStage = 32768;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
+// A value the compiler must recompute where it is used (not hoist and hold in a register across a loop)
+__device__ __forceinline__ u32 opaque(u32 x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// Forward fill of rid[x0, x1) (<= TPB * 16 entries, 0 = no mark): every entry becomes the last mark at
+// or before it (marks increase with x, so this is an inclusive max-scan)
+template <int TPB>
+__device__ __forceinline__ void fill_forward(uint16_t* rid, u32 x0, u32 x1) {
+  constexpr int kPer = 16;
+  __shared__ u32 wmax[TPB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u32 b0 = x0 + (u32)tid * kPer;
+  u32 v[kPer];
+  u32 m = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    v[k] = b0 + k < x1 ? (u32)rid[b0 + k] : 0u;
+    m = max(m, v[k]);
+  }
+  u32 incl = m;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const u32 y = __shfl_up(incl, dd);
+    if (lane >= dd) incl = max(incl, y);
+  }
+  if (lane == 63) wmax[wid] = incl;
+  __syncthreads();
+  u32 run = __shfl_up(incl, 1);
+  if (lane == 0) run = 0;
+  for (int w2 = 0; w2 < wid; ++w2) run = max(run, wmax[w2]);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    run = max(run, v[k]);
+    if (b0 + k < x1) rid[b0 + k] = (uint16_t)run;
+  }
+  __syncthreads();
+}
+constexpr u32 kFWin = 2048;  // bin_fsort: chunks per window of the item's run table
 template <typename A, bool FUSED, int kSPer>
 __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void bin_fsort_kernel(BinGeom g, const uint2* __restrict__ fitems, BinCtl* bc,
                                                           const u32* __restrict__ T, const u32* __restrict__ Bb,
@@ -1435,9 +1464,12 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
                                                           u32* __restrict__ off2, u64* hint, u64* whole_hint,
                                                           u32 whole_n, const u32* __restrict__ Ib, u32* done,
                                                           uint4* __restrict__ units, uint2* __restrict__ runs,
-                                                          int group_on, u32 item) {
+                                                          int group_on, u32 item, const uint2* __restrict__ cwin,
+                                                          const u32* __restrict__ P, const u32* __restrict__ Q,
+                                                          u32 nstride) {
   constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
-  constexpr size_t kSortLds = 4 * kMaxDigit + kStage;
+  // [hist | stage | the item's run marks (u16 per record) | its window of chunk places Q]
+  constexpr size_t kSortLds = 4 * kMaxDigit + kStage + 2 * kSItemMax + 4 * kFWin;
   typedef PlanLds<kPlanLdsFused, kPlanPTabFused> FusedPlanLds;
   constexpr size_t kLds = FUSED && sizeof(FusedPlanLds) > kSortLds ? sizeof(FusedPlanLds) : kSortLds;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
@@ -1486,31 +1518,76 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
   // offsets: few registers, so the fine sort keeps two workgroups per CU); a load past the item reads 0
   // without touching memory, a store at the window's end is dropped (counted stores, see BufOut)
   const u32 cnt = s1 - s0;
-  const BufOut ain = buf_out(addr_in + s0, cnt * 4u), vin = buf_out(val_in + s0, cnt * (u32)sizeof(A));
+  // Where the item's records are: record v of the bucket lies in the run of the chunk c with
+  // P[b][c] <= v < P[b][c + 1], at partition index Q[b][c] + v. The prefixes of the item's chunks (cwin:
+  // those of its first and last records, at most kFWin) go to LDS; every chunk's run marks its first record
+  // of the item with its window slot, a forward fill gives every record its run, and the record's index
+  // follows (recomputed where the values load: the marks and places stay in LDS, not in registers).
+  static_assert((kFWin + 1) * 4 <= kStage && kSItemMax <= 16 * kSTPB && kFWin < 65536 && kSItemMax <= 65536,
+                "the window's prefixes fit the stage; fill_forward's 16 per thread; u16 marks and places");
+  uint16_t* const rid = reinterpret_cast<uint16_t*>(stage + kStage);
+  u32* const Qw = reinterpret_cast<u32*>(stage + kStage + 2 * kSItemMax);
+  const u32 v0 = d.y * item;
+  const u32* const Pb = P + (size_t)b * (nstride + 1);
+  const u32* const Qb = Q + (size_t)b * nstride;
+  const uint2 cw = cwin[it];  // the chunks of the item's first and last records
+  const u32 span = cw.y - cw.x + 1;
+  const bool slow = span > kFWin;  // workgroup-uniform: the item spans more chunks than the window holds
+  if (!slow) {
+    u32* const Pw = reinterpret_cast<u32*>(stage);  // (the stage is free until the ranking)
+    for (u32 t = tid; t < span; t += kSTPB) {
+      Pw[t] = Pb[cw.x + t];
+      Qw[t] = Qb[cw.x + t];
+    }
+    if (tid == 0) Pw[span] = Pb[cw.x + span];  // (<= P[b][nch])
+    for (u32 x = tid; x < cnt; x += kSTPB) rid[x] = 0;
+    __syncthreads();
+    ph.mark(32);
+    for (u32 t = tid; t < span; t += kSTPB) {
+      const u32 lo = max(Pw[t], v0), hi = min(Pw[t + 1], v0 + cnt);
+      if (lo < hi) rid[lo - v0] = (uint16_t)(t + 1);
+    }
+    __syncthreads();
+    fill_forward<kSTPB>(rid, 0u, cnt);
+    ph.mark(33);
+  }
+  // record x of the item: its index in the partition buffer (slow: a binary search over the bucket's
+  // whole prefix row, for an item spread so thin over the chunks that its window would not hold it)
+  auto pos_of = [&](u32 x) -> u32 {
+    const u32 v = v0 + x;
+    if (!slow) return Qw[rid[x] - 1u] + v;
+    u32 lo = cw.x, hi = cw.y + 1;  // P[lo] <= v < P[hi]
+    while (hi - lo > 1) {
+      const u32 m = (lo + hi) >> 1;
+      if (Pb[m] <= v) lo = m;
+      else hi = m;
+    }
+    return Qb[lo] + v;
+  };
   // (kLate: the values are loaded only in their staging rounds, not held through the ranking -- the
   // registers of 16 records per thread then fit two workgroups per CU; cfg5 0.3118 -> 0.3073 ms,
   // profiles/r06/ab_fsort_late.txt)
-  constexpr bool kLate = kSPer > 8;
+  constexpr bool kLate = GLINT_FSORT_LATE_TRY && kSPer > 8;
   u32 a[kSPer];
   A v[kLate ? 1 : kSPer];
 #pragma unroll
-  for (int q = 0; q < kSPer; ++q) {  // branch-free: the whole item in flight at once
-    const u32 x = q * kSTPB + tid;
-    if ((u32)q * kSTPB < item) {  // launch-uniform (an item of fewer records than the registers hold)
-      a[q] = bget<u32>(ain, x * 4u);
-      if constexpr (!kLate) v[q] = bget<A>(vin, x * (u32)sizeof(A));
-    } else if constexpr (!kLate) {
-      v[q] = A(0);
-    }
-    if (x >= cnt || (u32)q * kSTPB >= item) a[q] = kEmptySlot;
+  for (int q = 0; q < kSPer; ++q) {  // the whole item in flight at once
+    const u32 x = q * kSTPB + opaque(tid);
+    const bool on = (u32)q * kSTPB < item && x < cnt;
+    const u32 ps = on ? pos_of(x) : 0u;
+    a[q] = on ? ld_mid(addr_in + ps) : kEmptySlot;
+    if constexpr (!kLate) v[q] = on ? ld_mid(val_in + ps) : A(0);
   }
   __syncthreads();
-  ph.mark(32);
-  u32 p[kSPer];  // the record's place in the item's slab order (kEmptySlot: no record)
+  ph.mark(34);
+  // the slab counts, then (after the scan) each record's place in the item's slab order from a second
+  // LDS atomic: a place taken in the first pass would hold a register per record through the scan
+  // (within a slab the order is any; kEmptySlot: no record)
 #pragma unroll
-  for (int q = 0; q < kSPer; ++q) p[q] = a[q] != kEmptySlot ? atomicAdd(&hist[fine_of(a[q], g)], 1u) : kEmptySlot;
+  for (int q = 0; q < kSPer; ++q)
+    if (a[q] != kEmptySlot) atomicAdd(&hist[fine_of(a[q], g)], 1u);
   __syncthreads();
-  ph.mark(33);
+  ph.mark(35);
   const u32 total = block_scan<kSTPB, 1>(
       g.nf, [&](u32 f) { return hist[f]; },
       [&](u32 f, u32 excl) {
@@ -1518,27 +1595,29 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
         put_row(f, excl);
       });
   if (tid == 0) put_row(g.nf, total);
-  ph.mark(34);
+  ph.mark(36);
   // the slab offsets (and the slab's low 4 bits: bin_apply2's groups of sparse slabs), staged as u16
   // and stored as whole-wave runs
   uint16_t* const ste = reinterpret_cast<uint16_t*>(stage);
+  u32 p[kSPer];
 #pragma unroll
   for (int q = 0; q < kSPer; ++q) {
-    if (p[q] == kEmptySlot) continue;
+    p[q] = kEmptySlot;
+    if (a[q] == kEmptySlot) continue;
     const u32 f = fine_of(a[q], g);
-    p[q] += hist[f];
+    p[q] = atomicAdd(&hist[f], 1u);
     ste[p[q]] = (uint16_t)((a[q] & (kSlab - 1)) | ((f & 15u) << kSlabBits));
   }
   __syncthreads();
   const BufOut eo = buf_out(e_out + s0, total * 2u), vo = buf_out(v_out + s0, total * (u32)sizeof(A));
 #pragma unroll
   for (int q = 0; q < kSPer; ++q) {  // total <= item <= kSPer * kSTPB
-    const u32 x = q * kSTPB + tid;
+    const u32 x = q * kSTPB + opaque(tid);
     if ((u32)q * kSTPB >= item) break;  // launch-uniform
     bput16(eo, x * 2u, x < total, ste[x]);
   }
   __syncthreads();
-  ph.mark(35);
+  ph.mark(37);
   A* const stv = reinterpret_cast<A*>(stage);
   for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
     if constexpr (kLate) {
@@ -1550,7 +1629,7 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
           const int q = q0 + k;
           lv[k] = A(0);
           if ((u32)q * kSTPB < item && p[q] != kEmptySlot && p[q] - r0 < kStageV)
-            lv[k] = bget<A>(vin, (q * kSTPB + tid) * (u32)sizeof(A));
+            lv[k] = ld_mid(val_in + pos_of(q * kSTPB + tid));
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1572,8 +1651,8 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
     }
     __syncthreads();
   }
-  ph.mark(36);
-  ph.flush(5);
+  ph.mark(38);
+  ph.flush(7);
   finish();
 }
 
@@ -1978,35 +2057,37 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     s->hot_age = hot_refresh ? 1u : s->hot_age + 1u;
   }
   s->bin_last_front = front;
-  // a push whose partition buffers pass 4 GiB stores through 64-bit addresses (WideOut)
-  const bool wide = (u64)n * sizeof(A) >= ((u64)1 << 32);
   // a small push (at most ~4 fine items per CU, cfg5) plans its buckets inside bin_fsort
   const bool small_push = (i64)g.nb + n / ((i64)kSTPB * kSPerSmall) + 1 <= (i64)4 * s->cus;
-  const int per = front == 0 && !small_push ? kAPerPlain : kAPer;  // records per thread of a partition chunk
-  const i64 nchunks_max = (n + (i64)kATPB * per - 1) / ((i64)kATPB * per);
+  // records per thread of a partition chunk (a validating push loads whole keys: 8 per thread would spill)
+  const int per = front == 0 && (!small_push || GLINT_SMALL_PER8) && (!hook || GLINT_VALIDATE_PER8) ? kAPerPlain : kAPer;
+  const u32 kchunk = (u32)kATPB * (u32)per;
+  const i64 nchunks_max = (n + kchunk - 1) / kchunk;
   // partition workgroups per CU: what fits at once (the hot front end's LDS table allows fewer)
   static const int hot_occ = resident_per_cu(bin_part_kernel<V, MAT, true, 0, false>, kATPB);
   const int wpc = dedup ? kPartWgPerCuDedup : front == 1 ? std::min(kPartWgPerCuPlain, hot_occ) : kPartWgPerCuPlain;
   const u32 G = (u32)std::max<i64>(1, std::min<i64>(nchunks_max, (i64)s->cus * wpc));
-  if (G > (u32)kMaxSegs) return GLINT_EINVAL;
   const u32 item = (u32)kSTPB * (small_push ? kSPerSmall : kSPerLarge);
   const i64 max_fitems = (i64)g.nb + n / item + 1;
   // apply units: a slab's units close at kUnitCap records or kRunMax runs, so at most
   // floor(H / cap) + floor(runs / kRunMax) + 1 per non-empty slab
   const i64 max_units = (i64)g.nslab + n / kUnitCap + std::min<i64>(n, max_fitems * g.nf) / kRunMax + 1;
-  // R, Roff, Bb, Ib, the fine items, off2, the apply units, the dedup front end's hot tags, the dump
-  // area of wide stores and the record buffers (coarse: u32 address + A value; fine: u16 slab offset + A
-  // value). The [BinCtl | T] headers and the hot front end's tables live in buffers of their own (stable
+  // The chunk table (a spare row past the last chunk), the buckets' chunk prefixes P and places Q, Bb,
+  // Ib, the fine items and their first chunks, off2, the apply units, the dedup front end's hot tags and
+  // the record buffers (coarse: u32 address + A value; fine: u16 slab offset + A value). The
+  // [BinCtl | T] headers and the hot front end's tables live in buffers of their own (stable
   // addresses: emptied by the kernels of the push before, not by memsets)
-  const size_t b_seg = pad256((size_t)G * g.nb * 4);
+  const u32 nstride = (u32)nchunks_max, ctstride = nstride + 1;  // (a spare column past the last chunk)
+  const size_t b_ct = pad256((size_t)ctstride * g.nb * 4);
+  const size_t b_pq = pad256((size_t)g.nb * (nstride + 1) * 4) + pad256((size_t)g.nb * nstride * 4);
   const size_t b_nb = pad256((size_t)g.nb * 4);
-  const size_t b_fit = pad256((size_t)max_fitems * 8), b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 4);
+  const size_t b_fit = 2 * pad256((size_t)max_fitems * 8);
+  const size_t b_off2 = pad256((size_t)max_fitems * (g.nf + 1) * 4);
   const size_t b_units = pad256((size_t)max_units * 16) + pad256((size_t)max_units * kRunMax * 8);
   const size_t b_hot = pad256((size_t)kHotSlots * 4);
   const size_t b_wpart = front == 1 ? pad256((size_t)G * kWideSlots * sizeof(A)) : 0;
   const size_t b_a = pad256((size_t)n * 4), b_v = pad256((size_t)n * sizeof(A)), b_e = pad256((size_t)n * 2);
-  const size_t need =
-      2 * b_seg + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + kDumpBytes + b_wpart + b_a + 2 * b_v + b_e;
+  const size_t need = b_ct + b_pq + 2 * b_nb + b_fit + b_off2 + b_units + b_hot + b_wpart + b_a + 2 * b_v + b_e;
   int rc = grow(&s->d_bin, &s->bin_bytes, need);
   if (rc) return rc;
   constexpr size_t kHdr = 12288;  // one [BinCtl (256 B) | T (<= kMaxDigit u32) | done (<= kMaxDigit u32)] header
@@ -2036,13 +2117,16 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   u32* T = (u32*)(hdr + 256);
   u32* done = T + kMaxDigit;  // the fused plan: items of each bucket sorted so far
   char* p = (char*)s->d_bin;
-  u32* R = (u32*)p;
-  u32* Roff = (u32*)(p + b_seg);
-  p += 2 * b_seg;
+  u32* ct = (u32*)p;
+  p += b_ct;
+  u32* P = (u32*)p;
+  u32* Q = (u32*)(p + pad256((size_t)g.nb * (nstride + 1) * 4));
+  p += b_pq;
   u32* Bb = (u32*)p;
   u32* Ib = (u32*)(p + b_nb);
   p += 2 * b_nb;
   uint2* fitems = (uint2*)p;
+  uint2* cwin = (uint2*)(p + pad256((size_t)max_fitems * 8));
   p += b_fit;
   u32* off2 = (u32*)p;
   p += b_off2;
@@ -2051,8 +2135,6 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   p += b_units;
   u32* hot_tags = (u32*)p;
   p += b_hot;
-  void* dump = p;
-  p += kDumpBytes;
   u32* wkey = front == 1 ? (u32*)s->d_hot : nullptr;
   u32* wcnt = front == 1 ? (u32*)((char*)s->d_hot + b_wk) : nullptr;
   unsigned long long* wbest = front == 1 ? (unsigned long long*)((char*)s->d_hot + 2 * b_wk) : nullptr;
@@ -2073,55 +2155,49 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     bin_hot_select_kernel<<<(1u << kWideHashBits) / 256u, 256, 0, st>>>(wkey, wcnt, kWideMin, wbest);
     HIPCHK(hipGetLastError());
   }
-  if (dedup) {
+  // (a validating push's dedup front end sums no hot elements: they would reach the shard before its
+  // verdict)
+  const bool dedup_hot = dedup && !hook;
+  if (dedup_hot) {
     bin_hot_pick_kernel<MAT><<<1, kHotTPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, kHotMin, hot_tags);
     HIPCHK(hipGetLastError());
   }
-  const unsigned long long* count_hot = front == 1 ? wbest : nullptr;  // the hot records are not partitioned
   BinCtl* const nbc = (BinCtl*)nhdr;
   u32* const nT = (u32*)(nhdr + 256);
-  {
-    // the count's chunks are the partition's (its per-workgroup counts are the partition's places)
-    // (hook: a validating gated push, whose count validates the tail records)
-    auto pick = [&](auto per) {
-      constexpr int P = decltype(per)::value;
-      if (hook) return a.part.kind == 0 ? bin_count_kernel<MAT, 0, true, P> : bin_count_kernel<MAT, -1, true, P>;
-      return a.part.kind == 0 ? bin_count_kernel<MAT, 0, false, P> : bin_count_kernel<MAT, -1, false, P>;
+  LaunchCtl* const vctl = hook ? a.ctl : nullptr;
+  // (hook: a validating gated push, whose partition validates the tail records)
+  if (dedup) {
+    auto kern = a.part.kind == 0 ? (hook ? bin_part_dedup_kernel<V, MAT, 0, true> : bin_part_dedup_kernel<V, MAT, 0, false>)
+                                 : (hook ? bin_part_dedup_kernel<V, MAT, -1, true> : bin_part_dedup_kernel<V, MAT, -1, false>);
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, addr_a, val_a, a.err, bc, ct, ctstride,
+                              dedup_hot ? hot_tags : nullptr, a.data, nbc, nT, vctl, whole_next);
+  } else {
+    auto pick = [&](auto pp, auto vv) {
+      constexpr int PP = decltype(pp)::value;
+      constexpr bool VV = decltype(vv)::value;
+      return a.part.kind == 0 ? (front == 1 ? bin_part_kernel<V, MAT, true, 0, VV> : bin_part_kernel<V, MAT, false, 0, VV, PP>)
+                              : (front == 1 ? bin_part_kernel<V, MAT, true, -1, VV> : bin_part_kernel<V, MAT, false, -1, VV, PP>);
     };
-    auto kern = per == kAPerPlain ? pick(std::integral_constant<int, kAPerPlain>{})
-                                  : pick(std::integral_constant<int, kAPer>{});
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, n, a.part, a.ctl, a.ntiles, fb, g, T, R, bc, Roff, count_hot, nbc, nT,
-                              hook ? a.ctl : nullptr, whole_next);
+    auto pick2 = [&](auto vv) {
+      return per == kAPerPlain ? pick(std::integral_constant<int, kAPerPlain>{}, vv) : pick(std::integral_constant<int, kAPer>{}, vv);
+    };
+    auto kern = hook ? pick2(std::true_type{}) : pick2(std::false_type{});
+    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, addr_a, val_a, a.err, bc, ct, ctstride,
+                              wbest, wpart, nbc, nT, vctl, whole_next);
   }
   HIPCHK(hipGetLastError());
-  s->bin_par ^= 1;  // this push's header is [hdr]; bin_count zeroed the other one for the next push
-  if (hook) {  // the verdict (and a rejected batch's cancel) and the head's apply, before any partition
+  s->bin_par ^= 1;  // this push's header is [hdr]; bin_part zeroed the other one for the next push
+  if (hook) {  // the verdict (and a rejected batch's cancel) and the head's apply, before anything is applied
     rc = (*hook)(bc, T, g.nb);
     if (rc) return rc;
   }
-  if (dedup) {
-    auto kern = a.part.kind == 0 ? (wide ? bin_part_dedup_kernel<V, MAT, 0, true> : bin_part_dedup_kernel<V, MAT, 0, false>)
-                                 : (wide ? bin_part_dedup_kernel<V, MAT, -1, true> : bin_part_dedup_kernel<V, MAT, -1, false>);
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, R, addr_a, val_a, a.err, bc, T,
-                              fitems, hot_tags, a.data, item, Roff, Bb, Ib, dump);
-  } else {
-    auto pick = [&](auto pp) {
-      constexpr int PP = decltype(pp)::value;
-      return a.part.kind == 0
-                 ? (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, 0, true> : bin_part_kernel<V, MAT, true, 0, false>)
-                               : (wide ? bin_part_kernel<V, MAT, false, 0, true, PP> : bin_part_kernel<V, MAT, false, 0, false, PP>))
-                 : (front == 1 ? (wide ? bin_part_kernel<V, MAT, true, -1, true> : bin_part_kernel<V, MAT, true, -1, false>)
-                               : (wide ? bin_part_kernel<V, MAT, false, -1, true, PP> : bin_part_kernel<V, MAT, false, -1, false, PP>));
-    };
-    auto kern = per == kAPerPlain ? pick(std::integral_constant<int, kAPerPlain>{}) : pick(std::integral_constant<int, kAPer>{});
-    kern<<<G, kATPB, 0, st>>>(a.keys, a.cols, a.vals, n, a.part, a.ctl, a.ntiles, fb, g, addr_a, val_a, a.err, bc, T,
-                              fitems, wbest, wpart, item, Roff, Bb, Ib, dump);
-  }
-  HIPCHK(hipGetLastError());
   if (front == 1) {
-    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data);
+    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, vctl);
     HIPCHK(hipGetLastError());
   }
+  bin_scan_kernel<<<g.nb, kScanTPB, 0, st>>>(g, ct, ctstride, n, a.ctl, a.ntiles, fb, kchunk, nstride, bc, T, Bb, Ib,
+                                             fitems, cwin, P, Q, item);
+  HIPCHK(hipGetLastError());
   // Groups of sparse slabs for vector shards; a matrix shard's sparse slabs stay units of their own: its
   // records cluster in a slab's few hot rows, and grouping cost cfg5 0.309 -> 0.337 ms while it takes
   // cfg3 1.077 -> 1.038 (profiles/r05/ab_group_unitcap.txt).
@@ -2139,12 +2215,12 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   if (fused) {
     bin_fsort_kernel<A, true, kSPerSmall><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
                                                                       off2, bhint, whint, (u32)n, Ib, done, units, runs,
-                                                                      group_on, item);
+                                                                      group_on, item, cwin, P, Q, nstride);
     HIPCHK(hipGetLastError());
   } else {
     bin_fsort_kernel<A, false, kSPerLarge><<<(unsigned)max_fitems, kSTPB, 0, st>>>(g, fitems, bc, T, Bb, addr_a, val_a, e_b, val_b,
                                                                        off2, bhint, whint, (u32)n, Ib, done, units, runs,
-                                                                       group_on, item);
+                                                                       group_on, item, cwin, P, Q, nstride);
     HIPCHK(hipGetLastError());
     bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on, item);
     HIPCHK(hipGetLastError());

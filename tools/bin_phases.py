@@ -20,7 +20,8 @@ PHASES = {
                              "clear+sync"]),
     "bin_part (dedup)": (8, ["setup", "hash insert", "issue loads", "sync+extract+sync", "rank+sync", "scan",
                              "stage+sync", "store+sync", "clear+sync", "hv clear+sync"]),
-    "bin_fsort (v2)": (32, ["load+sync", "rank+sync", "scan", "stage e+store", "values"]),
+    "bin_fsort (v2)": (32, ["window+clear", "marks+fill", "loads+sync", "rank+sync", "scan", "stage e+store",
+                            "values"]),
     "bin_plan (v2)": (48, ["stage+walk", "groups+scan", "atomic+sync", "emit+sync"]),
     "bin_apply2 (v2)": (56, ["records", "publish+sync", "prefetch issue", "write-back", "sync"]),
 }
