@@ -1044,12 +1044,10 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
   for (u32 base = 0; base < nch; base += (u32)kScanTPB * kScanPer) {  // kScanPer loads in flight
     u32 w[kScanPer];
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-      const u32 c = base + (u32)k * kScanTPB + tid;
-      w[k] = c < nch ? row[c] : 0u;
-    }
+    for (int k = 0; k < kScanPer; ++k)  // (clamped, unconditional loads: all in flight together)
+      w[k] = row[min(base + (u32)k * kScanTPB + tid, nch - 1u)];
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) s += w[k] >> 16;
+    for (int k = 0; k < kScanPer; ++k) s += base + (u32)k * kScanTPB + tid < nch ? w[k] >> 16 : 0u;
   }
   const u32 tb = block_sum<kScanTPB>(s);
   const u32 J = bucket_items(tb, item);
@@ -1072,8 +1070,10 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
     u32 w[kScanPer];
     u32 sum = 0;
 #pragma unroll
+    for (int k = 0; k < kScanPer; ++k) w[k] = row[min(c0 + k, nch - 1u)];
+#pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      w[k] = c0 + k < nch ? row[c0 + k] : 0u;
+      if (c0 + k >= nch) w[k] = 0u;
       sum += w[k] >> 16;
     }
     u32 incl = sum;
@@ -1422,21 +1422,25 @@ __device__ __forceinline__ u32 opaque(u32 x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-// Forward fill of rid[x0, x1) (<= TPB * 16 entries, 0 = no mark): every entry becomes the last mark at
-// or before it (marks increase with x, so this is an inclusive max-scan)
+// Forward fill of rid[0, x1) (<= TPB * 16 entries, 0 = no mark; the array holds whole blocks of 16):
+// every entry becomes the last mark at or before it (marks increase with x, so this is an inclusive
+// max-scan). 16 entries per thread, read and written as two 16-byte LDS accesses.
 template <int TPB>
-__device__ __forceinline__ void fill_forward(uint16_t* rid, u32 x0, u32 x1) {
+__device__ __forceinline__ void fill_forward(uint16_t* rid, u32 x1) {
   constexpr int kPer = 16;
   __shared__ u32 wmax[TPB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const u32 b0 = x0 + (u32)tid * kPer;
-  u32 v[kPer];
+  const u32 b0 = (u32)tid * kPer;
+  const bool mine = b0 < x1;
+  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+  if (mine) {
+    q0 = reinterpret_cast<const uint4*>(rid + b0)[0];
+    q1 = reinterpret_cast<const uint4*>(rid + b0)[1];
+  }
+  u32 h[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};  // two u16 per word, low first
   u32 m = 0;
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    v[k] = b0 + k < x1 ? (u32)rid[b0 + k] : 0u;
-    m = max(m, v[k]);
-  }
+  for (int k = 0; k < 8; ++k) m = max(m, max(h[k] & 0xFFFFu, h[k] >> 16));
   u32 incl = m;
 #pragma unroll
   for (int dd = 1; dd < 64; dd <<= 1) {
@@ -1449,9 +1453,14 @@ __device__ __forceinline__ void fill_forward(uint16_t* rid, u32 x0, u32 x1) {
   if (lane == 0) run = 0;
   for (int w2 = 0; w2 < wid; ++w2) run = max(run, wmax[w2]);
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    run = max(run, v[k]);
-    if (b0 + k < x1) rid[b0 + k] = (uint16_t)run;
+  for (int k = 0; k < 8; ++k) {
+    const u32 lo = run = max(run, h[k] & 0xFFFFu);
+    const u32 hi = run = max(run, h[k] >> 16);
+    h[k] = lo | (hi << 16);
+  }
+  if (mine) {
+    reinterpret_cast<uint4*>(rid + b0)[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    reinterpret_cast<uint4*>(rid + b0)[1] = make_uint4(h[4], h[5], h[6], h[7]);
   }
   __syncthreads();
 }
@@ -1523,7 +1532,7 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
   // those of its first and last records, at most kFWin) go to LDS; every chunk's run marks its first record
   // of the item with its window slot, a forward fill gives every record its run, and the record's index
   // follows (recomputed where the values load: the marks and places stay in LDS, not in registers).
-  static_assert((kFWin + 1) * 4 <= kStage && kSItemMax <= 16 * kSTPB && kFWin < 65536 && kSItemMax <= 65536,
+  static_assert((kFWin + 1) * 4 <= kStage && kSItemMax <= 16 * kSTPB && kFWin < 65536 && kSItemMax % 16 == 0,
                 "the window's prefixes fit the stage; fill_forward's 16 per thread; u16 marks and places");
   uint16_t* const rid = reinterpret_cast<uint16_t*>(stage + kStage);
   u32* const Qw = reinterpret_cast<u32*>(stage + kStage + 2 * kSItemMax);
@@ -1535,12 +1544,17 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
   const bool slow = span > kFWin;  // workgroup-uniform: the item spans more chunks than the window holds
   if (!slow) {
     u32* const Pw = reinterpret_cast<u32*>(stage);  // (the stage is free until the ranking)
-    for (u32 t = tid; t < span; t += kSTPB) {
-      Pw[t] = Pb[cw.x + t];
-      Qw[t] = Qb[cw.x + t];
+    static_assert(kFWin == 2 * kSTPB, "two window entries per thread");
+    {  // (clamped, unconditional loads: all four in flight together)
+      const u32 t0 = tid, t1 = tid + kSTPB;
+      const u32 p0 = Pb[cw.x + min(t0, span)], p1 = Pb[cw.x + min(t1, span)];  // (P[b][c] up to c = nch)
+      const u32 q0 = Qb[cw.x + min(t0, span - 1)], q1 = Qb[cw.x + min(t1, span - 1)];
+      if (t0 <= span) Pw[t0] = p0;
+      if (t1 <= span) Pw[t1] = p1;
+      if (t0 < span) Qw[t0] = q0;
+      if (t1 < span) Qw[t1] = q1;
     }
-    if (tid == 0) Pw[span] = Pb[cw.x + span];  // (<= P[b][nch])
-    for (u32 x = tid; x < cnt; x += kSTPB) rid[x] = 0;
+    for (u32 x = tid * 8u; x < cnt; x += kSTPB * 8u) reinterpret_cast<uint4*>(rid + x)[0] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     ph.mark(32);
     for (u32 t = tid; t < span; t += kSTPB) {
@@ -1548,14 +1562,16 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
       if (lo < hi) rid[lo - v0] = (uint16_t)(t + 1);
     }
     __syncthreads();
-    fill_forward<kSTPB>(rid, 0u, cnt);
+    fill_forward<kSTPB>(rid, cnt);
     ph.mark(33);
   }
   // record x of the item: its index in the partition buffer (slow: a binary search over the bucket's
-  // whole prefix row, for an item spread so thin over the chunks that its window would not hold it)
-  auto pos_of = [&](u32 x) -> u32 {
+  // prefix row between the item's first and last chunks, for an item spread so thin over the chunks that
+  // its window would not hold it). The two are separate code paths (a search loop's loads in the same
+  // path would make every record wait for the loads of the one before).
+  auto pos_fast = [&](u32 x) -> u32 { return Qw[rid[x] - 1u] + v0 + x; };
+  auto pos_slow = [&](u32 x) -> u32 {
     const u32 v = v0 + x;
-    if (!slow) return Qw[rid[x] - 1u] + v;
     u32 lo = cw.x, hi = cw.y + 1;  // P[lo] <= v < P[hi]
     while (hi - lo > 1) {
       const u32 m = (lo + hi) >> 1;
@@ -1564,20 +1580,22 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
     }
     return Qb[lo] + v;
   };
-  // (kLate: the values are loaded only in their staging rounds, not held through the ranking -- the
-  // registers of 16 records per thread then fit two workgroups per CU; cfg5 0.3118 -> 0.3073 ms,
-  // profiles/r06/ab_fsort_late.txt)
+  // (kLate: the values are loaded only in their staging rounds, not held through the ranking)
   constexpr bool kLate = GLINT_FSORT_LATE_TRY && kSPer > 8;
   u32 a[kSPer];
   A v[kLate ? 1 : kSPer];
+  auto load_item = [&](auto pos_of) {
 #pragma unroll
-  for (int q = 0; q < kSPer; ++q) {  // the whole item in flight at once
-    const u32 x = q * kSTPB + opaque(tid);
-    const bool on = (u32)q * kSTPB < item && x < cnt;
-    const u32 ps = on ? pos_of(x) : 0u;
-    a[q] = on ? ld_mid(addr_in + ps) : kEmptySlot;
-    if constexpr (!kLate) v[q] = on ? ld_mid(val_in + ps) : A(0);
-  }
+    for (int q = 0; q < kSPer; ++q) {  // the whole item in flight at once
+      const u32 x = q * kSTPB + opaque(tid);
+      const bool on = (u32)q * kSTPB < item && x < cnt;
+      const u32 ps = on ? pos_of(x) : 0u;
+      a[q] = on ? ld_mid(addr_in + ps) : kEmptySlot;
+      if constexpr (!kLate) v[q] = on ? ld_mid(val_in + ps) : A(0);
+    }
+  };
+  if (slow) load_item(pos_slow);
+  else load_item(pos_fast);
   __syncthreads();
   ph.mark(34);
   // the slab counts, then (after the scan) each record's place in the item's slab order from a second
@@ -1629,7 +1647,7 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
           const int q = q0 + k;
           lv[k] = A(0);
           if ((u32)q * kSTPB < item && p[q] != kEmptySlot && p[q] - r0 < kStageV)
-            lv[k] = ld_mid(val_in + pos_of(q * kSTPB + tid));
+            lv[k] = ld_mid(val_in + (slow ? pos_slow(q * kSTPB + tid) : pos_fast(q * kSTPB + tid)));
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
