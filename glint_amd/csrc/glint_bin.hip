@@ -1062,34 +1062,35 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
   const u32 ib = base2[1];
   u32* const Pb = P + (size_t)b * (nstride + 1);
   u32* const Qb = Q + (size_t)b * nstride;
-  // tiles of kScanTPB x kScanPer chunks: every thread's kScanPer entries in registers, scanned, then only
-  // stores (a load between stores would wait for them: one counter for both)
+  // tiles of kScanTPB x kScanPer chunks, column k of a tile = chunks base + k kScanTPB + tid (coalesced
+  // loads and stores): every column's entries in registers, each column scanned across the workgroup
+  // (one barrier for all of them), then only stores (a load between stores would wait for them: one
+  // counter for both)
+  __shared__ u32 wtk[kScanPer][kScanTPB / 64];
   u32 carry = 0, clast = 0;
   for (u32 base = 0; base < nch; base += (u32)kScanTPB * kScanPer) {
-    const u32 c0 = base + (u32)tid * kScanPer;
-    u32 w[kScanPer];
-    u32 sum = 0;
+    u32 w[kScanPer], incl[kScanPer];
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) w[k] = row[min(c0 + k, nch - 1u)];
+    for (int k = 0; k < kScanPer; ++k) w[k] = row[min(base + (u32)k * kScanTPB + tid, nch - 1u)];
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      if (c0 + k >= nch) w[k] = 0u;
-      sum += w[k] >> 16;
-    }
-    u32 incl = sum;
+      if (base + (u32)k * kScanTPB + tid >= nch) w[k] = 0u;
+      const u32 cnt = w[k] >> 16;
+      incl[k] = cnt;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const u32 y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
+      for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(incl[k], d);
+        if (lane >= d) incl[k] += y;
+      }
+      if (lane == 63) wtk[k][wid] = incl[k];
     }
-    if (lane == 63) wt[wid] = incl;
     __syncthreads();
-    u32 pre, tot;
-    wave_totals<kScanTPB / 64>(wt, lane, wid, pre, tot);
-    u32 run = carry + pre + incl - sum;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      const u32 c = c0 + k, cnt = w[k] >> 16;
+      u32 pre, tot;
+      wave_totals<kScanTPB / 64>(wtk[k], lane, wid, pre, tot);
+      const u32 c = base + (u32)k * kScanTPB + tid, cnt = w[k] >> 16;
+      const u32 run = carry + pre + incl[k] - cnt;
       if (c < nch) {
         Pb[c] = run;
         Qb[c] = c * kchunk + (w[k] & 0xFFFFu) - run;
@@ -1103,9 +1104,8 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
         }
         for (u32 k1 = (run + item) / item; k1 * item <= run + cnt; ++k1) cwin[ib + k1 - 1].y = c;
       }
-      run += cnt;
+      carry += tot;
     }
-    carry += tot;
     __syncthreads();
   }
   const u32 cl = block_max<kScanTPB>(clast);  // the bucket's last chunk with records
@@ -1413,10 +1413,7 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
 #ifndef GLINT_VALIDATE_PER8
 #define GLINT_VALIDATE_PER8 1
 #endif
-#ifndef GLINT_FSORT_LATE_TRY
-#define GLINT_FSORT_LATE_TRY 0
-#endif
-constexpr u32 kStage = 32768;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
+constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
 // A value the compiler must recompute where it is used (not hoist and hold in a register across a loop)
 __device__ __forceinline__ u32 opaque(u32 x) {
   asm volatile("" : "+v"(x));
@@ -1477,8 +1474,11 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
                                                           const u32* __restrict__ P, const u32* __restrict__ Q,
                                                           u32 nstride) {
   constexpr u32 kStageV = kStage / (u32)sizeof(A);   // values per round
-  // [hist | stage | the item's run marks (u16 per record) | its window of chunk places Q]
-  constexpr size_t kSortLds = 4 * kMaxDigit + kStage + 2 * kSItemMax + 4 * kFWin;
+  // [hist | stage]; until the ranking the stage holds the item's window of chunk prefixes P and places Q
+  // and its run marks (u16 per record)
+  constexpr size_t kSortLds = 4 * kMaxDigit + kStage;
+  constexpr u32 kOffQ = ((kFWin + 1) * 4 + 255) / 256 * 256, kOffRid = kOffQ + 4 * kFWin;
+  static_assert(kOffRid + 2 * kSItemMax <= kStage, "the window and the marks overlay the stage");
   typedef PlanLds<kPlanLdsFused, kPlanPTabFused> FusedPlanLds;
   constexpr size_t kLds = FUSED && sizeof(FusedPlanLds) > kSortLds ? sizeof(FusedPlanLds) : kSortLds;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
@@ -1498,7 +1498,25 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
   const u32 it = blockIdx.x;
   if (it >= bc->nfitems) return;  // the grid is the item count's upper bound
   const uint2 d = fitems[it];
+  const uint2 cw = cwin[it];  // the chunks of the item's first and last records
   const u32 b = d.x;
+  const u32* const Pb = P + (size_t)b * (nstride + 1);
+  const u32* const Qb = Q + (size_t)b * nstride;
+  const u32 span = cw.y - cw.x + 1;
+  const bool slow = span > kFWin;  // workgroup-uniform: the item spans more chunks than the window holds
+  u32* const Pw = reinterpret_cast<u32*>(stage);  // (the stage is free until the ranking)
+  u32* const Qw = reinterpret_cast<u32*>(stage + kOffQ);
+  uint16_t* const rid = reinterpret_cast<uint16_t*>(stage + kOffRid);
+  static_assert(kFWin == 2 * kSTPB, "two window entries per thread");
+  {  // the window's loads first (in flight with the bucket's T and Bb); clamped, unconditional
+    const u32 t0 = tid, t1 = tid + kSTPB, sp = min(span, kFWin);
+    const u32 p0 = Pb[cw.x + min(t0, sp)], p1 = Pb[cw.x + min(t1, sp)];  // (P[b][c] up to c = nch)
+    const u32 q0 = Qb[cw.x + min(t0, sp - 1)], q1 = Qb[cw.x + min(t1, sp - 1)];
+    if (t0 <= sp) Pw[t0] = p0;
+    if (t1 <= sp) Pw[t1] = p1;
+    if (t0 < sp) Qw[t0] = q0;
+    if (t1 < sp) Qw[t1] = q1;
+  }
   const u32 s0 = Bb[b] + d.y * item, s1 = Bb[b] + min(T[b], (d.y + 1) * item);
   const u32 nf1 = g.nf + 1;
   u32* const orow = off2 + (size_t)it * nf1;
@@ -1532,28 +1550,10 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
   // those of its first and last records, at most kFWin) go to LDS; every chunk's run marks its first record
   // of the item with its window slot, a forward fill gives every record its run, and the record's index
   // follows (recomputed where the values load: the marks and places stay in LDS, not in registers).
-  static_assert((kFWin + 1) * 4 <= kStage && kSItemMax <= 16 * kSTPB && kFWin < 65536 && kSItemMax % 16 == 0,
-                "the window's prefixes fit the stage; fill_forward's 16 per thread; u16 marks and places");
-  uint16_t* const rid = reinterpret_cast<uint16_t*>(stage + kStage);
-  u32* const Qw = reinterpret_cast<u32*>(stage + kStage + 2 * kSItemMax);
+  static_assert(kSItemMax <= 16 * kSTPB && kFWin < 65536 && kSItemMax % 16 == 0,
+                "fill_forward's 16 per thread; u16 marks and window slots");
   const u32 v0 = d.y * item;
-  const u32* const Pb = P + (size_t)b * (nstride + 1);
-  const u32* const Qb = Q + (size_t)b * nstride;
-  const uint2 cw = cwin[it];  // the chunks of the item's first and last records
-  const u32 span = cw.y - cw.x + 1;
-  const bool slow = span > kFWin;  // workgroup-uniform: the item spans more chunks than the window holds
   if (!slow) {
-    u32* const Pw = reinterpret_cast<u32*>(stage);  // (the stage is free until the ranking)
-    static_assert(kFWin == 2 * kSTPB, "two window entries per thread");
-    {  // (clamped, unconditional loads: all four in flight together)
-      const u32 t0 = tid, t1 = tid + kSTPB;
-      const u32 p0 = Pb[cw.x + min(t0, span)], p1 = Pb[cw.x + min(t1, span)];  // (P[b][c] up to c = nch)
-      const u32 q0 = Qb[cw.x + min(t0, span - 1)], q1 = Qb[cw.x + min(t1, span - 1)];
-      if (t0 <= span) Pw[t0] = p0;
-      if (t1 <= span) Pw[t1] = p1;
-      if (t0 < span) Qw[t0] = q0;
-      if (t1 < span) Qw[t1] = q1;
-    }
     for (u32 x = tid * 8u; x < cnt; x += kSTPB * 8u) reinterpret_cast<uint4*>(rid + x)[0] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     ph.mark(32);
@@ -1580,10 +1580,8 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
     }
     return Qb[lo] + v;
   };
-  // (kLate: the values are loaded only in their staging rounds, not held through the ranking)
-  constexpr bool kLate = GLINT_FSORT_LATE_TRY && kSPer > 8;
   u32 a[kSPer];
-  A v[kLate ? 1 : kSPer];
+  A v[kSPer];
   auto load_item = [&](auto pos_of) {
 #pragma unroll
     for (int q = 0; q < kSPer; ++q) {  // the whole item in flight at once
@@ -1591,7 +1589,7 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
       const bool on = (u32)q * kSTPB < item && x < cnt;
       const u32 ps = on ? pos_of(x) : 0u;
       a[q] = on ? ld_mid(addr_in + ps) : kEmptySlot;
-      if constexpr (!kLate) v[q] = on ? ld_mid(val_in + ps) : A(0);
+      v[q] = on ? ld_mid(val_in + ps) : A(0);
     }
   };
   if (slow) load_item(pos_slow);
@@ -1638,28 +1636,9 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
   ph.mark(37);
   A* const stv = reinterpret_cast<A*>(stage);
   for (u32 r0 = 0; r0 < total; r0 += kStageV) {  // the values, kStageV per round
-    if constexpr (kLate) {
 #pragma unroll
-      for (int q0 = 0; q0 < kSPer; q0 += 4) {  // four loads in flight per thread, then their LDS stores
-        A lv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = q0 + k;
-          lv[k] = A(0);
-          if ((u32)q * kSTPB < item && p[q] != kEmptySlot && p[q] - r0 < kStageV)
-            lv[k] = ld_mid(val_in + (slow ? pos_slow(q * kSTPB + tid) : pos_fast(q * kSTPB + tid)));
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = q0 + k;
-          if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = lv[k];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < kSPer; ++q)
-        if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
-    }
+    for (int q = 0; q < kSPer; ++q)
+      if (p[q] != kEmptySlot && p[q] - r0 < kStageV) stv[p[q] - r0] = v[q];
     __syncthreads();
     constexpr int kRound = (int)(kStageV / kSTPB);
 #pragma unroll
