@@ -9,20 +9,23 @@
 // in LDS and written back with one coalesced read-modify-write of the touched element pairs.
 // Nothing is reserved across workgroups at run time: every writer owns its output range.
 //
-//   bin_count   per partition workgroup w: records per coarse bucket of w's chunks -> R[w][b]; its add
-//               to the bucket total T[b] returns where w's records of b start inside the bucket
-//               (Roff[w][b]), so every bucket is one contiguous range of the partition buffer.
-//   bin_part    per 8192-record chunk (optionally after summing duplicate elements in an LDS hash
-//               table), the chunk's records ranked by bucket in LDS and appended to the bucket ranges
-//               as runs (u32 address + value).
-//   bin_fsort   per fine item (<= 16384 records of one bucket): ranked by slab in LDS and written back
-//               slab-sorted (u16 slab offset + value), with the item's per-slab offsets (off2).
+//   bin_part    per 4096- or 8192-record chunk c of the tail (optionally after summing duplicate
+//               elements in an LDS hash table): the chunk's records ranked by bucket in LDS and stored
+//               to the chunk's own range of the partition buffer (u32 address + value), grouped by
+//               bucket, with the chunk's column of the chunk table ct[b][c] (run start | length). No
+//               count pass: every chunk's output is one contiguous range.
+//   bin_scan    per bucket: its chunk prefixes P[b][c] and places Q[b][c] (record v of the bucket is at
+//               Q[b][c] + v), its total, output range and fine items (each with the chunks of its first
+//               and last records).
+//   bin_fsort   per fine item (<= 12288 records of one bucket, gathered from its chunks' runs): ranked by
+//               slab in LDS and written slab-sorted (u16 slab offset + value) to the item's own range,
+//               with the item's per-slab offsets (off2).
 //   bin_plan    per bucket: every slab's runs (one per item) cut into apply units (fused into
 //               bin_fsort for small pushes).
 //   bin_apply2  per apply unit: LDS accumulation of the slab, coalesced RMW of the touched lines
 //               (units of a slab cut into several flush with device atomics instead).
-// Record indices are u32 (a push of < 2^32 records); buffer offsets are 64-bit wherever a push's
-// buffers pass 4 GiB (WIDE partition stores).
+// Record indices are u32 (a push of < 2^32 records); a partition chunk's stores go through a buffer
+// window at its own range, and the fine sort's gathers are 64-bit addressed, so buffers may pass 4 GiB.
 #include "glint_device.h"
 #include "glint_host.h"
 
@@ -135,7 +138,7 @@ struct PhaseClock {
 // two neighbouring runs share stay in L2 for the unit of the next slab (XCD-grouped unit order). Same box,
 // two rounds (profiles/r06/ab_nt_mid.txt), with the per-push fine item size below: cfg4b exchange 2.42 ms
 // non-temporal -> 2.20 cached (round 5: 2.37), cfg3 1.055 -> 1.046, cfg5 0.318 -> 0.315.
-// (build-time knobs: GLINT_BIN_NT for the push's own records, read by bin_count / bin_part;
+// (build-time knobs: GLINT_BIN_NT for the push's own records, read by bin_part;
 // GLINT_BIN_NT_MID for the intermediates)
 #ifndef GLINT_BIN_NT
 #define GLINT_BIN_NT 1
@@ -352,11 +355,11 @@ __device__ __forceinline__ u32 hot_mix(u32 x) {  // murmur3 fmix32
 
 constexpr int kWideSlots = 8192;  // the plain + hot front end's hot table (see bin_hot_select)
 __device__ __forceinline__ u32 wide_slot(u32 a) { return hot_mix(a) & (kWideSlots - 1); }
-// The verdict of a validating gated push whose tail is binned (after bin_count validated the tail and
+// The verdict of a validating gated push whose tail is binned (after bin_part validated the tail and
 // push_check the records before the break): 0 or ~(first rejected record) to the caller's gate word; a
 // rejected batch is cancelled before anything is applied -- no head (push_apply sees cancel), no tail
-// (the break is cleared, so every binned kernel sees an empty tail, and the counts already taken are
-// zeroed, so no fine item reads the partition buffer).
+// (the break is cleared / cancel set, so bin_scan sees an empty tail and every bucket empty, and
+// bin_hot_reduce drops the partition's hot sums). T is zeroed here too (bin_scan rewrites it).
 __global__ __launch_bounds__(256) void push_validate_gate_binned_kernel(LaunchCtl* ctl, u64* gate, BinCtl* bc,
                                                                         u32* __restrict__ T, u32 nb) {
   const u64 b = ctl->bad;
@@ -530,7 +533,7 @@ __device__ __forceinline__ u32 part_emit(const u32 (&ad)[P], const A (&va)[P], u
 __device__ __forceinline__ void part_next_header(const BinGeom& g, BinCtl* next_bc, u32* __restrict__ next_T,
                                                  LaunchCtl* next_ctl) {
   const int tid = threadIdx.x;
-  for (u32 b = tid; b < g.nb; b += kATPB) {
+  for (u32 b = tid; b < kMaxDigit; b += kATPB) {  // (every slot: the next push may have more buckets)
     next_T[b] = 0;
     next_T[kMaxDigit + b] = 0;  // the fused plan's per-bucket item counters
   }
@@ -1033,7 +1036,6 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
                                                             uint2* __restrict__ fitems, uint2* __restrict__ cwin,
                                                             u32* __restrict__ P, u32* __restrict__ Q, u32 item) {
   __shared__ u32 base2[2];
-  __shared__ u32 wt[kScanTPB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 b = blockIdx.x;
   const i64 r0 = tail_start(lctl, ntiles, from_break, n);
@@ -1407,12 +1409,6 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
 // (plan_bucket<true>), so no plan launch follows and the buckets' plans overlap the other items' sorts.
-#ifndef GLINT_SMALL_PER8
-#define GLINT_SMALL_PER8 0
-#endif
-#ifndef GLINT_VALIDATE_PER8
-#define GLINT_VALIDATE_PER8 1
-#endif
 constexpr u32 kStage = 65536;  // bin_fsort: bytes of the item's u16 offsets, then its values in rounds
 // A value the compiler must recompute where it is used (not hoist and hold in a register across a loop)
 __device__ __forceinline__ u32 opaque(u32 x) {
@@ -1976,11 +1972,11 @@ int resident_per_cu(K kernel, int tpb, size_t dyn_lds = 0) {
 #define GLINT_BIN_CB 7  // (build-time knob: coarse digit bits at least)
 #endif
 constexpr u32 kCoarseBitsMin = GLINT_BIN_CB;
-BinGeom bin_geometry(i64 elems) {
+BinGeom bin_geometry(i64 elems, u32 cbmin) {
   const i64 slabs = (elems + kSlab - 1) / kSlab;
   u32 sb = 0;
   while (((i64)1 << sb) < slabs) ++sb;
-  const u32 cb = std::min<u32>(sb, std::max<u32>(kCoarseBitsMin, sb > 10u ? sb - 10u : 0u));
+  const u32 cb = std::min<u32>(sb, std::max<u32>(cbmin, sb > 10u ? sb - 10u : 0u));
   BinGeom g;
   g.fb = sb - cb;
   g.nb = 1u << cb;
@@ -2045,7 +2041,6 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   typedef typename LdsAcc<V>::T A;
   const i64 n = a.n;
   if (!push_binnable(s, n)) return GLINT_EINVAL;
-  const BinGeom g = bin_geometry(s->elems);
   const int front = bin_front(s);
   const bool dedup = front == 2;
   bool hot_refresh = true;
@@ -2055,9 +2050,16 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
   }
   s->bin_last_front = front;
   // a small push (at most ~4 fine items per CU, cfg5) plans its buckets inside bin_fsort
-  const bool small_push = (i64)g.nb + n / ((i64)kSTPB * kSPerSmall) + 1 <= (i64)4 * s->cus;
-  // records per thread of a partition chunk (a validating push loads whole keys: 8 per thread would spill)
-  const int per = front == 0 && (!small_push || GLINT_SMALL_PER8) && (!hook || GLINT_VALIDATE_PER8) ? kAPerPlain : kAPer;
+  const bool small_push =
+      (i64)bin_geometry(s->elems, kCoarseBitsMin).nb + n / ((i64)kSTPB * kSPerSmall) + 1 <= (i64)4 * s->cus;
+  // records per thread of a partition chunk: 8 for a large push's plain front end, 4 otherwise (the hot
+  // and dedup tables share the LDS; a small push wants more chunks)
+  const int per = front == 0 && !small_push ? kAPerPlain : kAPer;
+  // Coarse buckets: 128 for chunks of 8 records per thread, 64 for chunks of 4 -- runs of ~64 records
+  // per bucket and chunk either way, which the fine sort gathers. Same box, 2 rounds
+  // (profiles/r06/ab_chunk_local.txt): 64 buckets for every push took cfg5 0.316 -> 0.303 ms and cfg3
+  // 0.965 -> 0.956, but cfg4b (8-record chunks) 1.85 -> 1.93.
+  const BinGeom g = bin_geometry(s->elems, per == kAPerPlain ? kCoarseBitsMin : kCoarseBitsMin - 1u);
   const u32 kchunk = (u32)kATPB * (u32)per;
   const i64 nchunks_max = (n + kchunk - 1) / kchunk;
   // partition workgroups per CU: what fits at once (the hot front end's LDS table allows fewer)
