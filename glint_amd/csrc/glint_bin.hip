@@ -1123,26 +1123,26 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
 }
 
 // ==== v2 fine stage: one sort pass per fine item, a plan per bucket, an apply that gathers runs =========
-// After the coarse partition (bucket b = the contiguous range [Bb[b], Bb[b] + T[b]) of the partition
-// buffer, no holes but the dedup front end's marked ones), bucket b is cut into fine items of 8 or 16 x 1024
-// records in bucket order. bin_fsort loads one item with every load in flight, ranks its records by fine
-// digit (slab of the bucket) in LDS and writes them back IN PLACE of the item's range (other buffers),
-// sorted by slab, with the item's slab offsets off2[item][0..nf] -- no count pass, no global cursor,
-// contiguous reads and whole-wave stores. A slab's records are then one run per item of its bucket
-// (~32 records for uniform keys into 2^28). bin_plan (one workgroup per bucket) reads the bucket's off2
-// rows and cuts every slab's runs into apply units of <= kUnitCap records at item boundaries (a slab with
-// one unit is exclusive: plain read-modify-write; a hot slab's units flush with device atomics).
-// bin_apply2 sums a unit's runs in LDS and writes the slab back as bin_apply does.
+// After the chunk-local partition and bin_scan (bucket b = its runs in chunk order, one per chunk;
+// record v of the bucket at partition index Q[b][c] + v), bucket b is cut into fine items of 12 x 1024
+// records in bucket order. bin_fsort gathers one item's records from its chunks' runs with every load in
+// flight, ranks them by fine digit (slab of the bucket) in LDS and writes them to the item's own range
+// [Bb[b] + j item, ...) of the fine buffers, sorted by slab, with the item's slab offsets
+// off2[item][0..nf] -- no global cursor, whole-wave stores. A slab's records are then one run per item
+// of its bucket. bin_plan (one workgroup per bucket) reads the bucket's off2 rows and cuts every slab's
+// runs into apply units of <= kUnitCap records at item boundaries (a slab with one unit is exclusive:
+// plain read-modify-write; a hot slab's units flush with device atomics). bin_apply2 sums a unit's runs
+// in LDS and writes the slab back.
 #ifndef GLINT_FSORT_TPB
 #define GLINT_FSORT_TPB 1024
 #endif
-// Records per thread of a fine item: 16 for every push (items of 16384 records: fewer, longer runs per
-// slab for the apply and half the plan's rows of 8 per thread), at two workgroups per CU -- the values
-// are loaded only in their staging rounds (kLate in bin_fsort_kernel), so one workgroup's loads are in
-// flight while the other ranks and stores. Same box, 16 against 8 per thread for large pushes
-// (profiles/r06/ab_fsort_per16.txt): cfg4b 2.170 -> 2.139 ms, cfg3 1.039 -> 1.030 (held in registers
-// at one workgroup per CU, 16 had measured slower: ab_nt_mid.txt s16). Build-time knobs
-// GLINT_FSORT_PER_SMALL / _LARGE (small: the pushes with the plan fused in, see push_binned).
+// Records per thread of a fine item: 12 for every push, the values held in registers from their load to
+// their staging round (two rounds of 8192 through the 64 KiB stage), at two workgroups per CU (64
+// VGPRs). Same boxes (profiles/r06/ab_chunk_local.txt): 16 per thread with the values loaded again in
+// each staging round measured cfg4b 2.10 against 1.89 ms, cfg3 1.06 against 0.99; 8 per thread 1.92 /
+// 0.99 / cfg5 0.339 against 0.328. (Before the chunk-local partition, with contiguous items, 16 late
+// had been the best: ab_fsort_per16.txt.) Build-time knobs GLINT_FSORT_PER_SMALL / _LARGE (small: the
+// pushes with the plan fused in, see push_binned).
 #ifndef GLINT_FSORT_PER_SMALL
 #define GLINT_FSORT_PER_SMALL 12
 #endif
@@ -1985,9 +1985,13 @@ BinGeom bin_geometry(i64 elems, u32 cbmin) {
   return g;
 }
 
-// u32 record indices and element addresses
+// u32 record indices and element addresses. (Then the chunk table -- nb <= 1024 rows of
+// ceil(n / 4096) + 1 u32 -- stays below 2^32 bytes: one buffer window in bin_part.)
+constexpr u64 kBinMaxRecs = (1ull << 32) - 2ull * kATPB * (kAPer > kAPerPlain ? kAPer : kAPerPlain);
+static_assert((u64)kATPB * (u64)kAPer >= 4096 && (u64)kMaxDigit * ((kBinMaxRecs + 4095) / 4096 + 1) * 4 < (1ull << 32),
+              "the chunk table's window: chunks of >= 4096 records");
 bool push_binnable(const glint_shard* s, i64 n) {
-  return n < ((i64)1 << 32) - 2 * (i64)kATPB * (kAPer > kAPerPlain ? kAPer : kAPerPlain) && s->elems < ((i64)1 << 32) - 1;
+  return (u64)n < kBinMaxRecs && s->elems < ((i64)1 << 32) - 1;
 }
 
 int launch_validate_gate_binned(LaunchCtl* ctl, u64* gate, void* bc, u32* T, u32 nb, hipStream_t st) {
