@@ -32,15 +32,19 @@ SHAPES = {
     "push_apply": (["ld16"], ["st16"]),
     "push_scatter": (["ld8", "*gather8"], ["*atomic8"]),
     "bin_count": (["ld4s8", "ld4"], []),
-    "bin_part": (["ld4s8", "ld8", "ld4"], ["*st4runs", "*st8runs"]),
-    "bin_part_dedup": (["ld4s8", "ld8", "ld4"], ["*st4runs", "*st8runs"]),
+    # (round 6: the chunk-local partition stores each chunk as one contiguous range; bin_scan reads the
+    # chunk table's bucket rows and writes each bucket's prefix / place rows)
+    "bin_part": (["ld4s8", "ld8", "ld4"], ["st4", "st8"]),
+    "bin_part_dedup": (["ld4s8", "ld8", "ld4"], ["st4", "st8"]),
+    "bin_scan": (["ld4"], ["st4"]),
     "bin_fcount": (["ld4"], []),
     "bin_fpart": (["ld4", "ld8"], ["*st4runs", "*st8runs"]),
     "bin_apply": (["ld4", "ld8", "rmw16"], ["rmw16"]),
     "bin_hot": (["ld8"], ["st8"]),
-    # v2 fine stage: the item sort reads its item contiguously and writes it back (u16 offsets, values)
-    # as whole-wave runs; the apply gathers ~16-32-record runs per item and read-modify-writes lines
-    "bin_fsort": (["ld4", "ld8"], ["st8"]),
+    # v2 fine stage: the item sort gathers its item from its chunks' runs (~64 records each) and writes
+    # it (u16 offsets, values) as whole-wave runs; the apply gathers ~16-32-record runs per item and
+    # read-modify-writes lines
+    "bin_fsort": (["*ld4", "*ld8"], ["st8"]),
     "bin_plan": (["ld4"], ["st8"]),
     "bin_apply2": (["*ld4", "*ld8", "rmw16"], ["rmw16"]),
     # one push over several shards (glint_vec_push_dev_shards): the key check streams the keys, the
@@ -97,11 +101,13 @@ def main():
     kernels = {}
     total = 0.0
     # pushes profiled: the most dispatched of the kernels that run once per push -- push_check (the
-    # checked path), bin_count (every binned push; whole-push bins run no check) and push_scatter (a
+    # checked path), bin_scan (every binned push, bin_count before round 6; whole-push bins run no
+    # check) and push_scatter (a
     # whole-push scatter runs alone) -- (the apply may run once per window of records, so a kernel's
     # bytes per push = its mean per dispatch x dispatches / pushes)
     once = [c for k, c in nf.items()
-            if k.startswith(("glint::push_check_kernel", "glint::bin_count_kernel", "glint::push_scatter_kernel",
+            if k.startswith(("glint::push_check_kernel", "glint::bin_count_kernel", "glint::bin_scan_kernel",
+                             "glint::push_scatter_kernel",
                              "glint::set_scatter_kernel"))]
     pushes = max(once) if once else max(list(nf.values()) + [1])
     for name in sorted(set(fetch) | set(write)):
