@@ -1143,6 +1143,9 @@ __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32
 // 0.99 / cfg5 0.339 against 0.328. (Before the chunk-local partition, with contiguous items, 16 late
 // had been the best: ab_fsort_per16.txt.) Build-time knobs GLINT_FSORT_PER_SMALL / _LARGE (small: the
 // pushes with the plan fused in, see push_binned).
+#ifndef GLINT_PLAN_SPLIT
+#define GLINT_PLAN_SPLIT 2
+#endif
 #ifndef GLINT_FSORT_PER_SMALL
 #define GLINT_FSORT_PER_SMALL 12
 #endif
@@ -1404,7 +1407,11 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
                                                             int group_on, u32 item) {
   typedef PlanLds<kPlanLds, kPlanPTab> PL;
   __shared__ PL L;
-  plan_bucket<false, PL, kPlanTPB>(blockIdx.x, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item, 0u, g.nf);
+  constexpr u32 kS = GLINT_PLAN_SPLIT;  // workgroups per bucket, each planning a range of its slabs
+  const u32 b = blockIdx.x / kS, s = blockIdx.x % kS, fs = g.nf >= kS ? g.nf / kS : g.nf;
+  if (s * fs >= g.nf) return;
+  plan_bucket<false, PL, kPlanTPB>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item, s * fs,
+                                   s + 1 == kS ? g.nf : (s + 1) * fs);
 }
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
@@ -2225,7 +2232,7 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
                                                                        off2, bhint, whint, (u32)n, Ib, done, units, runs,
                                                                        group_on, item, cwin, P, Q, nstride);
     HIPCHK(hipGetLastError());
-    bin_plan_kernel<<<g.nb, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on, item);
+    bin_plan_kernel<<<g.nb * GLINT_PLAN_SPLIT, kPlanTPB, 0, st>>>(g, T, Bb, Ib, off2, bc, units, runs, group_on, item);
     HIPCHK(hipGetLastError());
   }
   // a persistent grid of the resident workgroups: each pipelines its units two deep, in XCD-grouped
