@@ -1408,10 +1408,12 @@ __global__ __launch_bounds__(kPlanTPB) void bin_plan_kernel(BinGeom g, const u32
   typedef PlanLds<kPlanLds, kPlanPTab> PL;
   __shared__ PL L;
   constexpr u32 kS = GLINT_PLAN_SPLIT;  // workgroups per bucket, each planning a range of its slabs
-  const u32 b = blockIdx.x / kS, s = blockIdx.x % kS, fs = g.nf >= kS ? g.nf / kS : g.nf;
+  // (plan_bucket's ranges start at multiples of 64 slabs: a bucket of fewer than 64 kS slabs has fewer
+  // ranges, the spare workgroups return)
+  const u32 b = blockIdx.x / kS, s = blockIdx.x % kS, fs = max(64u, g.nf / kS);
   if (s * fs >= g.nf) return;
   plan_bucket<false, PL, kPlanTPB>(b, g, T, Bb, Ib, off2, bc, units, runs, group_on, L, item, s * fs,
-                                   s + 1 == kS ? g.nf : (s + 1) * fs);
+                                   min(g.nf, (s + 1) * fs));
 }
 
 // FUSED: the plan runs here too -- the workgroup of a bucket's last item to finish plans the bucket
