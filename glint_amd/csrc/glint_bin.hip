@@ -1546,15 +1546,15 @@ __global__ __launch_bounds__(kSTPB) __attribute__((amdgpu_waves_per_eu(8))) void
     return;
   }
   PhaseClock ph(32);
-  // The item's records through buffer windows over its own ranges (workgroup-uniform descriptors, 32-bit
-  // offsets: few registers, so the fine sort keeps two workgroups per CU); a load past the item reads 0
-  // without touching memory, a store at the window's end is dropped (counted stores, see BufOut)
+  // (the item's outputs go through buffer windows over its own ranges: workgroup-uniform descriptors,
+  // 32-bit offsets, a store at the window's end dropped -- counted stores, see BufOut)
   const u32 cnt = s1 - s0;
   // Where the item's records are: record v of the bucket lies in the run of the chunk c with
   // P[b][c] <= v < P[b][c + 1], at partition index Q[b][c] + v. The prefixes of the item's chunks (cwin:
   // those of its first and last records, at most kFWin) go to LDS; every chunk's run marks its first record
   // of the item with its window slot, a forward fill gives every record its run, and the record's index
-  // follows (recomputed where the values load: the marks and places stay in LDS, not in registers).
+  // follows. (Marks past the item's last record are never cleared: a forward fill carries them only to
+  // later places, which no record reads.)
   static_assert(kSItemMax <= 16 * kSTPB && kFWin < 65536 && kSItemMax % 16 == 0,
                 "fill_forward's 16 per thread; u16 marks and window slots");
   const u32 v0 = d.y * item;
