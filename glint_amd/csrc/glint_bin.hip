@@ -636,16 +636,17 @@ __global__ __launch_bounds__(256) void bin_hot_select_kernel(u32* __restrict__ g
 // group sums are added in group order -- the result is the same on every run.
 constexpr int kRedSlots = 64, kRedTPB = 1024, kRedGroups = kRedTPB / kRedSlots;
 // (the picks stay for the next pushes: push_binned clears them itself before it samples again)
+// (run by bin_scan's workgroups past its buckets, blk = which kRedSlots slots: one launch fewer)
 template <typename V>
-__global__ __launch_bounds__(kRedTPB) void bin_hot_reduce_kernel(const unsigned long long* __restrict__ best, u32 G,
-                                                                 const typename LdsAcc<V>::T* __restrict__ partial,
-                                                                 V* __restrict__ data, const LaunchCtl* gated) {
+__device__ __forceinline__ void hot_reduce_block(u32 blk, const unsigned long long* __restrict__ best, u32 G,
+                                                 const typename LdsAcc<V>::T* __restrict__ partial,
+                                                 V* __restrict__ data, const LaunchCtl* gated) {
   typedef typename LdsAcc<V>::T A;
   if (gated && gated->cancel) return;  // a validating push its verdict rejected: nothing is applied
   __shared__ A gs[kRedGroups][kRedSlots];
   __shared__ u32 gany[kRedGroups][kRedSlots];
   const int tid = threadIdx.x, ls = tid % kRedSlots, grp = tid / kRedSlots;
-  const u32 sl = blockIdx.x * (u32)kRedSlots + (u32)ls;
+  const u32 sl = blk * (u32)kRedSlots + (u32)ls;
   const u32 per = (G + kRedGroups - 1) / kRedGroups;
   const u32 w0 = grp * per, w1 = min(G, w0 + per);
   A sum = hot_zero<A>();
@@ -1027,14 +1028,24 @@ __global__ __launch_bounds__(kATPB) void bin_part_dedup_kernel(
 // fine sort's output and its items [Ib[b], Ib[b] + items) -- each bucket takes both with one atomic, in
 // any order -- with cwin[item] = the chunks holding the item's first and last records. Two passes over
 // the bucket's row of the chunk table (the second one hits in cache): its total, then the prefixes.
+// The hot split's sums (bin_hot_reduce) ride along as workgroups past the buckets (best != nullptr).
 constexpr int kScanTPB = 1024;
 constexpr int kScanPer = 8;
+static_assert(kScanTPB == kRedTPB, "one launch for both");
+template <typename V>
 __global__ __launch_bounds__(kScanTPB) void bin_scan_kernel(BinGeom g, const u32* __restrict__ ct, u32 ctstride, i64 n,
                                                             const LaunchCtl* lctl, u32 ntiles, int from_break,
                                                             u32 kchunk, u32 nstride, BinCtl* bc, u32* __restrict__ T,
                                                             u32* __restrict__ Bb, u32* __restrict__ Ib,
                                                             uint2* __restrict__ fitems, uint2* __restrict__ cwin,
-                                                            u32* __restrict__ P, u32* __restrict__ Q, u32 item) {
+                                                            u32* __restrict__ P, u32* __restrict__ Q, u32 item,
+                                                            const unsigned long long* __restrict__ best, u32 G,
+                                                            const typename LdsAcc<V>::T* __restrict__ partial,
+                                                            V* __restrict__ data, const LaunchCtl* gated) {
+  if (blockIdx.x >= g.nb) {
+    hot_reduce_block<V>(blockIdx.x - g.nb, best, G, partial, data, gated);
+    return;
+  }
   __shared__ u32 base2[2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 b = blockIdx.x;
@@ -2203,12 +2214,10 @@ int push_binned(glint_shard* s, const PushArgs<V>& a, bool from_break, hipStream
     rc = (*hook)(bc, T, g.nb);
     if (rc) return rc;
   }
-  if (front == 1) {
-    bin_hot_reduce_kernel<V><<<kWideSlots / kRedSlots, kRedTPB, 0, st>>>(wbest, G, wpart, a.data, vctl);
-    HIPCHK(hipGetLastError());
-  }
-  bin_scan_kernel<<<g.nb, kScanTPB, 0, st>>>(g, ct, ctstride, n, a.ctl, a.ntiles, fb, kchunk, nstride, bc, T, Bb, Ib,
-                                             fitems, cwin, P, Q, item);
+  // (front 1: the hot split's sums added by the same launch's workgroups past the buckets)
+  const u32 red = front == 1 ? (u32)(kWideSlots / kRedSlots) : 0u;
+  bin_scan_kernel<V><<<g.nb + red, kScanTPB, 0, st>>>(g, ct, ctstride, n, a.ctl, a.ntiles, fb, kchunk, nstride, bc, T,
+                                                      Bb, Ib, fitems, cwin, P, Q, item, wbest, G, wpart, a.data, vctl);
   HIPCHK(hipGetLastError());
   // Groups of sparse slabs for vector shards; a matrix shard's sparse slabs stay units of their own: its
   // records cluster in a slab's few hot rows, and grouping cost cfg5 0.309 -> 0.337 ms while it takes
